@@ -1,0 +1,111 @@
+// ba_device.h — device math for the MI355X bundle-adjustment kernels.
+//
+// Camera model = the reference's AngleReprojectionError (Optimizer.h:54-76):
+//   R = AngleAxisToRotationMatrix(w)   (ceres rotation.h, column-major)
+//   p = R X + t ;  q = K p ;  r = (q0/q2 - u, q1/q2 - v)
+// Fixed cameras follow PointOnlyReprojectionError (Optimizer.h:96-107):
+//   p = hnormalized(E [X;1]) with the float 4x4 extrinsic E.
+//
+// The Jacobian is analytic but structured like Ceres' Jet evaluation: dR/dw
+// is the forward derivative of the very same Rodrigues formula (including the
+// first-order branch for theta^2 <= DBL_EPSILON), computed once per camera;
+// the per-observation chain rule then matches autodiff term for term.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bahip {
+
+// Camera record: 48 doubles per camera (384 B), shared by all observations of
+// that camera.  Variable camera:
+//   [0..8]  R (col-major)       [9..35] dR/dw_k (k-major, col-major each)
+//   [36..38] t                  [39..47] K (col-major, double of float)
+// Fixed camera: [0..15] E (col-major 4x4, double of float), [39..47] K.
+constexpr int kCamRec = 48;
+constexpr int kRecR = 0, kRecdR = 9, kRecT = 36, kRecK = 39;
+
+struct D3 {  // value + 3 partial derivatives (d/dw0, d/dw1, d/dw2)
+  double a, d[3];
+};
+__host__ __device__ inline D3 mk(double a, double d0, double d1, double d2) { D3 r; r.a = a; r.d[0] = d0; r.d[1] = d1; r.d[2] = d2; return r; }
+__host__ __device__ inline D3 operator+(D3 f, D3 g) { return mk(f.a + g.a, f.d[0] + g.d[0], f.d[1] + g.d[1], f.d[2] + g.d[2]); }
+__host__ __device__ inline D3 operator-(D3 f, D3 g) { return mk(f.a - g.a, f.d[0] - g.d[0], f.d[1] - g.d[1], f.d[2] - g.d[2]); }
+__host__ __device__ inline D3 operator-(D3 f) { return mk(-f.a, -f.d[0], -f.d[1], -f.d[2]); }
+__host__ __device__ inline D3 operator*(D3 f, D3 g) {
+  return mk(f.a * g.a, f.a * g.d[0] + f.d[0] * g.a, f.a * g.d[1] + f.d[1] * g.a, f.a * g.d[2] + f.d[2] * g.a);
+}
+__host__ __device__ inline D3 operator/(D3 f, D3 g) {
+  const double gi = 1.0 / g.a, fg = f.a * gi;
+  return mk(fg, (f.d[0] - fg * g.d[0]) * gi, (f.d[1] - fg * g.d[1]) * gi, (f.d[2] - fg * g.d[2]) * gi);
+}
+__host__ __device__ inline D3 rsub(double s, D3 f) { return mk(s - f.a, -f.d[0], -f.d[1], -f.d[2]); }
+__host__ __device__ inline D3 dsqrt(D3 f) {
+  const double t = sqrt(f.a), ti = 1.0 / (2.0 * t);
+  return mk(t, f.d[0] * ti, f.d[1] * ti, f.d[2] * ti);
+}
+__host__ __device__ inline D3 dcos(D3 f) { const double s = -sin(f.a); return mk(cos(f.a), s * f.d[0], s * f.d[1], s * f.d[2]); }
+__host__ __device__ inline D3 dsin(D3 f) { const double c = cos(f.a); return mk(sin(f.a), c * f.d[0], c * f.d[1], c * f.d[2]); }
+
+// ceres::AngleAxisToRotationMatrix on duals; R column-major (R[c*3+r]).
+__host__ __device__ inline void angle_axis_to_R_d3(const double w[3], D3 R[9]) {
+  const D3 a0 = mk(w[0], 1, 0, 0), a1 = mk(w[1], 0, 1, 0), a2 = mk(w[2], 0, 0, 1);
+  const D3 theta2 = a0 * a0 + a1 * a1 + a2 * a2;
+  if (theta2.a > 2.220446049250313080847e-16) {
+    const D3 theta = dsqrt(theta2);
+    const D3 wx = a0 / theta, wy = a1 / theta, wz = a2 / theta;
+    const D3 c = dcos(theta), s = dsin(theta);
+    const D3 oc = rsub(1.0, c);
+    R[0] = c + wx * wx * oc;
+    R[1] = wz * s + wx * wy * oc;
+    R[2] = -(wy * s) + wx * wz * oc;
+    R[3] = wx * wy * oc - wz * s;
+    R[4] = c + wy * wy * oc;
+    R[5] = wx * s + wy * wz * oc;
+    R[6] = wy * s + wx * wz * oc;
+    R[7] = -(wx * s) + wy * wz * oc;
+    R[8] = c + wz * wz * oc;
+  } else {
+    R[0] = mk(1, 0, 0, 0); R[1] = a2;             R[2] = -a1;
+    R[3] = -a2;            R[4] = mk(1, 0, 0, 0); R[5] = a0;
+    R[6] = a1;             R[7] = -a0;            R[8] = mk(1, 0, 0, 0);
+  }
+}
+
+// Value-only Rodrigues (same branches, same arithmetic order as the dual one).
+__host__ __device__ inline void angle_axis_to_R(const double w[3], double R[9]) {
+  const double theta2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  if (theta2 > 2.220446049250313080847e-16) {
+    const double theta = sqrt(theta2);
+    const double wx = w[0] / theta, wy = w[1] / theta, wz = w[2] / theta;
+    const double c = cos(theta), s = sin(theta);
+    const double oc = 1.0 - c;
+    R[0] = c + wx * wx * oc;
+    R[1] = wz * s + wx * wy * oc;
+    R[2] = -(wy * s) + wx * wz * oc;
+    R[3] = wx * wy * oc - wz * s;
+    R[4] = c + wy * wy * oc;
+    R[5] = wx * s + wy * wz * oc;
+    R[6] = wy * s + wx * wz * oc;
+    R[7] = -(wx * s) + wy * wz * oc;
+    R[8] = c + wz * wz * oc;
+  } else {
+    R[0] = 1;     R[1] = w[2];  R[2] = -w[1];
+    R[3] = -w[2]; R[4] = 1;     R[5] = w[0];
+    R[6] = w[1];  R[7] = -w[0]; R[8] = 1;
+  }
+}
+
+// ceres::HuberLoss(a) + Corrector: returns rho(s); *scale = sqrt(rho'(s)).
+__host__ __device__ inline double huber(double s, double a, double b, double* scale) {
+  if (a > 0.0 && s > b) {
+    const double r = sqrt(s);
+    double rho1 = a / r;
+    rho1 = rho1 > 2.2250738585072014e-308 ? rho1 : 2.2250738585072014e-308;
+    *scale = sqrt(rho1);
+    return 2.0 * a * r - b;
+  }
+  *scale = 1.0;
+  return s;
+}
+
+}  // namespace bahip

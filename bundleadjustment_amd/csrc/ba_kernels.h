@@ -1,0 +1,94 @@
+// ba_kernels.h — launch interface of the CDNA4 (gfx950) kernels of one LM
+// iteration.  See DESIGN.md §3 for the data layout and the per-kernel
+// roofline.  All arrays live in HBM, observations sorted by (point, camera).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bahip {
+
+constexpr int kThreads = 256;
+constexpr int kMaxBlocks = 2048;        // grid cap of the streaming kernels
+
+// Scalar reduction slots (device buffer d_scal[kNumSlots]).
+enum Slot {
+  SL_COST = 0,      // robustified cost at x (linearisation)
+  SL_LIN_BAD,       // non-finite residual / jacobian count
+  SL_GMAX_P,        // max |x - (x - g)| over point params
+  SL_GN2_P,         // sum (x - (x - g))^2 over point params
+  SL_XN2_P,         // sum x^2 over active point params
+  SL_MCC_NEG,       // sum (J d)^T (r + J d / 2)  (model_cost_change = -this)
+  SL_CCOST,         // robustified cost at the candidate point
+  SL_STEP2_P,       // sum (x - x')^2 over point params
+  SL_CAND_BAD,      // non-finite candidate residual count
+  SL_STEP_BAD,      // non-finite step component count (linear solver failure)
+  SL_ELIM_BAD,      // failed 3x3 point-block Cholesky count
+  SL_GMAX_C, SL_GN2_C, SL_XN2_C, SL_STEP2_C,
+  SL_CHOL_BAD,      // non-positive pivot in the reduced camera system
+  kNumSlots
+};
+
+struct DevProblem {
+  int nc, np, no, nvc;       // cameras, points, observations, active variable cameras
+  int n;                     // reduced system order 6*nvc
+  int ld;                    // leading dimension of the dense reduced matrix
+  double huber_a, huber_b;
+  const int* obs_cam;        // [no]  sorted by (point, camera)
+  const int* obs_pt;         // [no]
+  const float2* uv;          // [no]
+  const int* pt_off;         // [np+1] CSR of observations by point
+  const int* cam_off;        // [nvc+1] CSR of observations by active variable camera
+  const int* cam_obs;        // [..] sorted-observation indices grouped by camera
+  const int* vc;             // [nc] compact variable-camera index or -1
+  const int* cam_of_vc;      // [nvc] camera id of a compact index
+  const uint8_t* cam_fixed;  // [nc]
+  const uint8_t* pt_var;     // [np] 1 = variable point with >=1 residual
+  const float* K;            // [9*nc]
+  const float* extr;         // [16*nc] (fixed cameras)
+};
+
+// Device workspace pointers (see ba_solver.hip for sizes).
+struct DevWork {
+  double* cams;  double* pts;        // x
+  double* cams_c; double* pts_c;     // candidate x'
+  double* rec;   double* rec_c;      // camera records at x / x'
+  double* r;     double* J;          // [2][no], [18][no]
+  double* Hpp;   double* gp;         // [6][np], [3][np]
+  double* scale_p; double* diag_p;   // [3][np]
+  double* Linv;  double* u;          // [6][np], [3][np]
+  double* Hcc;   double* gc;         // [nvc][21], [nvc][6]
+  double* scale_c; double* diag_c;   // [nvc][6]
+  double* delta_c;                   // [nvc][6]
+  double* W;                         // [no][18]  (E L^-T per observation)
+  double* S;                         // [(n+1) x ld] reduced system, row n = rhs
+  double* y;                         // [n] reduced solution
+  const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}
+  const int2* pairs;                 // observation pairs per block
+  double* part;                      // [kNumSlots][kMaxBlocks]
+  double* scal;                      // [kNumSlots]
+};
+
+// --- launchers (all asynchronous on `s`) ---
+void launch_cam_prep(const DevProblem& P, const double* cams, double* rec, bool deriv, hipStream_t s);
+void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s);
+void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
+                           double max_diag, hipStream_t s);
+void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s);
+void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
+                      hipStream_t s);
+void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
+void launch_obs_what(const DevProblem& P, const DevWork& W, hipStream_t s);
+void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s);
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s);
+void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
+void launch_cholesky_solve(const DevProblem& P, const DevWork& W, hipStream_t s);
+void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s);
+void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s);
+// Fold the partials of `slots` (bitmask) into d_scal; kernels producing
+// partials always use grid = nblocks_of(...)
+void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s);
+void launch_residuals(const DevProblem& P, const double* rec, const double* pts, double* r_raw, hipStream_t s);
+
+int grid_for(int n);
+
+}  // namespace bahip

@@ -1,0 +1,949 @@
+// ba_kernels.hip — CDNA4 (gfx950, wave64) kernels of one Levenberg-Marquardt
+// iteration of the reference's Ceres DENSE_SCHUR bundle adjustment
+// (ba_project/src/ba/Optimizer.cpp:80-90, 216-333; Optimizer.h:49-194),
+// re-designed for MI355X:
+//
+//   linearise  (per observation, HBM stream)   r, J  (Huber-corrected)
+//   assemble   (per point / per camera)        Hpp, gp, Hcc, gc, scaling, LM diag
+//   eliminate  (per point / per observation)   L^-1 of (Hpp + D), W = E L^-T
+//   reduce     (per camera, per camera pair)   S = A_cc - sum W W^T, rhs
+//   factor     (dense blocked Cholesky)        S = L L^T, forward folded in
+//   candidate  (per point, HBM stream)         back-substitution, model cost
+//                                              change, candidate cost
+//
+// Every reduction is a fixed-order tree (wave shuffles + LDS, then a
+// fixed-order fold of per-block partials): results are bitwise reproducible
+// run to run.  No floating-point atomics anywhere.
+#include "ba_kernels.h"
+#include "ba_device.h"
+
+namespace bahip {
+
+int grid_for(int n) {
+  int g = (n + kThreads - 1) / kThreads;
+  if (g < 1) g = 1;
+  return g > kMaxBlocks ? kMaxBlocks : g;
+}
+
+// ---------------------------------------------------------------------------
+// reductions
+// ---------------------------------------------------------------------------
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+__device__ inline double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_down(v, off, 64));
+  return v;
+}
+// Block-wide sum of NV values per thread (fixed order).  Result valid in
+// thread 0: out[k].  lds must hold NV * (blockDim/64) doubles.
+template <int NV>
+__device__ inline void block_sum(double (&v)[NV], double* lds, double (&out)[NV]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const double s = wave_sum(v[k]);
+    if (lane == 0) lds[k * 16 + w] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      double s = 0.0;
+      for (int i = 0; i < nw; ++i) s += lds[k * 16 + i];
+      out[k] = s;
+    }
+  }
+  __syncthreads();
+}
+__device__ inline double block_max1(double v, double* lds) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  if (lane == 0) lds[w] = v;
+  __syncthreads();
+  double m = 0.0;
+  if (threadIdx.x == 0) for (int i = 0; i < nw; ++i) m = fmax(m, lds[i]);
+  __syncthreads();
+  return m;
+}
+
+__device__ inline double* part_of(double* part, int slot) { return part + (size_t)slot * kMaxBlocks; }
+
+// ---------------------------------------------------------------------------
+// camera records: R, dR/dw (forward derivative of ceres' Rodrigues), t, K
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_cam_prep(int nc, const double* __restrict__ cams, const float* __restrict__ K,
+                                                  const uint8_t* __restrict__ cam_fixed, const float* __restrict__ extr,
+                                                  double* __restrict__ rec, int deriv) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  double* o = rec + (size_t)c * kCamRec;
+  for (int k = 0; k < 9; ++k) o[kRecK + k] = (double)K[9 * c + k];
+  if (cam_fixed && cam_fixed[c]) {
+    for (int k = 0; k < 16; ++k) o[k] = (double)extr[16 * c + k];
+    return;
+  }
+  const double w[3] = {cams[6 * c], cams[6 * c + 1], cams[6 * c + 2]};
+  if (deriv) {
+    D3 R[9];
+    angle_axis_to_R_d3(w, R);
+    for (int i = 0; i < 9; ++i) {
+      o[kRecR + i] = R[i].a;
+      for (int k = 0; k < 3; ++k) o[kRecdR + k * 9 + i] = R[i].d[k];
+    }
+  } else {
+    double R[9];
+    angle_axis_to_R(w, R);
+    for (int i = 0; i < 9; ++i) o[kRecR + i] = R[i];
+  }
+  for (int k = 0; k < 3; ++k) o[kRecT + k] = cams[6 * c + 3 + k];
+}
+
+// Project one observation; value only.  Returns residual (u,v) in r.
+__device__ inline void project_value(const double* __restrict__ cr, bool cvar, double X0, double X1, double X2,
+                                     float2 uv, double r[2]) {
+  double p[3];
+  if (cvar) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) p[i] = cr[kRecR + i] * X0 + cr[kRecR + 3 + i] * X1 + cr[kRecR + 6 + i] * X2 + cr[kRecT + i];
+  } else {
+    double ph[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ph[i] = X0 * cr[i] + X1 * cr[4 + i] + X2 * cr[8 + i] + cr[12 + i];
+    p[0] = ph[0] / ph[3]; p[1] = ph[1] / ph[3]; p[2] = ph[2] / ph[3];
+  }
+  const double* Kc = cr + kRecK;
+  double q[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) q[i] = p[0] * Kc[i] + p[1] * Kc[3 + i] + p[2] * Kc[6 + i];
+  r[0] = q[0] / q[2] - (double)uv.x;
+  r[1] = q[1] / q[2] - (double)uv.y;
+}
+
+// ---------------------------------------------------------------------------
+// linearisation: one thread per observation (sorted by point), SoA outputs
+//   r[row][no], J[row*9 + param][no]   (param 0..5 camera, 6..8 point)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_linearize(DevProblem P, const double* __restrict__ rec,
+                                                   const double* __restrict__ pts, double* __restrict__ r,
+                                                   double* __restrict__ J, double* __restrict__ part) {
+  __shared__ double lds[2 * 16];
+  double acc[2] = {0.0, 0.0};  // cost, bad
+  const size_t no = (size_t)P.no;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < P.no; o += gridDim.x * blockDim.x) {
+    const int c = P.obs_cam[o], p = P.obs_pt[o];
+    const float2 uv = P.uv[o];
+    const double* __restrict__ cr = rec + (size_t)c * kCamRec;
+    const bool cvar = P.vc[c] >= 0;
+    const bool pvar = P.pt_var[p] != 0;
+    const double X0 = pts[3 * p], X1 = pts[3 * p + 1], X2 = pts[3 * p + 2];
+    double pc[3], dp[3][9];
+    if (cvar) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        pc[i] = cr[kRecR + i] * X0 + cr[kRecR + 3 + i] * X1 + cr[kRecR + 6 + i] * X2 + cr[kRecT + i];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+          dp[i][k] = cr[kRecdR + k * 9 + i] * X0 + cr[kRecdR + k * 9 + 3 + i] * X1 + cr[kRecdR + k * 9 + 6 + i] * X2;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dp[i][3 + k] = (i == k) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dp[i][6 + k] = cr[kRecR + k * 3 + i];
+      }
+    } else {
+      double ph[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ph[i] = X0 * cr[i] + X1 * cr[4 + i] + X2 * cr[8 + i] + cr[12 + i];
+      const double inv = 1.0 / ph[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        pc[i] = ph[i] * inv;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dp[i][k] = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dp[i][6 + k] = (cr[k * 4 + i] - pc[i] * cr[k * 4 + 3]) * inv;
+      }
+    }
+    const double* Kc = cr + kRecK;
+    double q[3], dq[3][9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      q[i] = pc[0] * Kc[i] + pc[1] * Kc[3 + i] + pc[2] * Kc[6 + i];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) dq[i][k] = dp[0][k] * Kc[i] + dp[1][k] * Kc[3 + i] + dp[2][k] * Kc[6 + i];
+    }
+    const double iq = 1.0 / q[2];
+    const double pr0 = q[0] * iq, pr1 = q[1] * iq;
+    const double r0 = pr0 - (double)uv.x, r1 = pr1 - (double)uv.y;
+    double scale;
+    const double rho = huber(r0 * r0 + r1 * r1, P.huber_a, P.huber_b, &scale);
+    acc[0] += 0.5 * rho;
+    bool fin = isfinite(r0) && isfinite(r1);
+    r[o] = r0 * scale;
+    r[no + o] = r1 * scale;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const bool live = (k < 6) ? cvar : pvar;
+      const double j0 = live ? (dq[0][k] - pr0 * dq[2][k]) * iq * scale : 0.0;
+      const double j1 = live ? (dq[1][k] - pr1 * dq[2][k]) * iq * scale : 0.0;
+      fin = fin && isfinite(j0) && isfinite(j1);
+      J[(size_t)k * no + o] = j0;
+      J[(size_t)(9 + k) * no + o] = j1;
+    }
+    acc[1] += fin ? 0.0 : 1.0;
+  }
+  double out[2];
+  block_sum<2>(acc, lds, out);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_COST)[blockIdx.x] = out[0];
+    part_of(part, SL_LIN_BAD)[blockIdx.x] = out[1];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// point blocks: Hpp (xx,xy,xz,yy,yz,zz), gp, jacobi scale, LM diagonal, norms
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const double* __restrict__ r,
+                                                        const double* __restrict__ J, const double* __restrict__ pts,
+                                                        double* __restrict__ Hpp, double* __restrict__ gp,
+                                                        double* __restrict__ scale_p, double* __restrict__ diag_p,
+                                                        int compute_scale, double min_diag, double max_diag,
+                                                        double* __restrict__ part) {
+  __shared__ double lds[3 * 16];
+  double acc[2] = {0.0, 0.0};  // gn2, xn2
+  double gmax = 0.0;
+  const size_t no = (size_t)P.no, np = (size_t)P.np;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
+    if (!P.pt_var[p]) continue;
+    double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+    const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+    for (int o = o0; o < o1; ++o) {
+#pragma unroll
+      for (int row = 0; row < 2; ++row) {
+        const double a = J[(size_t)(row * 9 + 6) * no + o], b = J[(size_t)(row * 9 + 7) * no + o],
+                     c = J[(size_t)(row * 9 + 8) * no + o], rr = r[row * no + o];
+        H[0] += a * a; H[1] += a * b; H[2] += a * c; H[3] += b * b; H[4] += b * c; H[5] += c * c;
+        g[0] += a * rr; g[1] += b * rr; g[2] += c * rr;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Hpp[k * np + p] = H[k];
+    const double hd[3] = {H[0], H[3], H[5]};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      gp[k * np + p] = g[k];
+      double s;
+      if (compute_scale) {
+        s = 1.0 / (1.0 + sqrt(hd[k]));
+        scale_p[k * np + p] = s;
+      } else {
+        s = scale_p[k * np + p];
+      }
+      diag_p[k * np + p] = fmin(fmax(hd[k] * s * s, min_diag), max_diag);
+      const double x = pts[3 * p + k];
+      const double d = x - (x + (-g[k]));
+      gmax = fmax(gmax, fabs(d));
+      acc[0] += d * d;
+      acc[1] += x * x;
+    }
+  }
+  double out[2];
+  block_sum<2>(acc, lds, out);
+  const double m = block_max1(gmax, lds + 32);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_GN2_P)[blockIdx.x] = out[0];
+    part_of(part, SL_XN2_P)[blockIdx.x] = out[1];
+    part_of(part, SL_GMAX_P)[blockIdx.x] = m;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// camera blocks: one workgroup per active variable camera, Hcc (21, lower
+// row-major) and gc (6) from its observations (camera-major index list).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_cam_assemble(DevProblem P, const double* __restrict__ r,
+                                                      const double* __restrict__ J, double* __restrict__ Hcc,
+                                                      double* __restrict__ gc) {
+  __shared__ double lds[27 * 16];
+  const int v = blockIdx.x;
+  const size_t no = (size_t)P.no;
+  double acc[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+  const int i0 = P.cam_off[v], i1 = P.cam_off[v + 1];
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int o = P.cam_obs[i];
+#pragma unroll
+    for (int row = 0; row < 2; ++row) {
+      double j[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) j[k] = J[(size_t)(row * 9 + k) * no + o];
+      const double rr = r[row * no + o];
+      int t = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int b = 0; b <= a; ++b) acc[t++] += j[a] * j[b];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) acc[21 + a] += j[a] * rr;
+    }
+  }
+  double out[27];
+  block_sum<27>(acc, lds, out);
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 21; ++k) Hcc[(size_t)v * 21 + k] = out[k];
+    for (int k = 0; k < 6; ++k) gc[(size_t)v * 6 + k] = out[21 + k];
+  }
+}
+
+__device__ inline int tri(int a, int b) { return a * (a + 1) / 2 + b; }  // a >= b
+
+__global__ __launch_bounds__(256) void k_cam_norms(DevProblem P, const double* __restrict__ cams, const double* __restrict__ Hcc,
+                                                   const double* __restrict__ gc, double* __restrict__ scale_c,
+                                                   double* __restrict__ diag_c, int compute_scale, double min_diag,
+                                                   double max_diag, double* __restrict__ part) {
+  __shared__ double lds[3 * 16];
+  double acc[2] = {0.0, 0.0};
+  double gmax = 0.0;
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < P.nvc; v += gridDim.x * blockDim.x) {
+    const int c = P.cam_of_vc[v];
+    for (int a = 0; a < 6; ++a) {
+      const double h = Hcc[(size_t)v * 21 + tri(a, a)];
+      double s;
+      if (compute_scale) {
+        s = 1.0 / (1.0 + sqrt(h));
+        scale_c[(size_t)v * 6 + a] = s;
+      } else {
+        s = scale_c[(size_t)v * 6 + a];
+      }
+      diag_c[(size_t)v * 6 + a] = fmin(fmax(h * s * s, min_diag), max_diag);
+      const double x = cams[6 * c + a], g = gc[(size_t)v * 6 + a];
+      const double d = x - (x + (-g));
+      gmax = fmax(gmax, fabs(d));
+      acc[0] += d * d;
+      acc[1] += x * x;
+    }
+  }
+  double out[2];
+  block_sum<2>(acc, lds, out);
+  const double m = block_max1(gmax, lds + 32);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_GN2_C)[blockIdx.x] = out[0];
+    part_of(part, SL_XN2_C)[blockIdx.x] = out[1];
+    part_of(part, SL_GMAX_C)[blockIdx.x] = m;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// point elimination: A = s Hpp s + D^2, L L^T = A, store L^-1 and u = L^-1 s*g
+// D = sqrt(diag / radius) (ceres lm_diagonal_), added as D*D.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* __restrict__ Hpp,
+                                                    const double* __restrict__ gp, const double* __restrict__ scale_p,
+                                                    const double* __restrict__ diag_p, double radius,
+                                                    double* __restrict__ Linv, double* __restrict__ u,
+                                                    double* __restrict__ part) {
+  __shared__ double lds[16];
+  double acc[1] = {0.0};
+  const size_t np = (size_t)P.np;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
+    if (!P.pt_var[p]) continue;
+    double s[3], D2[3], gs[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      s[k] = scale_p[k * np + p];
+      const double D = sqrt(diag_p[k * np + p] / radius);
+      D2[k] = D * D;
+      gs[k] = gp[k * np + p] * s[k];
+    }
+    const double h00 = Hpp[0 * np + p] * s[0] * s[0] + D2[0];
+    const double h10 = Hpp[1 * np + p] * s[0] * s[1];
+    const double h20 = Hpp[2 * np + p] * s[0] * s[2];
+    const double h11 = Hpp[3 * np + p] * s[1] * s[1] + D2[1];
+    const double h21 = Hpp[4 * np + p] * s[1] * s[2];
+    const double h22 = Hpp[5 * np + p] * s[2] * s[2] + D2[2];
+    bool ok = h00 > 0.0;
+    const double l00 = sqrt(h00);
+    const double l10 = h10 / l00, l20 = h20 / l00;
+    const double d11 = h11 - l10 * l10;
+    ok = ok && d11 > 0.0;
+    const double l11 = sqrt(d11);
+    const double l21 = (h21 - l20 * l10) / l11;
+    const double d22 = h22 - l20 * l20 - l21 * l21;
+    ok = ok && d22 > 0.0;
+    const double l22 = sqrt(d22);
+    const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+    const double i10 = -(l10 * i00) * i11;
+    const double i21 = -(l21 * i11) * i22;
+    const double i20 = -(l20 * i00 + l21 * i10) * i22;
+    Linv[0 * np + p] = i00; Linv[1 * np + p] = i10; Linv[2 * np + p] = i11;
+    Linv[3 * np + p] = i20; Linv[4 * np + p] = i21; Linv[5 * np + p] = i22;
+    u[0 * np + p] = i00 * gs[0];
+    u[1 * np + p] = i10 * gs[0] + i11 * gs[1];
+    u[2 * np + p] = i20 * gs[0] + i21 * gs[1] + i22 * gs[2];
+    acc[0] += ok ? 0.0 : 1.0;
+  }
+  double out[1];
+  block_sum<1>(acc, lds, out);
+  if (threadIdx.x == 0) part_of(part, SL_ELIM_BAD)[blockIdx.x] = out[0];
+}
+
+// ---------------------------------------------------------------------------
+// per observation (variable camera & point): W = diag(s_c) Jc^T Jp diag(s_p) L^-T
+// stored AoS [no][18] (6x3 row-major) so a pair gather reads 144 contiguous B.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_obs_what(DevProblem P, const double* __restrict__ J,
+                                                  const double* __restrict__ scale_c, const double* __restrict__ scale_p,
+                                                  const double* __restrict__ Linv, double* __restrict__ W) {
+  const size_t no = (size_t)P.no, np = (size_t)P.np;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < P.no; o += gridDim.x * blockDim.x) {
+    const int c = P.obs_cam[o], p = P.obs_pt[o];
+    const int v = P.vc[c];
+    if (v < 0 || !P.pt_var[p]) continue;
+    double jc0[6], jc1[6], jp0[3], jp1[3], sp[3];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const double sc = scale_c[(size_t)v * 6 + k];
+      jc0[k] = J[(size_t)k * no + o] * sc;
+      jc1[k] = J[(size_t)(9 + k) * no + o] * sc;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      sp[k] = scale_p[k * np + p];
+      jp0[k] = J[(size_t)(6 + k) * no + o] * sp[k];
+      jp1[k] = J[(size_t)(15 + k) * no + o] * sp[k];
+    }
+    const double i00 = Linv[0 * np + p], i10 = Linv[1 * np + p], i11 = Linv[2 * np + p];
+    const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
+    double* w = W + (size_t)o * 18;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const double e0 = jc0[a] * jp0[0] + jc1[a] * jp1[0];
+      const double e1 = jc0[a] * jp0[1] + jc1[a] * jp1[1];
+      const double e2 = jc0[a] * jp0[2] + jc1[a] * jp1[2];
+      w[a * 3 + 0] = e0 * i00;
+      w[a * 3 + 1] = e0 * i10 + e1 * i11;
+      w[a * 3 + 2] = e0 * i20 + e1 * i21 + e2 * i22;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// diagonal Schur blocks and rhs (local part): one workgroup per camera
+//   S_cc = -sum W W^T (lower 21) ; b_c = -sum W u_p
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const double* __restrict__ W,
+                                                        const double* __restrict__ u, double* __restrict__ S) {
+  __shared__ double lds[27 * 16];
+  const int v = blockIdx.x;
+  const size_t np = (size_t)P.np;
+  double acc[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+  const int i0 = P.cam_off[v], i1 = P.cam_off[v + 1];
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int o = P.cam_obs[i];
+    const int p = P.obs_pt[o];
+    if (!P.pt_var[p]) continue;
+    double w[18];
+    const double2* w2 = reinterpret_cast<const double2*>(W + (size_t)o * 18);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) { const double2 t = w2[k]; w[2 * k] = t.x; w[2 * k + 1] = t.y; }
+    const double u0 = u[p], u1 = u[np + p], u2 = u[2 * np + p];
+    int t = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+#pragma unroll
+      for (int b = 0; b <= a; ++b) acc[t++] += w[a * 3] * w[b * 3] + w[a * 3 + 1] * w[b * 3 + 1] + w[a * 3 + 2] * w[b * 3 + 2];
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] += w[a * 3] * u0 + w[a * 3 + 1] * u1 + w[a * 3 + 2] * u2;
+  }
+  double out[27];
+  block_sum<27>(acc, lds, out);
+  if (threadIdx.x == 0) {
+    const size_t ld = (size_t)P.ld;
+    int t = 0;
+    for (int a = 0; a < 6; ++a)
+      for (int b = 0; b <= a; ++b) S[(size_t)(6 * v + a) * ld + 6 * v + b] = -out[t++];
+    for (int a = 0; a < 6; ++a) S[(size_t)P.n * ld + 6 * v + a] = -out[21 + a];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// off-diagonal Schur blocks: one wave per camera pair block (I >= J), lanes
+// stride over its observation pairs, fixed-order shuffle reduction.
+//   S_IJ (rows I, cols J) = -sum W_oI W_oJ^T
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* __restrict__ blocks, int nblocks,
+                                                     const int2* __restrict__ pairs, const double* __restrict__ W,
+                                                     double* __restrict__ S) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const size_t ld = (size_t)P.ld;
+  for (int bi = wave; bi < nblocks; bi += nwaves) {
+    const int4 blk = blocks[bi];
+    double acc[36];
+#pragma unroll
+    for (int k = 0; k < 36; ++k) acc[k] = 0.0;
+    for (int e = blk.z + lane; e < blk.w; e += 64) {
+      const int2 pr = pairs[e];
+      double a[18], b[18];
+      const double2* wa = reinterpret_cast<const double2*>(W + (size_t)pr.x * 18);
+      const double2* wb = reinterpret_cast<const double2*>(W + (size_t)pr.y * 18);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const double2 ta = wa[k], tb = wb[k];
+        a[2 * k] = ta.x; a[2 * k + 1] = ta.y; b[2 * k] = tb.x; b[2 * k + 1] = tb.y;
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          acc[i * 6 + j] += a[i * 3] * b[j * 3] + a[i * 3 + 1] * b[j * 3 + 1] + a[i * 3 + 2] * b[j * 3 + 2];
+    }
+#pragma unroll
+    for (int k = 0; k < 36; ++k) acc[k] = wave_sum(acc[k]);
+    if (lane == 0) {
+      const int I = blk.x, Jb = blk.y;
+      if (I != Jb) {
+        for (int i = 0; i < 6; ++i)
+          for (int j = 0; j < 6; ++j) S[(size_t)(6 * I + i) * ld + 6 * Jb + j] = -acc[i * 6 + j];
+      } else {  // duplicate observations of one point by one camera
+        for (int i = 0; i < 6; ++i)
+          for (int j = 0; j <= i; ++j) S[(size_t)(6 * I + i) * ld + 6 * I + j] -= acc[i * 6 + j];
+      }
+    }
+  }
+}
+
+// S_cc += s Hcc s + D^2 ;  b_c += s * g_c      (after any cross-rank reduction)
+__global__ __launch_bounds__(256) void k_cam_add_diag(DevProblem P, const double* __restrict__ Hcc,
+                                                      const double* __restrict__ gc, const double* __restrict__ scale_c,
+                                                      const double* __restrict__ diag_c, double radius,
+                                                      double* __restrict__ S) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= P.nvc) return;
+  const size_t ld = (size_t)P.ld;
+  double s[6];
+  for (int a = 0; a < 6; ++a) s[a] = scale_c[(size_t)v * 6 + a];
+  for (int a = 0; a < 6; ++a) {
+    for (int b = 0; b <= a; ++b) {
+      double h = Hcc[(size_t)v * 21 + tri(a, b)] * s[a] * s[b];
+      if (a == b) {
+        const double D = sqrt(diag_c[(size_t)v * 6 + a] / radius);
+        h += D * D;
+      }
+      S[(size_t)(6 * v + a) * ld + 6 * v + b] += h;
+    }
+    S[(size_t)P.n * ld + 6 * v + a] += gc[(size_t)v * 6 + a] * s[a];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Dense blocked Cholesky of the reduced camera system, lower, row-major,
+// (n+1) x n trapezoid: row n carries the rhs, so the factorisation leaves
+// z = L^-1 b in row n (forward substitution folded into the panel solves).
+// ---------------------------------------------------------------------------
+constexpr int NB = 64;
+
+// Factor the bsz x bsz diagonal block at (k,k): one wave.
+__global__ __launch_bounds__(64) void k_potrf_diag(double* __restrict__ A, int ld, int k, int bsz,
+                                                   double* __restrict__ scal) {
+  __shared__ double T[NB][NB + 1];
+  const int lane = threadIdx.x;
+  for (int i = 0; i < bsz; ++i)
+    if (lane <= i) T[i][lane] = A[(size_t)(k + i) * ld + k + lane];
+  __syncthreads();
+  int bad = 0;
+  for (int j = 0; j < bsz; ++j) {
+    if (lane == j) {
+      const double d = T[j][j];
+      if (!(d > 0.0) || !isfinite(d)) bad = 1;
+      T[j][j] = sqrt(d);
+    }
+    __syncthreads();
+    if (lane > j && lane < bsz) T[lane][j] = T[lane][j] / T[j][j];
+    __syncthreads();
+    if (lane > j && lane < bsz) {
+      const double ltj = T[lane][j];
+      for (int i = lane; i < bsz; ++i) T[i][lane] -= T[i][j] * ltj;
+    }
+    __syncthreads();
+  }
+  for (int i = 0; i < bsz; ++i)
+    if (lane <= i) A[(size_t)(k + i) * ld + k + lane] = T[i][lane];
+  const unsigned long long m = __ballot(bad);
+  if (lane == 0 && m) scal[SL_CHOL_BAD] += 1.0;
+}
+
+// Panel: rows [k+bsz, nrows): X = A_row L_kk^-T.  One thread per row.
+__global__ __launch_bounds__(256) void k_trsm_panel(double* __restrict__ A, int ld, int nrows, int k, int bsz) {
+  __shared__ double L[NB][NB + 1];
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+    const int i = e / NB, j = e % NB;
+    double v;
+    if (i < bsz && j < bsz) v = (j <= i) ? A[(size_t)(k + i) * ld + k + j] : 0.0;
+    else v = (i == j) ? 1.0 : 0.0;
+    L[i][j] = v;
+  }
+  __syncthreads();
+  const int row = k + bsz + blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= nrows) return;
+  double x[NB];
+  double* a = A + (size_t)row * ld + k;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) x[j] = (j < bsz) ? a[j] : 0.0;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    double s = x[j];
+#pragma unroll
+    for (int t = 0; t < j; ++t) s -= x[t] * L[j][t];
+    x[j] = s / L[j][j];
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+    if (j < bsz) a[j] = x[j];
+}
+
+// Trailing update: A[i][j] -= sum_t A[i][k+t] A[j][k+t] for rows i >= k+bsz,
+// cols k+bsz <= j <= min(i, ncols-1).  64x64 tiles, lower tiles only.
+__global__ __launch_bounds__(256) void k_syrk_update(double* __restrict__ A, int ld, int nrows, int ncols, int k,
+                                                     int bsz) {
+  __shared__ double As[NB][NB + 1];
+  __shared__ double Bs[NB][NB + 1];
+  // map blockIdx.x -> lower tile (I, J), J <= I
+  const int t = blockIdx.x;
+  int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  while (I * (I + 1) / 2 > t) --I;
+  const int J = t - I * (I + 1) / 2;
+  const int r0 = k + bsz + I * NB, c0 = k + bsz + J * NB;
+  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+    const int i = e / NB, kk = e % NB;
+    const int ri = r0 + i, cj = c0 + i;
+    As[i][kk] = (ri < nrows && kk < bsz) ? A[(size_t)ri * ld + k + kk] : 0.0;
+    Bs[i][kk] = (cj < ncols && kk < bsz) ? A[(size_t)cj * ld + k + kk] : 0.0;
+  }
+  __syncthreads();
+  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
+  double acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+  for (int kk = 0; kk < bsz; ++kk) {
+    double av[4], bv[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) av[a] = As[ty + 16 * a][kk];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) bv[b] = Bs[tx + 16 * b][kk];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] += av[a] * bv[b];
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int ri = r0 + ty + 16 * a;
+    if (ri >= nrows) continue;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int cj = c0 + tx + 16 * b;
+      if (cj < ncols && cj <= ri) A[(size_t)ri * ld + cj] -= acc[a][b];
+    }
+  }
+}
+
+// Back substitution L^T y = z with z = row n of A; one workgroup, blocked
+// from the bottom.  The diagonal block is staged in LDS and solved by wave 0
+// with register-resident z (shuffle broadcast), then all waves apply the
+// block's columns to the remaining z (coalesced along t).
+__global__ __launch_bounds__(1024) void k_trsv_back(double* __restrict__ A, int ld, int n, double* __restrict__ y) {
+  __shared__ double Ld[NB][NB + 1];
+  __shared__ double yb[NB];
+  double* z = A + (size_t)n * ld;
+  const int nblk = (n + NB - 1) / NB;
+  for (int kb = nblk - 1; kb >= 0; --kb) {
+    const int s0 = kb * NB, e0 = min(n, s0 + NB), bsz = e0 - s0;
+    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
+      const int i = e / NB, j = e % NB;
+      Ld[i][j] = (i < bsz && j <= i) ? A[(size_t)(s0 + i) * ld + s0 + j] : 0.0;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      double zl = lane < bsz ? z[s0 + lane] : 0.0;
+      for (int j = bsz - 1; j >= 0; --j) {
+        const double yj = __shfl(zl, j, 64) / Ld[j][j];
+        if (lane < j) zl -= Ld[j][lane] * yj;
+        if (lane == j) { yb[j] = yj; y[s0 + j] = yj; }
+      }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < s0; t += blockDim.x) {
+      double acc = 0.0;
+      for (int j = 0; j < bsz; ++j) acc += A[(size_t)(s0 + j) * ld + t] * yb[j];
+      z[t] -= acc;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// candidate cameras: x' = x + s * (-y), value-only records at x'
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_cam_candidate(DevProblem P, const double* __restrict__ cams,
+                                                       const double* __restrict__ y, const double* __restrict__ scale_c,
+                                                       double* __restrict__ cams_c, double* __restrict__ delta_c,
+                                                       double* __restrict__ rec_c, double* __restrict__ part) {
+  __shared__ double lds[2 * 16];
+  double acc[2] = {0.0, 0.0};  // step2, bad
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < P.nc; c += gridDim.x * blockDim.x) {
+    const int v = P.vc[c];
+    double x[6], xc[6];
+    for (int a = 0; a < 6; ++a) x[a] = cams[6 * c + a];
+    if (v >= 0) {
+      for (int a = 0; a < 6; ++a) {
+        const double step = -y[6 * v + a];
+        const double d = step * scale_c[(size_t)v * 6 + a];
+        delta_c[(size_t)v * 6 + a] = d;
+        xc[a] = x[a] + d;
+        const double e = x[a] - xc[a];
+        acc[0] += e * e;
+        if (!isfinite(d)) acc[1] += 1.0;
+      }
+    } else {
+      for (int a = 0; a < 6; ++a) xc[a] = x[a];
+    }
+    for (int a = 0; a < 6; ++a) cams_c[6 * c + a] = xc[a];
+    double* o = rec_c + (size_t)c * kCamRec;
+    for (int k = 0; k < 9; ++k) o[kRecK + k] = (double)P.K[9 * c + k];
+    if (P.cam_fixed && P.cam_fixed[c]) {
+      for (int k = 0; k < 16; ++k) o[k] = (double)P.extr[16 * c + k];
+    } else {
+      double R[9];
+      angle_axis_to_R(xc, R);
+      for (int i = 0; i < 9; ++i) o[kRecR + i] = R[i];
+      for (int k = 0; k < 3; ++k) o[kRecT + k] = xc[3 + k];
+    }
+  }
+  double out[2];
+  block_sum<2>(acc, lds, out);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_STEP2_C)[blockIdx.x] = out[0];
+    part_of(part, SL_STEP_BAD)[blockIdx.x] += out[1];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// back-substitution + model cost change + candidate cost, one thread per
+// point (all points; fixed / unobserved points keep x' = x):
+//   y_p = L^-T (u_p - sum W_o^T y_c) ; d_p = s_p * (-y_p) ; X' = X + d_p
+//   per observation: Jd = Jc d_c + Jp d_p ; m += Jd.(r + Jd/2)
+//                    candidate residual at (camera', X') -> Huber cost
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_backsub_candidate(DevProblem P, const double* __restrict__ pts,
+                                                           double* __restrict__ pts_c, const double* __restrict__ W,
+                                                           const double* __restrict__ u, const double* __restrict__ Linv,
+                                                           const double* __restrict__ y, const double* __restrict__ scale_p,
+                                                           const double* __restrict__ J, const double* __restrict__ r,
+                                                           const double* __restrict__ delta_c,
+                                                           const double* __restrict__ rec_c, double* __restrict__ part) {
+  __shared__ double lds[5 * 16];
+  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // mneg, ccost, step2, step_bad, cand_bad
+  const size_t no = (size_t)P.no, np = (size_t)P.np;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
+    const double X[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
+    double dX[3] = {0.0, 0.0, 0.0}, Xc[3] = {X[0], X[1], X[2]};
+    const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+    const bool pvar = P.pt_var[p] != 0;
+    if (pvar) {
+      double w[3] = {u[p], u[np + p], u[2 * np + p]};
+      for (int o = o0; o < o1; ++o) {
+        const int v = P.vc[P.obs_cam[o]];
+        if (v < 0) continue;
+        const double* wo = W + (size_t)o * 18;
+        const double* yc = y + 6 * v;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          const double ya = yc[a];
+          w[0] -= wo[a * 3] * ya; w[1] -= wo[a * 3 + 1] * ya; w[2] -= wo[a * 3 + 2] * ya;
+        }
+      }
+      const double i00 = Linv[0 * np + p], i10 = Linv[1 * np + p], i11 = Linv[2 * np + p];
+      const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
+      const double yp[3] = {i00 * w[0] + i10 * w[1] + i20 * w[2], i11 * w[1] + i21 * w[2], i22 * w[2]};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        dX[k] = (-yp[k]) * scale_p[k * np + p];
+        Xc[k] = X[k] + dX[k];
+        const double e = X[k] - Xc[k];
+        acc[2] += e * e;
+        if (!isfinite(dX[k])) acc[3] += 1.0;
+      }
+    }
+    pts_c[3 * p] = Xc[0]; pts_c[3 * p + 1] = Xc[1]; pts_c[3 * p + 2] = Xc[2];
+    for (int o = o0; o < o1; ++o) {
+      const int c = P.obs_cam[o];
+      const int v = P.vc[c];
+      double jd0 = 0.0, jd1 = 0.0;
+      if (v >= 0) {
+        const double* dc = delta_c + (size_t)v * 6;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          jd0 += J[(size_t)a * no + o] * dc[a];
+          jd1 += J[(size_t)(9 + a) * no + o] * dc[a];
+        }
+      }
+      if (pvar) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          jd0 += J[(size_t)(6 + k) * no + o] * dX[k];
+          jd1 += J[(size_t)(15 + k) * no + o] * dX[k];
+        }
+      }
+      acc[0] += jd0 * (r[o] + jd0 / 2.0) + jd1 * (r[no + o] + jd1 / 2.0);
+      double rc[2];
+      project_value(rec_c + (size_t)c * kCamRec, !(P.cam_fixed && P.cam_fixed[c]), Xc[0], Xc[1], Xc[2], P.uv[o], rc);
+      double sc;
+      const double rho = huber(rc[0] * rc[0] + rc[1] * rc[1], P.huber_a, P.huber_b, &sc);
+      acc[1] += 0.5 * rho;
+      if (!isfinite(rc[0]) || !isfinite(rc[1])) acc[4] += 1.0;
+    }
+  }
+  double out[5];
+  block_sum<5>(acc, lds, out);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_MCC_NEG)[blockIdx.x] = out[0];
+    part_of(part, SL_CCOST)[blockIdx.x] = out[1];
+    part_of(part, SL_STEP2_P)[blockIdx.x] = out[2];
+    part_of(part, SL_STEP_BAD)[blockIdx.x] += out[3];
+    part_of(part, SL_CAND_BAD)[blockIdx.x] = out[4];
+  }
+}
+
+// Raw residuals (no loss) at given records, for ba_eval_residuals.
+__global__ __launch_bounds__(256) void k_residuals(DevProblem P, const double* __restrict__ rec,
+                                                   const double* __restrict__ pts, double* __restrict__ rr) {
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < P.no; o += gridDim.x * blockDim.x) {
+    const int c = P.obs_cam[o], p = P.obs_pt[o];
+    double res[2];
+    project_value(rec + (size_t)c * kCamRec, !(P.cam_fixed && P.cam_fixed[c]), pts[3 * p], pts[3 * p + 1],
+                  pts[3 * p + 2], P.uv[o], res);
+    rr[2 * o] = res[0];
+    rr[2 * o + 1] = res[1];
+  }
+}
+
+// Fold partials -> scalars (fixed order), then clear the partials.
+__global__ __launch_bounds__(1024) void k_reduce(double* __restrict__ part, double* __restrict__ scal,
+                                                 uint32_t sum_mask, uint32_t max_mask) {
+  __shared__ double lds[16];
+  for (int slot = 0; slot < kNumSlots; ++slot) {
+    const bool is_sum = (sum_mask >> slot) & 1u, is_max = (max_mask >> slot) & 1u;
+    if (!is_sum && !is_max) continue;
+    double* pp = part + (size_t)slot * kMaxBlocks;
+    double v = is_max ? 0.0 : 0.0;
+    for (int i = threadIdx.x; i < kMaxBlocks; i += blockDim.x) {
+      v = is_max ? fmax(v, pp[i]) : v + pp[i];
+      pp[i] = 0.0;
+    }
+    double res;
+    if (is_max) {
+      res = block_max1(v, lds);
+    } else {
+      double a[1] = {v}, o[1];
+      block_sum<1>(a, lds, o);
+      res = o[0];
+    }
+    if (threadIdx.x == 0) scal[slot] = res;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+void launch_cam_prep(const DevProblem& P, const double* cams, double* rec, bool deriv, hipStream_t s) {
+  if (P.nc == 0) return;
+  hipLaunchKernelGGL(k_cam_prep, dim3((P.nc + 255) / 256), dim3(256), 0, s, P.nc, cams, P.K, P.cam_fixed, P.extr,
+                     rec, deriv ? 1 : 0);
+}
+void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  hipLaunchKernelGGL(k_linearize, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.rec, W.pts, W.r, W.J, W.part);
+}
+void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
+                           double max_diag, hipStream_t s) {
+  hipLaunchKernelGGL(k_point_assemble, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.r, W.J, W.pts, W.Hpp, W.gp,
+                     W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
+}
+void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  if (P.nvc == 0) return;
+  hipLaunchKernelGGL(k_cam_assemble, dim3(P.nvc), dim3(kThreads), 0, s, P, W.r, W.J, W.Hcc, W.gc);
+}
+void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_cam_norms, dim3(grid_for(P.nvc)), dim3(kThreads), 0, s, P, W.cams, W.Hcc, W.gc, W.scale_c,
+                     W.diag_c, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
+}
+void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
+  hipLaunchKernelGGL(k_point_elim, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.Hpp, W.gp, W.scale_p, W.diag_p,
+                     radius, W.Linv, W.u, W.part);
+}
+void launch_obs_what(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  hipLaunchKernelGGL(k_obs_what, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.J, W.scale_c, W.scale_p, W.Linv,
+                     W.W);
+}
+void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  if (P.nvc == 0) return;
+  hipLaunchKernelGGL(k_cam_schur_diag, dim3(P.nvc), dim3(kThreads), 0, s, P, W.W, W.u, W.S);
+}
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  if (W.nblocks == 0) return;
+  int waves = W.nblocks;
+  int grid = (waves + 3) / 4;
+  if (grid > 4 * kMaxBlocks) grid = 4 * kMaxBlocks;
+  hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
+}
+void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
+  if (P.nvc == 0) return;
+  hipLaunchKernelGGL(k_cam_add_diag, dim3((P.nvc + 255) / 256), dim3(256), 0, s, P, W.Hcc, W.gc, W.scale_c, W.diag_c,
+                     radius, W.S);
+}
+void launch_cholesky_solve(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  const int n = P.n;
+  if (n == 0) return;
+  const int nrows = n + 1;
+  for (int k = 0; k < n; k += NB) {
+    const int b = std::min(NB, n - k);
+    hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(64), 0, s, W.S, P.ld, k, b, W.scal);
+    const int prow = nrows - (k + b);
+    if (prow > 0) {
+      hipLaunchKernelGGL(k_trsm_panel, dim3((prow + 255) / 256), dim3(256), 0, s, W.S, P.ld, nrows, k, b);
+      const int T = (prow + NB - 1) / NB;
+      hipLaunchKernelGGL(k_syrk_update, dim3(T * (T + 1) / 2), dim3(256), 0, s, W.S, P.ld, nrows, n, k, b);
+    }
+  }
+  hipLaunchKernelGGL(k_trsv_back, dim3(1), dim3(1024), 0, s, W.S, P.ld, n, W.y);
+}
+void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  hipLaunchKernelGGL(k_cam_candidate, dim3(grid_for(P.nc)), dim3(kThreads), 0, s, P, W.cams, W.y, W.scale_c,
+                     W.cams_c, W.delta_c, W.rec_c, W.part);
+}
+void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  hipLaunchKernelGGL(k_backsub_candidate, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.W, W.u,
+                     W.Linv, W.y, W.scale_p, W.J, W.r, W.delta_c, W.rec_c, W.part);
+}
+void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, s, W.part, W.scal, sum_mask, max_mask);
+}
+void launch_residuals(const DevProblem& P, const double* rec, const double* pts, double* r_raw, hipStream_t s) {
+  hipLaunchKernelGGL(k_residuals, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, rec, pts, r_raw);
+}
+
+}  // namespace bahip

@@ -1,0 +1,708 @@
+// ba_solver.hip — host side of libba_hip.so: problem structure, device
+// workspace, the Levenberg-Marquardt driver and the extern "C" ABI
+// (include/ba_hip.h).
+//
+// The driver restates ceres::TrustRegionMinimizer + LevenbergMarquardtStrategy
+// with the options of BAOptimizer::configureSolver (reference
+// ba_project/src/ba/Optimizer.cpp:80-90) and drives the CDNA4 kernels of
+// ba_kernels.hip.  Per LM iteration the host reads back one small scalar
+// record (cost, model cost change, norms, failure counts) to take Ceres'
+// accept / reject / terminate decisions; all vectors stay in HBM.
+//
+// Multi-GPU: every rank owns a disjoint set of points with all their
+// observations; cameras are replicated.  RCCL all-reduces (over xGMI) the
+// per-camera blocks after linearisation, the dense reduced camera system
+// after point elimination, and the scalar record after the candidate pass.
+// All ranks then take identical decisions.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/ba_hip.h"
+#include "ba_device.h"
+#include "ba_kernels.h"
+
+using namespace bahip;
+
+namespace {
+
+struct BaError {
+  int code;
+  std::string msg;
+};
+
+#define HIP_OK(expr)                                                                                  \
+  do {                                                                                                \
+    hipError_t _e = (expr);                                                                           \
+    if (_e != hipSuccess)                                                                             \
+      throw BaError{_e == hipErrorOutOfMemory ? BA_ERR_OUT_OF_MEMORY : BA_ERR_DEVICE,                 \
+                    std::string(#expr) + ": " + hipGetErrorString(_e)};                               \
+  } while (0)
+#define NCCL_OK(expr)                                                                                 \
+  do {                                                                                                \
+    ncclResult_t _r = (expr);                                                                         \
+    if (_r != ncclSuccess) throw BaError{BA_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(_r)}; \
+  } while (0)
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+struct ba_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+
+  // multi-GPU
+  int nranks = 1, rank = 0;
+  ncclComm_t comm = nullptr;
+
+  // problem
+  bool have_problem = false;
+  int nc = 0, np = 0, no = 0, nvc = 0, n = 0, ld = 0;
+  std::vector<int> perm;         // sorted obs -> caller obs
+  std::vector<int> cam_of_vc;
+  std::vector<uint8_t> cam_fixed_h;
+  double huber_a = 0.0;
+  DevProblem P{};
+  DevWork W{};
+  std::vector<void*> allocs;     // device buffers of the current problem
+  double* h_scal = nullptr;      // pinned scalar record
+
+  // solver state
+  std::vector<ba_iteration> log;
+  bool scale_valid = false;
+  double t_lin = 0.0, t_solve = 0.0;
+
+  template <typename T>
+  T* dalloc(size_t count) {
+    if (count == 0) count = 1;
+    void* p = nullptr;
+    HIP_OK(hipMalloc(&p, count * sizeof(T)));
+    allocs.push_back(p);
+    return static_cast<T*>(p);
+  }
+  template <typename T>
+  T* upload(const std::vector<T>& v) {
+    T* d = dalloc<T>(v.size());
+    if (!v.empty()) HIP_OK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, stream));
+    return d;
+  }
+  void free_problem() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (void* p : allocs) (void)hipFree(p);
+    allocs.clear();
+    have_problem = false;
+    scale_valid = false;
+    log.clear();
+  }
+
+  void allreduce(double* d, size_t count, ncclRedOp_t op = ncclSum) {
+    if (nranks <= 1 || count == 0) return;
+    NCCL_OK(ncclAllReduce(d, d, count, ncclDouble, op, comm, stream));
+  }
+  void read_scalars() {
+    HIP_OK(hipMemcpyAsync(h_scal, W.scal, sizeof(double) * kNumSlots, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+  }
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// structure build
+// ---------------------------------------------------------------------------
+void set_problem(ba_ctx* ctx, const ba_problem* pb) {
+  if (!pb) throw BaError{BA_ERR_INVALID_ARGUMENT, "problem is NULL"};
+  const int nc = pb->n_cams, np = pb->n_pts, no = pb->n_obs;
+  if (nc < 0 || np < 0 || no < 0) throw BaError{BA_ERR_INVALID_ARGUMENT, "negative size"};
+  if ((nc > 0 && (!pb->cams || !pb->K)) || (np > 0 && !pb->pts) ||
+      (no > 0 && (!pb->obs_cam || !pb->obs_pt || !pb->obs_uv)))
+    throw BaError{BA_ERR_INVALID_ARGUMENT, "missing array"};
+  bool any_fixed = false;
+  for (int c = 0; c < nc; ++c) any_fixed |= (pb->cam_fixed && pb->cam_fixed[c]);
+  if (any_fixed && !pb->cam_fixed_extr) throw BaError{BA_ERR_INVALID_ARGUMENT, "cam_fixed_extr required for fixed cameras"};
+  for (int o = 0; o < no; ++o) {
+    if (pb->obs_cam[o] < 0 || pb->obs_cam[o] >= nc || pb->obs_pt[o] < 0 || pb->obs_pt[o] >= np)
+      throw BaError{BA_ERR_INVALID_ARGUMENT, "observation index out of range at obs " + std::to_string(o)};
+  }
+  ctx->free_problem();
+  HIP_OK(hipSetDevice(ctx->device));
+  ctx->nc = nc; ctx->np = np; ctx->no = no;
+  ctx->huber_a = pb->huber_a;
+  ctx->cam_fixed_h.assign(nc, 0);
+  for (int c = 0; c < nc; ++c) ctx->cam_fixed_h[c] = pb->cam_fixed ? pb->cam_fixed[c] : 0;
+  std::vector<uint8_t> pt_fixed(np, 0);
+  for (int p = 0; p < np; ++p) pt_fixed[p] = pb->pt_fixed ? pb->pt_fixed[p] : 0;
+
+  // sort observations by (point, camera, caller index): counting sort by point
+  std::vector<int> pt_off(np + 1, 0);
+  for (int o = 0; o < no; ++o) pt_off[pb->obs_pt[o] + 1]++;
+  for (int p = 0; p < np; ++p) pt_off[p + 1] += pt_off[p];
+  std::vector<int> perm(no);
+  {
+    std::vector<int> fill(pt_off.begin(), pt_off.end() - 1);
+    for (int o = 0; o < no; ++o) perm[fill[pb->obs_pt[o]]++] = o;
+    for (int p = 0; p < np; ++p) {
+      auto b = perm.begin() + pt_off[p], e = perm.begin() + pt_off[p + 1];
+      if (e - b > 1)
+        std::stable_sort(b, e, [&](int a, int c) { return pb->obs_cam[a] < pb->obs_cam[c]; });
+    }
+  }
+  // active blocks
+  std::vector<int> vc(nc, -1);
+  std::vector<uint8_t> pt_var(np, 0), cam_used(nc, 0);
+  for (int o = 0; o < no; ++o) {
+    const int c = pb->obs_cam[o], p = pb->obs_pt[o];
+    if (!ctx->cam_fixed_h[c]) cam_used[c] = 1;
+    if (!pt_fixed[p]) pt_var[p] = 1;
+  }
+  ctx->cam_of_vc.clear();
+  for (int c = 0; c < nc; ++c)
+    if (cam_used[c]) { vc[c] = (int)ctx->cam_of_vc.size(); ctx->cam_of_vc.push_back(c); }
+  const int nvc = (int)ctx->cam_of_vc.size();
+  ctx->nvc = nvc;
+  ctx->n = 6 * nvc;
+  ctx->ld = ctx->n;
+
+  std::vector<int> obs_cam(no), obs_pt(no);
+  std::vector<float2> uv(no);
+  for (int s = 0; s < no; ++s) {
+    const int o = perm[s];
+    obs_cam[s] = pb->obs_cam[o];
+    obs_pt[s] = pb->obs_pt[o];
+    uv[s] = make_float2(pb->obs_uv[2 * o], pb->obs_uv[2 * o + 1]);
+  }
+  // observations by variable camera (increasing sorted index)
+  std::vector<int> cam_off(nvc + 1, 0);
+  for (int s = 0; s < no; ++s) if (vc[obs_cam[s]] >= 0) cam_off[vc[obs_cam[s]] + 1]++;
+  for (int v = 0; v < nvc; ++v) cam_off[v + 1] += cam_off[v];
+  std::vector<int> cam_obs(cam_off[nvc]);
+  {
+    std::vector<int> fill(cam_off.begin(), cam_off.end() - 1);
+    for (int s = 0; s < no; ++s) if (vc[obs_cam[s]] >= 0) cam_obs[fill[vc[obs_cam[s]]]++] = s;
+  }
+  // Schur pair lists: for every variable point, every pair of its observations
+  // by variable cameras contributes W_a W_b^T to block (vc_a, vc_b), vc_a >= vc_b.
+  std::vector<int4> blocks;
+  std::vector<int2> pairs;
+  {
+    struct PE { int64_t key; int a, b; };
+    std::vector<PE> pe;
+    size_t est = 0;
+    for (int p = 0; p < np; ++p) if (pt_var[p]) { const size_t k = pt_off[p + 1] - pt_off[p]; est += k * (k - 1) / 2; }
+    pe.reserve(est);
+    std::vector<int> lst;
+    for (int p = 0; p < np; ++p) {
+      if (!pt_var[p]) continue;
+      lst.clear();
+      for (int s = pt_off[p]; s < pt_off[p + 1]; ++s) if (vc[obs_cam[s]] >= 0) lst.push_back(s);
+      for (size_t i = 0; i < lst.size(); ++i)
+        for (size_t j = 0; j < i; ++j) {
+          const int a = lst[i], b = lst[j];        // vc[a] >= vc[b] (sorted by camera)
+          const int I = vc[obs_cam[a]], J = vc[obs_cam[b]];
+          const int64_t key = (int64_t)I * nvc + J;
+          pe.push_back({key, a, b});
+          if (I == J) pe.push_back({key, b, a});    // duplicate camera on one point
+        }
+    }
+    // stable counting/radix by key keeps point order inside a block
+    std::stable_sort(pe.begin(), pe.end(), [](const PE& x, const PE& y) { return x.key < y.key; });
+    pairs.resize(pe.size());
+    for (size_t i = 0; i < pe.size(); ++i) {
+      pairs[i] = make_int2(pe[i].a, pe[i].b);
+      if (i == 0 || pe[i].key != pe[i - 1].key) {
+        if (!blocks.empty()) blocks.back().w = (int)i;
+        blocks.push_back(make_int4((int)(pe[i].key / nvc), (int)(pe[i].key % nvc), (int)i, 0));
+      }
+    }
+    if (!blocks.empty()) blocks.back().w = (int)pe.size();
+  }
+
+  // ---- device upload
+  DevProblem& P = ctx->P;
+  P = DevProblem{};
+  P.nc = nc; P.np = np; P.no = no; P.nvc = nvc; P.n = ctx->n; P.ld = ctx->ld;
+  P.huber_a = pb->huber_a;
+  P.huber_b = pb->huber_a * pb->huber_a;
+  P.obs_cam = ctx->upload(obs_cam);
+  P.obs_pt = ctx->upload(obs_pt);
+  P.uv = ctx->upload(uv);
+  P.pt_off = ctx->upload(pt_off);
+  P.cam_off = ctx->upload(cam_off);
+  P.cam_obs = ctx->upload(cam_obs);
+  P.vc = ctx->upload(vc);
+  P.cam_of_vc = ctx->upload(ctx->cam_of_vc);
+  P.cam_fixed = ctx->upload(ctx->cam_fixed_h);
+  P.pt_var = ctx->upload(pt_var);
+  P.K = ctx->upload(std::vector<float>(pb->K, pb->K + 9 * (size_t)nc));
+  {
+    std::vector<float> ex(16 * (size_t)nc, 0.0f);
+    if (pb->cam_fixed_extr)
+      for (int c = 0; c < nc; ++c)
+        if (ctx->cam_fixed_h[c]) std::memcpy(&ex[16 * (size_t)c], pb->cam_fixed_extr + 16 * (size_t)c, 16 * sizeof(float));
+    P.extr = ctx->upload(ex);
+  }
+  DevWork& W = ctx->W;
+  W = DevWork{};
+  W.cams = ctx->upload(std::vector<double>(pb->cams, pb->cams + 6 * (size_t)nc));
+  W.pts = ctx->upload(std::vector<double>(pb->pts, pb->pts + 3 * (size_t)np));
+  W.cams_c = ctx->dalloc<double>(6 * (size_t)nc);
+  W.pts_c = ctx->dalloc<double>(3 * (size_t)np);
+  W.rec = ctx->dalloc<double>((size_t)kCamRec * nc);
+  W.rec_c = ctx->dalloc<double>((size_t)kCamRec * nc);
+  W.r = ctx->dalloc<double>(2 * (size_t)no);
+  W.J = ctx->dalloc<double>(18 * (size_t)no);
+  W.Hpp = ctx->dalloc<double>(6 * (size_t)np);
+  W.gp = ctx->dalloc<double>(3 * (size_t)np);
+  W.scale_p = ctx->dalloc<double>(3 * (size_t)np);
+  W.diag_p = ctx->dalloc<double>(3 * (size_t)np);
+  W.Linv = ctx->dalloc<double>(6 * (size_t)np);
+  W.u = ctx->dalloc<double>(3 * (size_t)np);
+  W.Hcc = ctx->dalloc<double>(21 * (size_t)nvc);
+  W.gc = ctx->dalloc<double>(6 * (size_t)nvc);
+  W.scale_c = ctx->dalloc<double>(6 * (size_t)nvc);
+  W.diag_c = ctx->dalloc<double>(6 * (size_t)nvc);
+  W.delta_c = ctx->dalloc<double>(6 * (size_t)nvc);
+  W.W = ctx->dalloc<double>(18 * (size_t)no);
+  W.S = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
+  W.y = ctx->dalloc<double>(std::max(ctx->n, 1));
+  W.blocks = ctx->upload(blocks);
+  W.nblocks = (int)blocks.size();
+  W.pairs = ctx->upload(pairs);
+  W.part = ctx->dalloc<double>((size_t)kNumSlots * kMaxBlocks);
+  W.scal = ctx->dalloc<double>(kNumSlots);
+  HIP_OK(hipMemsetAsync(W.part, 0, sizeof(double) * kNumSlots * kMaxBlocks, ctx->stream));
+  HIP_OK(hipMemsetAsync(W.scal, 0, sizeof(double) * kNumSlots, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  ctx->perm.swap(perm);
+  ctx->have_problem = true;
+}
+
+// ---------------------------------------------------------------------------
+// LM phases
+// ---------------------------------------------------------------------------
+struct LinResult { double cost, gmax, gnorm, xnorm; bool ok; };
+
+constexpr uint32_t bit(int s) { return 1u << s; }
+
+LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max_diag, float* rj_ms = nullptr) {
+  const hipStream_t s = ctx->stream;
+  DevProblem& P = ctx->P;
+  DevWork& W = ctx->W;
+  launch_cam_prep(P, W.cams, W.rec, true, s);
+  if (rj_ms) HIP_OK(hipEventRecord(ctx->ev[2], s));
+  launch_linearize(P, W, s);
+  if (rj_ms) HIP_OK(hipEventRecord(ctx->ev[3], s));
+  launch_point_assemble(P, W, compute_scale, min_diag, max_diag, s);
+  launch_cam_assemble(P, W, s);
+  launch_reduce(W, bit(SL_COST) | bit(SL_LIN_BAD) | bit(SL_GN2_P) | bit(SL_XN2_P), bit(SL_GMAX_P), s);
+  if (ctx->nranks > 1) {
+    ctx->allreduce(W.Hcc, 21 * (size_t)ctx->nvc);
+    ctx->allreduce(W.gc, 6 * (size_t)ctx->nvc);
+    ctx->allreduce(W.scal + SL_COST, 2);          // COST, LIN_BAD
+    ctx->allreduce(W.scal + SL_GN2_P, 2);         // GN2_P, XN2_P
+    ctx->allreduce(W.scal + SL_GMAX_P, 1, ncclMax);
+  }
+  launch_cam_norms(P, W, compute_scale, min_diag, max_diag, s);
+  launch_reduce(W, bit(SL_GN2_C) | bit(SL_XN2_C), bit(SL_GMAX_C), s);
+  ctx->read_scalars();
+  if (rj_ms) HIP_OK(hipEventElapsedTime(rj_ms, ctx->ev[2], ctx->ev[3]));
+  const double* h = ctx->h_scal;
+  LinResult r;
+  r.cost = h[SL_COST];
+  r.gmax = std::max(h[SL_GMAX_P], h[SL_GMAX_C]);
+  r.gnorm = std::sqrt(h[SL_GN2_P] + h[SL_GN2_C]);
+  r.xnorm = std::sqrt(h[SL_XN2_P] + h[SL_XN2_C]);
+  r.ok = h[SL_LIN_BAD] == 0.0 && std::isfinite(r.cost);
+  if (compute_scale) ctx->scale_valid = true;
+  return r;
+}
+
+struct StepResult { bool linear_ok; double mcc, cand_cost, step_norm; };
+
+StepResult solve_step(ba_ctx* ctx, double radius) {
+  const hipStream_t s = ctx->stream;
+  DevProblem& P = ctx->P;
+  DevWork& W = ctx->W;
+  if (ctx->n > 0) HIP_OK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)(ctx->n + 1) * ctx->ld, s));
+  HIP_OK(hipMemsetAsync(W.scal + SL_CHOL_BAD, 0, sizeof(double), s));
+  launch_point_elim(P, W, radius, s);
+  launch_obs_what(P, W, s);
+  launch_cam_schur_diag(P, W, s);
+  launch_schur_pairs(P, W, s);
+  launch_reduce(W, bit(SL_ELIM_BAD), 0, s);
+  if (ctx->nranks > 1) {
+    ctx->allreduce(W.S, (size_t)(ctx->n + 1) * ctx->ld);
+    ctx->allreduce(W.scal + SL_ELIM_BAD, 1);
+  }
+  launch_cam_add_diag(P, W, radius, s);
+  launch_cholesky_solve(P, W, s);
+  launch_cam_candidate(P, W, s);
+  launch_backsub_candidate(P, W, s);
+  launch_reduce(W, bit(SL_MCC_NEG) | bit(SL_CCOST) | bit(SL_STEP2_P) | bit(SL_CAND_BAD) | bit(SL_STEP_BAD) |
+                       bit(SL_STEP2_C), 0, s);
+  if (ctx->nranks > 1) {
+    ctx->allreduce(W.scal + SL_MCC_NEG, 5);  // MCC_NEG, CCOST, STEP2_P, CAND_BAD, STEP_BAD
+  }
+  ctx->read_scalars();
+  const double* h = ctx->h_scal;
+  StepResult r;
+  r.linear_ok = h[SL_ELIM_BAD] == 0.0 && h[SL_CHOL_BAD] == 0.0 && h[SL_STEP_BAD] == 0.0;
+  r.mcc = -h[SL_MCC_NEG];
+  r.cand_cost = h[SL_CAND_BAD] > 0.0 || !std::isfinite(h[SL_CCOST]) ? std::numeric_limits<double>::max() : h[SL_CCOST];
+  r.step_norm = std::sqrt(h[SL_STEP2_P] + h[SL_STEP2_C]);
+  return r;
+}
+
+void accept_candidate(ba_ctx* ctx) {
+  std::swap(ctx->W.cams, ctx->W.cams_c);
+  std::swap(ctx->W.pts, ctx->W.pts_c);
+}
+
+// ---------------------------------------------------------------------------
+// ceres TrustRegionMinimizer (LM, monotonic) restated over the device phases
+// ---------------------------------------------------------------------------
+void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
+  if (!ctx->have_problem) throw BaError{BA_ERR_NO_PROBLEM, "ba_solve before ba_set_problem"};
+  ba_options o;
+  if (opt) o = *opt; else ba_default_options(&o);
+  const double t0 = now_s();
+  ctx->log.clear();
+  ctx->t_lin = ctx->t_solve = 0.0;
+  ba_summary S{};
+  auto push = [&](const ba_iteration& it) { ctx->log.push_back(it); };
+  double radius = o.initial_trust_region_radius, decrease_factor = 2.0;
+  int consecutive_invalid = 0;
+
+  double tl = now_s();
+  LinResult L = linearize(ctx, o.jacobi_scaling != 0, o.min_lm_diagonal, o.max_lm_diagonal);
+  ctx->t_lin += now_s() - tl;
+  if (!o.jacobi_scaling) {
+    // scale = 1: write ones (kernels always read scale arrays)
+    std::vector<double> ones(3 * (size_t)ctx->np, 1.0), onesc(6 * (size_t)ctx->nvc, 1.0);
+    HIP_OK(hipMemcpy(ctx->W.scale_p, ones.data(), ones.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(ctx->W.scale_c, onesc.data(), onesc.size() * sizeof(double), hipMemcpyHostToDevice));
+    L = linearize(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal);
+  }
+  S.initial_cost = L.cost;
+  if (!L.ok) {
+    S.final_cost = L.cost;
+    S.termination_type = BA_FAILURE;
+    S.total_time_s = now_s() - t0;
+    if (sum) *sum = S;
+    return;
+  }
+  {
+    ba_iteration it{};
+    it.iteration = 0; it.step_is_valid = 1; it.step_is_successful = 1;
+    it.cost = L.cost; it.gradient_max_norm = L.gmax; it.gradient_norm = L.gnorm;
+    it.trust_region_radius = radius;
+    it.iteration_time_s = now_s() - t0;
+    push(it);
+  }
+  double x_cost = L.cost, x_norm = L.xnorm, gmax = L.gmax, gnorm = L.gnorm;
+  int iteration = 0;
+  int termination = BA_NO_CONVERGENCE;
+  bool last_success = true;
+  auto can_continue = [&]() {
+    if (iteration >= o.max_num_iterations) { termination = BA_NO_CONVERGENCE; return false; }
+    if (last_success && gmax <= o.gradient_tolerance) { termination = BA_CONVERGENCE; return false; }
+    if (radius <= o.min_trust_region_radius) { termination = BA_CONVERGENCE; return false; }
+    return true;
+  };
+  while (can_continue()) {
+    const double ti = now_s();
+    ++iteration;
+    ba_iteration it{};
+    it.iteration = iteration;
+    double ts = now_s();
+    StepResult st = solve_step(ctx, radius);
+    ctx->t_solve += now_s() - ts;
+    const bool valid = st.linear_ok && st.mcc > 0.0;
+    it.model_cost_change = st.mcc;
+    if (!valid) {
+      if (++consecutive_invalid >= o.max_num_consecutive_invalid_steps) { termination = BA_FAILURE; break; }
+      radius = radius / decrease_factor;
+      decrease_factor *= 2.0;
+      it.cost = x_cost; it.gradient_max_norm = gmax; it.gradient_norm = gnorm;
+      it.trust_region_radius = radius; it.step_is_valid = 0; it.step_is_successful = 0;
+      last_success = false;
+      S.num_unsuccessful_steps++;
+      it.iteration_time_s = now_s() - ti;
+      push(it);
+      continue;
+    }
+    consecutive_invalid = 0;
+    it.step_norm = st.step_norm;
+    if (st.step_norm <= o.parameter_tolerance * (x_norm + o.parameter_tolerance)) { termination = BA_CONVERGENCE; break; }
+    const double cost_change = x_cost - st.cand_cost;
+    it.cost_change = cost_change;
+    if (std::fabs(cost_change) <= o.function_tolerance * x_cost) { termination = BA_CONVERGENCE; break; }
+    const double rel = st.cand_cost >= std::numeric_limits<double>::max() ? std::numeric_limits<double>::lowest()
+                                                                          : (x_cost - st.cand_cost) / st.mcc;
+    it.relative_decrease = rel;
+    if (rel > o.min_relative_decrease) {
+      accept_candidate(ctx);
+      tl = now_s();
+      L = linearize(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal);
+      ctx->t_lin += now_s() - tl;
+      if (!L.ok) { termination = BA_FAILURE; x_cost = L.cost; break; }
+      x_cost = L.cost; x_norm = L.xnorm; gmax = L.gmax; gnorm = L.gnorm;
+      radius = std::min(o.max_trust_region_radius, radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3)));
+      decrease_factor = 2.0;
+      last_success = true;
+      S.num_successful_steps++;
+      it.cost = x_cost; it.step_is_successful = 1;
+    } else {
+      radius = radius / decrease_factor;
+      decrease_factor *= 2.0;
+      last_success = false;
+      S.num_unsuccessful_steps++;
+      it.cost = st.cand_cost; it.step_is_successful = 0;
+    }
+    it.gradient_max_norm = gmax; it.gradient_norm = gnorm; it.trust_region_radius = radius; it.step_is_valid = 1;
+    it.iteration_time_s = now_s() - ti;
+    push(it);
+  }
+  S.final_cost = x_cost;
+  S.termination_type = termination;
+  S.num_iterations = iteration;
+  S.total_time_s = now_s() - t0;
+  S.linearize_time_s = ctx->t_lin;
+  S.solve_time_s = ctx->t_solve;
+  if (sum) *sum = S;
+}
+
+void get_params(ba_ctx* ctx, double* cams, double* pts) {
+  if (!ctx->have_problem) throw BaError{BA_ERR_NO_PROBLEM, "no problem"};
+  if (cams && ctx->nc) HIP_OK(hipMemcpy(cams, ctx->W.cams, 6 * sizeof(double) * ctx->nc, hipMemcpyDeviceToHost));
+  if (pts && ctx->np) HIP_OK(hipMemcpy(pts, ctx->W.pts, 3 * sizeof(double) * ctx->np, hipMemcpyDeviceToHost));
+}
+
+}  // namespace
+
+// ============================================================================
+// extern "C" ABI
+// ============================================================================
+template <typename F>
+static int guarded(ba_ctx* ctx, F&& f) {
+  try {
+    f();
+    return BA_OK;
+  } catch (const BaError& e) {
+    if (ctx) ctx->err = e.msg;
+    return e.code;
+  } catch (const std::exception& e) {
+    if (ctx) ctx->err = e.what();
+    return BA_ERR_DEVICE;
+  } catch (...) {
+    if (ctx) ctx->err = "unknown error";
+    return BA_ERR_DEVICE;
+  }
+}
+
+extern "C" {
+
+int ba_abi_version(void) { return BA_ABI_VERSION; }
+
+void ba_default_options(ba_options* o) {
+  if (!o) return;
+  o->max_num_iterations = 50;
+  o->max_num_consecutive_invalid_steps = 5;
+  o->jacobi_scaling = 1;
+  o->linear_solver = BA_DENSE_SCHUR;
+  o->function_tolerance = 1e-6;
+  o->gradient_tolerance = 1e-10;
+  o->parameter_tolerance = 1e-8;
+  o->initial_trust_region_radius = 1e4;
+  o->max_trust_region_radius = 1e16;
+  o->min_trust_region_radius = 1e-32;
+  o->min_relative_decrease = 1e-3;
+  o->min_lm_diagonal = 1e-6;
+  o->max_lm_diagonal = 1e32;
+}
+
+int ba_create(ba_ctx** out, int device) {
+  if (!out) return BA_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  ba_ctx* ctx = new ba_ctx();
+  try {
+    int ndev = 0;
+    HIP_OK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) throw BaError{BA_ERR_INVALID_ARGUMENT, "invalid device " + std::to_string(device)};
+    ctx->device = device;
+    HIP_OK(hipSetDevice(device));
+    HIP_OK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    for (auto& e : ctx->ev) HIP_OK(hipEventCreate(&e));
+    HIP_OK(hipHostMalloc(&ctx->h_scal, sizeof(double) * kNumSlots, hipHostMallocDefault));
+  } catch (const BaError& e) {
+    std::fprintf(stderr, "ba_create: %s\n", e.msg.c_str());
+    delete ctx;
+    return e.code;
+  }
+  *out = ctx;
+  return BA_OK;
+}
+
+int ba_destroy(ba_ctx* ctx) {
+  if (!ctx) return BA_OK;
+  (void)hipSetDevice(ctx->device);
+  ctx->free_problem();
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
+  if (ctx->h_scal) (void)hipHostFree(ctx->h_scal);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return BA_OK;
+}
+
+const char* ba_last_error(const ba_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int ba_comm_unique_id(char id[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  if (!id) return BA_ERR_INVALID_ARGUMENT;
+  ncclUniqueId uid;
+  if (ncclGetUniqueId(&uid) != ncclSuccess) return BA_ERR_COMM;
+  std::memcpy(id, &uid, 128);
+  return BA_OK;
+}
+
+int ba_comm_init(ba_ctx* ctx, const char id[128], int nranks, int rank) {
+  if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] {
+    HIP_OK(hipSetDevice(ctx->device));
+    if (ctx->comm) { ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    if (nranks > 1) {
+      ncclUniqueId uid;
+      std::memcpy(&uid, id, 128);
+      NCCL_OK(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
+    }
+  });
+}
+
+int ba_set_problem(ba_ctx* ctx, const ba_problem* problem) {
+  if (!ctx) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] { set_problem(ctx, problem); });
+}
+
+int ba_set_params(ba_ctx* ctx, const double* cams, const double* pts) {
+  if (!ctx) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] {
+    if (!ctx->have_problem) throw BaError{BA_ERR_NO_PROBLEM, "no problem"};
+    if (cams && ctx->nc) HIP_OK(hipMemcpy(ctx->W.cams, cams, 6 * sizeof(double) * ctx->nc, hipMemcpyHostToDevice));
+    if (pts && ctx->np) HIP_OK(hipMemcpy(ctx->W.pts, pts, 3 * sizeof(double) * ctx->np, hipMemcpyHostToDevice));
+  });
+}
+
+int ba_solve(ba_ctx* ctx, const ba_options* opt, ba_summary* summary) {
+  if (!ctx) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] { HIP_OK(hipSetDevice(ctx->device)); solve(ctx, opt, summary); });
+}
+
+int ba_get_params(ba_ctx* ctx, double* cams, double* pts) {
+  if (!ctx) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] { get_params(ctx, cams, pts); });
+}
+
+int ba_get_iteration_log(ba_ctx* ctx, ba_iteration* out, int n) {
+  if (!ctx) return -BA_ERR_INVALID_ARGUMENT;
+  const int avail = (int)ctx->log.size();
+  if (out && n > 0) std::memcpy(out, ctx->log.data(), sizeof(ba_iteration) * std::min(n, avail));
+  return avail;
+}
+
+int ba_eval_residuals(ba_ctx* ctx, double* r, double* cost) {
+  if (!ctx) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] {
+    if (!ctx->have_problem) throw BaError{BA_ERR_NO_PROBLEM, "no problem"};
+    HIP_OK(hipSetDevice(ctx->device));
+    const int no = ctx->no;
+    double* d_r = nullptr;
+    HIP_OK(hipMalloc(&d_r, sizeof(double) * 2 * std::max(no, 1)));
+    launch_cam_prep(ctx->P, ctx->W.cams, ctx->W.rec_c, false, ctx->stream);
+    launch_residuals(ctx->P, ctx->W.rec_c, ctx->W.pts, d_r, ctx->stream);
+    std::vector<double> rs(2 * (size_t)no);
+    HIP_OK(hipMemcpyAsync(rs.data(), d_r, sizeof(double) * 2 * no, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(d_r);
+    double c = 0.0;
+    const double a = ctx->huber_a, b = a * a;
+    for (int s = 0; s < no; ++s) {
+      const int o = ctx->perm[s];
+      if (r) { r[2 * o] = rs[2 * s]; r[2 * o + 1] = rs[2 * s + 1]; }
+      double sc;
+      c += 0.5 * huber(rs[2 * s] * rs[2 * s] + rs[2 * s + 1] * rs[2 * s + 1], a, b, &sc);
+    }
+    if (cost) *cost = c;
+  });
+}
+
+int ba_linearize(ba_ctx* ctx, double* r, double* J, double* cost) {
+  if (!ctx) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] {
+    if (!ctx->have_problem) throw BaError{BA_ERR_NO_PROBLEM, "no problem"};
+    HIP_OK(hipSetDevice(ctx->device));
+    ba_options o;
+    ba_default_options(&o);
+    LinResult L = linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
+    const int no = ctx->no;
+    std::vector<double> rs(2 * (size_t)no), Js(18 * (size_t)no);
+    HIP_OK(hipMemcpy(rs.data(), ctx->W.r, sizeof(double) * rs.size(), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(Js.data(), ctx->W.J, sizeof(double) * Js.size(), hipMemcpyDeviceToHost));
+    for (int s = 0; s < no; ++s) {
+      const int o2 = ctx->perm[s];
+      if (r) { r[2 * o2] = rs[s]; r[2 * o2 + 1] = rs[(size_t)no + s]; }
+      if (J)
+        for (int k = 0; k < 18; ++k) J[(size_t)o2 * 18 + k] = Js[(size_t)k * no + s];
+    }
+    if (cost) *cost = L.cost;
+  });
+}
+
+int ba_synchronize(ba_ctx* ctx) {
+  if (!ctx) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] { HIP_OK(hipStreamSynchronize(ctx->stream)); });
+}
+
+int ba_bench_iterations(ba_ctx* ctx, int iters, double radius, double* ms_per_iter, double* ms_rj_kernel) {
+  if (!ctx || iters < 1) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] {
+    if (!ctx->have_problem) throw BaError{BA_ERR_NO_PROBLEM, "no problem"};
+    HIP_OK(hipSetDevice(ctx->device));
+    ba_options o;
+    ba_default_options(&o);
+    if (!ctx->scale_valid) linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
+    double rj_total = 0.0;
+    HIP_OK(hipEventRecord(ctx->ev[0], ctx->stream));
+    for (int i = 0; i < iters; ++i) {
+      float rj = 0.0f;
+      linearize(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, &rj);
+      rj_total += rj;
+      solve_step(ctx, radius);
+    }
+    HIP_OK(hipEventRecord(ctx->ev[1], ctx->stream));
+    HIP_OK(hipEventSynchronize(ctx->ev[1]));
+    float total = 0.0f;
+    HIP_OK(hipEventElapsedTime(&total, ctx->ev[0], ctx->ev[1]));
+    if (ms_per_iter) *ms_per_iter = total / iters;
+    if (ms_rj_kernel) *ms_rj_kernel = rj_total / iters;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,185 @@
+"""Host-side Python handle on libba_hip.so: one `Solver` per (process, GPU).
+
+Mirrors the ceres::Problem / ceres::Solve seam the reference uses
+(ba_project/src/ba/Optimizer.cpp:225-242): build the problem, solve with the
+options of BAOptimizer::configureSolver (Optimizer.cpp:80-90), read back the
+parameters.  Everything numeric runs in the HIP library.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+from .problem import Problem
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+@dataclass
+class Options:
+    """ceres::Solver::Options fields used by the reference (+ Ceres defaults)."""
+    max_num_iterations: int = 50
+    max_num_consecutive_invalid_steps: int = 5
+    jacobi_scaling: bool = True
+    function_tolerance: float = 1e-6
+    gradient_tolerance: float = 1e-10
+    parameter_tolerance: float = 1e-8
+    initial_trust_region_radius: float = 1e4
+    max_trust_region_radius: float = 1e16
+    min_trust_region_radius: float = 1e-32
+    min_relative_decrease: float = 1e-3
+    min_lm_diagonal: float = 1e-6
+    max_lm_diagonal: float = 1e32
+
+    def to_c(self) -> N.ba_options:
+        o = N.ba_options()
+        o.max_num_iterations = int(self.max_num_iterations)
+        o.max_num_consecutive_invalid_steps = int(self.max_num_consecutive_invalid_steps)
+        o.jacobi_scaling = int(bool(self.jacobi_scaling))
+        o.linear_solver = 0
+        for f in ("function_tolerance", "gradient_tolerance", "parameter_tolerance",
+                  "initial_trust_region_radius", "max_trust_region_radius", "min_trust_region_radius",
+                  "min_relative_decrease", "min_lm_diagonal", "max_lm_diagonal"):
+            setattr(o, f, float(getattr(self, f)))
+        return o
+
+
+@dataclass
+class Summary:
+    initial_cost: float
+    final_cost: float
+    num_iterations: int
+    num_successful_steps: int
+    num_unsuccessful_steps: int
+    termination_type: str
+    total_time_s: float
+    linearize_time_s: float
+    solve_time_s: float
+
+
+ITER_FIELDS = [f for f, _ in N.ba_iteration._fields_ if f != "reserved"]
+
+
+class Solver:
+    """A ba_ctx on one HIP device."""
+
+    def __init__(self, device: int = 0):
+        self.lib = N.load_library()
+        h = C.c_void_p()
+        st = self.lib.ba_create(C.byref(h), int(device))
+        if st != N.BA_OK:
+            raise N.BAError(st, f"ba_create(device={device}) failed")
+        self.h = h
+        self.problem: Problem | None = None
+        self._keep = []
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ba_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, st: int, what: str):
+        if st != N.BA_OK:
+            raise N.BAError(st, f"{what}: {self.lib.ba_last_error(self.h).decode(errors='replace')}")
+
+    # -- multi-GPU ------------------------------------------------------
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = N.load_library()
+        buf = C.create_string_buffer(128)
+        st = lib.ba_comm_unique_id(buf)
+        if st != N.BA_OK:
+            raise N.BAError(st, "ba_comm_unique_id")
+        return buf.raw
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        assert len(uid) == 128
+        self._check(self.lib.ba_comm_init(self.h, C.c_char_p(uid), int(nranks), int(rank)), "ba_comm_init")
+
+    # -- problem ----------------------------------------------------------
+    def set_problem(self, problem: Problem):
+        p = problem.normalized()
+        s = N.ba_problem()
+        s.n_cams, s.n_pts, s.n_obs = p.n_cams, p.n_pts, p.n_obs
+        s.cams, s.K, s.pts = _ptr(p.cams), _ptr(p.K), _ptr(p.pts)
+        s.cam_fixed, s.cam_fixed_extr, s.pt_fixed = _ptr(p.cam_fixed), _ptr(p.cam_fixed_extr), _ptr(p.pt_fixed)
+        s.obs_cam, s.obs_pt, s.obs_uv = _ptr(p.obs_cam), _ptr(p.obs_pt), _ptr(p.obs_uv)
+        s.huber_a = p.huber_a
+        self._check(self.lib.ba_set_problem(self.h, C.byref(s)), "ba_set_problem")
+        self.problem = p
+
+    def set_params(self, cams: np.ndarray | None, pts: np.ndarray | None):
+        c = None if cams is None else np.ascontiguousarray(cams, np.float64)
+        q = None if pts is None else np.ascontiguousarray(pts, np.float64)
+        self._check(self.lib.ba_set_params(self.h, _ptr(c), _ptr(q)), "ba_set_params")
+
+    def solve(self, options: Options | None = None) -> Summary:
+        o = (options or Options()).to_c()
+        s = N.ba_summary()
+        self._check(self.lib.ba_solve(self.h, C.byref(o), C.byref(s)), "ba_solve")
+        return Summary(s.initial_cost, s.final_cost, s.num_iterations, s.num_successful_steps,
+                       s.num_unsuccessful_steps, N.TERMINATION_NAMES.get(s.termination_type, str(s.termination_type)),
+                       s.total_time_s, s.linearize_time_s, s.solve_time_s)
+
+    def params(self) -> tuple[np.ndarray, np.ndarray]:
+        p = self.problem
+        cams = np.empty((p.n_cams, 6))
+        pts = np.empty((p.n_pts, 3))
+        self._check(self.lib.ba_get_params(self.h, _ptr(cams), _ptr(pts)), "ba_get_params")
+        return cams, pts
+
+    def iteration_log(self) -> list[dict]:
+        n = self.lib.ba_get_iteration_log(self.h, None, 0)
+        arr = (N.ba_iteration * max(n, 1))()
+        self.lib.ba_get_iteration_log(self.h, arr, n)
+        return [{f: getattr(arr[i], f) for f in ITER_FIELDS} for i in range(n)]
+
+    def residuals(self) -> tuple[np.ndarray, float]:
+        r = np.empty((self.problem.n_obs, 2))
+        cost = C.c_double()
+        self._check(self.lib.ba_eval_residuals(self.h, _ptr(r), C.byref(cost)), "ba_eval_residuals")
+        return r, cost.value
+
+    def linearize(self) -> tuple[np.ndarray, np.ndarray, float]:
+        n = self.problem.n_obs
+        r = np.empty((n, 2))
+        J = np.empty((n, 2, 9))
+        cost = C.c_double()
+        self._check(self.lib.ba_linearize(self.h, _ptr(r), _ptr(J), C.byref(cost)), "ba_linearize")
+        return r, J, cost.value
+
+    def synchronize(self):
+        self._check(self.lib.ba_synchronize(self.h), "ba_synchronize")
+
+    def bench_iterations(self, iters: int, radius: float = 1e4) -> tuple[float, float]:
+        ms = C.c_double()
+        rj = C.c_double()
+        self._check(self.lib.ba_bench_iterations(self.h, int(iters), float(radius), C.byref(ms), C.byref(rj)),
+                    "ba_bench_iterations")
+        return ms.value, rj.value
+
+
+def solve(problem: Problem, options: Options | None = None, device: int = 0):
+    """One-shot convenience: returns (cams, pts, summary, iteration_log)."""
+    with Solver(device) as s:
+        s.set_problem(problem)
+        summ = s.solve(options)
+        cams, pts = s.params()
+        return cams, pts, summ, s.iteration_log()

@@ -1,0 +1,189 @@
+/*
+ * ba_hip.h — C-ABI of libba_hip.so, the MI355X-native replacement for the
+ * reference's Ceres Problem/Solve bundle-adjustment path.
+ *
+ * Reference seam being replaced (MatteoWohlrapp/BundleAdjustment,
+ * ba_project/src/ba):
+ *   ceres::Problem problem;                                 Optimizer.cpp:229
+ *   problem.AddResidualBlock(cost, HuberLoss(sqrt(5.991)),  Optimizer.cpp:312-329
+ *                            cam6*, pt3*)                   (also :486-490, :645-691)
+ *   configureSolver(options)  -> LM, DENSE_SCHUR, ...       Optimizer.cpp:80-90
+ *   ceres::Solve(options, &problem, &summary)               Optimizer.cpp:242, 442, 570
+ *
+ * Conventions (match the reference's parameter layout, Optimizer.h:54-76):
+ *   camera block  double[6] = [wx, wy, wz, tx, ty, tz]: world->camera,
+ *                 angle-axis + translation, additive update (no manifold).
+ *   point block   double[3] world position.
+ *   K             float[9]  column-major 3x3 (Eigen Matrix3f storage).
+ *   fixed camera  float[16] column-major 4x4 world->camera extrinsic, used
+ *                 exactly like PointOnlyReprojectionError (Optimizer.h:96-107).
+ *   observation   (camera index, point index, float2 pixel).
+ *   Residual kind per observation (chosen like prepareConstraints,
+ *   Optimizer.cpp:306-329 / 472-490 / 668-691):
+ *     camera variable, point variable -> AngleReprojectionError      (2x[6,3])
+ *     camera fixed,    point variable -> PointOnlyReprojectionError  (2x[3])
+ *     camera variable, point fixed    -> PoseOnlyAngleReprojectionError (2x[6])
+ *     both fixed                      -> constant block (cost only)
+ *   Each residual carries ceres::HuberLoss(huber_a) (huber_a <= 0: no loss).
+ *
+ * Error behaviour: no exceptions cross the ABI.  Every call returns a status
+ * (BA_OK == 0); ba_last_error(ctx) describes the last failure.  Solver
+ * non-convergence is NOT an error: it is reported in ba_summary exactly like
+ * ceres::Solver::Summary::termination_type (which the reference ignores).
+ *
+ * Threading: a ba_ctx is not thread-safe; use one context per calling thread.
+ * All calls block until their results are on the host.
+ */
+#ifndef BA_HIP_H_
+#define BA_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BA_ABI_VERSION 1
+
+enum ba_status {
+  BA_OK = 0,
+  BA_ERR_INVALID_ARGUMENT = 1,
+  BA_ERR_DEVICE = 2,          /* HIP runtime / kernel failure */
+  BA_ERR_OUT_OF_MEMORY = 3,
+  BA_ERR_NO_PROBLEM = 4,      /* ba_solve before ba_set_problem */
+  BA_ERR_COMM = 5             /* RCCL failure */
+};
+
+enum ba_termination {          /* ceres::TerminationType subset */
+  BA_CONVERGENCE = 0,
+  BA_NO_CONVERGENCE = 1,
+  BA_FAILURE = 2
+};
+
+enum ba_linear_solver {
+  BA_DENSE_SCHUR = 0           /* ceres::DENSE_SCHUR (Optimizer.cpp:85) */
+};
+
+typedef struct ba_ctx ba_ctx;
+
+/* Problem description (caller-owned host SoA; copied to the device by
+ * ba_set_problem).  Replaces the AddResidualBlock loop of prepareConstraints. */
+typedef struct {
+  int32_t n_cams, n_pts, n_obs, reserved;
+  const double*  cams;            /* [6*n_cams]                             */
+  const uint8_t* cam_fixed;       /* [n_cams] 1 = constant (may be NULL)    */
+  const float*   cam_fixed_extr;  /* [16*n_cams] col-major; read for fixed cams (may be NULL if none) */
+  const float*   K;               /* [9*n_cams] col-major                   */
+  const double*  pts;             /* [3*n_pts]                              */
+  const uint8_t* pt_fixed;        /* [n_pts] 1 = constant (may be NULL)     */
+  const int32_t* obs_cam;         /* [n_obs]                                */
+  const int32_t* obs_pt;          /* [n_obs]                                */
+  const float*   obs_uv;          /* [2*n_obs]                              */
+  double huber_a;                 /* sqrt(5.991) in the reference           */
+} ba_problem;
+
+/* ceres::Solver::Options fields the reference touches (configureSolver,
+ * Optimizer.cpp:80-90) plus the Ceres defaults it inherits. */
+typedef struct {
+  int32_t max_num_iterations;                 /* m_nMaxItPerBA (Optimizer.h:203,212) */
+  int32_t max_num_consecutive_invalid_steps;  /* 5  */
+  int32_t jacobi_scaling;                     /* 1  */
+  int32_t linear_solver;                      /* BA_DENSE_SCHUR */
+  double function_tolerance;                  /* 1e-6  */
+  double gradient_tolerance;                  /* 1e-10 */
+  double parameter_tolerance;                 /* 1e-8  */
+  double initial_trust_region_radius;         /* 1e4   */
+  double max_trust_region_radius;             /* 1e16  */
+  double min_trust_region_radius;             /* 1e-32 */
+  double min_relative_decrease;               /* 1e-3  */
+  double min_lm_diagonal;                     /* 1e-6  */
+  double max_lm_diagonal;                     /* 1e32  */
+} ba_options;
+
+/* ceres::Solver::Summary subset */
+typedef struct {
+  double initial_cost;
+  double final_cost;
+  int32_t num_iterations;
+  int32_t num_successful_steps;
+  int32_t num_unsuccessful_steps;
+  int32_t termination_type;        /* enum ba_termination */
+  double total_time_s;             /* wall time of ba_solve */
+  double linearize_time_s;         /* device time: residual+Jacobian+assembly */
+  double solve_time_s;             /* device time: Schur + reduced solve + back-sub + candidate */
+} ba_summary;
+
+/* ceres::IterationSummary subset (one record per minimizer iteration,
+ * iteration 0 = initial evaluation). */
+typedef struct {
+  int32_t iteration;
+  int32_t step_is_valid;
+  int32_t step_is_successful;
+  int32_t reserved;
+  double cost;
+  double cost_change;
+  double gradient_max_norm;
+  double gradient_norm;
+  double step_norm;
+  double relative_decrease;
+  double trust_region_radius;
+  double model_cost_change;
+  double iteration_time_s;
+} ba_iteration;
+
+int ba_abi_version(void);
+void ba_default_options(ba_options* opt);       /* Ceres defaults, max_num_iterations = 50 */
+
+/* Context on one HIP device (the process's GPU).  Owns device buffers, the
+ * HIP stream and (after ba_comm_init) the RCCL communicator. */
+int ba_create(ba_ctx** ctx, int device);
+int ba_destroy(ba_ctx* ctx);
+const char* ba_last_error(const ba_ctx* ctx);
+
+/* Multi-GPU (points sharded across ranks; cameras replicated).  Every rank
+ * calls ba_comm_init with the same 128-byte id produced by ba_comm_unique_id
+ * on rank 0 (exchange it with any host transport, e.g. torch.distributed).
+ * Per LM iteration the ranks all-reduce the camera-side system over RCCL. */
+int ba_comm_unique_id(char id[128]);
+int ba_comm_init(ba_ctx* ctx, const char id[128], int nranks, int rank);
+
+/* Copy a problem to the device and build its (fixed) structure. */
+int ba_set_problem(ba_ctx* ctx, const ba_problem* problem);
+
+/* Replace the parameter values of the current problem (same structure). */
+int ba_set_params(ba_ctx* ctx, const double* cams, const double* pts);
+
+/* Levenberg-Marquardt with DENSE_SCHUR (ceres::Solve semantics). */
+int ba_solve(ba_ctx* ctx, const ba_options* opt, ba_summary* summary);
+
+/* Current parameters (after ba_solve: the returned minimum). */
+int ba_get_params(ba_ctx* ctx, double* cams, double* pts);
+
+/* Iteration log of the last ba_solve: copies min(n, available) records,
+ * returns the number available (or <0 on error). */
+int ba_get_iteration_log(ba_ctx* ctx, ba_iteration* out, int n);
+
+/* Raw functor residuals r[2*n_obs] in caller observation order and the total
+ * robustified cost 0.5*sum(rho) (used for pruning and tests). */
+int ba_eval_residuals(ba_ctx* ctx, double* r, double* cost);
+
+/* Linearisation at the current parameters in caller order: Huber-corrected
+ * residuals r[2*n_obs] and Jacobian J[n_obs][2][9] (camera 6 | point 3;
+ * zero blocks for constant parameter blocks).  Test/inspection entry point. */
+int ba_linearize(ba_ctx* ctx, double* r, double* J, double* cost);
+
+/* Blocks until all device work of the context is done. */
+int ba_synchronize(ba_ctx* ctx);
+
+/* Timing hooks for bench.py: one LM iteration = linearise + assemble + Schur
+ * + reduced solve + back-substitution + candidate evaluation at a fixed
+ * trust-region radius (no accept/reject bookkeeping).  Runs `iters`
+ * iterations on the context's stream and returns the device-measured
+ * (HIP events) average milliseconds of the whole iteration and of the
+ * residual+Jacobian kernel alone. */
+int ba_bench_iterations(ba_ctx* ctx, int iters, double radius, double* ms_per_iter, double* ms_rj_kernel);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BA_HIP_H_ */

@@ -1,0 +1,1025 @@
+// =============================================================================
+//  ORACLE — TEST INFRASTRUCTURE ONLY.  Never linked into, called by, or shipped
+//  with the product (libba_hip.so).  Only tests/, __graft_entry__.smoke() and
+//  bench.py's cpu_baseline leg may load it, and only as the checker / the
+//  labelled "CPU restatement, not Ceres" baseline.
+//
+//  What it is: a plain C++17 CPU restatement of the reference's bundle-
+//  adjustment hot path (MatteoWohlrapp/BundleAdjustment, ba_project/src/ba):
+//
+//    * the three cost functors the application uses, templated on a scalar
+//      type exactly like the reference and differentiated by a forward-mode
+//      Jet (the same mechanism as ceres::AutoDiffCostFunction):
+//        AngleReprojectionError          Optimizer.h:49-88   (2 x [6,3])
+//        PointOnlyReprojectionError      Optimizer.h:91-120  (2 x [3])
+//        PoseOnlyAngleReprojectionError  Optimizer.h:156-194 (2 x [6])
+//    * ceres::HuberLoss(sqrt(5.991)) + Ceres' Corrector
+//        (Optimizer.cpp:312, 489, 645, 686)
+//    * ceres AngleAxisToRotationMatrix / RotationMatrixToAngleAxis
+//        (called Optimizer.h:61,167; Optimizer.cpp:264,298,450,464,592,631)
+//    * Ceres' TrustRegionMinimizer + LevenbergMarquardtStrategy with the
+//      options of BAOptimizer::configureSolver (Optimizer.cpp:80-90) and
+//      Ceres defaults for everything else
+//    * the DENSE_SCHUR linear solver (Optimizer.cpp:85): Schur elimination of
+//      point (e-)blocks, dense Cholesky of the reduced camera system, back-
+//      substitution.
+//
+//  Ceres itself is a third-party dependency that is NOT vendored in the
+//  reference (CMakeLists.txt:22, version unpinned: libceres-dev from
+//  ubuntu:latest = Ceres 2.0.0 / 2.2.0).  Its algorithm is restated here from
+//  its published source/documentation (trust_region_minimizer.cc,
+//  levenberg_marquardt_strategy.cc, trust_region_step_evaluator.cc,
+//  corrector.cc, loss_function.cc, rotation.h, jet.h).
+//
+//  PARITY UNPINNED: the reference holds no golden vectors, fixtures or tests
+//  for this path and cannot be built here (Ceres, Eigen,
+//  OpenCV absent).  This restatement is cross-checked instead by known-answer
+//  tests (rotation round trips, noise-free convergence to ground truth) and by
+//  an independent torch-fp64 restatement of the functors (tests/golden/).
+// =============================================================================
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <vector>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace oracle {
+
+// ----------------------------------------------------------------------------
+// Forward-mode dual number with N derivative slots (ceres/jet.h semantics).
+// ----------------------------------------------------------------------------
+template <int N>
+struct Jet {
+  double a;
+  double v[N];
+  Jet() : a(0) { for (int i = 0; i < N; ++i) v[i] = 0; }
+  explicit Jet(double x) : a(x) { for (int i = 0; i < N; ++i) v[i] = 0; }
+  Jet(double x, int k) : a(x) { for (int i = 0; i < N; ++i) v[i] = 0; v[k] = 1.0; }
+};
+template <int N> inline Jet<N> operator+(const Jet<N>& f, const Jet<N>& g) { Jet<N> h(f.a + g.a); for (int i = 0; i < N; ++i) h.v[i] = f.v[i] + g.v[i]; return h; }
+template <int N> inline Jet<N> operator-(const Jet<N>& f, const Jet<N>& g) { Jet<N> h(f.a - g.a); for (int i = 0; i < N; ++i) h.v[i] = f.v[i] - g.v[i]; return h; }
+template <int N> inline Jet<N> operator-(const Jet<N>& f) { Jet<N> h(-f.a); for (int i = 0; i < N; ++i) h.v[i] = -f.v[i]; return h; }
+template <int N> inline Jet<N> operator*(const Jet<N>& f, const Jet<N>& g) { Jet<N> h(f.a * g.a); for (int i = 0; i < N; ++i) h.v[i] = f.a * g.v[i] + f.v[i] * g.a; return h; }
+template <int N> inline Jet<N> operator/(const Jet<N>& f, const Jet<N>& g) {
+  // ceres: a/b, derivative (f.v - (f.a/g.a) g.v) / g.a
+  const double ginv = 1.0 / g.a; const double fg = f.a * ginv;
+  Jet<N> h(fg); for (int i = 0; i < N; ++i) h.v[i] = (f.v[i] - fg * g.v[i]) * ginv; return h;
+}
+template <int N> inline Jet<N> operator+(const Jet<N>& f, double s) { Jet<N> h = f; h.a += s; return h; }
+template <int N> inline Jet<N> operator+(double s, const Jet<N>& f) { Jet<N> h = f; h.a += s; return h; }
+template <int N> inline Jet<N> operator-(const Jet<N>& f, double s) { Jet<N> h = f; h.a -= s; return h; }
+template <int N> inline Jet<N> operator-(double s, const Jet<N>& f) { Jet<N> h(s - f.a); for (int i = 0; i < N; ++i) h.v[i] = -f.v[i]; return h; }
+template <int N> inline Jet<N> operator*(const Jet<N>& f, double s) { Jet<N> h(f.a * s); for (int i = 0; i < N; ++i) h.v[i] = f.v[i] * s; return h; }
+template <int N> inline Jet<N> operator*(double s, const Jet<N>& f) { return f * s; }
+template <int N> inline Jet<N> operator/(const Jet<N>& f, double s) { const double si = 1.0 / s; Jet<N> h(f.a * si); for (int i = 0; i < N; ++i) h.v[i] = f.v[i] * si; return h; }
+template <int N> inline bool operator>(const Jet<N>& f, double s) { return f.a > s; }
+template <int N> inline Jet<N> sqrt(const Jet<N>& f) { const double t = std::sqrt(f.a); const double ti = 1.0 / (2.0 * t); Jet<N> h(t); for (int i = 0; i < N; ++i) h.v[i] = f.v[i] * ti; return h; }
+template <int N> inline Jet<N> cos(const Jet<N>& f) { Jet<N> h(std::cos(f.a)); const double d = -std::sin(f.a); for (int i = 0; i < N; ++i) h.v[i] = d * f.v[i]; return h; }
+template <int N> inline Jet<N> sin(const Jet<N>& f) { Jet<N> h(std::sin(f.a)); const double d = std::cos(f.a); for (int i = 0; i < N; ++i) h.v[i] = d * f.v[i]; return h; }
+using std::sqrt; using std::sin; using std::cos;
+
+inline double scalar_of(double x) { return x; }
+template <int N> inline double scalar_of(const Jet<N>& x) { return x.a; }
+
+// ----------------------------------------------------------------------------
+// ceres/rotation.h restated.  R is column-major (ceres ColumnMajorAdapter3x3),
+// which is also how Eigen reads it at Optimizer.h:62 (Matrix<T,3,3>(rotMat)).
+// ----------------------------------------------------------------------------
+template <typename T>
+void AngleAxisToRotationMatrix(const T* aa, T* R) {
+  auto Rm = [&](int r, int c) -> T& { return R[c * 3 + r]; };
+  const T theta2 = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
+  if (scalar_of(theta2) > std::numeric_limits<double>::epsilon()) {
+    const T theta = sqrt(theta2);
+    const T wx = aa[0] / theta, wy = aa[1] / theta, wz = aa[2] / theta;
+    const T c = cos(theta), s = sin(theta);
+    const T one_c = 1.0 - c;
+    Rm(0, 0) = c + wx * wx * one_c;
+    Rm(1, 0) = wz * s + wx * wy * one_c;
+    Rm(2, 0) = -(wy * s) + wx * wz * one_c;
+    Rm(0, 1) = wx * wy * one_c - wz * s;
+    Rm(1, 1) = c + wy * wy * one_c;
+    Rm(2, 1) = wx * s + wy * wz * one_c;
+    Rm(0, 2) = wy * s + wx * wz * one_c;
+    Rm(1, 2) = -(wx * s) + wy * wz * one_c;
+    Rm(2, 2) = c + wz * wz * one_c;
+  } else {
+    // first-order Taylor expansion near zero (ceres)
+    Rm(0, 0) = T(1.0); Rm(1, 0) = aa[2];  Rm(2, 0) = -aa[1];
+    Rm(0, 1) = -aa[2]; Rm(1, 1) = T(1.0); Rm(2, 1) = aa[0];
+    Rm(0, 2) = aa[1];  Rm(1, 2) = -aa[0]; Rm(2, 2) = T(1.0);
+  }
+}
+
+// RotationMatrixToAngleAxis = RotationMatrixToQuaternion (Shepperd) followed by
+// QuaternionToAngleAxis (atan2 with the cos<0 flip).  R column-major.
+void RotationMatrixToAngleAxis(const double* R, double* aa) {
+  auto Rm = [&](int r, int c) { return R[c * 3 + r]; };
+  double q[4];
+  const double trace = Rm(0, 0) + Rm(1, 1) + Rm(2, 2);
+  if (trace >= 0.0) {
+    double t = std::sqrt(trace + 1.0);
+    q[0] = 0.5 * t;
+    t = 0.5 / t;
+    q[1] = (Rm(2, 1) - Rm(1, 2)) * t;
+    q[2] = (Rm(0, 2) - Rm(2, 0)) * t;
+    q[3] = (Rm(1, 0) - Rm(0, 1)) * t;
+  } else {
+    int i = 0;
+    if (Rm(1, 1) > Rm(0, 0)) i = 1;
+    if (Rm(2, 2) > Rm(i, i)) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    double t = std::sqrt(Rm(i, i) - Rm(j, j) - Rm(k, k) + 1.0);
+    q[i + 1] = 0.5 * t;
+    t = 0.5 / t;
+    q[0] = (Rm(k, j) - Rm(j, k)) * t;
+    q[j + 1] = (Rm(j, i) + Rm(i, j)) * t;
+    q[k + 1] = (Rm(k, i) + Rm(i, k)) * t;
+  }
+  const double q1 = q[1], q2 = q[2], q3 = q[3];
+  const double sin_sq = q1 * q1 + q2 * q2 + q3 * q3;
+  if (sin_sq > 0.0) {
+    const double sin_theta = std::sqrt(sin_sq);
+    const double cos_theta = q[0];
+    const double two_theta = 2.0 * ((cos_theta < 0.0) ? std::atan2(-sin_theta, -cos_theta)
+                                                       : std::atan2(sin_theta, cos_theta));
+    const double k = two_theta / sin_theta;
+    aa[0] = q1 * k; aa[1] = q2 * k; aa[2] = q3 * k;
+  } else {
+    aa[0] = q1 * 2.0; aa[1] = q2 * 2.0; aa[2] = q3 * 2.0;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// The three functors, restated from Optimizer.h.  K and the observation are
+// float in the reference (Matrix3f / Vector2f) and promoted to T.
+// K and extr are column-major (Eigen default storage).
+// ----------------------------------------------------------------------------
+template <typename T>
+inline void project_K(const float* K, const T* p, T* res, float u, float v) {
+  // (cameraIntrinsics.cast<T>() * p).hnormalized() - observed_pos.cast<T>()
+  T q[3];
+  for (int i = 0; i < 3; ++i)
+    q[i] = p[0] * double(K[0 * 3 + i]) + p[1] * double(K[1 * 3 + i]) + p[2] * double(K[2 * 3 + i]);
+  res[0] = q[0] / q[2] - double(u);
+  res[1] = q[1] / q[2] - double(v);
+}
+
+// AngleReprojectionError::operator()  (Optimizer.h:54-76)
+template <typename T>
+void angle_reprojection(const T* cam, const T* pt, const float* K, float u, float v, T* res) {
+  T R[9];
+  AngleAxisToRotationMatrix(cam, R);
+  T p[3];
+  for (int i = 0; i < 3; ++i) p[i] = R[0 * 3 + i] * pt[0] + R[1 * 3 + i] * pt[1] + R[2 * 3 + i] * pt[2] + cam[3 + i];
+  project_K(K, p, res, u, v);
+}
+
+// PointOnlyReprojectionError::operator()  (Optimizer.h:96-107)
+template <typename T>
+void point_only_reprojection(const T* pt, const float* extr, const float* K, float u, float v, T* res) {
+  T ph[4];
+  for (int i = 0; i < 4; ++i)
+    ph[i] = pt[0] * double(extr[0 * 4 + i]) + pt[1] * double(extr[1 * 4 + i]) + pt[2] * double(extr[2 * 4 + i]) + double(extr[3 * 4 + i]);
+  T p[3] = {ph[0] / ph[3], ph[1] / ph[3], ph[2] / ph[3]};
+  project_K(K, p, res, u, v);
+}
+
+// PoseOnlyAngleReprojectionError::operator()  (Optimizer.h:163-182);  the point
+// is a constant Vector4f (x,y,z,1).
+template <typename T>
+void pose_only_angle_reprojection(const T* cam, const double* X, const float* K, float u, float v, T* res) {
+  T R[9];
+  AngleAxisToRotationMatrix(cam, R);
+  T p[3];
+  for (int i = 0; i < 3; ++i) p[i] = R[0 * 3 + i] * X[0] + R[1 * 3 + i] * X[1] + R[2 * 3 + i] * X[2] + cam[3 + i];
+  project_K(K, p, res, u, v);
+}
+
+// ----------------------------------------------------------------------------
+// ceres::HuberLoss::Evaluate + Corrector (rho'' <= 0 branch: sqrt(rho') scaling)
+// ----------------------------------------------------------------------------
+struct Huber {
+  double a, b;
+  bool on;
+  explicit Huber(double a_) : a(a_), b(a_ * a_), on(a_ > 0) {}
+  // returns rho0, sets scale = sqrt(rho1)
+  double eval(double s, double* scale) const {
+    if (!on) { *scale = 1.0; return s; }
+    if (s > b) {
+      const double r = std::sqrt(s);
+      const double rho1 = std::max(std::numeric_limits<double>::min(), a / r);
+      *scale = std::sqrt(rho1);
+      return 2.0 * a * r - b;
+    }
+    *scale = 1.0;
+    return s;
+  }
+};
+
+// ----------------------------------------------------------------------------
+// Problem (same data meaning as the product ABI, restated independently).
+// ----------------------------------------------------------------------------
+enum RBType { RB_ANGLE = 0, RB_POINT_ONLY = 1, RB_POSE_ONLY = 2, RB_CONST = 3 };
+
+struct Problem {
+  int nc, np, no;
+  double* cams;           // 6*nc, in/out
+  const uint8_t* cam_fixed;
+  const float* cam_extr;  // 16*nc col-major (fixed cameras)
+  const float* K;         // 9*nc col-major
+  double* pts;            // 3*np in/out
+  const uint8_t* pt_fixed;
+  const int32_t* obs_cam;
+  const int32_t* obs_pt;
+  const float* obs_uv;
+  double huber_a;
+  // derived
+  std::vector<int> type;      // per obs
+  std::vector<int> cam_col;   // per cam: column offset of its 6-block or -1
+  std::vector<int> pt_col;    // per point: column offset or -1
+  int ncols = 0;
+  std::vector<int> var_cams, var_pts;   // active (in problem) blocks
+};
+
+static void build_structure(Problem& P) {
+  P.type.resize(P.no);
+  std::vector<char> cam_used(P.nc, 0), pt_used(P.np, 0);
+  for (int o = 0; o < P.no; ++o) {
+    const int c = P.obs_cam[o], p = P.obs_pt[o];
+    const bool cf = P.cam_fixed && P.cam_fixed[c];
+    const bool pf = P.pt_fixed && P.pt_fixed[p];
+    int t = cf ? (pf ? RB_CONST : RB_POINT_ONLY) : (pf ? RB_POSE_ONLY : RB_ANGLE);
+    P.type[o] = t;
+    if (!cf) cam_used[c] = 1;
+    if (!pf) pt_used[p] = 1;
+  }
+  P.cam_col.assign(P.nc, -1);
+  P.pt_col.assign(P.np, -1);
+  int col = 0;
+  for (int c = 0; c < P.nc; ++c) if (cam_used[c]) { P.cam_col[c] = col; col += 6; P.var_cams.push_back(c); }
+  for (int p = 0; p < P.np; ++p) if (pt_used[p]) { P.pt_col[p] = col; col += 3; P.var_pts.push_back(p); }
+  P.ncols = col;
+}
+
+// x <-> problem parameters
+static void gather_x(const Problem& P, std::vector<double>& x) {
+  x.resize(P.ncols);
+  for (int c : P.var_cams) for (int k = 0; k < 6; ++k) x[P.cam_col[c] + k] = P.cams[6 * c + k];
+  for (int p : P.var_pts) for (int k = 0; k < 3; ++k) x[P.pt_col[p] + k] = P.pts[3 * p + k];
+}
+static void scatter_x(Problem& P, const std::vector<double>& x) {
+  for (int c : P.var_cams) for (int k = 0; k < 6; ++k) P.cams[6 * c + k] = x[P.cam_col[c] + k];
+  for (int p : P.var_pts) for (int k = 0; k < 3; ++k) P.pts[3 * p + k] = x[P.pt_col[p] + k];
+}
+
+// Per-obs linearisation: corrected residual r (2), corrected jacobian blocks
+// Jc (2x6 row-major) and Jp (2x3 row-major); returns block cost 0.5*rho.
+struct Lin { double r[2]; double Jc[12]; double Jp[6]; };
+
+static inline const double* param_cam(const Problem& P, const std::vector<double>& x, int c) {
+  return P.cam_col[c] >= 0 ? &x[P.cam_col[c]] : &P.cams[6 * c];
+}
+static inline const double* param_pt(const Problem& P, const std::vector<double>& x, int p) {
+  return P.pt_col[p] >= 0 ? &x[P.pt_col[p]] : &P.pts[3 * p];
+}
+
+static double eval_obs(const Problem& P, const std::vector<double>& x, int o, Lin* L, bool* finite) {
+  const int c = P.obs_cam[o], p = P.obs_pt[o];
+  const float u = P.obs_uv[2 * o], v = P.obs_uv[2 * o + 1];
+  const float* K = P.K + 9 * c;
+  const double* cam = param_cam(P, x, c);
+  const double* pt = param_pt(P, x, p);
+  double r[2];
+  double Jc[12] = {0}, Jp[6] = {0};
+  // Cost-only evaluation: ceres calls the functor with T = double (no Jets),
+  // so the divisions are true divisions rather than Jet reciprocal-multiply.
+  const int kind = L ? P.type[o] : RB_CONST;
+  switch (kind) {
+    case RB_ANGLE: {
+      Jet<9> jc[6], jp[3], res[2];
+      for (int k = 0; k < 6; ++k) jc[k] = Jet<9>(cam[k], k);
+      for (int k = 0; k < 3; ++k) jp[k] = Jet<9>(pt[k], 6 + k);
+      angle_reprojection(jc, jp, K, u, v, res);
+      for (int i = 0; i < 2; ++i) {
+        r[i] = res[i].a;
+        for (int k = 0; k < 6; ++k) Jc[i * 6 + k] = res[i].v[k];
+        for (int k = 0; k < 3; ++k) Jp[i * 3 + k] = res[i].v[6 + k];
+      }
+      break;
+    }
+    case RB_POINT_ONLY: {
+      Jet<3> jp[3], res[2];
+      for (int k = 0; k < 3; ++k) jp[k] = Jet<3>(pt[k], k);
+      point_only_reprojection(jp, P.cam_extr + 16 * c, K, u, v, res);
+      for (int i = 0; i < 2; ++i) { r[i] = res[i].a; for (int k = 0; k < 3; ++k) Jp[i * 3 + k] = res[i].v[k]; }
+      break;
+    }
+    case RB_POSE_ONLY: {
+      Jet<6> jc[6], res[2];
+      for (int k = 0; k < 6; ++k) jc[k] = Jet<6>(cam[k], k);
+      pose_only_angle_reprojection(jc, pt, K, u, v, res);
+      for (int i = 0; i < 2; ++i) { r[i] = res[i].a; for (int k = 0; k < 6; ++k) Jc[i * 6 + k] = res[i].v[k]; }
+      break;
+    }
+    default: {  // constant block: value only
+      if (P.cam_fixed && P.cam_fixed[c]) {
+        double pr[3] = {pt[0], pt[1], pt[2]};
+        point_only_reprojection(pr, P.cam_extr + 16 * c, K, u, v, r);
+      } else {
+        angle_reprojection(cam, pt, K, u, v, r);
+      }
+    }
+  }
+  const double sq = r[0] * r[0] + r[1] * r[1];
+  *finite = std::isfinite(r[0]) && std::isfinite(r[1]);
+  Huber h(P.huber_a);
+  double scale;
+  const double rho = h.eval(sq, &scale);
+  if (L) {
+    L->r[0] = r[0] * scale; L->r[1] = r[1] * scale;
+    for (int k = 0; k < 12; ++k) L->Jc[k] = Jc[k] * scale;
+    for (int k = 0; k < 6; ++k) L->Jp[k] = Jp[k] * scale;
+    if (P.type[o] == RB_POINT_ONLY || P.type[o] == RB_CONST) for (int k = 0; k < 12; ++k) L->Jc[k] = 0;
+    if (P.type[o] == RB_POSE_ONLY || P.type[o] == RB_CONST) for (int k = 0; k < 6; ++k) L->Jp[k] = 0;
+  }
+  return 0.5 * rho;
+}
+
+// cost only (ceres Evaluator with residuals = jacobians = nullptr)
+static bool eval_cost(const Problem& P, const std::vector<double>& x, double* cost) {
+  double total = 0.0;
+  bool ok = true;
+#pragma omp parallel for reduction(+ : total) reduction(&& : ok) schedule(static)
+  for (int o = 0; o < P.no; ++o) {
+    bool f;
+    total += eval_obs(P, x, o, nullptr, &f);
+    ok = ok && f;
+  }
+  *cost = total;
+  return ok && std::isfinite(total);
+}
+
+static bool eval_lin(const Problem& P, const std::vector<double>& x, std::vector<Lin>& L, double* cost) {
+  L.resize(P.no);
+  double total = 0.0;
+  bool ok = true;
+#pragma omp parallel for reduction(+ : total) reduction(&& : ok) schedule(static)
+  for (int o = 0; o < P.no; ++o) {
+    bool f;
+    total += eval_obs(P, x, o, &L[o], &f);
+    bool jf = true;
+    for (int k = 0; k < 12; ++k) jf = jf && std::isfinite(L[o].Jc[k]);
+    for (int k = 0; k < 6; ++k) jf = jf && std::isfinite(L[o].Jp[k]);
+    ok = ok && f && jf;
+  }
+  *cost = total;
+  return ok && std::isfinite(total);
+}
+
+// gradient g = J^T r  and squared column norms of J (both unscaled)
+static void gradient_colnorm(const Problem& P, const std::vector<Lin>& L, std::vector<double>& g,
+                             std::vector<double>& cn) {
+  g.assign(P.ncols, 0.0);
+  cn.assign(P.ncols, 0.0);
+  for (int o = 0; o < P.no; ++o) {
+    const int c = P.obs_cam[o], p = P.obs_pt[o];
+    const Lin& l = L[o];
+    const int cc = (P.type[o] == RB_ANGLE || P.type[o] == RB_POSE_ONLY) ? P.cam_col[c] : -1;
+    const int pc = (P.type[o] == RB_ANGLE || P.type[o] == RB_POINT_ONLY) ? P.pt_col[p] : -1;
+    if (cc >= 0)
+      for (int k = 0; k < 6; ++k) {
+        g[cc + k] += l.Jc[k] * l.r[0] + l.Jc[6 + k] * l.r[1];
+        cn[cc + k] += l.Jc[k] * l.Jc[k] + l.Jc[6 + k] * l.Jc[6 + k];
+      }
+    if (pc >= 0)
+      for (int k = 0; k < 3; ++k) {
+        g[pc + k] += l.Jp[k] * l.r[0] + l.Jp[3 + k] * l.r[1];
+        cn[pc + k] += l.Jp[k] * l.Jp[k] + l.Jp[3 + k] * l.Jp[3 + k];
+      }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Dense Cholesky (lower, row-major, in place).  Returns false on a
+// non-positive / non-finite pivot (Eigen LLT info() != Success).
+// ----------------------------------------------------------------------------
+static bool cholesky(std::vector<double>& A, int n) {
+  const int nb = 64;
+  for (int k = 0; k < n; k += nb) {
+    const int b = std::min(nb, n - k);
+    // factor diagonal block
+    for (int j = k; j < k + b; ++j) {
+      double d = A[(size_t)j * n + j];
+      for (int t = k; t < j; ++t) d -= A[(size_t)j * n + t] * A[(size_t)j * n + t];
+      if (!(d > 0.0) || !std::isfinite(d)) return false;
+      d = std::sqrt(d);
+      A[(size_t)j * n + j] = d;
+      for (int i = j + 1; i < k + b; ++i) {
+        double s = A[(size_t)i * n + j];
+        for (int t = k; t < j; ++t) s -= A[(size_t)i * n + t] * A[(size_t)j * n + t];
+        A[(size_t)i * n + j] = s / d;
+      }
+    }
+    // panel below
+#pragma omp parallel for schedule(static)
+    for (int i = k + b; i < n; ++i) {
+      for (int j = k; j < k + b; ++j) {
+        double s = A[(size_t)i * n + j];
+        for (int t = k; t < j; ++t) s -= A[(size_t)i * n + t] * A[(size_t)j * n + t];
+        A[(size_t)i * n + j] = s / A[(size_t)j * n + j];
+      }
+    }
+    // trailing update (lower)
+#pragma omp parallel for schedule(dynamic, 8)
+    for (int i = k + b; i < n; ++i) {
+      const double* ai = &A[(size_t)i * n + k];
+      for (int j = k + b; j <= i; ++j) {
+        const double* aj = &A[(size_t)j * n + k];
+        double s = 0.0;
+        for (int t = 0; t < b; ++t) s += ai[t] * aj[t];
+        A[(size_t)i * n + j] -= s;
+      }
+    }
+  }
+  return true;
+}
+static void chol_solve(const std::vector<double>& L, int n, std::vector<double>& b) {
+  for (int i = 0; i < n; ++i) {
+    double s = b[i];
+    for (int t = 0; t < i; ++t) s -= L[(size_t)i * n + t] * b[t];
+    b[i] = s / L[(size_t)i * n + i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double s = b[i];
+    for (int t = i + 1; t < n; ++t) s -= L[(size_t)t * n + i] * b[t];
+    b[i] = s / L[(size_t)i * n + i];
+  }
+}
+
+// 3x3 SPD inverse through LLT (Eigen selfadjointView.llt().solve(I))
+static bool inv3_spd(const double A[9], double Ai[9]) {
+  double l00 = A[0];
+  if (!(l00 > 0)) return false;
+  l00 = std::sqrt(l00);
+  const double l10 = A[3] / l00, l20 = A[6] / l00;
+  double l11 = A[4] - l10 * l10;
+  if (!(l11 > 0)) return false;
+  l11 = std::sqrt(l11);
+  const double l21 = (A[7] - l20 * l10) / l11;
+  double l22 = A[8] - l20 * l20 - l21 * l21;
+  if (!(l22 > 0)) return false;
+  l22 = std::sqrt(l22);
+  for (int col = 0; col < 3; ++col) {
+    double e[3] = {0, 0, 0};
+    e[col] = 1.0;
+    double z0 = e[0] / l00, z1 = (e[1] - l10 * z0) / l11, z2 = (e[2] - l20 * z0 - l21 * z1) / l22;
+    double y2 = z2 / l22, y1 = (z1 - l21 * y2) / l11, y0 = (z0 - l10 * y1 - l20 * y2) / l00;
+    Ai[0 * 3 + col] = y0; Ai[1 * 3 + col] = y1; Ai[2 * 3 + col] = y2;
+  }
+  return true;
+}
+
+// ----------------------------------------------------------------------------
+// DENSE_SCHUR restated: solve (Js^T Js + diag(D)^2) y = Js^T r  where Js is
+// the column-scaled jacobian (Js = J diag(s)).  Points are the eliminated
+// e-blocks, cameras the f-blocks.  Returns false on solver failure.
+// ----------------------------------------------------------------------------
+struct Schur {
+  // per variable point: list of obs
+  std::vector<std::vector<int>> pt_obs;
+  std::vector<int> fidx;   // per cam: f-block index or -1
+  int nf = 0;
+};
+
+static bool dense_schur_solve(const Problem& P, const Schur& S, const std::vector<Lin>& L,
+                              const std::vector<double>& s, const std::vector<double>& D,
+                              std::vector<double>& y) {
+  const int nf = S.nf, n = 6 * nf;
+  y.assign(P.ncols, 0.0);
+  std::vector<double> lhs((size_t)n * n, 0.0), rhs(n, 0.0);
+  auto scJc = [&](int o, double* Jc) {  // scaled camera jacobian 2x6
+    const int cc = P.cam_col[P.obs_cam[o]];
+    for (int i = 0; i < 2; ++i) for (int k = 0; k < 6; ++k) Jc[i * 6 + k] = L[o].Jc[i * 6 + k] * s[cc + k];
+  };
+  auto scJp = [&](int o, double* Jp) {
+    const int pc = P.pt_col[P.obs_pt[o]];
+    for (int i = 0; i < 2; ++i) for (int k = 0; k < 3; ++k) Jp[i * 3 + k] = L[o].Jp[i * 3 + k] * s[pc + k];
+  };
+  const bool has_cam = nf > 0;
+  // F^T F + D_f^2 and F^T r over all residuals that touch a variable camera
+  for (int o = 0; o < P.no; ++o) {
+    const int t = P.type[o];
+    if (t != RB_ANGLE && t != RB_POSE_ONLY) continue;
+    const int f = S.fidx[P.obs_cam[o]];
+    double Jc[12];
+    scJc(o, Jc);
+    for (int a = 0; a < 6; ++a) {
+      rhs[6 * f + a] += Jc[a] * L[o].r[0] + Jc[6 + a] * L[o].r[1];
+      for (int b = 0; b <= a; ++b)
+        lhs[(size_t)(6 * f + a) * n + 6 * f + b] += Jc[a] * Jc[b] + Jc[6 + a] * Jc[6 + b];
+    }
+  }
+  for (int c : P.var_cams) {
+    const int f = S.fidx[c], cc = P.cam_col[c];
+    for (int a = 0; a < 6; ++a) lhs[(size_t)(6 * f + a) * n + 6 * f + a] += D[cc + a] * D[cc + a];
+  }
+  // eliminate points
+  const int npv = (int)P.var_pts.size();
+  std::vector<double> ete_inv((size_t)npv * 9), ge((size_t)npv * 3);
+  bool ok = true;
+  int nthreads = 1;
+#ifdef _OPENMP
+  nthreads = omp_get_max_threads();
+#endif
+  // per-thread lhs accumulation, reduced in thread order
+  const size_t lhs_bytes = (size_t)n * n * sizeof(double);
+  int nacc = std::max(1, std::min(nthreads, (int)(2e9 / std::max<size_t>(lhs_bytes, 1))));
+  std::vector<std::vector<double>> acc_l(nacc, std::vector<double>()), acc_r(nacc, std::vector<double>(n, 0.0));
+  for (auto& a : acc_l) a.assign((size_t)n * n, 0.0);
+#pragma omp parallel num_threads(nacc) reduction(&& : ok)
+  {
+    int tid = 0;
+#ifdef _OPENMP
+    tid = omp_get_thread_num();
+#endif
+    std::vector<double>& al = acc_l[tid];
+    std::vector<double>& ar = acc_r[tid];
+    std::vector<int> fl;
+    std::vector<double> FtE;  // per distinct f-block in chunk: 6x3
+#pragma omp for schedule(dynamic, 64)
+    for (int ip = 0; ip < npv; ++ip) {
+      const int p = P.var_pts[ip], pc = P.pt_col[p];
+      double ete[9] = {0}, g[3] = {0};
+      fl.clear();
+      FtE.clear();
+      for (int o : S.pt_obs[ip]) {
+        double Jp[6];
+        scJp(o, Jp);
+        for (int a = 0; a < 3; ++a) {
+          g[a] += Jp[a] * L[o].r[0] + Jp[3 + a] * L[o].r[1];
+          for (int b = 0; b < 3; ++b) ete[a * 3 + b] += Jp[a] * Jp[b] + Jp[3 + a] * Jp[3 + b];
+        }
+        if (P.type[o] == RB_ANGLE) {
+          const int f = S.fidx[P.obs_cam[o]];
+          int slot = -1;
+          for (size_t q = 0; q < fl.size(); ++q) if (fl[q] == f) slot = (int)q;
+          if (slot < 0) { slot = (int)fl.size(); fl.push_back(f); FtE.resize(FtE.size() + 18, 0.0); }
+          double Jc[12];
+          scJc(o, Jc);
+          double* B = &FtE[(size_t)slot * 18];
+          for (int a = 0; a < 6; ++a) for (int b = 0; b < 3; ++b) B[a * 3 + b] += Jc[a] * Jp[b] + Jc[6 + a] * Jp[3 + b];
+        }
+      }
+      for (int a = 0; a < 3; ++a) ete[a * 3 + a] += D[pc + a] * D[pc + a];
+      double* inv = &ete_inv[(size_t)ip * 9];
+      if (!inv3_spd(ete, inv)) { ok = false; continue; }
+      for (int a = 0; a < 3; ++a) ge[(size_t)ip * 3 + a] = g[a];
+      const int m = (int)fl.size();
+      // tmp_q = FtE_q * inv  (6x3)
+      std::vector<double> T((size_t)m * 18);
+      for (int q = 0; q < m; ++q)
+        for (int a = 0; a < 6; ++a)
+          for (int b = 0; b < 3; ++b) {
+            double v = 0;
+            for (int t = 0; t < 3; ++t) v += FtE[(size_t)q * 18 + a * 3 + t] * inv[t * 3 + b];
+            T[(size_t)q * 18 + a * 3 + b] = v;
+          }
+      for (int q = 0; q < m; ++q) {
+        const int fq = fl[q];
+        for (int a = 0; a < 6; ++a) {
+          double v = 0;
+          for (int t = 0; t < 3; ++t) v += T[(size_t)q * 18 + a * 3 + t] * g[t];
+          ar[6 * fq + a] -= v;
+        }
+        for (int w = 0; w < m; ++w) {
+          const int fw = fl[w];
+          if (fw > fq) continue;  // lower triangle only: block (fq, fw) with fw <= fq
+          for (int a = 0; a < 6; ++a)
+            for (int b = 0; b < 6; ++b) {
+              if (fw == fq && b > a) continue;
+              double v = 0;
+              for (int t = 0; t < 3; ++t) v += T[(size_t)q * 18 + a * 3 + t] * FtE[(size_t)w * 18 + b * 3 + t];
+              al[(size_t)(6 * fq + a) * n + 6 * fw + b] -= v;
+            }
+        }
+      }
+    }
+  }
+  if (!ok) return false;
+  for (int t = 0; t < nacc; ++t) {
+    for (size_t i = 0; i < lhs.size(); ++i) lhs[i] += acc_l[t][i];
+    for (int i = 0; i < n; ++i) rhs[i] += acc_r[t][i];
+  }
+  std::vector<double> yf(rhs);
+  if (has_cam) {
+    if (!cholesky(lhs, n)) return false;
+    chol_solve(lhs, n, yf);
+  }
+  for (int c : P.var_cams) for (int a = 0; a < 6; ++a) y[P.cam_col[c] + a] = yf[6 * S.fidx[c] + a];
+  // back substitution  y_e = inv (g_e - sum_f (F^T E)^T y_f)
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int ip = 0; ip < npv; ++ip) {
+    const int p = P.var_pts[ip], pc = P.pt_col[p];
+    double w[3] = {ge[(size_t)ip * 3], ge[(size_t)ip * 3 + 1], ge[(size_t)ip * 3 + 2]};
+    for (int o : S.pt_obs[ip]) {
+      if (P.type[o] != RB_ANGLE) continue;
+      double Jp[6], Jc[12];
+      scJp(o, Jp);
+      scJc(o, Jc);
+      const int f = S.fidx[P.obs_cam[o]];
+      double z[2] = {0, 0};
+      for (int k = 0; k < 6; ++k) { z[0] += Jc[k] * yf[6 * f + k]; z[1] += Jc[6 + k] * yf[6 * f + k]; }
+      for (int a = 0; a < 3; ++a) w[a] -= Jp[a] * z[0] + Jp[3 + a] * z[1];
+    }
+    const double* inv = &ete_inv[(size_t)ip * 9];
+    for (int a = 0; a < 3; ++a) y[pc + a] = inv[a * 3] * w[0] + inv[a * 3 + 1] * w[1] + inv[a * 3 + 2] * w[2];
+  }
+  for (double v : y) if (!std::isfinite(v)) return false;
+  return true;
+}
+
+// ----------------------------------------------------------------------------
+// Ceres TrustRegionMinimizer + LevenbergMarquardtStrategy restated.
+// ----------------------------------------------------------------------------
+struct Options {
+  int max_num_iterations;
+  int max_num_consecutive_invalid_steps;
+  int jacobi_scaling;
+  int pad;
+  double function_tolerance, gradient_tolerance, parameter_tolerance;
+  double initial_trust_region_radius, max_trust_region_radius, min_trust_region_radius;
+  double min_relative_decrease, min_lm_diagonal, max_lm_diagonal;
+};
+
+enum { LOG_ITER = 0, LOG_COST, LOG_COST_CHANGE, LOG_GMAX, LOG_GNORM, LOG_STEP_NORM, LOG_REL_DEC,
+       LOG_RADIUS, LOG_VALID, LOG_SUCCESS, LOG_MCC, LOG_WIDTH = 12 };
+enum { TERM_CONVERGENCE = 0, TERM_NO_CONVERGENCE = 1, TERM_FAILURE = 2 };
+
+struct Summary {
+  double initial_cost, final_cost;
+  int num_iterations, num_successful, num_unsuccessful, termination;
+};
+
+static double norm2(const std::vector<double>& v) { double s = 0; for (double a : v) s += a * a; return std::sqrt(s); }
+
+static void prepare_schur(const Problem& P, Schur& S) {
+  S.fidx.assign(P.nc, -1);
+  S.nf = 0;
+  for (int c : P.var_cams) S.fidx[c] = S.nf++;
+  std::vector<int> vp(P.np, -1);
+  for (size_t i = 0; i < P.var_pts.size(); ++i) vp[P.var_pts[i]] = (int)i;
+  S.pt_obs.assign(P.var_pts.size(), {});
+  for (int o = 0; o < P.no; ++o)
+    if (P.type[o] == RB_ANGLE || P.type[o] == RB_POINT_ONLY) S.pt_obs[vp[P.obs_pt[o]]].push_back(o);
+}
+
+// model_cost_change = -(Js step)^T (r + Js step / 2), step = -y (scaled space)
+static double model_cost_change(const Problem& P, const std::vector<Lin>& L, const std::vector<double>& scale,
+                                const std::vector<double>& y) {
+  double m = 0.0;
+#pragma omp parallel for reduction(+ : m) schedule(static)
+  for (int o = 0; o < P.no; ++o) {
+    const int t = P.type[o];
+    double js[2] = {0, 0};
+    if (t == RB_ANGLE || t == RB_POSE_ONLY) {
+      const int cc = P.cam_col[P.obs_cam[o]];
+      for (int k = 0; k < 6; ++k) {
+        const double st = -y[cc + k];
+        js[0] += (L[o].Jc[k] * scale[cc + k]) * st;
+        js[1] += (L[o].Jc[6 + k] * scale[cc + k]) * st;
+      }
+    }
+    if (t == RB_ANGLE || t == RB_POINT_ONLY) {
+      const int pc = P.pt_col[P.obs_pt[o]];
+      for (int k = 0; k < 3; ++k) {
+        const double st = -y[pc + k];
+        js[0] += (L[o].Jp[k] * scale[pc + k]) * st;
+        js[1] += (L[o].Jp[3 + k] * scale[pc + k]) * st;
+      }
+    }
+    m += js[0] * (L[o].r[0] + js[0] / 2.0) + js[1] * (L[o].r[1] + js[1] / 2.0);
+  }
+  return -m;
+}
+
+// CPU baseline timing: the same per-iteration work as the GPU bench step
+// (linearise + gradient/column norms + LM diagonal + DENSE_SCHUR solve +
+// model cost change + candidate cost) at a fixed trust-region radius.
+static double bench_iteration_seconds(Problem& P, int iters, double radius) {
+  build_structure(P);
+  Schur S;
+  prepare_schur(P, S);
+  const int n = P.ncols;
+  std::vector<double> x, g, cn, scale(n, 1.0), D(n), y, cand(n);
+  std::vector<Lin> L;
+  gather_x(P, x);
+  double cost;
+  eval_lin(P, x, L, &cost);
+  gradient_colnorm(P, L, g, cn);
+  for (int i = 0; i < n; ++i) scale[i] = 1.0 / (1.0 + std::sqrt(cn[i]));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int it = 0; it < iters; ++it) {
+    eval_lin(P, x, L, &cost);
+    gradient_colnorm(P, L, g, cn);
+    for (int i = 0; i < n; ++i) {
+      const double d = std::min(std::max(cn[i] * scale[i] * scale[i], 1e-6), 1e32);
+      D[i] = std::sqrt(d / radius);
+    }
+    dense_schur_solve(P, S, L, scale, D, y);
+    volatile double mcc = model_cost_change(P, L, scale, y);
+    (void)mcc;
+    for (int i = 0; i < n; ++i) cand[i] = x[i] + (-y[i]) * scale[i];
+    double cc;
+    eval_cost(P, cand, &cc);
+  }
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / iters;
+}
+
+static int minimize(Problem& P, const Options& opt, double* log, int max_log, Summary* sum) {
+  build_structure(P);
+  Schur S;
+  prepare_schur(P, S);
+  const int n = P.ncols;
+  std::vector<double> x, cand, g, cn, scale(n, 1.0), diag(n, 0.0), D(n), y, delta(n);
+  std::vector<Lin> L;
+  gather_x(P, x);
+  int nlog = 0;
+  auto push_log = [&](const double* rec) {
+    if (log && nlog < max_log) std::memcpy(log + (size_t)nlog * LOG_WIDTH, rec, sizeof(double) * LOG_WIDTH);
+    ++nlog;
+  };
+  sum->num_successful = sum->num_unsuccessful = 0;
+  double x_cost;
+  if (n == 0) {  // nothing to optimise (ceres: no non-constant parameter blocks)
+    eval_cost(P, x, &x_cost);
+    sum->initial_cost = sum->final_cost = x_cost;
+    sum->termination = TERM_CONVERGENCE;
+    sum->num_iterations = 0;
+    return 0;
+  }
+  double x_norm = norm2(x);
+  double radius = opt.initial_trust_region_radius, decrease_factor = 2.0;
+  bool reuse_diagonal = false;
+  int consecutive_invalid = 0;
+
+  // ---- EvaluateGradientAndJacobian
+  auto evaluate_gj = [&](int iteration, double* gmax, double* gnorm) -> bool {
+    if (!eval_lin(P, x, L, &x_cost)) return false;
+    gradient_colnorm(P, L, g, cn);
+    double gm = 0, gn = 0;
+    for (int i = 0; i < n; ++i) {
+      const double pg = x[i] + (-g[i]);  // Plus(x, -gradient)
+      const double d = x[i] - pg;
+      gm = std::max(gm, std::fabs(d));
+      gn += d * d;
+    }
+    *gmax = gm; *gnorm = std::sqrt(gn);
+    if (opt.jacobi_scaling) {
+      if (iteration == 0)
+        for (int i = 0; i < n; ++i) scale[i] = 1.0 / (1.0 + std::sqrt(cn[i]));
+    }
+    return true;
+  };
+
+  double rec[LOG_WIDTH];
+  std::memset(rec, 0, sizeof rec);
+  double gmax = 0, gnorm = 0;
+  if (!evaluate_gj(0, &gmax, &gnorm)) {
+    sum->termination = TERM_FAILURE;
+    sum->initial_cost = sum->final_cost = x_cost;
+    sum->num_iterations = 0;
+    return 0;
+  }
+  sum->initial_cost = x_cost;
+  double min_cost = x_cost;
+  rec[LOG_ITER] = 0; rec[LOG_COST] = x_cost; rec[LOG_GMAX] = gmax; rec[LOG_GNORM] = gnorm;
+  rec[LOG_RADIUS] = radius; rec[LOG_VALID] = 1; rec[LOG_SUCCESS] = 1;
+  push_log(rec);
+  int iteration = 0;
+  int termination = TERM_NO_CONVERGENCE;
+  bool last_success = true;
+  // FinalizeIterationAndCheckIfMinimizerCanContinue for iteration 0
+  auto can_continue = [&](double cur_gmax) -> bool {
+    if (iteration >= opt.max_num_iterations) { termination = TERM_NO_CONVERGENCE; return false; }
+    if (last_success && cur_gmax <= opt.gradient_tolerance) { termination = TERM_CONVERGENCE; return false; }
+    if (radius <= opt.min_trust_region_radius) { termination = TERM_CONVERGENCE; return false; }
+    return true;
+  };
+  double cur_gmax = gmax, cur_gnorm = gnorm;
+  while (can_continue(cur_gmax)) {
+    ++iteration;
+    std::memset(rec, 0, sizeof rec);
+    rec[LOG_ITER] = iteration;
+    // ---- LevenbergMarquardtStrategy::ComputeStep
+    if (!reuse_diagonal) {
+      for (int i = 0; i < n; ++i) {
+        const double sc = scale[i];
+        diag[i] = std::min(std::max(cn[i] * sc * sc, opt.min_lm_diagonal), opt.max_lm_diagonal);
+      }
+    }
+    for (int i = 0; i < n; ++i) D[i] = std::sqrt(diag[i] / radius);
+    bool solved = dense_schur_solve(P, S, L, scale, D, y);
+    reuse_diagonal = true;
+    bool valid = false;
+    double mcc = 0.0;
+    if (solved) {
+      mcc = model_cost_change(P, L, scale, y);
+      valid = mcc > 0.0;
+      if (valid) for (int i = 0; i < n; ++i) delta[i] = (-y[i]) * scale[i];
+    }
+    rec[LOG_MCC] = mcc;
+    if (!valid) {
+      // HandleInvalidStep
+      if (++consecutive_invalid >= opt.max_num_consecutive_invalid_steps) { termination = TERM_FAILURE; break; }
+      radius = radius / decrease_factor; decrease_factor *= 2.0; reuse_diagonal = true;  // StepRejected(0)
+      rec[LOG_COST] = x_cost; rec[LOG_GMAX] = cur_gmax; rec[LOG_GNORM] = cur_gnorm;
+      rec[LOG_RADIUS] = radius; rec[LOG_VALID] = 0; rec[LOG_SUCCESS] = 0;
+      last_success = false;
+      sum->num_unsuccessful++;
+      push_log(rec);
+      continue;
+    }
+    consecutive_invalid = 0;
+    // ComputeCandidatePointAndEvaluateCost
+    cand.resize(n);
+    for (int i = 0; i < n; ++i) cand[i] = x[i] + delta[i];
+    double cand_cost;
+    if (!eval_cost(P, cand, &cand_cost)) cand_cost = std::numeric_limits<double>::max();
+    // ParameterToleranceReached
+    double sn = 0;
+    for (int i = 0; i < n; ++i) { const double d = x[i] - cand[i]; sn += d * d; }
+    const double step_norm = std::sqrt(sn);
+    rec[LOG_STEP_NORM] = step_norm;
+    if (step_norm <= opt.parameter_tolerance * (x_norm + opt.parameter_tolerance)) {
+      termination = TERM_CONVERGENCE; break;
+    }
+    // FunctionToleranceReached
+    const double cost_change = x_cost - cand_cost;
+    rec[LOG_COST_CHANGE] = cost_change;
+    if (std::fabs(cost_change) <= opt.function_tolerance * x_cost) { termination = TERM_CONVERGENCE; break; }
+    // IsStepSuccessful (monotonic TrustRegionStepEvaluator::StepQuality)
+    const double rel = cand_cost >= std::numeric_limits<double>::max()
+                           ? std::numeric_limits<double>::lowest()
+                           : (x_cost - cand_cost) / mcc;
+    rec[LOG_REL_DEC] = rel;
+    if (rel > opt.min_relative_decrease) {
+      // HandleSuccessfulStep
+      x = cand;
+      x_norm = norm2(x);
+      if (!evaluate_gj(iteration, &cur_gmax, &cur_gnorm)) { termination = TERM_FAILURE; break; }
+      radius = std::min(opt.max_trust_region_radius,
+                        radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3)));
+      decrease_factor = 2.0;
+      reuse_diagonal = false;
+      last_success = true;
+      if (x_cost < min_cost) min_cost = x_cost;
+      sum->num_successful++;
+      rec[LOG_COST] = x_cost; rec[LOG_SUCCESS] = 1;
+    } else {
+      radius = radius / decrease_factor; decrease_factor *= 2.0; reuse_diagonal = true;
+      last_success = false;
+      sum->num_unsuccessful++;
+      rec[LOG_COST] = cand_cost; rec[LOG_SUCCESS] = 0;
+    }
+    rec[LOG_GMAX] = cur_gmax; rec[LOG_GNORM] = cur_gnorm; rec[LOG_RADIUS] = radius; rec[LOG_VALID] = 1;
+    push_log(rec);
+  }
+  scatter_x(P, x);
+  sum->final_cost = x_cost;
+  sum->termination = termination;
+  sum->num_iterations = iteration;
+  return nlog;
+}
+
+}  // namespace oracle
+
+// ============================================================================
+// C entry points for ctypes (tests / bench cpu_baseline only).
+// ============================================================================
+extern "C" {
+
+typedef struct {
+  int32_t n_cams, n_pts, n_obs, pad;
+  double* cams;
+  const uint8_t* cam_fixed;
+  const float* cam_fixed_extr;
+  const float* K;
+  double* pts;
+  const uint8_t* pt_fixed;
+  const int32_t* obs_cam;
+  const int32_t* obs_pt;
+  const float* obs_uv;
+  double huber_a;
+} oracle_problem;
+
+static oracle::Problem to_problem(const oracle_problem* p) {
+  oracle::Problem P;
+  P.nc = p->n_cams; P.np = p->n_pts; P.no = p->n_obs;
+  P.cams = p->cams; P.cam_fixed = p->cam_fixed; P.cam_extr = p->cam_fixed_extr; P.K = p->K;
+  P.pts = p->pts; P.pt_fixed = p->pt_fixed; P.obs_cam = p->obs_cam; P.obs_pt = p->obs_pt;
+  P.obs_uv = p->obs_uv; P.huber_a = p->huber_a;
+  return P;
+}
+
+void oracle_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
+}
+
+// Levenberg-Marquardt + DENSE_SCHUR solve in place.  iter_log: [max_log][12].
+// summary: [initial_cost, final_cost, num_iterations, num_successful,
+//           num_unsuccessful, termination].  Returns number of log records.
+int oracle_solve(const oracle_problem* prob, const oracle::Options* opt, double* iter_log, int max_log,
+                 double* summary) {
+  oracle::Problem P = to_problem(prob);
+  oracle::Summary s{};
+  int nlog = oracle::minimize(P, *opt, iter_log, max_log, &s);
+  summary[0] = s.initial_cost; summary[1] = s.final_cost; summary[2] = s.num_iterations;
+  summary[3] = s.num_successful; summary[4] = s.num_unsuccessful; summary[5] = s.termination;
+  return nlog;
+}
+
+// Corrected residuals r[2N], jacobian J[N][2][9] (cam 6 | point 3, zeros for
+// constant blocks) and total cost at the given parameters.
+int oracle_linearize(const oracle_problem* prob, double* r, double* J, double* cost) {
+  oracle::Problem P = to_problem(prob);
+  oracle::build_structure(P);
+  std::vector<double> x;
+  oracle::gather_x(P, x);
+  std::vector<oracle::Lin> L;
+  bool ok = oracle::eval_lin(P, x, L, cost);
+  for (int o = 0; o < P.no; ++o) {
+    r[2 * o] = L[o].r[0]; r[2 * o + 1] = L[o].r[1];
+    for (int i = 0; i < 2; ++i) {
+      for (int k = 0; k < 6; ++k) J[(size_t)o * 18 + i * 9 + k] = L[o].Jc[i * 6 + k];
+      for (int k = 0; k < 3; ++k) J[(size_t)o * 18 + i * 9 + 6 + k] = L[o].Jp[i * 3 + k];
+    }
+  }
+  return ok ? 0 : 1;
+}
+
+// Raw (uncorrected) residuals of the functors.
+void oracle_residuals(const oracle_problem* prob, double* r) {
+  oracle::Problem P = to_problem(prob);
+  oracle::build_structure(P);
+  for (int o = 0; o < P.no; ++o) {
+    const int c = P.obs_cam[o], p = P.obs_pt[o];
+    const float u = P.obs_uv[2 * o], v = P.obs_uv[2 * o + 1];
+    if (P.cam_fixed && P.cam_fixed[c]) {
+      oracle::point_only_reprojection(P.pts + 3 * p, P.cam_extr + 16 * c, P.K + 9 * c, u, v, r + 2 * o);
+    } else {
+      oracle::angle_reprojection(P.cams + 6 * c, P.pts + 3 * p, P.K + 9 * c, u, v, r + 2 * o);
+    }
+  }
+}
+
+// Seconds per LM iteration (CPU baseline; same work as ba_bench_iterations).
+double oracle_bench(const oracle_problem* prob, int iters, double radius) {
+  oracle::Problem P = to_problem(prob);
+  return oracle::bench_iteration_seconds(P, iters, radius);
+}
+
+int oracle_max_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+void oracle_angle_axis_to_R(const double* aa, double* R) { oracle::AngleAxisToRotationMatrix(aa, R); }
+void oracle_R_to_angle_axis(const double* R, double* aa) { oracle::RotationMatrixToAngleAxis(R, aa); }
+
+void oracle_angle_axis_to_R_jac(const double* aa, double* R, double* dR /*[3][9]*/) {
+  oracle::Jet<3> a[3], Rj[9];
+  for (int k = 0; k < 3; ++k) a[k] = oracle::Jet<3>(aa[k], k);
+  oracle::AngleAxisToRotationMatrix(a, Rj);
+  for (int i = 0; i < 9; ++i) { R[i] = Rj[i].a; for (int k = 0; k < 3; ++k) dR[k * 9 + i] = Rj[i].v[k]; }
+}
+
+void oracle_default_options(oracle::Options* o) {
+  o->max_num_iterations = 50;
+  o->max_num_consecutive_invalid_steps = 5;
+  o->jacobi_scaling = 1;
+  o->pad = 0;
+  o->function_tolerance = 1e-6;
+  o->gradient_tolerance = 1e-10;
+  o->parameter_tolerance = 1e-8;
+  o->initial_trust_region_radius = 1e4;
+  o->max_trust_region_radius = 1e16;
+  o->min_trust_region_radius = 1e-32;
+  o->min_relative_decrease = 1e-3;
+  o->min_lm_diagonal = 1e-6;
+  o->max_lm_diagonal = 1e32;
+}
+
+}  // extern "C"

@@ -1,0 +1,32 @@
+#!/usr/bin/env bash
+# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel trace.
+# Every GPU step has its own time limit; a fault / abort / timeout stops the
+# script (no further GPU work), a plain test failure does not.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+OUT=gpurun_out
+STEPS=${STEPS:-20}
+stop_on_fault() {  # $1 = exit status of a GPU step
+  case "$1" in
+    0|1) return 0 ;;
+    *) echo "GPU step exited with $1 — stopping"; exit "$1" ;;
+  esac
+}
+echo "== rocm-smi"; (rocm-smi --showproductname 2>&1 | head -20) || true
+echo "== pytest -m gpu"
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -rA > $OUT/pytest_gpu.log 2>&1
+rc=$?; tail -30 $OUT/pytest_gpu.log; stop_on_fault $rc
+echo "== smoke"
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+rc=$?; tail -5 $OUT/smoke.log; stop_on_fault $rc
+echo "== bench"
+timeout -k 10 600 python3 -u bench.py --steps "$STEPS" --warmup 3 > $OUT/bench.json 2> $OUT/bench.err
+rc=$?; cat $OUT/bench.json; tail -5 $OUT/bench.err; stop_on_fault $rc
+echo "== rocprofv3 kernel trace"
+export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
+  python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err
+rc=$?; tail -3 $OUT/prof.err; stop_on_fault $rc
+find $OUT/prof -name "*stats*" | head
+exit 0
