@@ -1,0 +1,482 @@
+// ba_chol.hip — dense blocked Cholesky of the reduced camera system on gfx950.
+//
+// The reference solves the reduced camera system of DENSE_SCHUR with a dense
+// Cholesky (Eigen LLT; Optimizer.cpp:85).  Here the (n+1) x n lower
+// trapezoid A (row n = right-hand side b) is factored in 64-wide block
+// columns into a separate lower-trapezoidal L (row n of L = z = L^-1 b).
+//
+// One launch per block step k ("look-ahead"), grid = lower tiles of the
+// trailing matrix (64 x 64, MFMA f64 16x16x4 contractions):
+//   tile (0,0) [critical]:  P = A_{k+1,k} V_k^T  (-> L), C = A_{k+1,k+1} - P P^T,
+//                           factor C = L L^T and invert it (V_{k+1} = L^-1)
+//   tile (I,J) [others]:    P_I = A_{I,k} V_k^T, P_J = A_{J,k} V_k^T,
+//                           A_{IJ} -= P_I P_J^T ; the J = k+1 column also
+//                           stores P_I = L_{I,k}
+// so the serial chain per 64 columns is one panel GEMM, one tile update and
+// the 64-column factor + inverse of the critical workgroup.  Back
+// substitution L^T y = z then uses the explicit V_K (no triangular solves).
+#include "ba_kernels.h"
+
+namespace bahip {
+
+constexpr int CB = 64;           // block size
+constexpr int LDP = CB + 1;      // padded LDS row (doubles)
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// Diagnostic build only (tools/chol_bench.hip defines BA_CHOL_STAMPS): the
+// critical workgroup records s_memtime at phase boundaries into g_stamps.
+#ifdef BA_CHOL_STAMPS
+__device__ unsigned long long g_stamps[64];
+#define CHOL_STAMP(i)                                                                         \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    unsigned long long t_;                                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (threadIdx.x == 0) g_stamps[i] = t_;                                                   \
+  } while (0)
+#else
+#define CHOL_STAMP(i) do {} while (0)
+#endif
+
+// Stage a 64x64 block M[r0 + i][c0 + j] (i < rmax - r0, j < cmax - c0, else
+// 0) into LDS; all 8 loads per thread are issued before any LDS store.
+__device__ inline void stage64(double (*D)[LDP], const double* __restrict__ M, size_t ld, int r0, int c0, int rmax,
+                               int cmax) {
+  double2 v[8];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int e = tid + 256 * it;          // 2048 double2
+    const int i = e >> 5, j = (e & 31) * 2;
+    const int ri = r0 + i, cj = c0 + j;
+    const double* src = M + (size_t)ri * ld + cj;
+    if (ri < rmax && cj + 1 < cmax && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
+      v[it] = *reinterpret_cast<const double2*>(src);
+    } else {
+      v[it].x = (ri < rmax && cj < cmax) ? src[0] : 0.0;
+      v[it].y = (ri < rmax && cj + 1 < cmax) ? src[1] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int e = tid + 256 * it;
+    const int i = e >> 5, j = (e & 31) * 2;
+    D[i][j] = v[it].x;
+    D[i][j + 1] = v[it].y;
+  }
+}
+
+// C (64x64, distributed as 4 waves x 2x2 MFMA tiles of 16x16) = sum_k Xs[i][k] Ys[j][k]
+__device__ inline void mfma_xyT_64(const double (*Xs)[LDP], const double (*Ys)[LDP], d4 acc[2][2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int k0 = 0; k0 < CB; k0 += 4) {
+    const double x0 = Xs[r0 + li][k0 + lk], x1 = Xs[r0 + 16 + li][k0 + lk];
+    const double y0 = Ys[c0 + li][k0 + lk], y1 = Ys[c0 + 16 + li][k0 + lk];
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, y0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, y1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, y0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, y1, acc[1][1], 0, 0, 0);
+  }
+}
+
+// accumulator element (a, b, reg) -> tile-local (row, col); v_mfma_f64_16x16x4
+// D layout: col = lane & 15, row = (lane >> 4) + 4 * reg
+__device__ inline void acc_pos(int a, int b, int reg, int* row, int* col) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  *row = (w >> 1) * 32 + 16 * a + (lane >> 4) + 4 * reg;
+  *col = (w & 1) * 32 + 16 * b + (lane & 15);
+}
+
+// Dst (LDS) = acc (op: 0 store, 1 Dst = Dst - acc)
+__device__ inline void acc_to_lds(double (*D)[LDP], const d4 acc[2][2], int op) {
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int rr, cc;
+        acc_pos(a, b, g, &rr, &cc);
+        if (op == 0) D[rr][cc] = acc[a][b][g];
+        else D[rr][cc] -= acc[a][b][g];
+      }
+}
+
+// Store rows [0, m) x cols [0, w) of an LDS tile to global (coalesced).
+__device__ inline void lds_to_global(const double (*Sx)[LDP], double* __restrict__ G, size_t ld, int r0, int c0,
+                                     int m, int w) {
+  for (int e = threadIdx.x; e < CB * CB; e += 256) {
+    const int i = e / CB, j = e % CB;
+    if (i < m && j < w) G[(size_t)(r0 + i) * ld + c0 + j] = Sx[i][j];
+  }
+}
+
+// Factor + inverse of the diagonal 64-block, the serial heart of the solve.
+//
+// T (LDS) holds the lower part of the block (b columns, m <= 64 rows; rows
+// b..m-1 are extra panel rows: the rhs row of the last step).  It is
+// factored in four 16-column sub-panels (right-looking, blocked):
+//   sweep  16 column steps, division-free (LDL^T form): column j and the
+//          pivot row j of U (unscaled inverse of the sub-panel's 16x16
+//          diagonal block) are published to double-buffered LDS, one
+//          barrier, then every row r > j does  f = a_rj / d_j,
+//          a_rt -= f a_tj (t in the sub-panel, t > j),  U_r -= f U_j.
+//          Thread (r = tid >> 2, q = tid & 3) owns a_{r, c0+4q..c0+4q+3}.
+//   scale  L_rt = a_rt / sqrt(d_t), L_tt = sqrt(d_t); X_pp = U / sqrt(d_r)
+//   update trailing rows/cols: T_RS -= L_{R,p} L_{S,p}^T, 16x16 MFMA tiles.
+// then the off-diagonal blocks of X = L^-1 follow by block distance:
+//   X_ip = -X_ii sum_{k=p}^{i-1} L_ik X_kp   (MFMA, 3 rounds).
+// Per column the chain is one barrier, one LDS round trip and one
+// reciprocal; the O(b^3) work runs on MFMA.  (A full-width register sweep
+// measured ~1300 cycles per column: its 16+16 broadcast reads per thread
+// saturate LDS bandwidth; this one reads 6 doubles per thread per column.)
+// On exit T holds L (b columns, rows < m) and X holds L^-1 (b x b).
+struct CholLds {
+  double colv[2][CB];      // column broadcast of the sub-panel sweep
+  int bad;
+};
+
+// 1/d to ~1 ulp: hardware reciprocal + two Newton steps
+__device__ __forceinline__ double recip(double d) {
+  double y = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-d, y, 1.0);
+  return fma(y, e, y);
+}
+
+// D (16x16, MFMA accumulator layout) += sgn * sum_{k < K} Xs[xr + i][xc + k] * Ys[yr + j][yc + k]
+template <int K>
+__device__ __forceinline__ d4 mfma_tile(d4 acc, const double (*Xs)[LDP], int xr, int xc, const double (*Ys)[LDP],
+                                        int yr, int yc, double sgn) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const double x = sgn * Xs[xr + li][xc + k0 + lk];
+    const double y = Ys[yr + li][yc + k0 + lk];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// same with the second operand transposed: Ys[yr + k][yc + j]
+template <int K>
+__device__ __forceinline__ d4 mfma_tile_n(d4 acc, const double (*Xs)[LDP], int xr, int xc, const double (*Ys)[LDP],
+                                          int yr, int yc, double sgn) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const double x = sgn * Xs[xr + li][xc + k0 + lk];
+    const double y = Ys[yr + k0 + lk][yc + li];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ d4 tile_load(const double (*S)[LDP], int r0, int c0) {
+  const int lane = threadIdx.x & 63;
+  d4 v;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) v[g] = S[r0 + (lane >> 4) + 4 * g][c0 + (lane & 15)];
+  return v;
+}
+
+__device__ __forceinline__ void tile_store(double (*S)[LDP], int r0, int c0, d4 v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) S[r0 + (lane >> 4) + 4 * g][c0 + (lane & 15)] = v[g];
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(static_cast<int>(bits), lane);
+  const int hi = __builtin_amdgcn_readlane(static_cast<int>(bits >> 32), lane);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
+// 16-column sub-panel sweep by ONE wave (lane = row, registers = columns):
+// no barriers on the chain; each column is broadcast through LDS by the
+// same wave (LDS is in order per wave).  Division-free: f_r = a_rj / d_j, a_rt -= f_r a_tj (t > j).
+// The pivots d_t end up on the diagonal (a_tt), so the scaling
+// 1/sqrt(d_t) is computed once per lane in parallel and broadcast.
+// Writes the scaled L columns c0..c0+15 (rows c0..m-1) into T.
+__device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0, int b, int m) {
+  const int r = threadIdx.x & 63;
+  double a[16];
+#pragma unroll
+  for (int cc = 0; cc < 16; ++cc) {
+    const int t = c0 + cc;
+    a[cc] = (r >= c0 && r < m && t < b && (t <= r || r >= b)) ? T[r][t] : 0.0;
+  }
+  // column jj travels through LDS (same wave: in-order, no barrier); the next
+  // column is updated and published first, the rest of the row afterwards
+  W.colv[0][r] = a[0];
+#pragma unroll
+  for (int jj = 0; jj < 16; ++jj) {
+    const int j = c0 + jj;
+    if (j >= b) break;                       // uniform
+    const int buf = jj & 1;
+    const double d = W.colv[buf][j];
+    double ct[16];
+#pragma unroll
+    for (int t = jj + 1; t < 16; ++t) ct[t] = W.colv[buf][c0 + t];
+    const double f = (r > j && r < m) ? a[jj] * recip(d) : 0.0;
+    if (jj + 1 < 16) {
+      a[jj + 1] -= f * ct[jj + 1];
+      W.colv[buf ^ 1][r] = a[jj + 1];
+    }
+#pragma unroll
+    for (int t = jj + 2; t < 16; ++t) a[t] -= f * ct[t];
+  }
+  // own pivot (lanes c0..c0+15): d_r = a_rr
+  double d_own = 1.0;
+#pragma unroll
+  for (int cc = 0; cc < 16; ++cc)
+    if (r == c0 + cc) d_own = a[cc];
+  if (r >= c0 && r < c0 + 16 && r < b && !(d_own > 0.0 && isfinite(d_own))) W.bad = 1;
+  const double rs_own = 1.0 / sqrt(d_own);
+  if (r >= c0 && r < m) {
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) {
+      const int t = c0 + cc;
+      const double rs = readlane_f64(rs_own, c0 + cc);
+      double lv = 0.0;
+      if (t < b) {
+        if (t < r) lv = a[cc] * rs;
+        else if (t == r) lv = a[cc] * rs;   // sqrt(d_t) = d_t / sqrt(d_t)
+      }
+      T[r][t] = lv;
+    }
+  }
+}
+
+// X_pp = L_pp^-1 for the four 16x16 diagonal blocks, one wave each (lane
+// c < 16 solves L_pp x = e_c by forward substitution; L values are uniform
+// LDS broadcasts, 1/L_ii = 1/L_ii computed once per row).
+__device__ __forceinline__ void diag_inverse16(const double (*T)[LDP], double (*X)[LDP], int b) {
+  const int w = threadIdx.x >> 6, c = threadIdx.x & 15;
+  const int c0 = 16 * w;
+  if (c0 >= b || (threadIdx.x & 63) >= 16) return;
+  double x[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    double s = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < i; ++k) s -= T[c0 + i][c0 + k] * x[k];
+    x[i] = (c0 + i < b) ? s / T[c0 + i][c0 + i] : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) X[c0 + i][c0 + c] = x[i];
+}
+
+__device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z)[LDP], CholLds& W, int b, int m) {
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  CHOL_STAMP(2);
+  for (int p = 0; p < 4; ++p) {
+    const int c0 = 16 * p;
+    if (c0 >= b) break;                      // uniform
+    if (w == 0) panel_sweep(T, W, c0, b, m);
+    __syncthreads();
+    // trailing update of the remaining sub-panels: tiles (i, s), p < s <= i
+    {
+      const int nt = 3 - p;                  // tile rows below the sub-panel
+      const int ntiles = nt * (nt + 1) / 2;
+      for (int e = w; e < ntiles; e += 4) {
+        int i = 0, s2 = e;
+        while (s2 > i) { s2 -= i + 1; ++i; }  // e -> (i, s2), s2 <= i
+        const int ti = p + 1 + i, ts = p + 1 + s2;
+        if (16 * ti >= m || 16 * ts >= b) continue;
+        d4 acc = tile_load(T, 16 * ti, 16 * ts);
+        acc = mfma_tile<16>(acc, T, 16 * ti, c0, T, 16 * ts, c0, -1.0);
+        tile_store(T, 16 * ti, 16 * ts, acc);
+      }
+    }
+    __syncthreads();
+  }
+  CHOL_STAMP(3);
+  diag_inverse16(T, X, b);
+  __syncthreads();
+  // off-diagonal blocks of X = L^-1, by block distance dd
+  for (int dd = 1; dd < 4; ++dd) {
+    const int i = dd + w, pp = w;            // wave w: block (dd + w, w)
+    const bool act = i < 4 && 16 * i < b;
+    if (act) {
+      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+      for (int k = pp; k < i; ++k) acc = mfma_tile_n<16>(acc, T, 16 * i, 16 * k, X, 16 * k, 16 * pp, 1.0);
+      tile_store(Z, 16 * w, 0, acc);
+    }
+    __syncthreads();
+    if (act) {
+      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+      acc = mfma_tile_n<16>(acc, X, 16 * i, 16 * i, Z, 16 * w, 0, -1.0);
+      tile_store(X, 16 * i, 16 * pp, acc);
+    }
+    __syncthreads();
+  }
+  CHOL_STAMP(4);
+}
+
+// One block step.  k < 0: factor block 0 only (grid 1x1).
+//   A    working matrix ((n+1) x ld), trailing part updated in place
+//   L    output factor ((n+1) x ld)
+//   Vbuf [T][64][64] inverses of the diagonal blocks
+__global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, double* __restrict__ L, int ld, int n,
+                                                   int k, double* __restrict__ Vbuf, double* __restrict__ scal) {
+  const int I = blockIdx.y, J = blockIdx.x;
+  if (J > I) return;
+  __shared__ double S0[CB][LDP];
+  __shared__ double S1[CB][LDP];
+  __shared__ double S2[CB][LDP];
+  __shared__ CholLds cw;
+  const int nrows = n + 1;
+  const size_t lds = (size_t)ld;
+  const int s = (k + 1) * CB;                 // first row/col of the trailing matrix
+  const int kc = k * CB;                      // column offset of block k
+  const int kb = k >= 0 ? min(CB, n - kc) : 0;
+  const int r0 = s + I * CB, c0 = s + J * CB;
+  const double* Vk = k >= 0 ? Vbuf + (size_t)k * CB * CB : nullptr;
+  if (I == 0 && J == 0) {
+    // ---- critical workgroup: next diagonal block
+    const int b = min(CB, n - s);             // its order
+    const int m = min(CB, nrows - s);         // rows in the tile (b or b + 1 with the rhs row)
+    CHOL_STAMP(0);
+    stage64(S0, A, lds, s, s, nrows, s + b);  // A_{k+1,k+1} (+ rhs row)
+    if (k >= 0) {
+      stage64(S1, A, lds, s, kc, nrows, kc + kb);   // A_{k+1,k}
+      stage64(S2, Vk, CB, 0, 0, CB, CB);
+      __syncthreads();
+      d4 acc[2][2];
+      mfma_xyT_64(S1, S2, acc);              // P = A_{k+1,k} V_k^T
+      __syncthreads();
+      acc_to_lds(S1, acc, 0);
+      __syncthreads();
+      lds_to_global(S1, L, lds, s, kc, m, kb);       // L_{k+1,k}
+      mfma_xyT_64(S1, S1, acc);              // P P^T
+      acc_to_lds(S0, acc, 1);                // C = A - P P^T
+    }
+    if (threadIdx.x == 0) cw.bad = 0;
+    CHOL_STAMP(1);
+    factor_invert_blk(S0, S2, S1, cw, b, m);   // rows b..m-1 (rhs) come out as L rows too
+    CHOL_STAMP(5);
+    __syncthreads();
+    for (int e = threadIdx.x; e < CB * CB; e += 256) {
+      const int i = e / CB, j = e % CB;
+      if (i < m && j < b && (j <= i)) L[(size_t)(s + i) * ld + s + j] = S0[i][j];
+      Vbuf[(size_t)(k + 1) * CB * CB + e] = (j <= i && i < b && j < b) ? S2[i][j] : (i == j ? 1.0 : 0.0);
+    }
+    CHOL_STAMP(6);
+    if (threadIdx.x == 0 && cw.bad) scal[SL_CHOL_BAD] += 1.0;
+    return;
+  }
+  // ---- trailing tile (I, J) != (0, 0)
+  if (k < 0) return;
+  if (r0 >= nrows || c0 >= n) return;
+  stage64(S2, Vk, CB, 0, 0, CB, CB);
+  stage64(S0, A, lds, r0, kc, nrows, kc + kb);   // A_{I,k}
+  if (I != J) stage64(S1, A, lds, c0, kc, n, kc + kb);  // A_{J,k}
+  __syncthreads();
+  d4 acc[2][2];
+  mfma_xyT_64(S0, S2, acc);                  // P_I
+  d4 accJ[2][2];
+  if (I != J) mfma_xyT_64(S1, S2, accJ);     // P_J
+  __syncthreads();
+  acc_to_lds(S0, acc, 0);
+  if (I != J) acc_to_lds(S1, accJ, 0);
+  __syncthreads();
+  const int mI = min(CB, nrows - r0);
+  if (J == 0) lds_to_global(S0, L, lds, r0, kc, mI, kb);   // L_{I,k} final
+  mfma_xyT_64(S0, I != J ? S1 : S0, acc);    // P_I P_J^T
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int rr, cc;
+        acc_pos(a, b, g, &rr, &cc);
+        const int ri = r0 + rr, cj = c0 + cc;
+        if (ri < nrows && cj < n && cj <= ri) A[(size_t)ri * ld + cj] -= acc[a][b][g];
+      }
+}
+
+// ---------------------------------------------------------------------------
+// back substitution L^T y = z (z = row n of L), one workgroup, right-looking
+// over 64-blocks from the bottom: y_K = V_K^T z_K ; z_J -= L_KJ^T y_K (J < K).
+// z is kept in LDS when it fits (n <= kBackLds), else updated in place.
+// ---------------------------------------------------------------------------
+constexpr int kBackLds = 12288;
+__global__ __launch_bounds__(512) void k_chol_back(double* __restrict__ Lm, int ld, int n,
+                                                    const double* __restrict__ Vall, double* __restrict__ y) {
+  __shared__ double Vs[CB][LDP];
+  __shared__ double yb[CB];
+  __shared__ double zl[kBackLds];
+  double* zg = Lm + (size_t)n * ld;
+  const bool in_lds = n <= kBackLds;
+  double* z = in_lds ? zl : zg;
+  const int tid = threadIdx.x;
+  if (in_lds)
+    for (int t = tid; t < n; t += blockDim.x) zl[t] = zg[t];
+  const int nblk = (n + CB - 1) / CB;
+  for (int K = nblk - 1; K >= 0; --K) {
+    const int s0 = K * CB, bsz = min(CB, n - s0);
+    const double* V = Vall + (size_t)K * CB * CB;
+    for (int e = tid; e < CB * CB; e += blockDim.x) Vs[e / CB][e % CB] = V[e];
+    __syncthreads();
+    {  // y_K[j] = sum_{i >= j} V[i][j] z[s0 + i]   (8 threads per j)
+      const int j = tid >> 3, h = tid & 7;
+      double t = 0.0;
+      if (j < bsz)
+        for (int i = j + h; i < bsz; i += 8) t += Vs[i][j] * z[s0 + i];
+      for (int off = 4; off > 0; off >>= 1) t += __shfl_down(t, off, 8);
+      if (h == 0 && j < CB) yb[j] = (j < bsz) ? t : 0.0;
+    }
+    __syncthreads();
+    if (tid < bsz) y[s0 + tid] = yb[tid];
+    for (int t = tid; t < s0; t += blockDim.x) {  // z[t] -= sum_j L[s0+j][t] y_K[j]
+      // two batches of 32 loads in flight (rows past a partial last block
+      // are clamped; yb is zero there)
+      const double* Lc = Lm + (size_t)s0 * ld + t;
+      double acc = 0.0;
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        double lv[CB / 2];
+        const double* Lh = Lc + (size_t)(half * (CB / 2)) * ld;
+#pragma unroll
+        for (int j = 0; j < CB / 2; ++j) {
+          const int jj = half * (CB / 2) + j;
+          lv[j] = Lh[(size_t)(jj < bsz ? j : -half * (CB / 2)) * ld];
+        }
+#pragma unroll
+        for (int j = 0; j < CB / 2; ++j) acc += lv[j] * yb[half * (CB / 2) + j];
+      }
+      z[t] -= acc;
+    }
+    __syncthreads();
+  }
+}
+
+void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  const int n = P.n;
+  if (n == 0) return;
+  const int nrows = n + 1;
+  const int T = (n + CB - 1) / CB;
+  hipLaunchKernelGGL(k_chol_step, dim3(1, 1), dim3(256), 0, s, W.S, W.Lf, P.ld, n, -1, W.Vbuf, W.scal);
+  for (int k = 0; k + 1 < T; ++k) {
+    const int st = (k + 1) * CB;
+    const int tr = (nrows - st + CB - 1) / CB, tc = (n - st + CB - 1) / CB;
+    hipLaunchKernelGGL(k_chol_step, dim3(tc, tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf, W.scal);
+  }
+  hipLaunchKernelGGL(k_chol_back, dim3(1), dim3(512), 0, s, W.Lf, P.ld, n, W.Vbuf, W.y);
+}
+
+}  // namespace bahip

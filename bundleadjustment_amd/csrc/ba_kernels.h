@@ -52,7 +52,8 @@ struct DevWork {
   double* cams;  double* pts;        // x
   double* cams_c; double* pts_c;     // candidate x'
   double* rec;   double* rec_c;      // camera records at x / x'
-  double* r;     double* J;          // [2][no], [18][no]
+  double* JR;                        // [no][20] AoS: Jc row0 (6), Jc row1 (6), Jp rows (3+3), r (2)
+  double* delta_p;                   // [np][3] point step (scaled back)
   double* Hpp;   double* gp;         // [6][np], [3][np]
   double* scale_p; double* diag_p;   // [3][np]
   double* Linv;  double* u;          // [6][np], [3][np]
@@ -60,8 +61,10 @@ struct DevWork {
   double* scale_c; double* diag_c;   // [nvc][6]
   double* delta_c;                   // [nvc][6]
   double* W;                         // [no][18]  (E L^-T per observation)
-  double* S;                         // [(n+1) x ld] reduced system, row n = rhs
+  double* S;                         // [(n+1) x ld] reduced system, row n = rhs (working matrix)
+  double* Lf;                        // [(n+1) x ld] Cholesky factor, row n = L^-1 rhs
   double* y;                         // [n] reduced solution
+  double* Vbuf;                      // [ceil(n/64)][64][64] inverses of the diagonal Cholesky blocks
   const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}
   const int2* pairs;                 // observation pairs per block
   double* part;                      // [kNumSlots][kMaxBlocks]
@@ -76,12 +79,11 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
 void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
                       hipStream_t s);
-void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
-void launch_obs_what(const DevProblem& P, const DevWork& W, hipStream_t s);
+void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);  // + W = E L^-T
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
-void launch_cholesky_solve(const DevProblem& P, const DevWork& W, hipStream_t s);
+void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, hipStream_t s);  // ba_chol.hip
 void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s);
 // Fold the partials of `slots` (bitmask) into d_scal; kernels producing

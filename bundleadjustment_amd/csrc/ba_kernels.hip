@@ -124,15 +124,23 @@ __device__ inline void project_value(const double* __restrict__ cr, bool cvar, d
 }
 
 // ---------------------------------------------------------------------------
-// linearisation: one thread per observation (sorted by point), SoA outputs
-//   r[row][no], J[row*9 + param][no]   (param 0..5 camera, 6..8 point)
+// Per-observation Jacobian/residual record (AoS, 20 doubles = 160 B):
+//   [0..5]  Jc row 0   [6..11] Jc row 1   [12..14] Jp row 0   [15..17] Jp row 1
+//   [18] r0  [19] r1          (Huber-corrected)
+// One record per observation in (point, camera) order: the per-point and
+// per-observation passes stream it, the per-camera passes gather whole
+// records (1-2 cache lines each instead of 14 scattered SoA lines).
+// ---------------------------------------------------------------------------
+constexpr int kJR = 20;
+
+// ---------------------------------------------------------------------------
+// linearisation: one thread per observation (sorted by point)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_linearize(DevProblem P, const double* __restrict__ rec,
-                                                   const double* __restrict__ pts, double* __restrict__ r,
-                                                   double* __restrict__ J, double* __restrict__ part) {
+                                                   const double* __restrict__ pts, double* __restrict__ JR,
+                                                   double* __restrict__ part) {
   __shared__ double lds[2 * 16];
   double acc[2] = {0.0, 0.0};  // cost, bad
-  const size_t no = (size_t)P.no;
   for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < P.no; o += gridDim.x * blockDim.x) {
     const int c = P.obs_cam[o], p = P.obs_pt[o];
     const float2 uv = P.uv[o];
@@ -182,51 +190,63 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem P, const double* _
     const double rho = huber(r0 * r0 + r1 * r1, P.huber_a, P.huber_b, &scale);
     acc[0] += 0.5 * rho;
     bool fin = isfinite(r0) && isfinite(r1);
-    r[o] = r0 * scale;
-    r[no + o] = r1 * scale;
+    double out[kJR];
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
       const bool live = (k < 6) ? cvar : pvar;
       const double j0 = live ? (dq[0][k] - pr0 * dq[2][k]) * iq * scale : 0.0;
       const double j1 = live ? (dq[1][k] - pr1 * dq[2][k]) * iq * scale : 0.0;
       fin = fin && isfinite(j0) && isfinite(j1);
-      J[(size_t)k * no + o] = j0;
-      J[(size_t)(9 + k) * no + o] = j1;
+      if (k < 6) { out[k] = j0; out[6 + k] = j1; }
+      else { out[12 + k - 6] = j0; out[15 + k - 6] = j1; }
     }
+    out[18] = r0 * scale;
+    out[19] = r1 * scale;
+    double2* dst = reinterpret_cast<double2*>(JR + (size_t)o * kJR);
+#pragma unroll
+    for (int k = 0; k < kJR / 2; ++k) dst[k] = make_double2(out[2 * k], out[2 * k + 1]);
     acc[1] += fin ? 0.0 : 1.0;
   }
-  double out[2];
-  block_sum<2>(acc, lds, out);
+  double tot[2];
+  block_sum<2>(acc, lds, tot);
   if (threadIdx.x == 0) {
-    part_of(part, SL_COST)[blockIdx.x] = out[0];
-    part_of(part, SL_LIN_BAD)[blockIdx.x] = out[1];
+    part_of(part, SL_COST)[blockIdx.x] = tot[0];
+    part_of(part, SL_LIN_BAD)[blockIdx.x] = tot[1];
   }
+}
+
+__device__ inline void load_jr(const double* __restrict__ JR, int o, double (&v)[kJR]) {
+  const double2* s = reinterpret_cast<const double2*>(JR + (size_t)o * kJR);
+#pragma unroll
+  for (int k = 0; k < kJR / 2; ++k) { const double2 t = s[k]; v[2 * k] = t.x; v[2 * k + 1] = t.y; }
 }
 
 // ---------------------------------------------------------------------------
 // point blocks: Hpp (xx,xy,xz,yy,yz,zz), gp, jacobi scale, LM diagonal, norms
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const double* __restrict__ r,
-                                                        const double* __restrict__ J, const double* __restrict__ pts,
-                                                        double* __restrict__ Hpp, double* __restrict__ gp,
-                                                        double* __restrict__ scale_p, double* __restrict__ diag_p,
-                                                        int compute_scale, double min_diag, double max_diag,
-                                                        double* __restrict__ part) {
+__global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const double* __restrict__ JR,
+                                                        const double* __restrict__ pts, double* __restrict__ Hpp,
+                                                        double* __restrict__ gp, double* __restrict__ scale_p,
+                                                        double* __restrict__ diag_p, int compute_scale,
+                                                        double min_diag, double max_diag, double* __restrict__ part) {
   __shared__ double lds[3 * 16];
   double acc[2] = {0.0, 0.0};  // gn2, xn2
   double gmax = 0.0;
-  const size_t no = (size_t)P.no, np = (size_t)P.np;
+  const size_t np = (size_t)P.np;
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
     if (!P.pt_var[p]) continue;
     double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
     const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
     for (int o = o0; o < o1; ++o) {
+      const double2* s = reinterpret_cast<const double2*>(JR + (size_t)o * kJR + 12);
+      const double2 t0 = s[0], t1 = s[1], t2 = s[2], t3 = s[3];
+      const double jp[2][3] = {{t0.x, t0.y, t1.x}, {t1.y, t2.x, t2.y}};
+      const double rr[2] = {t3.x, t3.y};
 #pragma unroll
       for (int row = 0; row < 2; ++row) {
-        const double a = J[(size_t)(row * 9 + 6) * no + o], b = J[(size_t)(row * 9 + 7) * no + o],
-                     c = J[(size_t)(row * 9 + 8) * no + o], rr = r[row * no + o];
+        const double a = jp[row][0], b = jp[row][1], c = jp[row][2];
         H[0] += a * a; H[1] += a * b; H[2] += a * c; H[3] += b * b; H[4] += b * c; H[5] += c * c;
-        g[0] += a * rr; g[1] += b * rr; g[2] += c * rr;
+        g[0] += a * rr[row]; g[1] += b * rr[row]; g[2] += c * rr[row];
       }
     }
 #pragma unroll
@@ -262,33 +282,34 @@ __global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const doub
 
 // ---------------------------------------------------------------------------
 // camera blocks: one workgroup per active variable camera, Hcc (21, lower
-// row-major) and gc (6) from its observations (camera-major index list).
+// row-major) and gc (6), gathering its observations' records.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_cam_assemble(DevProblem P, const double* __restrict__ r,
-                                                      const double* __restrict__ J, double* __restrict__ Hcc,
-                                                      double* __restrict__ gc) {
+__global__ __launch_bounds__(256) void k_cam_assemble(DevProblem P, const double* __restrict__ JR,
+                                                      double* __restrict__ Hcc, double* __restrict__ gc) {
   __shared__ double lds[27 * 16];
   const int v = blockIdx.x;
-  const size_t no = (size_t)P.no;
   double acc[27];
 #pragma unroll
   for (int k = 0; k < 27; ++k) acc[k] = 0.0;
   const int i0 = P.cam_off[v], i1 = P.cam_off[v + 1];
   for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int o = P.cam_obs[i];
+    const double2* s = reinterpret_cast<const double2*>(JR + (size_t)o * kJR);
+    double jc[12];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { const double2 t = s[k]; jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
+    const double2 rt = s[9];
+    const double rr[2] = {rt.x, rt.y};
 #pragma unroll
     for (int row = 0; row < 2; ++row) {
-      double j[6];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) j[k] = J[(size_t)(row * 9 + k) * no + o];
-      const double rr = r[row * no + o];
+      const double* j = jc + 6 * row;
       int t = 0;
 #pragma unroll
       for (int a = 0; a < 6; ++a)
 #pragma unroll
         for (int b = 0; b <= a; ++b) acc[t++] += j[a] * j[b];
 #pragma unroll
-      for (int a = 0; a < 6; ++a) acc[21 + a] += j[a] * rr;
+      for (int a = 0; a < 6; ++a) acc[21 + a] += j[a] * rr[row];
     }
   }
   double out[27];
@@ -338,14 +359,17 @@ __global__ __launch_bounds__(256) void k_cam_norms(DevProblem P, const double* _
 }
 
 // ---------------------------------------------------------------------------
-// point elimination: A = s Hpp s + D^2, L L^T = A, store L^-1 and u = L^-1 s*g
-// D = sqrt(diag / radius) (ceres lm_diagonal_), added as D*D.
+// point elimination fused with W: per point (one thread)
+//   A = s Hpp s + D^2 (D = sqrt(diag / radius), ceres lm_diagonal_), L L^T = A,
+//   store L^-1 and u = L^-1 (s g); then for each of its observations with a
+//   variable camera: W_o = diag(s_c) Jc^T Jp diag(s_p) L^-T  (6x3, AoS [no][18])
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* __restrict__ Hpp,
-                                                    const double* __restrict__ gp, const double* __restrict__ scale_p,
-                                                    const double* __restrict__ diag_p, double radius,
-                                                    double* __restrict__ Linv, double* __restrict__ u,
-                                                    double* __restrict__ part) {
+__global__ __launch_bounds__(256) void k_point_elim_w(DevProblem P, const double* __restrict__ Hpp,
+                                                      const double* __restrict__ gp, const double* __restrict__ scale_p,
+                                                      const double* __restrict__ diag_p, double radius,
+                                                      const double* __restrict__ JR, const double* __restrict__ scale_c,
+                                                      double* __restrict__ Linv, double* __restrict__ u,
+                                                      double* __restrict__ W, double* __restrict__ part) {
   __shared__ double lds[16];
   double acc[1] = {0.0};
   const size_t np = (size_t)P.np;
@@ -385,6 +409,31 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
     u[1 * np + p] = i10 * gs[0] + i11 * gs[1];
     u[2 * np + p] = i20 * gs[0] + i21 * gs[1] + i22 * gs[2];
     acc[0] += ok ? 0.0 : 1.0;
+    const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+    for (int o = o0; o < o1; ++o) {
+      const int v = P.vc[P.obs_cam[o]];
+      if (v < 0) continue;
+      double j[kJR];
+      load_jr(JR, o, j);
+      double jp0[3], jp1[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { jp0[k] = j[12 + k] * s[k]; jp1[k] = j[15 + k] * s[k]; }
+      double w[18];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const double sc = scale_c[(size_t)v * 6 + a];
+        const double c0 = j[a] * sc, c1 = j[6 + a] * sc;
+        const double e0 = c0 * jp0[0] + c1 * jp1[0];
+        const double e1 = c0 * jp0[1] + c1 * jp1[1];
+        const double e2 = c0 * jp0[2] + c1 * jp1[2];
+        w[a * 3 + 0] = e0 * i00;
+        w[a * 3 + 1] = e0 * i10 + e1 * i11;
+        w[a * 3 + 2] = e0 * i20 + e1 * i21 + e2 * i22;
+      }
+      double2* dst = reinterpret_cast<double2*>(W + (size_t)o * 18);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) dst[k] = make_double2(w[2 * k], w[2 * k + 1]);
+    }
   }
   double out[1];
   block_sum<1>(acc, lds, out);
@@ -392,42 +441,101 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
 }
 
 // ---------------------------------------------------------------------------
-// per observation (variable camera & point): W = diag(s_c) Jc^T Jp diag(s_p) L^-T
-// stored AoS [no][18] (6x3 row-major) so a pair gather reads 144 contiguous B.
+// back-substitution, one thread per point (all points; fixed / unobserved
+// points keep x' = x):  y_p = L^-T (u_p - sum W_o^T y_c) ; d_p = s_p (-y_p)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_obs_what(DevProblem P, const double* __restrict__ J,
-                                                  const double* __restrict__ scale_c, const double* __restrict__ scale_p,
-                                                  const double* __restrict__ Linv, double* __restrict__ W) {
-  const size_t no = (size_t)P.no, np = (size_t)P.np;
+__global__ __launch_bounds__(256) void k_backsub(DevProblem P, const double* __restrict__ pts,
+                                                 double* __restrict__ pts_c, double* __restrict__ delta_p,
+                                                 const double* __restrict__ W, const double* __restrict__ u,
+                                                 const double* __restrict__ Linv, const double* __restrict__ y,
+                                                 const double* __restrict__ scale_p, double* __restrict__ part) {
+  __shared__ double lds[2 * 16];
+  double acc[2] = {0.0, 0.0};  // step2, step_bad
+  const size_t np = (size_t)P.np;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
+    const double X[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
+    double dX[3] = {0.0, 0.0, 0.0}, Xc[3] = {X[0], X[1], X[2]};
+    if (P.pt_var[p]) {
+      double w[3] = {u[p], u[np + p], u[2 * np + p]};
+      const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+      for (int o = o0; o < o1; ++o) {
+        const int v = P.vc[P.obs_cam[o]];
+        if (v < 0) continue;
+        const double2* wo = reinterpret_cast<const double2*>(W + (size_t)o * 18);
+        double wv[18];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) { const double2 t = wo[k]; wv[2 * k] = t.x; wv[2 * k + 1] = t.y; }
+        const double* yc = y + 6 * v;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          const double ya = yc[a];
+          w[0] -= wv[a * 3] * ya; w[1] -= wv[a * 3 + 1] * ya; w[2] -= wv[a * 3 + 2] * ya;
+        }
+      }
+      const double i00 = Linv[0 * np + p], i10 = Linv[1 * np + p], i11 = Linv[2 * np + p];
+      const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
+      const double yp[3] = {i00 * w[0] + i10 * w[1] + i20 * w[2], i11 * w[1] + i21 * w[2], i22 * w[2]};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        dX[k] = (-yp[k]) * scale_p[k * np + p];
+        Xc[k] = X[k] + dX[k];
+        const double e = X[k] - Xc[k];
+        acc[0] += e * e;
+        if (!isfinite(dX[k])) acc[1] += 1.0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { pts_c[3 * p + k] = Xc[k]; delta_p[3 * p + k] = dX[k]; }
+  }
+  double out[2];
+  block_sum<2>(acc, lds, out);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_STEP2_P)[blockIdx.x] = out[0];
+    part_of(part, SL_STEP_BAD)[blockIdx.x] += out[1];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// model cost change + candidate cost, one thread per observation:
+//   Jd = Jc d_c + Jp d_p ; m += Jd.(r + Jd/2)    (model_cost_change = -sum m)
+//   candidate residual at (camera', X') -> Huber cost
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_candidate(DevProblem P, const double* __restrict__ JR,
+                                                   const double* __restrict__ delta_c,
+                                                   const double* __restrict__ delta_p,
+                                                   const double* __restrict__ rec_c,
+                                                   const double* __restrict__ pts_c, double* __restrict__ part) {
+  __shared__ double lds[3 * 16];
+  double acc[3] = {0.0, 0.0, 0.0};  // mneg, ccost, cand_bad
   for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < P.no; o += gridDim.x * blockDim.x) {
     const int c = P.obs_cam[o], p = P.obs_pt[o];
     const int v = P.vc[c];
-    if (v < 0 || !P.pt_var[p]) continue;
-    double jc0[6], jc1[6], jp0[3], jp1[3], sp[3];
+    double j[kJR];
+    load_jr(JR, o, j);
+    double jd0 = 0.0, jd1 = 0.0;
+    if (v >= 0) {
+      const double* dc = delta_c + (size_t)v * 6;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const double sc = scale_c[(size_t)v * 6 + k];
-      jc0[k] = J[(size_t)k * no + o] * sc;
-      jc1[k] = J[(size_t)(9 + k) * no + o] * sc;
+      for (int a = 0; a < 6; ++a) { jd0 += j[a] * dc[a]; jd1 += j[6 + a] * dc[a]; }
     }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      sp[k] = scale_p[k * np + p];
-      jp0[k] = J[(size_t)(6 + k) * no + o] * sp[k];
-      jp1[k] = J[(size_t)(15 + k) * no + o] * sp[k];
-    }
-    const double i00 = Linv[0 * np + p], i10 = Linv[1 * np + p], i11 = Linv[2 * np + p];
-    const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
-    double* w = W + (size_t)o * 18;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      const double e0 = jc0[a] * jp0[0] + jc1[a] * jp1[0];
-      const double e1 = jc0[a] * jp0[1] + jc1[a] * jp1[1];
-      const double e2 = jc0[a] * jp0[2] + jc1[a] * jp1[2];
-      w[a * 3 + 0] = e0 * i00;
-      w[a * 3 + 1] = e0 * i10 + e1 * i11;
-      w[a * 3 + 2] = e0 * i20 + e1 * i21 + e2 * i22;
-    }
+    const double dp0 = delta_p[3 * p], dp1 = delta_p[3 * p + 1], dp2 = delta_p[3 * p + 2];
+    jd0 += j[12] * dp0 + j[13] * dp1 + j[14] * dp2;
+    jd1 += j[15] * dp0 + j[16] * dp1 + j[17] * dp2;
+    acc[0] += jd0 * (j[18] + jd0 / 2.0) + jd1 * (j[19] + jd1 / 2.0);
+    double rc[2];
+    project_value(rec_c + (size_t)c * kCamRec, !(P.cam_fixed && P.cam_fixed[c]), pts_c[3 * p], pts_c[3 * p + 1],
+                  pts_c[3 * p + 2], P.uv[o], rc);
+    double sc;
+    const double rho = huber(rc[0] * rc[0] + rc[1] * rc[1], P.huber_a, P.huber_b, &sc);
+    acc[1] += 0.5 * rho;
+    if (!isfinite(rc[0]) || !isfinite(rc[1])) acc[2] += 1.0;
+  }
+  double out[3];
+  block_sum<3>(acc, lds, out);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_MCC_NEG)[blockIdx.x] = out[0];
+    part_of(part, SL_CCOST)[blockIdx.x] = out[1];
+    part_of(part, SL_CAND_BAD)[blockIdx.x] = out[2];
   }
 }
 
@@ -478,44 +586,68 @@ __global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const doub
 // stride over its observation pairs, fixed-order shuffle reduction.
 //   S_IJ (rows I, cols J) = -sum W_oI W_oJ^T
 // ---------------------------------------------------------------------------
+__device__ inline void load_w(const double* __restrict__ W, int o, double (&w)[18]) {
+  const double2* s = reinterpret_cast<const double2*>(W + (size_t)o * 18);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) { const double2 t = s[k]; w[2 * k] = t.x; w[2 * k + 1] = t.y; }
+}
+__device__ inline void acc_pair(double (&acc)[36], const double (&a)[18], const double (&b)[18]) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      acc[i * 6 + j] += a[i * 3] * b[j * 3] + a[i * 3 + 1] * b[j * 3 + 1] + a[i * 3 + 2] * b[j * 3 + 2];
+}
+
+// 16 lanes per block (4 blocks per wave): each lane accumulates every 16th
+// pair (two pairs' gathers in flight), then a 4-stage xor reduction inside
+// the 16-lane group; all 16 lanes then hold the sums and store 36/16 each.
 __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* __restrict__ blocks, int nblocks,
                                                      const int2* __restrict__ pairs, const double* __restrict__ W,
                                                      double* __restrict__ S) {
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, sl = lane & 15, sub = lane >> 4;
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const size_t ld = (size_t)P.ld;
-  for (int bi = wave; bi < nblocks; bi += nwaves) {
-    const int4 blk = blocks[bi];
+  for (int base = wave * 4; base < nblocks; base += nwaves * 4) {
+    const int bi = base + sub;
+    const bool live = bi < nblocks;
+    const int4 blk = live ? blocks[bi] : make_int4(0, 0, 0, 0);
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; ++k) acc[k] = 0.0;
-    for (int e = blk.z + lane; e < blk.w; e += 64) {
-      const int2 pr = pairs[e];
-      double a[18], b[18];
-      const double2* wa = reinterpret_cast<const double2*>(W + (size_t)pr.x * 18);
-      const double2* wb = reinterpret_cast<const double2*>(W + (size_t)pr.y * 18);
-#pragma unroll
-      for (int k = 0; k < 9; ++k) {
-        const double2 ta = wa[k], tb = wb[k];
-        a[2 * k] = ta.x; a[2 * k + 1] = ta.y; b[2 * k] = tb.x; b[2 * k + 1] = tb.y;
-      }
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 6; ++j)
-          acc[i * 6 + j] += a[i * 3] * b[j * 3] + a[i * 3 + 1] * b[j * 3 + 1] + a[i * 3 + 2] * b[j * 3 + 2];
+    int e = blk.z + sl;
+    for (; e + 16 < blk.w; e += 32) {
+      const int2 p0 = pairs[e], p1 = pairs[e + 16];
+      double a0[18], b0[18], a1[18], b1[18];
+      load_w(W, p0.x, a0); load_w(W, p0.y, b0);
+      load_w(W, p1.x, a1); load_w(W, p1.y, b1);
+      acc_pair(acc, a0, b0);
+      acc_pair(acc, a1, b1);
+    }
+    if (e < blk.w) {
+      const int2 p0 = pairs[e];
+      double a0[18], b0[18];
+      load_w(W, p0.x, a0); load_w(W, p0.y, b0);
+      acc_pair(acc, a0, b0);
     }
 #pragma unroll
-    for (int k = 0; k < 36; ++k) acc[k] = wave_sum(acc[k]);
-    if (lane == 0) {
+    for (int k = 0; k < 36; ++k) {
+      double v = acc[k];
+      v += __shfl_xor(v, 8, 16);
+      v += __shfl_xor(v, 4, 16);
+      v += __shfl_xor(v, 2, 16);
+      v += __shfl_xor(v, 1, 16);
+      acc[k] = v;
+    }
+    if (live) {
       const int I = blk.x, Jb = blk.y;
-      if (I != Jb) {
-        for (int i = 0; i < 6; ++i)
-          for (int j = 0; j < 6; ++j) S[(size_t)(6 * I + i) * ld + 6 * Jb + j] = -acc[i * 6 + j];
-      } else {  // duplicate observations of one point by one camera
-        for (int i = 0; i < 6; ++i)
-          for (int j = 0; j <= i; ++j) S[(size_t)(6 * I + i) * ld + 6 * I + j] -= acc[i * 6 + j];
+#pragma unroll
+      for (int k = 0; k < 36; ++k) {
+        if ((k & 15) != sl) continue;
+        const int i = k / 6, j = k % 6;
+        if (I != Jb) S[(size_t)(6 * I + i) * ld + 6 * Jb + j] = -acc[k];
+        else if (j <= i) S[(size_t)(6 * I + i) * ld + 6 * I + j] -= acc[k];  // duplicate obs of one point by one camera
       }
     }
   }
@@ -541,156 +673,6 @@ __global__ __launch_bounds__(256) void k_cam_add_diag(DevProblem P, const double
       S[(size_t)(6 * v + a) * ld + 6 * v + b] += h;
     }
     S[(size_t)P.n * ld + 6 * v + a] += gc[(size_t)v * 6 + a] * s[a];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Dense blocked Cholesky of the reduced camera system, lower, row-major,
-// (n+1) x n trapezoid: row n carries the rhs, so the factorisation leaves
-// z = L^-1 b in row n (forward substitution folded into the panel solves).
-// ---------------------------------------------------------------------------
-constexpr int NB = 64;
-
-// Factor the bsz x bsz diagonal block at (k,k): one wave.
-__global__ __launch_bounds__(64) void k_potrf_diag(double* __restrict__ A, int ld, int k, int bsz,
-                                                   double* __restrict__ scal) {
-  __shared__ double T[NB][NB + 1];
-  const int lane = threadIdx.x;
-  for (int i = 0; i < bsz; ++i)
-    if (lane <= i) T[i][lane] = A[(size_t)(k + i) * ld + k + lane];
-  __syncthreads();
-  int bad = 0;
-  for (int j = 0; j < bsz; ++j) {
-    if (lane == j) {
-      const double d = T[j][j];
-      if (!(d > 0.0) || !isfinite(d)) bad = 1;
-      T[j][j] = sqrt(d);
-    }
-    __syncthreads();
-    if (lane > j && lane < bsz) T[lane][j] = T[lane][j] / T[j][j];
-    __syncthreads();
-    if (lane > j && lane < bsz) {
-      const double ltj = T[lane][j];
-      for (int i = lane; i < bsz; ++i) T[i][lane] -= T[i][j] * ltj;
-    }
-    __syncthreads();
-  }
-  for (int i = 0; i < bsz; ++i)
-    if (lane <= i) A[(size_t)(k + i) * ld + k + lane] = T[i][lane];
-  const unsigned long long m = __ballot(bad);
-  if (lane == 0 && m) scal[SL_CHOL_BAD] += 1.0;
-}
-
-// Panel: rows [k+bsz, nrows): X = A_row L_kk^-T.  One thread per row.
-__global__ __launch_bounds__(256) void k_trsm_panel(double* __restrict__ A, int ld, int nrows, int k, int bsz) {
-  __shared__ double L[NB][NB + 1];
-  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-    const int i = e / NB, j = e % NB;
-    double v;
-    if (i < bsz && j < bsz) v = (j <= i) ? A[(size_t)(k + i) * ld + k + j] : 0.0;
-    else v = (i == j) ? 1.0 : 0.0;
-    L[i][j] = v;
-  }
-  __syncthreads();
-  const int row = k + bsz + blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= nrows) return;
-  double x[NB];
-  double* a = A + (size_t)row * ld + k;
-#pragma unroll
-  for (int j = 0; j < NB; ++j) x[j] = (j < bsz) ? a[j] : 0.0;
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    double s = x[j];
-#pragma unroll
-    for (int t = 0; t < j; ++t) s -= x[t] * L[j][t];
-    x[j] = s / L[j][j];
-  }
-#pragma unroll
-  for (int j = 0; j < NB; ++j)
-    if (j < bsz) a[j] = x[j];
-}
-
-// Trailing update: A[i][j] -= sum_t A[i][k+t] A[j][k+t] for rows i >= k+bsz,
-// cols k+bsz <= j <= min(i, ncols-1).  64x64 tiles, lower tiles only.
-__global__ __launch_bounds__(256) void k_syrk_update(double* __restrict__ A, int ld, int nrows, int ncols, int k,
-                                                     int bsz) {
-  __shared__ double As[NB][NB + 1];
-  __shared__ double Bs[NB][NB + 1];
-  // map blockIdx.x -> lower tile (I, J), J <= I
-  const int t = blockIdx.x;
-  int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-  while ((I + 1) * (I + 2) / 2 <= t) ++I;
-  while (I * (I + 1) / 2 > t) --I;
-  const int J = t - I * (I + 1) / 2;
-  const int r0 = k + bsz + I * NB, c0 = k + bsz + J * NB;
-  for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-    const int i = e / NB, kk = e % NB;
-    const int ri = r0 + i, cj = c0 + i;
-    As[i][kk] = (ri < nrows && kk < bsz) ? A[(size_t)ri * ld + k + kk] : 0.0;
-    Bs[i][kk] = (cj < ncols && kk < bsz) ? A[(size_t)cj * ld + k + kk] : 0.0;
-  }
-  __syncthreads();
-  const int ty = threadIdx.x / 16, tx = threadIdx.x % 16;
-  double acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
-  for (int kk = 0; kk < bsz; ++kk) {
-    double av[4], bv[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) av[a] = As[ty + 16 * a][kk];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) bv[b] = Bs[tx + 16 * b][kk];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] += av[a] * bv[b];
-  }
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int ri = r0 + ty + 16 * a;
-    if (ri >= nrows) continue;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int cj = c0 + tx + 16 * b;
-      if (cj < ncols && cj <= ri) A[(size_t)ri * ld + cj] -= acc[a][b];
-    }
-  }
-}
-
-// Back substitution L^T y = z with z = row n of A; one workgroup, blocked
-// from the bottom.  The diagonal block is staged in LDS and solved by wave 0
-// with register-resident z (shuffle broadcast), then all waves apply the
-// block's columns to the remaining z (coalesced along t).
-__global__ __launch_bounds__(1024) void k_trsv_back(double* __restrict__ A, int ld, int n, double* __restrict__ y) {
-  __shared__ double Ld[NB][NB + 1];
-  __shared__ double yb[NB];
-  double* z = A + (size_t)n * ld;
-  const int nblk = (n + NB - 1) / NB;
-  for (int kb = nblk - 1; kb >= 0; --kb) {
-    const int s0 = kb * NB, e0 = min(n, s0 + NB), bsz = e0 - s0;
-    for (int e = threadIdx.x; e < NB * NB; e += blockDim.x) {
-      const int i = e / NB, j = e % NB;
-      Ld[i][j] = (i < bsz && j <= i) ? A[(size_t)(s0 + i) * ld + s0 + j] : 0.0;
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-      const int lane = threadIdx.x;
-      double zl = lane < bsz ? z[s0 + lane] : 0.0;
-      for (int j = bsz - 1; j >= 0; --j) {
-        const double yj = __shfl(zl, j, 64) / Ld[j][j];
-        if (lane < j) zl -= Ld[j][lane] * yj;
-        if (lane == j) { yb[j] = yj; y[s0 + j] = yj; }
-      }
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < s0; t += blockDim.x) {
-      double acc = 0.0;
-      for (int j = 0; j < bsz; ++j) acc += A[(size_t)(s0 + j) * ld + t] * yb[j];
-      z[t] -= acc;
-    }
-    __syncthreads();
   }
 }
 
@@ -737,93 +719,6 @@ __global__ __launch_bounds__(256) void k_cam_candidate(DevProblem P, const doubl
   if (threadIdx.x == 0) {
     part_of(part, SL_STEP2_C)[blockIdx.x] = out[0];
     part_of(part, SL_STEP_BAD)[blockIdx.x] += out[1];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// back-substitution + model cost change + candidate cost, one thread per
-// point (all points; fixed / unobserved points keep x' = x):
-//   y_p = L^-T (u_p - sum W_o^T y_c) ; d_p = s_p * (-y_p) ; X' = X + d_p
-//   per observation: Jd = Jc d_c + Jp d_p ; m += Jd.(r + Jd/2)
-//                    candidate residual at (camera', X') -> Huber cost
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_backsub_candidate(DevProblem P, const double* __restrict__ pts,
-                                                           double* __restrict__ pts_c, const double* __restrict__ W,
-                                                           const double* __restrict__ u, const double* __restrict__ Linv,
-                                                           const double* __restrict__ y, const double* __restrict__ scale_p,
-                                                           const double* __restrict__ J, const double* __restrict__ r,
-                                                           const double* __restrict__ delta_c,
-                                                           const double* __restrict__ rec_c, double* __restrict__ part) {
-  __shared__ double lds[5 * 16];
-  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // mneg, ccost, step2, step_bad, cand_bad
-  const size_t no = (size_t)P.no, np = (size_t)P.np;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
-    const double X[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
-    double dX[3] = {0.0, 0.0, 0.0}, Xc[3] = {X[0], X[1], X[2]};
-    const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
-    const bool pvar = P.pt_var[p] != 0;
-    if (pvar) {
-      double w[3] = {u[p], u[np + p], u[2 * np + p]};
-      for (int o = o0; o < o1; ++o) {
-        const int v = P.vc[P.obs_cam[o]];
-        if (v < 0) continue;
-        const double* wo = W + (size_t)o * 18;
-        const double* yc = y + 6 * v;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          const double ya = yc[a];
-          w[0] -= wo[a * 3] * ya; w[1] -= wo[a * 3 + 1] * ya; w[2] -= wo[a * 3 + 2] * ya;
-        }
-      }
-      const double i00 = Linv[0 * np + p], i10 = Linv[1 * np + p], i11 = Linv[2 * np + p];
-      const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
-      const double yp[3] = {i00 * w[0] + i10 * w[1] + i20 * w[2], i11 * w[1] + i21 * w[2], i22 * w[2]};
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        dX[k] = (-yp[k]) * scale_p[k * np + p];
-        Xc[k] = X[k] + dX[k];
-        const double e = X[k] - Xc[k];
-        acc[2] += e * e;
-        if (!isfinite(dX[k])) acc[3] += 1.0;
-      }
-    }
-    pts_c[3 * p] = Xc[0]; pts_c[3 * p + 1] = Xc[1]; pts_c[3 * p + 2] = Xc[2];
-    for (int o = o0; o < o1; ++o) {
-      const int c = P.obs_cam[o];
-      const int v = P.vc[c];
-      double jd0 = 0.0, jd1 = 0.0;
-      if (v >= 0) {
-        const double* dc = delta_c + (size_t)v * 6;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          jd0 += J[(size_t)a * no + o] * dc[a];
-          jd1 += J[(size_t)(9 + a) * no + o] * dc[a];
-        }
-      }
-      if (pvar) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          jd0 += J[(size_t)(6 + k) * no + o] * dX[k];
-          jd1 += J[(size_t)(15 + k) * no + o] * dX[k];
-        }
-      }
-      acc[0] += jd0 * (r[o] + jd0 / 2.0) + jd1 * (r[no + o] + jd1 / 2.0);
-      double rc[2];
-      project_value(rec_c + (size_t)c * kCamRec, !(P.cam_fixed && P.cam_fixed[c]), Xc[0], Xc[1], Xc[2], P.uv[o], rc);
-      double sc;
-      const double rho = huber(rc[0] * rc[0] + rc[1] * rc[1], P.huber_a, P.huber_b, &sc);
-      acc[1] += 0.5 * rho;
-      if (!isfinite(rc[0]) || !isfinite(rc[1])) acc[4] += 1.0;
-    }
-  }
-  double out[5];
-  block_sum<5>(acc, lds, out);
-  if (threadIdx.x == 0) {
-    part_of(part, SL_MCC_NEG)[blockIdx.x] = out[0];
-    part_of(part, SL_CCOST)[blockIdx.x] = out[1];
-    part_of(part, SL_STEP2_P)[blockIdx.x] = out[2];
-    part_of(part, SL_STEP_BAD)[blockIdx.x] += out[3];
-    part_of(part, SL_CAND_BAD)[blockIdx.x] = out[4];
   }
 }
 
@@ -875,16 +770,16 @@ void launch_cam_prep(const DevProblem& P, const double* cams, double* rec, bool 
                      rec, deriv ? 1 : 0);
 }
 void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s) {
-  hipLaunchKernelGGL(k_linearize, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.rec, W.pts, W.r, W.J, W.part);
+  hipLaunchKernelGGL(k_linearize, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.rec, W.pts, W.JR, W.part);
 }
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
                            double max_diag, hipStream_t s) {
-  hipLaunchKernelGGL(k_point_assemble, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.r, W.J, W.pts, W.Hpp, W.gp,
+  hipLaunchKernelGGL(k_point_assemble, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.JR, W.pts, W.Hpp, W.gp,
                      W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
 }
 void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
-  hipLaunchKernelGGL(k_cam_assemble, dim3(P.nvc), dim3(kThreads), 0, s, P, W.r, W.J, W.Hcc, W.gc);
+  hipLaunchKernelGGL(k_cam_assemble, dim3(P.nvc), dim3(kThreads), 0, s, P, W.JR, W.Hcc, W.gc);
 }
 void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
                       hipStream_t s) {
@@ -892,12 +787,8 @@ void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale,
                      W.diag_c, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
 }
 void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
-  hipLaunchKernelGGL(k_point_elim, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.Hpp, W.gp, W.scale_p, W.diag_p,
-                     radius, W.Linv, W.u, W.part);
-}
-void launch_obs_what(const DevProblem& P, const DevWork& W, hipStream_t s) {
-  hipLaunchKernelGGL(k_obs_what, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.J, W.scale_c, W.scale_p, W.Linv,
-                     W.W);
+  hipLaunchKernelGGL(k_point_elim_w, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.Hpp, W.gp, W.scale_p, W.diag_p,
+                     radius, W.JR, W.scale_c, W.Linv, W.u, W.W, W.part);
 }
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
@@ -905,7 +796,7 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s)
 }
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (W.nblocks == 0) return;
-  int waves = W.nblocks;
+  int waves = (W.nblocks + 3) / 4;
   int grid = (waves + 3) / 4;
   if (grid > 4 * kMaxBlocks) grid = 4 * kMaxBlocks;
   hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
@@ -915,29 +806,15 @@ void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, h
   hipLaunchKernelGGL(k_cam_add_diag, dim3((P.nvc + 255) / 256), dim3(256), 0, s, P, W.Hcc, W.gc, W.scale_c, W.diag_c,
                      radius, W.S);
 }
-void launch_cholesky_solve(const DevProblem& P, const DevWork& W, hipStream_t s) {
-  const int n = P.n;
-  if (n == 0) return;
-  const int nrows = n + 1;
-  for (int k = 0; k < n; k += NB) {
-    const int b = std::min(NB, n - k);
-    hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(64), 0, s, W.S, P.ld, k, b, W.scal);
-    const int prow = nrows - (k + b);
-    if (prow > 0) {
-      hipLaunchKernelGGL(k_trsm_panel, dim3((prow + 255) / 256), dim3(256), 0, s, W.S, P.ld, nrows, k, b);
-      const int T = (prow + NB - 1) / NB;
-      hipLaunchKernelGGL(k_syrk_update, dim3(T * (T + 1) / 2), dim3(256), 0, s, W.S, P.ld, nrows, n, k, b);
-    }
-  }
-  hipLaunchKernelGGL(k_trsv_back, dim3(1), dim3(1024), 0, s, W.S, P.ld, n, W.y);
-}
 void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
   hipLaunchKernelGGL(k_cam_candidate, dim3(grid_for(P.nc)), dim3(kThreads), 0, s, P, W.cams, W.y, W.scale_c,
                      W.cams_c, W.delta_c, W.rec_c, W.part);
 }
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
-  hipLaunchKernelGGL(k_backsub_candidate, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.W, W.u,
-                     W.Linv, W.y, W.scale_p, W.J, W.r, W.delta_c, W.rec_c, W.part);
+  hipLaunchKernelGGL(k_backsub, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p, W.W, W.u,
+                     W.Linv, W.y, W.scale_p, W.part);
+  hipLaunchKernelGGL(k_candidate, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.JR, W.delta_c, W.delta_p,
+                     W.rec_c, W.pts_c, W.part);
 }
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, s, W.part, W.scal, sum_mask, max_mask);

@@ -264,8 +264,8 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.pts_c = ctx->dalloc<double>(3 * (size_t)np);
   W.rec = ctx->dalloc<double>((size_t)kCamRec * nc);
   W.rec_c = ctx->dalloc<double>((size_t)kCamRec * nc);
-  W.r = ctx->dalloc<double>(2 * (size_t)no);
-  W.J = ctx->dalloc<double>(18 * (size_t)no);
+  W.JR = ctx->dalloc<double>(20 * (size_t)no);
+  W.delta_p = ctx->dalloc<double>(3 * (size_t)np);
   W.Hpp = ctx->dalloc<double>(6 * (size_t)np);
   W.gp = ctx->dalloc<double>(3 * (size_t)np);
   W.scale_p = ctx->dalloc<double>(3 * (size_t)np);
@@ -279,7 +279,9 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.delta_c = ctx->dalloc<double>(6 * (size_t)nvc);
   W.W = ctx->dalloc<double>(18 * (size_t)no);
   W.S = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
+  W.Lf = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
   W.y = ctx->dalloc<double>(std::max(ctx->n, 1));
+  W.Vbuf = ctx->dalloc<double>((size_t)((ctx->n + 63) / 64 + 1) * 64 * 64);
   W.blocks = ctx->upload(blocks);
   W.nblocks = (int)blocks.size();
   W.pairs = ctx->upload(pairs);
@@ -341,7 +343,6 @@ StepResult solve_step(ba_ctx* ctx, double radius) {
   if (ctx->n > 0) HIP_OK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)(ctx->n + 1) * ctx->ld, s));
   HIP_OK(hipMemsetAsync(W.scal + SL_CHOL_BAD, 0, sizeof(double), s));
   launch_point_elim(P, W, radius, s);
-  launch_obs_what(P, W, s);
   launch_cam_schur_diag(P, W, s);
   launch_schur_pairs(P, W, s);
   launch_reduce(W, bit(SL_ELIM_BAD), 0, s);
@@ -350,7 +351,7 @@ StepResult solve_step(ba_ctx* ctx, double radius) {
     ctx->allreduce(W.scal + SL_ELIM_BAD, 1);
   }
   launch_cam_add_diag(P, W, radius, s);
-  launch_cholesky_solve(P, W, s);
+  launch_cholesky_solve2(P, W, s);
   launch_cam_candidate(P, W, s);
   launch_backsub_candidate(P, W, s);
   launch_reduce(W, bit(SL_MCC_NEG) | bit(SL_CCOST) | bit(SL_STEP2_P) | bit(SL_CAND_BAD) | bit(SL_STEP_BAD) |
@@ -662,14 +663,18 @@ int ba_linearize(ba_ctx* ctx, double* r, double* J, double* cost) {
     ba_default_options(&o);
     LinResult L = linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
     const int no = ctx->no;
-    std::vector<double> rs(2 * (size_t)no), Js(18 * (size_t)no);
-    HIP_OK(hipMemcpy(rs.data(), ctx->W.r, sizeof(double) * rs.size(), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(Js.data(), ctx->W.J, sizeof(double) * Js.size(), hipMemcpyDeviceToHost));
+    constexpr int kJR = 20;  // record layout of ba_kernels.hip
+    std::vector<double> rec(kJR * (size_t)no);
+    HIP_OK(hipMemcpy(rec.data(), ctx->W.JR, sizeof(double) * rec.size(), hipMemcpyDeviceToHost));
     for (int s = 0; s < no; ++s) {
       const int o2 = ctx->perm[s];
-      if (r) { r[2 * o2] = rs[s]; r[2 * o2 + 1] = rs[(size_t)no + s]; }
+      const double* q = &rec[(size_t)s * kJR];
+      if (r) { r[2 * o2] = q[18]; r[2 * o2 + 1] = q[19]; }
       if (J)
-        for (int k = 0; k < 18; ++k) J[(size_t)o2 * 18 + k] = Js[(size_t)k * no + s];
+        for (int row = 0; row < 2; ++row) {
+          for (int k = 0; k < 6; ++k) J[(size_t)o2 * 18 + row * 9 + k] = q[row * 6 + k];
+          for (int k = 0; k < 3; ++k) J[(size_t)o2 * 18 + row * 9 + 6 + k] = q[12 + row * 3 + k];
+        }
     }
     if (cost) *cost = L.cost;
   });

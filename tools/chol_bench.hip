@@ -1,0 +1,100 @@
+// chol_bench.hip — diagnostic harness for the reduced-camera Cholesky
+// (bundleadjustment_amd/csrc/ba_chol.hip), built with in-kernel s_memtime
+// stamps.  Factors a random SPD (n+1) x n trapezoid, times every block step
+// with HIP events, prints the critical workgroup's phase cycles, solves and
+// checks the solution against a CPU Cholesky.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DBA_CHOL_STAMPS -I bundleadjustment_amd/csrc \
+//         tools/chol_bench.hip -o tools/chol_bench && tools/chol_bench 1194
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+#include "ba_chol.hip"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
+
+using namespace bahip;
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 1194;
+  const int ld = n, nrows = n + 1;
+  std::mt19937_64 rng(7);
+  std::normal_distribution<double> N01;
+  // S = G G^T / m + diag, lower part stored; rhs row random
+  const int m = n + 16;
+  std::vector<double> G((size_t)n * m);
+  for (auto& v : G) v = N01(rng);
+  std::vector<double> A((size_t)nrows * ld, 0.0), full((size_t)n * n);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j <= i; ++j) {
+      double s = 0;
+      for (int k = 0; k < m; ++k) s += G[(size_t)i * m + k] * G[(size_t)j * m + k];
+      s /= m;
+      if (i == j) s += 1.0;
+      A[(size_t)i * ld + j] = s;
+      full[(size_t)i * n + j] = full[(size_t)j * n + i] = s;
+    }
+  std::vector<double> b(n);
+  for (auto& v : b) v = N01(rng);
+  for (int j = 0; j < n; ++j) A[(size_t)n * ld + j] = b[j];
+
+  double *dA, *dL, *dV, *dS, *dy;
+  const int T = (n + CB - 1) / CB;
+  CK(hipMalloc(&dA, sizeof(double) * A.size()));
+  CK(hipMalloc(&dL, sizeof(double) * A.size()));
+  CK(hipMalloc(&dV, sizeof(double) * (size_t)(T + 1) * CB * CB));
+  CK(hipMalloc(&dS, sizeof(double) * 64));
+  CK(hipMalloc(&dy, sizeof(double) * n));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipMemcpy(dA, A.data(), sizeof(double) * A.size(), hipMemcpyHostToDevice));
+    CK(hipMemset(dS, 0, sizeof(double) * 64));
+    double tot = 0;
+    const bool verbose = rep == 2;
+    for (int k = -1; k + 1 < T; ++k) {
+      const int st = (k + 1) * CB;
+      const int tr = (nrows - st + CB - 1) / CB, tc = (n - st + CB - 1) / CB;
+      dim3 grid = k < 0 ? dim3(1, 1) : dim3(tc, tr);
+      CK(hipEventRecord(e0));
+      hipLaunchKernelGGL(k_chol_step, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      tot += ms;
+      unsigned long long st_h[64];
+      CK(hipMemcpyFromSymbol(st_h, HIP_SYMBOL(g_stamps), sizeof(st_h)));
+      if (verbose && (k < 2 || k == T / 2 || k + 2 == T))
+        printf("step %3d grid %3dx%3d  %7.2f us | stage+gemm %6llu  init %6llu  factor %6llu  inverse %6llu  tail %6llu"
+               "  write %6llu cycles\n",
+               k, grid.x, grid.y, ms * 1e3, st_h[1] - st_h[0], st_h[2] - st_h[1], st_h[3] - st_h[2],
+               st_h[4] - st_h[3], st_h[5] - st_h[4], st_h[6] - st_h[5]);
+
+    }
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL(k_chol_back, dim3(1), dim3(512), 0, 0, dL, ld, n, dV, dy);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float mb;
+    CK(hipEventElapsedTime(&mb, e0, e1));
+    if (verbose) printf("factor total %.1f us (%d steps), back-solve %.1f us\n", tot * 1e3, T, mb * 1e3);
+  }
+  std::vector<double> y(n), Sh(64);
+  CK(hipMemcpy(y.data(), dy, sizeof(double) * n, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(Sh.data(), dS, sizeof(double) * 64, hipMemcpyDeviceToHost));
+  // residual |S y - b| / |b|
+  double rn = 0, bn = 0;
+  for (int i = 0; i < n; ++i) {
+    double s = 0;
+    for (int j = 0; j < n; ++j) s += full[(size_t)i * n + j] * y[j];
+    rn += (s - b[i]) * (s - b[i]);
+    bn += b[i] * b[i];
+  }
+  printf("n=%d  relative residual %.3e  chol_bad=%g\n", n, std::sqrt(rn / bn), Sh[SL_CHOL_BAD]);
+  return std::sqrt(rn / bn) < 1e-10 ? 0 : 3;
+}

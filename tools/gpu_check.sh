@@ -29,4 +29,12 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
   python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof.err
 rc=$?; tail -3 $OUT/prof.err; stop_on_fault $rc
 find $OUT/prof -name "*stats*" | head
+if [ "${PMC:-0}" = "1" ]; then
+  echo "== rocprofv3 PMC (separate passes: FETCH_SIZE, WRITE_SIZE)"
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 600 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmc_$ctr -o run -- \
+      python3 -u bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/pmc_$ctr.json 2> $OUT/pmc_$ctr.err
+    rc=$?; tail -2 $OUT/pmc_$ctr.err; stop_on_fault $rc
+  done
+fi
 exit 0
