@@ -67,6 +67,17 @@ class ba_iteration(C.Structure):
     ]
 
 
+class ba_prune_problem(C.Structure):
+    _fields_ = [
+        ("n_cams", C.c_int32), ("n_obs", C.c_int32),
+        ("extr", C.c_void_p), ("cam_center", C.c_void_p), ("K", C.c_void_p), ("obs_cam", C.c_void_p),
+        ("obs_X", C.c_void_p), ("obs_uv", C.c_void_p), ("obs_inv_sigma", C.c_void_p), ("obs_dist", C.c_void_p),
+    ]
+
+
+PRUNE_NAMES = {0: "INLIER", 1: "OUTLIER_BEHIND", 2: "OUTLIER_DEPTH", 3: "OUTLIER_CHI2"}
+
+
 # (name, restype, argtypes) — every symbol declared in include/ba_hip.h
 SIGNATURES = [
     ("ba_abi_version", C.c_int, []),
@@ -83,6 +94,7 @@ SIGNATURES = [
     ("ba_get_iteration_log", C.c_int, [C.c_void_p, C.POINTER(ba_iteration), C.c_int]),
     ("ba_eval_residuals", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]),
     ("ba_linearize", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]),
+    ("ba_prune", C.c_int, [C.c_void_p, C.POINTER(ba_prune_problem), C.c_void_p]),
     ("ba_synchronize", C.c_int, [C.c_void_p]),
     ("ba_bench_iterations", C.c_int, [C.c_void_p, C.c_int, C.c_double, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]),

@@ -91,6 +91,10 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s);
 void launch_residuals(const DevProblem& P, const double* rec, const double* pts, double* r_raw, hipStream_t s);
 
+// pruneCorrespondences per (keyframe, keypoint) pair (ba_prune.hip)
+void launch_prune(int n, const float* extr, const float* center, const float* K, const int* obs_cam, const float* X,
+                  const float* uv, const float* inv_sigma, const float* dist, uint8_t* out, hipStream_t s);
+
 int grid_for(int n);
 
 }  // namespace bahip

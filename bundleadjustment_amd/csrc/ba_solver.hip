@@ -680,6 +680,49 @@ int ba_linearize(ba_ctx* ctx, double* r, double* J, double* cost) {
   });
 }
 
+int ba_prune(ba_ctx* ctx, const ba_prune_problem* p, uint8_t* result) {
+  if (!ctx) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] {
+    if (!p || p->n_cams < 0 || p->n_obs < 0) throw BaError{BA_ERR_INVALID_ARGUMENT, "ba_prune: bad sizes"};
+    const int nc = p->n_cams, no = p->n_obs;
+    if (no == 0) return;
+    if (!p->extr || !p->cam_center || !p->K || !p->obs_cam || !p->obs_X || !p->obs_uv || !p->obs_inv_sigma ||
+        !p->obs_dist || !result)
+      throw BaError{BA_ERR_INVALID_ARGUMENT, "ba_prune: null array"};
+    for (int o = 0; o < no; ++o)
+      if (p->obs_cam[o] < 0 || p->obs_cam[o] >= nc)
+        throw BaError{BA_ERR_INVALID_ARGUMENT, "ba_prune: obs_cam[" + std::to_string(o) + "] out of range"};
+    HIP_OK(hipSetDevice(ctx->device));
+    // one staging buffer: cameras (16 + 3 + 9 floats) then pairs (1 int + 3 + 2 + 1 + 2 floats + 1 byte)
+    const size_t cam_b = sizeof(float) * 28 * (size_t)nc, obs_b = sizeof(float) * 9 * (size_t)no;
+    const size_t bytes = cam_b + obs_b + sizeof(int) * (size_t)no + (size_t)no;
+    char* d = nullptr;
+    HIP_OK(hipMalloc(&d, bytes));
+    std::vector<char> h(bytes - (size_t)no);
+    size_t off = 0;
+    auto put = [&](const void* src, size_t n) { std::memcpy(h.data() + off, src, n); off += n; };
+    put(p->extr, sizeof(float) * 16 * nc);
+    put(p->cam_center, sizeof(float) * 3 * nc);
+    put(p->K, sizeof(float) * 9 * nc);
+    put(p->obs_X, sizeof(float) * 3 * no);
+    put(p->obs_uv, sizeof(float) * 2 * no);
+    put(p->obs_inv_sigma, sizeof(float) * no);
+    put(p->obs_dist, sizeof(float) * 2 * no);
+    put(p->obs_cam, sizeof(int) * no);
+    auto f = [&](size_t o) { return reinterpret_cast<const float*>(d + o); };
+    const size_t oX = cam_b, oUV = oX + sizeof(float) * 3 * no, oS = oUV + sizeof(float) * 2 * no,
+                 oD = oS + sizeof(float) * no, oC = oD + sizeof(float) * 2 * no, oR = oC + sizeof(int) * no;
+    HIP_OK(hipMemcpyAsync(d, h.data(), h.size(), hipMemcpyHostToDevice, ctx->stream));
+    launch_prune(no, f(0), f(sizeof(float) * 16 * nc), f(sizeof(float) * 19 * nc),
+                 reinterpret_cast<const int*>(d + oC), f(oX), f(oUV), f(oS), f(oD),
+                 reinterpret_cast<uint8_t*>(d + oR), ctx->stream);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(result, d + oR, (size_t)no, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(d);
+  });
+}
+
 int ba_synchronize(ba_ctx* ctx) {
   if (!ctx) return BA_ERR_INVALID_ARGUMENT;
   return guarded(ctx, [&] { HIP_OK(hipStreamSynchronize(ctx->stream)); });

@@ -165,6 +165,20 @@ class Solver:
         self._check(self.lib.ba_linearize(self.h, _ptr(r), _ptr(J), C.byref(cost)), "ba_linearize")
         return r, J, cost.value
 
+    def prune(self, extr, cam_center, K, obs_cam, obs_X, obs_uv, obs_inv_sigma, obs_dist) -> np.ndarray:
+        """pruneCorrespondences (Optimizer.cpp:6-79) on the device for a batch of
+        (keyframe, keypoint) pairs; returns a uint8 ba_prune_result per pair."""
+        arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (extr, cam_center, K)]
+        oc = np.ascontiguousarray(obs_cam, dtype=np.int32)
+        oarrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (obs_X, obs_uv, obs_inv_sigma, obs_dist)]
+        n_cams, n_obs = arrs[0].size // 16, oc.size
+        pp = N.ba_prune_problem(n_cams=n_cams, n_obs=n_obs, extr=_ptr(arrs[0]), cam_center=_ptr(arrs[1]),
+                                K=_ptr(arrs[2]), obs_cam=_ptr(oc), obs_X=_ptr(oarrs[0]), obs_uv=_ptr(oarrs[1]),
+                                obs_inv_sigma=_ptr(oarrs[2]), obs_dist=_ptr(oarrs[3]))
+        out = np.empty(n_obs, np.uint8)
+        self._check(self.lib.ba_prune(self.h, C.byref(pp), _ptr(out)), "ba_prune")
+        return out
+
     def synchronize(self):
         self._check(self.lib.ba_synchronize(self.h), "ba_synchronize")
 

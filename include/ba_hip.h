@@ -172,6 +172,39 @@ int ba_eval_residuals(ba_ctx* ctx, double* r, double* cost);
  * zero blocks for constant parameter blocks).  Test/inspection entry point. */
 int ba_linearize(ba_ctx* ctx, double* r, double* J, double* cost);
 
+/* pruneCorrespondences (BAOptimizer, Optimizer.cpp:6-79) for a batch of
+ * (keyframe, keypoint) pairs, evaluated in float like the reference:
+ *   c = hnormalized(extr * [X;1]); outlier if c.z <= 0;
+ *   outlier if |X - cam_center| > max_dist or < min_dist;
+ *   outlier if |hnormalized(K c) - uv| * inv_sigma > 5.991 (a norm, not a
+ *   squared norm: Optimizer.cpp:56-59); otherwise inlier.
+ * Operation order (fixed here; Eigen's is not pinned): matrix-vector products
+ * accumulate column by column, norms as sqrt((x*x + y*y) + z*z), no fused
+ * multiply-adds, IEEE division and square root.
+ * The caller selects which pairs to evaluate (considerOutlier) and applies
+ * the results with Frame::setOutlier / setInlier. */
+typedef struct {
+  int32_t n_cams, n_obs;
+  const float*   extr;            /* [16*n_cams] col-major world->camera = getPose().inverse() */
+  const float*   cam_center;      /* [3*n_cams]  getWorldPos()                   */
+  const float*   K;               /* [9*n_cams]  col-major getIntrinsics()      */
+  const int32_t* obs_cam;         /* [n_obs]                                     */
+  const float*   obs_X;           /* [3*n_obs]   MapPoint::getPosition()          */
+  const float*   obs_uv;          /* [2*n_obs]   getKeypoint(i)->pt               */
+  const float*   obs_inv_sigma;   /* [n_obs]     (float)(1.0 / pow(1.2, octave))  */
+  const float*   obs_dist;        /* [2*n_obs]   getMinDistance, getMaxDistance   */
+} ba_prune_problem;
+
+enum ba_prune_result {
+  BA_INLIER = 0,
+  BA_OUTLIER_BEHIND = 1,          /* camspacePos.z() <= 0        (Optimizer.cpp:36-41) */
+  BA_OUTLIER_DEPTH = 2,           /* outside [minDist, maxDist]  (:43-51) */
+  BA_OUTLIER_CHI2 = 3             /* reprojection test           (:53-64) */
+};
+
+/* result[n_obs] receives a ba_prune_result per pair (runs on the device). */
+int ba_prune(ba_ctx* ctx, const ba_prune_problem* problem, uint8_t* result);
+
 /* Blocks until all device work of the context is done. */
 int ba_synchronize(ba_ctx* ctx);
 

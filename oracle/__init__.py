@@ -69,6 +69,7 @@ def lib():
         L.oracle_bench.restype = C.c_double
         L.oracle_bench.argtypes = [C.POINTER(_Problem), C.c_int, C.c_double]
         L.oracle_max_threads.restype = C.c_int
+        L.oracle_prune.argtypes = [C.c_int] + [C.c_void_p] * 9
         _lib = L
     return _lib
 
@@ -172,3 +173,14 @@ def R_to_angle_axis(R):
     w = np.empty(3)
     lib().oracle_R_to_angle_axis(_p(Rc), _p(w))
     return w
+
+
+def prune(extr, cam_center, K, obs_cam, obs_X, obs_uv, obs_inv_sigma, obs_dist):
+    """pruneCorrespondences restated (Optimizer.cpp:6-79), float; returns uint8
+    codes 0 inlier, 1 behind, 2 depth range, 3 chi test (see ba_prune)."""
+    f32 = [np.ascontiguousarray(a, dtype=np.float32) for a in (extr, cam_center, K)]
+    oc = np.ascontiguousarray(obs_cam, dtype=np.int32)
+    o32 = [np.ascontiguousarray(a, dtype=np.float32) for a in (obs_X, obs_uv, obs_inv_sigma, obs_dist)]
+    out = np.empty(oc.size, np.uint8)
+    lib().oracle_prune(int(oc.size), *[_p(a) for a in f32], _p(oc), *[_p(a) for a in o32], _p(out))
+    return out

@@ -1006,6 +1006,36 @@ void oracle_angle_axis_to_R_jac(const double* aa, double* R, double* dR /*[3][9]
   for (int i = 0; i < 9; ++i) { R[i] = Rj[i].a; for (int k = 0; k < 3; ++k) dR[k * 9 + i] = Rj[i].v[k]; }
 }
 
+// pruneCorrespondences restated (Optimizer.cpp:6-79), float arithmetic in the
+// operation order documented for ba_prune in include/ba_hip.h (column-wise
+// matrix-vector accumulation, sqrt((x*x + y*y) + z*z), no contraction: this
+// file is built with -ffp-contract=off).  result: 0 inlier, 1 behind the
+// camera (:36-41), 2 outside the depth range (:43-51), 3 chi test (:53-64).
+void oracle_prune(int n_obs, const float* extr, const float* center, const float* K, const int32_t* obs_cam,
+                  const float* X, const float* uv, const float* inv_sigma, const float* dist, uint8_t* result) {
+  for (int o = 0; o < n_obs; ++o) {
+    const int c = obs_cam[o];
+    const float* e = extr + 16 * c;
+    const float x0 = X[3 * o], x1 = X[3 * o + 1], x2 = X[3 * o + 2];
+    float v[4];
+    for (int i = 0; i < 4; ++i) v[i] = ((e[i] * x0 + e[4 + i] * x1) + e[8 + i] * x2) + e[12 + i];
+    const float cam[3] = {v[0] / v[3], v[1] / v[3], v[2] / v[3]};
+    if (cam[2] <= 0.0f) { result[o] = 1; continue; }
+    const float* ctr = center + 3 * c;
+    const float d0 = x0 - ctr[0], d1 = x1 - ctr[1], d2 = x2 - ctr[2];
+    const float wd = std::sqrt((d0 * d0 + d1 * d1) + d2 * d2);
+    if (wd > dist[2 * o + 1] || wd < dist[2 * o]) { result[o] = 2; continue; }
+    const float* k = K + 9 * c;
+    float q[3];
+    for (int i = 0; i < 3; ++i) q[i] = (k[i] * cam[0] + k[3 + i] * cam[1]) + k[6 + i] * cam[2];
+    const float e0 = q[0] / q[2] - uv[2 * o], e1 = q[1] / q[2] - uv[2 * o + 1];
+    const float nrm = std::sqrt(e0 * e0 + e1 * e1);
+    const float chi = nrm * inv_sigma[o];
+    const float thresh = 5.991;
+    result[o] = chi > thresh ? 3 : 0;
+  }
+}
+
 void oracle_default_options(oracle::Options* o) {
   o->max_num_iterations = 50;
   o->max_num_consecutive_invalid_steps = 5;

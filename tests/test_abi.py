@@ -59,6 +59,8 @@ int main(void) {
   F(ba_options, function_tolerance) F(ba_options, max_lm_diagonal)
   F(ba_summary, num_iterations) F(ba_summary, termination_type) F(ba_summary, solve_time_s)
   F(ba_iteration, cost) F(ba_iteration, model_cost_change) F(ba_iteration, iteration_time_s)
+  printf("ba_prune_problem %zu\n", sizeof(ba_prune_problem));
+  F(ba_prune_problem, extr) F(ba_prune_problem, obs_cam) F(ba_prune_problem, obs_dist)
   return 0;
 }
 """
@@ -72,7 +74,7 @@ def test_ctypes_layout_matches_c_compiler(tmp_path):
     vals = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True,
                                                           check=True).stdout.splitlines())
     types = {"ba_problem": N.ba_problem, "ba_options": N.ba_options, "ba_summary": N.ba_summary,
-             "ba_iteration": N.ba_iteration}
+             "ba_iteration": N.ba_iteration, "ba_prune_problem": N.ba_prune_problem}
     for k, v in vals.items():
         if "." in k:
             t, f = k.split(".")
