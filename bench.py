@@ -24,6 +24,7 @@ import json
 import math
 import os
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -51,6 +52,34 @@ def pmc_traffic(config: str):
         return None
 
 
+def uid_path(world: int) -> Path:
+    """Rendezvous file of one launch: keyed by the launcher (torch.distributed.run
+    is the parent of every rank) and its master port."""
+    key = f"{os.environ.get('MASTER_ADDR', '127.0.0.1')}_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}_{world}"
+    return Path(tempfile.gettempdir()) / f"ba_rccl_uid_{key}.bin"
+
+
+def rendezvous_uid(rank: int, world: int, timeout_s: float = 300.0) -> bytes:
+    from bundleadjustment_amd import Solver
+    path = uid_path(world)
+    if rank == 0:
+        uid = Solver.unique_id()
+        tmp = path.with_name(path.name + f".{os.getpid()}.tmp")
+        tmp.write_bytes(uid)
+        os.replace(tmp, path)          # atomic publish
+        return uid
+    deadline = time.time() + timeout_s
+    while time.time() < deadline:
+        try:
+            data = path.read_bytes()
+            if len(data) == 128:
+                return data
+        except FileNotFoundError:
+            pass
+        time.sleep(0.05)
+    raise RuntimeError(f"rank {rank}: no RCCL id at {path} after {timeout_s:.0f} s")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -59,6 +88,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    ap.add_argument("--comm", action="store_true", help="use an RCCL communicator even at one rank (tests)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -66,10 +96,6 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # host-side rendezvous / barrier only (gloo); GPU traffic is RCCL
-        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     import numpy as np
 
@@ -84,15 +110,19 @@ def main():
         f"(generated in {time.time() - t:.1f}s)")
 
     solver = Solver(local_rank)
-    if world > 1:
-        uid = [Solver.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        solver.comm_init(uid[0], world, rank)
+    use_comm = world > 1 or args.comm
+    if use_comm:
+        # RCCL communicator; the 128-byte id travels through a file keyed by the
+        # launcher (no second GPU runtime in this process for the rendezvous)
+        uid = rendezvous_uid(rank, world)
+        solver.comm_init(uid, world, rank)
+        if rank == 0:
+            uid_path(world).unlink(missing_ok=True)
     solver.set_problem(problem)
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        if use_comm:
+            solver.barrier()
 
     # warmup (first call also computes the Jacobi scaling, as LM iteration 0 does)
     solver.bench_iterations(max(1, args.warmup))
@@ -105,14 +135,9 @@ def main():
     dt = time.perf_counter() - t0
 
     n_obs_total = problem.n_obs
-    if dist is not None:
-        import torch
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt[0])
-        nn = torch.tensor([problem.n_obs], dtype=torch.float64)
-        dist.all_reduce(nn, op=dist.ReduceOp.SUM)
-        n_obs_total = int(nn[0])
+    if use_comm:   # max over ranks of the timed region, total observations
+        dt = float(solver.allreduce_host([dt], "max")[0])
+        n_obs_total = int(solver.allreduce_host([float(problem.n_obs)], "sum")[0])
 
     # algorithmic bytes of the residual+Jacobian kernel per launch:
     #   176 B/obs (uv 8 + two int32 idx 8 + r 16 + J 144) + 24 B/point + 48 B/camera
@@ -160,8 +185,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    solver.close()
     solver.close()
 
 

@@ -87,6 +87,7 @@ SIGNATURES = [
     ("ba_last_error", C.c_char_p, [C.c_void_p]),
     ("ba_comm_unique_id", C.c_int, [C.c_char_p]),
     ("ba_comm_init", C.c_int, [C.c_void_p, C.c_char_p, C.c_int, C.c_int]),
+    ("ba_comm_allreduce_host", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
     ("ba_set_problem", C.c_int, [C.c_void_p, C.POINTER(ba_problem)]),
     ("ba_set_params", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("ba_solve", C.c_int, [C.c_void_p, C.POINTER(ba_options), C.POINTER(ba_summary)]),

@@ -132,81 +132,161 @@ __device__ inline void project_value(const double* __restrict__ cr, bool cvar, d
 // records (1-2 cache lines each instead of 14 scattered SoA lines).
 // ---------------------------------------------------------------------------
 constexpr int kJR = 20;
+constexpr int kStageLd = kJR + 1;   // LDS row stride of staged records
 
 // ---------------------------------------------------------------------------
 // linearisation: one thread per observation (sorted by point)
 // ---------------------------------------------------------------------------
+// Camera record access: R, dR/dw, t as doubles and K (float-valued) — either
+// the global 48-double records or the block's LDS copy of the camera table.
+struct CamGlobal {
+  const double* r;
+  __device__ double R(int k) const { return r[kRecR + k]; }
+  __device__ double dR(int k) const { return r[kRecdR + k]; }
+  __device__ double T(int k) const { return r[kRecT + k]; }
+  __device__ double E(int k) const { return r[k]; }       // fixed camera: 4x4 extrinsic
+  __device__ double K(int k) const { return r[kRecK + k]; }
+};
+constexpr int kTblRec = 39;   // LDS camera row: R (9), dR (27), t (3) / 4x4 extrinsic (16)
+struct CamLds {
+  const double* r;
+  const float* k;
+  __device__ double R(int i) const { return r[kRecR + i]; }
+  __device__ double dR(int i) const { return r[kRecdR + i]; }
+  __device__ double T(int i) const { return r[kRecT + i]; }
+  __device__ double E(int i) const { return r[i]; }
+  __device__ double K(int i) const { return (double)k[i]; }
+};
+
+// r, J (Huber-corrected) of one observation into out[20]; returns rho
+template <class Cam>
+__device__ inline double lin_obs(const DevProblem& P, const Cam& cr, bool cvar, bool pvar, double X0, double X1,
+                                 double X2, float2 uv, double (&out)[kJR], bool& fin) {
+  double pc[3], dp[3][9];
+  if (cvar) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pc[i] = cr.R(i) * X0 + cr.R(3 + i) * X1 + cr.R(6 + i) * X2 + cr.T(i);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dp[i][k] = cr.dR(k * 9 + i) * X0 + cr.dR(k * 9 + 3 + i) * X1 + cr.dR(k * 9 + 6 + i) * X2;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dp[i][3 + k] = (i == k) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dp[i][6 + k] = cr.R(k * 3 + i);
+    }
+  } else {
+    double ph[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ph[i] = X0 * cr.E(i) + X1 * cr.E(4 + i) + X2 * cr.E(8 + i) + cr.E(12 + i);
+    const double inv = 1.0 / ph[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      pc[i] = ph[i] * inv;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) dp[i][k] = 0.0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dp[i][6 + k] = (cr.E(k * 4 + i) - pc[i] * cr.E(k * 4 + 3)) * inv;
+    }
+  }
+  double q[3], dq[3][9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    q[i] = pc[0] * cr.K(i) + pc[1] * cr.K(3 + i) + pc[2] * cr.K(6 + i);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) dq[i][k] = dp[0][k] * cr.K(i) + dp[1][k] * cr.K(3 + i) + dp[2][k] * cr.K(6 + i);
+  }
+  const double iq = 1.0 / q[2];
+  const double pr0 = q[0] * iq, pr1 = q[1] * iq;
+  const double r0 = pr0 - (double)uv.x, r1 = pr1 - (double)uv.y;
+  double scale;
+  const double rho = huber(r0 * r0 + r1 * r1, P.huber_a, P.huber_b, &scale);
+  fin = isfinite(r0) && isfinite(r1);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const bool live = (k < 6) ? cvar : pvar;
+    const double j0 = live ? (dq[0][k] - pr0 * dq[2][k]) * iq * scale : 0.0;
+    const double j1 = live ? (dq[1][k] - pr1 * dq[2][k]) * iq * scale : 0.0;
+    fin = fin && isfinite(j0) && isfinite(j1);
+    if (k < 6) { out[k] = j0; out[6 + k] = j1; }
+    else { out[12 + k - 6] = j0; out[15 + k - 6] = j1; }
+  }
+  out[18] = r0 * scale;
+  out[19] = r1 * scale;
+  return rho;
+}
+
+// Block body: NT observations per chunk; records staged in LDS (row stride
+// 21 doubles) so the global stores are contiguous — a row-per-lane store of
+// 160-B records is store-issue bound.
+template <int NT, class CamOf>
+__device__ inline void lin_chunks(const DevProblem& P, const double* __restrict__ pts, double* __restrict__ JR,
+                                  double* stage, const CamOf& cam_of, double (&acc)[2]) {
+  for (int base = blockIdx.x * NT; base < P.no; base += gridDim.x * NT) {
+    const int o = base + threadIdx.x;
+    const int nrec = min(NT, P.no - base);
+    if (o < P.no) {
+      const int c = P.obs_cam[o], p = P.obs_pt[o];
+      const float2 uv = P.uv[o];
+      const bool cvar = P.vc[c] >= 0;
+      const bool pvar = P.pt_var[p] != 0;
+      double out[kJR];
+      bool fin;
+      acc[0] += 0.5 * lin_obs(P, cam_of(c), cvar, pvar, pts[3 * p], pts[3 * p + 1], pts[3 * p + 2], uv, out, fin);
+      double* row = stage + threadIdx.x * kStageLd;
+#pragma unroll
+      for (int k = 0; k < kJR; ++k) row[k] = out[k];
+      acc[1] += fin ? 0.0 : 1.0;
+    }
+    __syncthreads();
+    double2* dst = reinterpret_cast<double2*>(JR + (size_t)base * kJR);
+    for (int e = threadIdx.x; e < nrec * (kJR / 2); e += NT) {
+      const int r = e / (kJR / 2), f = 2 * (e - r * (kJR / 2));
+      dst[e] = make_double2(stage[r * kStageLd + f], stage[r * kStageLd + f + 1]);
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void k_linearize(DevProblem P, const double* __restrict__ rec,
                                                    const double* __restrict__ pts, double* __restrict__ JR,
                                                    double* __restrict__ part) {
   __shared__ double lds[2 * 16];
+  __shared__ double stage[kThreads * kStageLd];
   double acc[2] = {0.0, 0.0};  // cost, bad
-  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < P.no; o += gridDim.x * blockDim.x) {
-    const int c = P.obs_cam[o], p = P.obs_pt[o];
-    const float2 uv = P.uv[o];
-    const double* __restrict__ cr = rec + (size_t)c * kCamRec;
-    const bool cvar = P.vc[c] >= 0;
-    const bool pvar = P.pt_var[p] != 0;
-    const double X0 = pts[3 * p], X1 = pts[3 * p + 1], X2 = pts[3 * p + 2];
-    double pc[3], dp[3][9];
-    if (cvar) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        pc[i] = cr[kRecR + i] * X0 + cr[kRecR + 3 + i] * X1 + cr[kRecR + 6 + i] * X2 + cr[kRecT + i];
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-          dp[i][k] = cr[kRecdR + k * 9 + i] * X0 + cr[kRecdR + k * 9 + 3 + i] * X1 + cr[kRecdR + k * 9 + 6 + i] * X2;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) dp[i][3 + k] = (i == k) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) dp[i][6 + k] = cr[kRecR + k * 3 + i];
-      }
-    } else {
-      double ph[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ph[i] = X0 * cr[i] + X1 * cr[4 + i] + X2 * cr[8 + i] + cr[12 + i];
-      const double inv = 1.0 / ph[3];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        pc[i] = ph[i] * inv;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) dp[i][k] = 0.0;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) dp[i][6 + k] = (cr[k * 4 + i] - pc[i] * cr[k * 4 + 3]) * inv;
-      }
-    }
-    const double* Kc = cr + kRecK;
-    double q[3], dq[3][9];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      q[i] = pc[0] * Kc[i] + pc[1] * Kc[3 + i] + pc[2] * Kc[6 + i];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) dq[i][k] = dp[0][k] * Kc[i] + dp[1][k] * Kc[3 + i] + dp[2][k] * Kc[6 + i];
-    }
-    const double iq = 1.0 / q[2];
-    const double pr0 = q[0] * iq, pr1 = q[1] * iq;
-    const double r0 = pr0 - (double)uv.x, r1 = pr1 - (double)uv.y;
-    double scale;
-    const double rho = huber(r0 * r0 + r1 * r1, P.huber_a, P.huber_b, &scale);
-    acc[0] += 0.5 * rho;
-    bool fin = isfinite(r0) && isfinite(r1);
-    double out[kJR];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      const bool live = (k < 6) ? cvar : pvar;
-      const double j0 = live ? (dq[0][k] - pr0 * dq[2][k]) * iq * scale : 0.0;
-      const double j1 = live ? (dq[1][k] - pr1 * dq[2][k]) * iq * scale : 0.0;
-      fin = fin && isfinite(j0) && isfinite(j1);
-      if (k < 6) { out[k] = j0; out[6 + k] = j1; }
-      else { out[12 + k - 6] = j0; out[15 + k - 6] = j1; }
-    }
-    out[18] = r0 * scale;
-    out[19] = r1 * scale;
-    double2* dst = reinterpret_cast<double2*>(JR + (size_t)o * kJR);
-#pragma unroll
-    for (int k = 0; k < kJR / 2; ++k) dst[k] = make_double2(out[2 * k], out[2 * k + 1]);
-    acc[1] += fin ? 0.0 : 1.0;
+  lin_chunks<kThreads>(P, pts, JR, stage, [&](int c) { return CamGlobal{rec + (size_t)c * kCamRec}; }, acc);
+  double tot[2];
+  block_sum<2>(acc, lds, tot);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_COST)[blockIdx.x] = tot[0];
+    part_of(part, SL_LIN_BAD)[blockIdx.x] = tot[1];
   }
+}
+
+// Small camera sets (nc <= kLinLdsCams): the whole camera table lives in
+// LDS, so the per-observation camera gathers hit LDS instead of the texture
+// path (the gathers, 24 x 16 B per lane from random cameras, saturate the
+// TA: measured 46 % issue stalls).  One 512-thread block per CU.
+constexpr int kLinLdsThreads = 512;
+constexpr int kLinLdsCams = 212;
+__global__ __launch_bounds__(kLinLdsThreads) void k_linearize_lds(DevProblem P, const double* __restrict__ rec,
+                                                                  const double* __restrict__ pts,
+                                                                  double* __restrict__ JR, double* __restrict__ part) {
+  __shared__ double lds[2 * 16];
+  __shared__ double stage[kLinLdsThreads * kStageLd];
+  __shared__ double tbl[kLinLdsCams * kTblRec];
+  __shared__ float ktb[kLinLdsCams * 9];
+  for (int e = threadIdx.x; e < P.nc * kTblRec; e += kLinLdsThreads) {
+    const int c = e / kTblRec, k = e - c * kTblRec;
+    tbl[e] = rec[(size_t)c * kCamRec + k];
+  }
+  for (int e = threadIdx.x; e < P.nc * 9; e += kLinLdsThreads) {
+    const int c = e / 9, k = e - c * 9;
+    ktb[e] = (float)rec[(size_t)c * kCamRec + kRecK + k];   // K is float-valued (Eigen Matrix3f)
+  }
+  __syncthreads();
+  double acc[2] = {0.0, 0.0};
+  lin_chunks<kLinLdsThreads>(P, pts, JR, stage,
+                             [&](int c) { return CamLds{tbl + c * kTblRec, ktb + c * 9}; }, acc);
   double tot[2];
   block_sum<2>(acc, lds, tot);
   if (threadIdx.x == 0) {
@@ -539,6 +619,93 @@ __global__ __launch_bounds__(256) void k_candidate(DevProblem P, const double* _
   }
 }
 
+// Same with the camera table (value-only candidate records + the camera
+// step) and the observation records staged in LDS: the JR records of a
+// chunk are read with contiguous 16-B-per-lane loads, the per-observation
+// camera data comes from LDS (nc <= kLinLdsCams).
+constexpr int kCandRec = 22;   // R (9) t (3) | extrinsic (16); camera step (6) at 16..21
+__global__ __launch_bounds__(kLinLdsThreads) void k_candidate_lds(DevProblem P, const double* __restrict__ JR,
+                                                                  const double* __restrict__ delta_c,
+                                                                  const double* __restrict__ delta_p,
+                                                                  const double* __restrict__ rec_c,
+                                                                  const double* __restrict__ pts_c,
+                                                                  double* __restrict__ part) {
+  __shared__ double lds[3 * 16];
+  __shared__ double stage[kLinLdsThreads * kStageLd];
+  __shared__ double tbl[kLinLdsCams * kCandRec];
+  __shared__ float ktb[kLinLdsCams * 9];
+  for (int e = threadIdx.x; e < P.nc * kCandRec; e += kLinLdsThreads) {
+    const int c = e / kCandRec, k = e - c * kCandRec;
+    double v;
+    if (k < 16) {
+      const bool fixed = P.cam_fixed && P.cam_fixed[c];
+      v = fixed ? rec_c[(size_t)c * kCamRec + k]
+                : (k < 9 ? rec_c[(size_t)c * kCamRec + kRecR + k] : (k < 12 ? rec_c[(size_t)c * kCamRec + kRecT + k - 9] : 0.0));
+    } else {
+      const int vc = P.vc[c];
+      v = vc >= 0 ? delta_c[(size_t)vc * 6 + (k - 16)] : 0.0;
+    }
+    tbl[e] = v;
+  }
+  for (int e = threadIdx.x; e < P.nc * 9; e += kLinLdsThreads) {
+    const int c = e / 9, k = e - c * 9;
+    ktb[e] = (float)rec_c[(size_t)c * kCamRec + kRecK + k];
+  }
+  double acc[3] = {0.0, 0.0, 0.0};  // mneg, ccost, cand_bad
+  for (int base = blockIdx.x * kLinLdsThreads; base < P.no; base += gridDim.x * kLinLdsThreads) {
+    const int nrec = min(kLinLdsThreads, P.no - base);
+    __syncthreads();   // table ready / previous chunk consumed
+    const double2* src = reinterpret_cast<const double2*>(JR + (size_t)base * kJR);
+    for (int e = threadIdx.x; e < nrec * (kJR / 2); e += kLinLdsThreads) {
+      const int r = e / (kJR / 2), f = 2 * (e - r * (kJR / 2));
+      const double2 t = src[e];
+      stage[r * kStageLd + f] = t.x;
+      stage[r * kStageLd + f + 1] = t.y;
+    }
+    __syncthreads();
+    const int o = base + threadIdx.x;
+    if (o < P.no) {
+      const int c = P.obs_cam[o], p = P.obs_pt[o];
+      const double* j = stage + threadIdx.x * kStageLd;
+      const double* cr = tbl + c * kCandRec;
+      double jd0 = 0.0, jd1 = 0.0;
+#pragma unroll
+      for (int a2 = 0; a2 < 6; ++a2) { jd0 += j[a2] * cr[16 + a2]; jd1 += j[6 + a2] * cr[16 + a2]; }
+      const double dp0 = delta_p[3 * p], dp1 = delta_p[3 * p + 1], dp2 = delta_p[3 * p + 2];
+      jd0 += j[12] * dp0 + j[13] * dp1 + j[14] * dp2;
+      jd1 += j[15] * dp0 + j[16] * dp1 + j[17] * dp2;
+      acc[0] += jd0 * (j[18] + jd0 / 2.0) + jd1 * (j[19] + jd1 / 2.0);
+      const double X0 = pts_c[3 * p], X1 = pts_c[3 * p + 1], X2 = pts_c[3 * p + 2];
+      double pc[3];
+      if (!(P.cam_fixed && P.cam_fixed[c])) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pc[i] = cr[i] * X0 + cr[3 + i] * X1 + cr[6 + i] * X2 + cr[9 + i];
+      } else {
+        double ph[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ph[i] = X0 * cr[i] + X1 * cr[4 + i] + X2 * cr[8 + i] + cr[12 + i];
+        pc[0] = ph[0] / ph[3]; pc[1] = ph[1] / ph[3]; pc[2] = ph[2] / ph[3];
+      }
+      const float* Kc = ktb + c * 9;
+      double q[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) q[i] = pc[0] * (double)Kc[i] + pc[1] * (double)Kc[3 + i] + pc[2] * (double)Kc[6 + i];
+      const float2 uv = P.uv[o];
+      const double rc0 = q[0] / q[2] - (double)uv.x, rc1 = q[1] / q[2] - (double)uv.y;
+      double sc;
+      acc[1] += 0.5 * huber(rc0 * rc0 + rc1 * rc1, P.huber_a, P.huber_b, &sc);
+      if (!isfinite(rc0) || !isfinite(rc1)) acc[2] += 1.0;
+    }
+  }
+  double out[3];
+  block_sum<3>(acc, lds, out);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_MCC_NEG)[blockIdx.x] = out[0];
+    part_of(part, SL_CCOST)[blockIdx.x] = out[1];
+    part_of(part, SL_CAND_BAD)[blockIdx.x] = out[2];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // diagonal Schur blocks and rhs (local part): one workgroup per camera
 //   S_cc = -sum W W^T (lower 21) ; b_c = -sum W u_p
@@ -769,7 +936,25 @@ void launch_cam_prep(const DevProblem& P, const double* cams, double* rec, bool 
   hipLaunchKernelGGL(k_cam_prep, dim3((P.nc + 255) / 256), dim3(256), 0, s, P.nc, cams, P.K, P.cam_fixed, P.extr,
                      rec, deriv ? 1 : 0);
 }
+// one 512-thread block per CU for the LDS-table kernels
+static int lds_grid(int n) {
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+      n_cu = 256;
+  }
+  int g = (n + kLinLdsThreads - 1) / kLinLdsThreads;
+  return g < 1 ? 1 : (g > n_cu ? n_cu : g);
+}
+
 void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  if (P.nc <= kLinLdsCams) {
+    const int g = lds_grid(P.no);
+    hipLaunchKernelGGL(k_linearize_lds, dim3(g), dim3(kLinLdsThreads), 0, s, P, W.rec, W.pts, W.JR, W.part);
+    return;
+  }
   hipLaunchKernelGGL(k_linearize, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.rec, W.pts, W.JR, W.part);
 }
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
@@ -813,6 +998,12 @@ void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) 
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
   hipLaunchKernelGGL(k_backsub, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p, W.W, W.u,
                      W.Linv, W.y, W.scale_p, W.part);
+  if (P.nc <= kLinLdsCams) {
+    const int g = lds_grid(P.no);
+    hipLaunchKernelGGL(k_candidate_lds, dim3(g), dim3(kLinLdsThreads), 0, s, P, W.JR, W.delta_c, W.delta_p, W.rec_c,
+                       W.pts_c, W.part);
+    return;
+  }
   hipLaunchKernelGGL(k_candidate, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.JR, W.delta_c, W.delta_p,
                      W.rec_c, W.pts_c, W.part);
 }

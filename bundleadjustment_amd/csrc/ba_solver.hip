@@ -111,7 +111,7 @@ struct ba_ctx {
   }
 
   void allreduce(double* d, size_t count, ncclRedOp_t op = ncclSum) {
-    if (nranks <= 1 || count == 0) return;
+    if (!comm || count == 0) return;   // a 1-rank communicator still runs the collectives (tests)
     NCCL_OK(ncclAllReduce(d, d, count, ncclDouble, op, comm, stream));
   }
   void read_scalars() {
@@ -169,6 +169,16 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
     const int c = pb->obs_cam[o], p = pb->obs_pt[o];
     if (!ctx->cam_fixed_h[c]) cam_used[c] = 1;
     if (!pt_fixed[p]) pt_var[p] = 1;
+  }
+  if (ctx->comm && ctx->nranks > 1 && nc > 0) {
+    // the reduced system spans the union of the ranks' observed cameras
+    uint8_t* d = nullptr;
+    HIP_OK(hipMalloc(&d, nc));
+    HIP_OK(hipMemcpyAsync(d, cam_used.data(), nc, hipMemcpyHostToDevice, ctx->stream));
+    NCCL_OK(ncclAllReduce(d, d, nc, ncclUint8, ncclMax, ctx->comm, ctx->stream));
+    HIP_OK(hipMemcpyAsync(cam_used.data(), d, nc, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(d);
   }
   ctx->cam_of_vc.clear();
   for (int c = 0; c < nc; ++c)
@@ -589,11 +599,28 @@ int ba_comm_init(ba_ctx* ctx, const char id[128], int nranks, int rank) {
     if (ctx->comm) { ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
     ctx->nranks = nranks;
     ctx->rank = rank;
-    if (nranks > 1) {
-      ncclUniqueId uid;
-      std::memcpy(&uid, id, 128);
-      NCCL_OK(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
-    }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    NCCL_OK(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
+  });
+}
+
+int ba_comm_allreduce_host(ba_ctx* ctx, double* values, int n, int op) {
+  if (!ctx || n < 0 || (n > 0 && !values) || (op != 0 && op != 1)) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] {
+    if (!ctx->comm) return;
+    HIP_OK(hipSetDevice(ctx->device));
+    const int m = n > 0 ? n : 1;
+    double* d = nullptr;
+    HIP_OK(hipMalloc(&d, sizeof(double) * m));
+    std::vector<double> h(m, 0.0);
+    if (n > 0) std::memcpy(h.data(), values, sizeof(double) * n);
+    HIP_OK(hipMemcpyAsync(d, h.data(), sizeof(double) * m, hipMemcpyHostToDevice, ctx->stream));
+    NCCL_OK(ncclAllReduce(d, d, m, ncclDouble, op == 0 ? ncclSum : ncclMax, ctx->comm, ctx->stream));
+    HIP_OK(hipMemcpyAsync(h.data(), d, sizeof(double) * m, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(d);
+    if (n > 0) std::memcpy(values, h.data(), sizeof(double) * n);
   });
 }
 

@@ -113,6 +113,17 @@ class Solver:
         assert len(uid) == 128
         self._check(self.lib.ba_comm_init(self.h, C.c_char_p(uid), int(nranks), int(rank)), "ba_comm_init")
 
+    def allreduce_host(self, values, op: str = "sum") -> np.ndarray:
+        """In-place RCCL reduction of a few host doubles across ranks (identity
+        without a communicator)."""
+        v = np.ascontiguousarray(values, dtype=np.float64).copy()
+        self._check(self.lib.ba_comm_allreduce_host(self.h, _ptr(v), int(v.size), 0 if op == "sum" else 1),
+                    "ba_comm_allreduce_host")
+        return v
+
+    def barrier(self):
+        self._check(self.lib.ba_comm_allreduce_host(self.h, None, 0, 0), "ba_comm_allreduce_host")
+
     # -- problem ----------------------------------------------------------
     def set_problem(self, problem: Problem):
         p = problem.normalized()

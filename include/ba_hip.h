@@ -147,6 +147,13 @@ const char* ba_last_error(const ba_ctx* ctx);
 int ba_comm_unique_id(char id[128]);
 int ba_comm_init(ba_ctx* ctx, const char id[128], int nranks, int rank);
 
+/* Host-visible collective over the context's communicator (RCCL): in-place
+ * reduction of n doubles across ranks (op 0 = sum, 1 = max); blocks until the
+ * result is on the host.  With n = 0 it is a barrier.  Without a
+ * communicator it is the identity.  Used for the bench's max-over-ranks
+ * timing, so no second GPU runtime is needed for host-side rendezvous. */
+int ba_comm_allreduce_host(ba_ctx* ctx, double* values, int n, int op);
+
 /* Copy a problem to the device and build its (fixed) structure. */
 int ba_set_problem(ba_ctx* ctx, const ba_problem* problem);
 

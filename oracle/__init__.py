@@ -70,6 +70,10 @@ def lib():
         L.oracle_bench.argtypes = [C.POINTER(_Problem), C.c_int, C.c_double]
         L.oracle_max_threads.restype = C.c_int
         L.oracle_prune.argtypes = [C.c_int] + [C.c_void_p] * 9
+        L.oracle_camera_colnorm2.argtypes = [C.POINTER(_Problem), C.c_void_p]
+        L.oracle_reduced_system.restype = C.c_int
+        L.oracle_reduced_system.argtypes = [C.POINTER(_Problem), C.c_void_p, C.c_double, C.c_int, C.c_void_p,
+                                            C.c_void_p]
         _lib = L
     return _lib
 
@@ -184,3 +188,28 @@ def prune(extr, cam_center, K, obs_cam, obs_X, obs_uv, obs_inv_sigma, obs_dist):
     out = np.empty(oc.size, np.uint8)
     lib().oracle_prune(int(oc.size), *[_p(a) for a in f32], _p(oc), *[_p(a) for a in o32], _p(out))
     return out
+
+
+def camera_colnorm2(problem):
+    """Camera column norms^2 of the corrected jacobian [n_cams, 6] (additive
+    over point shards)."""
+    cams, pts = problem.cams.copy(), problem.pts.copy()
+    s = _make(problem, cams, pts)
+    out = np.zeros((problem.n_cams, 6))
+    lib().oracle_camera_colnorm2(C.byref(s), _p(out))
+    return out
+
+
+def reduced_system(problem, radius=1e4, cam_colnorm2=None, add_cam_D=True):
+    """Reduced camera system (lower triangle, rhs) of one LM step at iteration-0
+    scaling; cam_colnorm2: global camera column norms for a point shard."""
+    cams, pts = problem.cams.copy(), problem.pts.copy()
+    s = _make(problem, cams, pts)
+    nmax = 6 * problem.n_cams
+    lhs = np.zeros((nmax, nmax))
+    rhs = np.zeros(nmax)
+    cn = None if cam_colnorm2 is None else np.ascontiguousarray(cam_colnorm2, dtype=np.float64)
+    n = lib().oracle_reduced_system(C.byref(s), _p(cn), float(radius), int(bool(add_cam_D)), _p(lhs), _p(rhs))
+    if n < 0:
+        raise RuntimeError("oracle_reduced_system failed")
+    return lhs.reshape(-1)[: n * n].reshape(n, n).copy(), rhs[:n].copy()

@@ -497,12 +497,17 @@ struct Schur {
   int nf = 0;
 };
 
-static bool dense_schur_solve(const Problem& P, const Schur& S, const std::vector<Lin>& L,
-                              const std::vector<double>& s, const std::vector<double>& D,
-                              std::vector<double>& y) {
+// Reduced camera system (lower triangle of lhs, rhs) of the scaled, damped
+// normal equations; the point blocks' inverses and gradients are returned
+// for the back substitution.  add_cam_D = false leaves out the camera LM
+// diagonal (a point shard's contribution in the distributed test: the
+// system is a sum over point shards plus the camera diagonal once).
+static bool assemble_schur(const Problem& P, const Schur& S, const std::vector<Lin>& L, const std::vector<double>& s,
+                           const std::vector<double>& D, bool add_cam_D, std::vector<double>& lhs,
+                           std::vector<double>& rhs, std::vector<double>& ete_inv, std::vector<double>& ge) {
   const int nf = S.nf, n = 6 * nf;
-  y.assign(P.ncols, 0.0);
-  std::vector<double> lhs((size_t)n * n, 0.0), rhs(n, 0.0);
+  lhs.assign((size_t)n * n, 0.0);
+  rhs.assign(n, 0.0);
   auto scJc = [&](int o, double* Jc) {  // scaled camera jacobian 2x6
     const int cc = P.cam_col[P.obs_cam[o]];
     for (int i = 0; i < 2; ++i) for (int k = 0; k < 6; ++k) Jc[i * 6 + k] = L[o].Jc[i * 6 + k] * s[cc + k];
@@ -511,7 +516,6 @@ static bool dense_schur_solve(const Problem& P, const Schur& S, const std::vecto
     const int pc = P.pt_col[P.obs_pt[o]];
     for (int i = 0; i < 2; ++i) for (int k = 0; k < 3; ++k) Jp[i * 3 + k] = L[o].Jp[i * 3 + k] * s[pc + k];
   };
-  const bool has_cam = nf > 0;
   // F^T F + D_f^2 and F^T r over all residuals that touch a variable camera
   for (int o = 0; o < P.no; ++o) {
     const int t = P.type[o];
@@ -525,13 +529,15 @@ static bool dense_schur_solve(const Problem& P, const Schur& S, const std::vecto
         lhs[(size_t)(6 * f + a) * n + 6 * f + b] += Jc[a] * Jc[b] + Jc[6 + a] * Jc[6 + b];
     }
   }
-  for (int c : P.var_cams) {
-    const int f = S.fidx[c], cc = P.cam_col[c];
-    for (int a = 0; a < 6; ++a) lhs[(size_t)(6 * f + a) * n + 6 * f + a] += D[cc + a] * D[cc + a];
-  }
+  if (add_cam_D)
+    for (int c : P.var_cams) {
+      const int f = S.fidx[c], cc = P.cam_col[c];
+      for (int a = 0; a < 6; ++a) lhs[(size_t)(6 * f + a) * n + 6 * f + a] += D[cc + a] * D[cc + a];
+    }
   // eliminate points
   const int npv = (int)P.var_pts.size();
-  std::vector<double> ete_inv((size_t)npv * 9), ge((size_t)npv * 3);
+  ete_inv.assign((size_t)npv * 9, 0.0);
+  ge.assign((size_t)npv * 3, 0.0);
   bool ok = true;
   int nthreads = 1;
 #ifdef _OPENMP
@@ -616,6 +622,26 @@ static bool dense_schur_solve(const Problem& P, const Schur& S, const std::vecto
     for (size_t i = 0; i < lhs.size(); ++i) lhs[i] += acc_l[t][i];
     for (int i = 0; i < n; ++i) rhs[i] += acc_r[t][i];
   }
+  return true;
+}
+
+static bool dense_schur_solve(const Problem& P, const Schur& S, const std::vector<Lin>& L,
+                              const std::vector<double>& s, const std::vector<double>& D,
+                              std::vector<double>& y) {
+  const int nf = S.nf, n = 6 * nf;
+  y.assign(P.ncols, 0.0);
+  std::vector<double> lhs, rhs, ete_inv, ge;
+  if (!assemble_schur(P, S, L, s, D, true, lhs, rhs, ete_inv, ge)) return false;
+  const int npv = (int)P.var_pts.size();
+  const bool has_cam = nf > 0;
+  auto scJc = [&](int o, double* Jc) {
+    const int cc = P.cam_col[P.obs_cam[o]];
+    for (int i = 0; i < 2; ++i) for (int k = 0; k < 6; ++k) Jc[i * 6 + k] = L[o].Jc[i * 6 + k] * s[cc + k];
+  };
+  auto scJp = [&](int o, double* Jp) {
+    const int pc = P.pt_col[P.obs_pt[o]];
+    for (int i = 0; i < 2; ++i) for (int k = 0; k < 3; ++k) Jp[i * 3 + k] = L[o].Jp[i * 3 + k] * s[pc + k];
+  };
   std::vector<double> yf(rhs);
   if (has_cam) {
     if (!cholesky(lhs, n)) return false;
@@ -1034,6 +1060,59 @@ void oracle_prune(int n_obs, const float* extr, const float* center, const float
     const float thresh = 5.991;
     result[o] = chi > thresh ? 3 : 0;
   }
+}
+
+// Column norms^2 of the (corrected) camera jacobian, [6*n_cams] (zero for
+// constant / unobserved cameras).  Additive over point shards.
+void oracle_camera_colnorm2(const oracle_problem* prob, double* out) {
+  oracle::Problem P = to_problem(prob);
+  oracle::build_structure(P);
+  std::vector<double> x, g, cn;
+  oracle::gather_x(P, x);
+  std::vector<oracle::Lin> L;
+  double cost;
+  oracle::eval_lin(P, x, L, &cost);
+  oracle::gradient_colnorm(P, L, g, cn);
+  for (int c = 0; c < P.nc; ++c)
+    for (int k = 0; k < 6; ++k) out[6 * c + k] = P.cam_col[c] >= 0 ? cn[P.cam_col[c] + k] : 0.0;
+}
+
+// Reduced camera system of one LM step at `radius` (Jacobi scaling and LM
+// diagonal as at iteration 0).  cam_colnorm2 [6*n_cams]: the camera column
+// norms to scale with (the global ones for a point shard; NULL = this
+// problem's own).  add_cam_D: add the camera LM diagonal (once over shards).
+// lhs: [n*n] row-major, lower triangle; rhs: [n].  Returns n = 6 x variable
+// cameras, or -1 on failure.  The distributed test checks that the sum over
+// point shards equals the unsharded system: the property the RCCL path uses.
+int oracle_reduced_system(const oracle_problem* prob, const double* cam_colnorm2, double radius, int add_cam_D,
+                          double* lhs_out, double* rhs_out) {
+  oracle::Problem P = to_problem(prob);
+  oracle::build_structure(P);
+  std::vector<double> x, g, cn;
+  oracle::gather_x(P, x);
+  std::vector<oracle::Lin> L;
+  double cost;
+  if (!oracle::eval_lin(P, x, L, &cost)) return -1;
+  oracle::gradient_colnorm(P, L, g, cn);
+  if (cam_colnorm2)
+    for (int c = 0; c < P.nc; ++c)
+      if (P.cam_col[c] >= 0)
+        for (int k = 0; k < 6; ++k) cn[P.cam_col[c] + k] = cam_colnorm2[6 * c + k];
+  const int ncol = P.ncols;
+  std::vector<double> s(ncol), D(ncol);
+  for (int i = 0; i < ncol; ++i) {
+    s[i] = 1.0 / (1.0 + std::sqrt(cn[i]));
+    const double d = std::min(std::max(cn[i] * s[i] * s[i], 1e-6), 1e32);
+    D[i] = std::sqrt(d / radius);
+  }
+  oracle::Schur S;
+  oracle::prepare_schur(P, S);
+  std::vector<double> lhs, rhs, ete_inv, ge;
+  if (!oracle::assemble_schur(P, S, L, s, D, add_cam_D != 0, lhs, rhs, ete_inv, ge)) return -1;
+  const int n = 6 * S.nf;
+  std::copy(lhs.begin(), lhs.end(), lhs_out);
+  std::copy(rhs.begin(), rhs.end(), rhs_out);
+  return n;
 }
 
 void oracle_default_options(oracle::Options* o) {

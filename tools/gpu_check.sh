@@ -23,6 +23,10 @@ rc=$?; tail -5 $OUT/smoke.log; stop_on_fault $rc
 echo "== bench"
 timeout -k 10 600 python3 -u bench.py --steps "$STEPS" --warmup 3 > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; cat $OUT/bench.json; tail -5 $OUT/bench.err; stop_on_fault $rc
+echo "== bench through torch.distributed.run with an RCCL communicator (1 rank)"
+timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+  --master-port 29533 bench.py --gpus 1 --steps 5 --warmup 1 --comm --no-cpu-baseline > $OUT/bench_comm.json 2> $OUT/bench_comm.err
+rc=$?; cat $OUT/bench_comm.json; tail -3 $OUT/bench_comm.err; stop_on_fault $rc
 echo "== rocprofv3 kernel trace"
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \

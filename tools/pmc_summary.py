@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic from rocprofv3 PMC passes (tools/pmc_linearize.sh).
+
+FETCH_SIZE and WRITE_SIZE come from separate passes (they do not fit one
+pass on gfx950).  Both are reported by rocprofv3 in KiB per dispatch;
+FETCH_SIZE is doubled per MI355X_MICROARCH.md (on gfx950 it reports half the
+bytes of wide streaming reads).  Writes profiles/pmc_<config>.json, which
+bench.py reads for roofline.traffic.
+
+usage: tools/pmc_summary.py <pmc_FETCH_SIZE dir> <pmc_WRITE_SIZE dir> <out.json> [algorithmic_bytes]
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+
+def per_kernel(d: Path, counter: str):
+    vals = defaultdict(list)
+    for f in d.rglob("*counter_collection.csv"):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] == counter:
+                    vals[row["Kernel_Name"]].append(float(row["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+
+
+def main():
+    fdir, wdir, out = Path(sys.argv[1]), Path(sys.argv[2]), Path(sys.argv[3])
+    algo = float(sys.argv[4]) if len(sys.argv) > 4 else None
+    fetch, nf = per_kernel(fdir, "FETCH_SIZE")
+    write, nw = per_kernel(wdir, "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fetch) | set(write)):
+        short = k.split("(")[0].replace("bahip::", "").strip()
+        fb = 2.0 * fetch.get(k, 0.0)
+        wb = write.get(k, 0.0)
+        res[short] = {"fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+                      "hbm_bytes_per_launch": fb + wb, "dispatches": [nf.get(k, 0), nw.get(k, 0)]}
+    res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes of `bench.py --steps 3`; "
+                    "FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md); KiB -> bytes")
+    if algo and "k_linearize" in res:
+        res["k_linearize"]["algorithmic_bytes"] = algo
+        res["k_linearize"]["traffic_over_algorithmic"] = res["k_linearize"]["hbm_bytes_per_launch"] / algo
+    out.write_text(json.dumps(res, indent=1))
+    for k, v in res.items():
+        if not k.startswith("_"):
+            print(f"{k:32s} fetch {v['fetch_bytes_per_launch'] / 1e6:9.2f} MB  write {v['write_bytes_per_launch'] / 1e6:9.2f} MB")
+
+
+if __name__ == "__main__":
+    main()
