@@ -9,6 +9,7 @@ namespace bahip {
 
 constexpr int kThreads = 256;
 constexpr int kMaxBlocks = 2048;        // grid cap of the streaming kernels
+constexpr int kCamSplit = 8;            // workgroups per camera in k_cam_schur_diag
 
 // Scalar reduction slots (device buffer d_scal[kNumSlots]).
 enum Slot {
@@ -67,6 +68,7 @@ struct DevWork {
   double* Vbuf;                      // [ceil(n/64)][64][64] inverses of the diagonal Cholesky blocks
   const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}
   const int2* pairs;                 // observation pairs per block
+  double* cpart;                     // [kCamSplit][nvc][27] per-slice camera sums
   double* part;                      // [kNumSlots][kMaxBlocks]
   double* scal;                      // [kNumSlots]
 };

@@ -72,6 +72,54 @@ __device__ inline double block_max1(double v, double* lds) {
 
 __device__ inline double* part_of(double* part, int slot) { return part + (size_t)slot * kMaxBlocks; }
 
+// Per-camera work is split over kCamSplit workgroups (one workgroup per
+// camera leaves CUs idle and is latency bound).  Each slice stores its 27
+// block sums; a second kernel adds the slices in slice order (deterministic;
+// the kernel boundary makes the slices visible across XCDs — an in-kernel
+// last-block fold needs agent-scope release fences, which write back the L2
+// and measured 2x slower).
+__device__ inline void cam_slice_store(const double (&tot)[27], double* __restrict__ cpart, int v, int nvc) {
+  if (threadIdx.x == 0) {
+    double* dst = cpart + ((size_t)blockIdx.y * nvc + v) * 27;
+#pragma unroll
+    for (int k = 0; k < 27; ++k) dst[k] = tot[k];
+  }
+}
+
+// fold the slices: mode 0 -> Hcc (21) / gc (6); mode 1 -> S diagonal block
+// (-sum W W^T, lower) and rhs row (-sum W u)
+__global__ __launch_bounds__(256) void k_cam_fold(DevProblem P, const double* __restrict__ cpart, int mode,
+                                                  double* __restrict__ Hcc, double* __restrict__ gc,
+                                                  double* __restrict__ S) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.nvc * 27) return;
+  const int v = e / 27, k = e - v * 27;
+  double acc = 0.0;
+  for (int sl = 0; sl < kCamSplit; ++sl) acc += cpart[((size_t)sl * P.nvc + v) * 27 + k];
+  if (mode == 0) {
+    if (k < 21) Hcc[(size_t)v * 21 + k] = acc;
+    else gc[(size_t)v * 6 + (k - 21)] = acc;
+  } else {
+    const size_t ld = (size_t)P.ld;
+    if (k < 21) {
+      int a2 = 0;
+      while ((a2 + 1) * (a2 + 2) / 2 <= k) ++a2;
+      const int b2 = k - a2 * (a2 + 1) / 2;
+      S[(size_t)(6 * v + a2) * ld + 6 * v + b2] = -acc;
+    } else {
+      S[(size_t)P.n * ld + 6 * v + (k - 21)] = -acc;
+    }
+  }
+}
+
+// observation range of slice blockIdx.y of camera v
+__device__ inline void cam_slice(const DevProblem& P, int v, int& i0, int& i1) {
+  const int a = P.cam_off[v], b = P.cam_off[v + 1];
+  const int len = (b - a + kCamSplit - 1) / kCamSplit;
+  i0 = min(b, a + (int)blockIdx.y * len);
+  i1 = min(b, i0 + len);
+}
+
 // ---------------------------------------------------------------------------
 // camera records: R, dR/dw (forward derivative of ceres' Rodrigues), t, K
 // ---------------------------------------------------------------------------
@@ -364,6 +412,8 @@ __global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const doub
 // camera blocks: one workgroup per active variable camera, Hcc (21, lower
 // row-major) and gc (6), gathering its observations' records.
 // ---------------------------------------------------------------------------
+// (one workgroup per camera: splitting it measured slower — the pass is
+// bound by the gathered record reads, 256 B fetched per 112 B used)
 __global__ __launch_bounds__(256) void k_cam_assemble(DevProblem P, const double* __restrict__ JR,
                                                       double* __restrict__ Hcc, double* __restrict__ gc) {
   __shared__ double lds[27 * 16];
@@ -711,14 +761,16 @@ __global__ __launch_bounds__(kLinLdsThreads) void k_candidate_lds(DevProblem P, 
 //   S_cc = -sum W W^T (lower 21) ; b_c = -sum W u_p
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const double* __restrict__ W,
-                                                        const double* __restrict__ u, double* __restrict__ S) {
+                                                        const double* __restrict__ u, double* __restrict__ S,
+                                                        double* __restrict__ cpart) {
   __shared__ double lds[27 * 16];
   const int v = blockIdx.x;
   const size_t np = (size_t)P.np;
   double acc[27];
 #pragma unroll
   for (int k = 0; k < 27; ++k) acc[k] = 0.0;
-  const int i0 = P.cam_off[v], i1 = P.cam_off[v + 1];
+  int i0, i1;
+  cam_slice(P, v, i0, i1);
   for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int o = P.cam_obs[i];
     const int p = P.obs_pt[o];
@@ -737,15 +789,9 @@ __global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const doub
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[21 + a] += w[a * 3] * u0 + w[a * 3 + 1] * u1 + w[a * 3 + 2] * u2;
   }
-  double out[27];
-  block_sum<27>(acc, lds, out);
-  if (threadIdx.x == 0) {
-    const size_t ld = (size_t)P.ld;
-    int t = 0;
-    for (int a = 0; a < 6; ++a)
-      for (int b = 0; b <= a; ++b) S[(size_t)(6 * v + a) * ld + 6 * v + b] = -out[t++];
-    for (int a = 0; a < 6; ++a) S[(size_t)P.n * ld + 6 * v + a] = -out[21 + a];
-  }
+  double tot[27];
+  block_sum<27>(acc, lds, tot);
+  cam_slice_store(tot, cpart, v, P.nvc);
 }
 
 // ---------------------------------------------------------------------------
@@ -977,7 +1023,8 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
 }
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
-  hipLaunchKernelGGL(k_cam_schur_diag, dim3(P.nvc), dim3(kThreads), 0, s, P, W.W, W.u, W.S);
+  hipLaunchKernelGGL(k_cam_schur_diag, dim3(P.nvc, kCamSplit), dim3(kThreads), 0, s, P, W.W, W.u, W.S, W.cpart);
+  hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, 1, W.Hcc, W.gc, W.S);
 }
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (W.nblocks == 0) return;

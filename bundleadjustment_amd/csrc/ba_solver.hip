@@ -297,6 +297,8 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.pairs = ctx->upload(pairs);
   W.part = ctx->dalloc<double>((size_t)kNumSlots * kMaxBlocks);
   W.scal = ctx->dalloc<double>(kNumSlots);
+  W.cpart = ctx->dalloc<double>((size_t)kCamSplit * 27 * std::max(nvc, 1));
+
   HIP_OK(hipMemsetAsync(W.part, 0, sizeof(double) * kNumSlots * kMaxBlocks, ctx->stream));
   HIP_OK(hipMemsetAsync(W.scal, 0, sizeof(double) * kNumSlots, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
