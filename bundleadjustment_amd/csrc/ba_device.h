@@ -21,8 +21,14 @@ namespace bahip {
 //   [0..8]  R (col-major)       [9..35] dR/dw_k (k-major, col-major each)
 //   [36..38] t                  [39..47] K (col-major, double of float)
 // Fixed camera: [0..15] E (col-major 4x4, double of float), [39..47] K.
-constexpr int kCamRec = 48;
-constexpr int kRecR = 0, kRecdR = 9, kRecT = 36, kRecK = 39;
+// Linearisation table (written with the derivatives, [48..87]): K folded
+// into the camera so the per-observation chain rule is 36 FMA shorter:
+//   variable: [0..8] K R  [9..35] K dR/dw_k  [36..38] K t      (col-major)
+//   fixed:    [0..11] K E(0:3, 0:4)  [12..15] E(3, 0:4)
+// (re-association of the Jet products K (R X + t): differs by rounding only)
+constexpr int kCamRec = 88;
+constexpr int kRecR = 0, kRecdR = 9, kRecT = 36, kRecK = 39, kRecL = 48, kLin = 40;
+constexpr int kLinKR = 0, kLinKdR = 9, kLinKt = 36, kLinKE = 0, kLinE3 = 12;
 
 struct D3 {  // value + 3 partial derivatives (d/dw0, d/dw1, d/dw2)
   double a, d[3];

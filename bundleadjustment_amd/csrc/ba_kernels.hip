@@ -123,31 +123,63 @@ __device__ inline void cam_slice(const DevProblem& P, int v, int& i0, int& i1) {
 // ---------------------------------------------------------------------------
 // camera records: R, dR/dw (forward derivative of ceres' Rodrigues), t, K
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_cam_prep(int nc, const double* __restrict__ cams, const float* __restrict__ K,
-                                                  const uint8_t* __restrict__ cam_fixed, const float* __restrict__ extr,
-                                                  double* __restrict__ rec, int deriv) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// One 64-lane block per camera; every lane evaluates the (cheap) Rodrigues
+// duals and writes the record entries e = lane, lane + 64 (short critical
+// path: a thread per camera serialises ~90 dependent stores).
+__device__ inline double cam_rec_entry(int e, const double* w, const double* t, const double* Kd, const D3* R,
+                                       const double* R0, bool deriv) {
+  if (e < 9) return deriv ? R[e].a : R0[e];
+  if (e < 36) { const int k = (e - 9) / 9, i = (e - 9) % 9; return deriv ? R[i].d[k] : 0.0; }
+  if (e < 39) return t[e - 36];
+  if (e < 48) return Kd[e - 39];
+  if (!deriv) return 0.0;
+  const int l = e - kRecL;
+  if (l < 36) {   // K M, M = R or dR/dw_k, col-major
+    const int m = l / 9, idx = l % 9, col = idx / 3, row = idx % 3;
+    double M0, M1, M2;
+    if (m == 0) { M0 = R[col * 3].a; M1 = R[col * 3 + 1].a; M2 = R[col * 3 + 2].a; }
+    else { M0 = R[col * 3].d[m - 1]; M1 = R[col * 3 + 1].d[m - 1]; M2 = R[col * 3 + 2].d[m - 1]; }
+    return Kd[row] * M0 + Kd[3 + row] * M1 + Kd[6 + row] * M2;
+  }
+  if (l < 39) { const int row = l - 36; return Kd[row] * t[0] + Kd[3 + row] * t[1] + Kd[6 + row] * t[2]; }
+  return 0.0;
+}
+
+__global__ __launch_bounds__(64) void k_cam_prep(int nc, const double* __restrict__ cams, const float* __restrict__ K,
+                                                 const uint8_t* __restrict__ cam_fixed, const float* __restrict__ extr,
+                                                 double* __restrict__ rec, int deriv) {
+  const int c = blockIdx.x, lane = threadIdx.x;
   if (c >= nc) return;
   double* o = rec + (size_t)c * kCamRec;
-  for (int k = 0; k < 9; ++k) o[kRecK + k] = (double)K[9 * c + k];
+  double Kd[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Kd[k] = (double)K[9 * c + k];
   if (cam_fixed && cam_fixed[c]) {
-    for (int k = 0; k < 16; ++k) o[k] = (double)extr[16 * c + k];
+    const float* E = extr + 16 * c;
+    for (int e = lane; e < kCamRec; e += 64) {
+      double v = 0.0;
+      if (e < 16) v = (double)E[e];
+      else if (e >= kRecK && e < kRecK + 9) v = Kd[e - kRecK];
+      else if (deriv && e >= kRecL) {
+        const int l = e - kRecL;
+        if (l < 12) {   // K E(0:3, col)
+          const int col = l / 3, row = l % 3;
+          v = Kd[row] * (double)E[col * 4] + Kd[3 + row] * (double)E[col * 4 + 1] + Kd[6 + row] * (double)E[col * 4 + 2];
+        } else if (l < 16) {
+          v = (double)E[(l - 12) * 4 + 3];
+        }
+      }
+      o[e] = v;
+    }
     return;
   }
   const double w[3] = {cams[6 * c], cams[6 * c + 1], cams[6 * c + 2]};
-  if (deriv) {
-    D3 R[9];
-    angle_axis_to_R_d3(w, R);
-    for (int i = 0; i < 9; ++i) {
-      o[kRecR + i] = R[i].a;
-      for (int k = 0; k < 3; ++k) o[kRecdR + k * 9 + i] = R[i].d[k];
-    }
-  } else {
-    double R[9];
-    angle_axis_to_R(w, R);
-    for (int i = 0; i < 9; ++i) o[kRecR + i] = R[i];
-  }
-  for (int k = 0; k < 3; ++k) o[kRecT + k] = cams[6 * c + 3 + k];
+  const double t[3] = {cams[6 * c + 3], cams[6 * c + 4], cams[6 * c + 5]};
+  D3 R[9];
+  double R0[9];
+  if (deriv) angle_axis_to_R_d3(w, R);
+  else angle_axis_to_R(w, R0);
+  for (int e = lane; e < kCamRec; e += 64) o[e] = cam_rec_entry(e, w, t, Kd, R, R0, deriv != 0);
 }
 
 // Project one observation; value only.  Returns residual (u,v) in r.
@@ -185,113 +217,276 @@ constexpr int kStageLd = kJR + 1;   // LDS row stride of staged records
 // ---------------------------------------------------------------------------
 // linearisation: one thread per observation (sorted by point)
 // ---------------------------------------------------------------------------
-// Camera record access: R, dR/dw, t as doubles and K (float-valued) — either
-// the global 48-double records or the block's LDS copy of the camera table.
+// Camera access for the linearisation: the K-folded table (kRecL, 40
+// doubles, read as 20 16-B loads) and K (float-valued) — either the global
+// records or the block's LDS copy of the camera table.
 struct CamGlobal {
   const double* r;
-  __device__ double R(int k) const { return r[kRecR + k]; }
-  __device__ double dR(int k) const { return r[kRecdR + k]; }
-  __device__ double T(int k) const { return r[kRecT + k]; }
-  __device__ double E(int k) const { return r[k]; }       // fixed camera: 4x4 extrinsic
+  bool v;
+  __device__ bool var() const { return v; }
+  __device__ void load(double (&t)[kLin]) const {
+    const double2* s = reinterpret_cast<const double2*>(r + kRecL);
+#pragma unroll
+    for (int k = 0; k < kLin / 2; ++k) { const double2 u = s[k]; t[2 * k] = u.x; t[2 * k + 1] = u.y; }
+  }
   __device__ double K(int k) const { return r[kRecK + k]; }
 };
-constexpr int kTblRec = 39;   // LDS camera row: R (9), dR (27), t (3) / 4x4 extrinsic (16)
+// LDS row: lin table (40) + variable flag (slot 40) + pad; stride 42 doubles
+// keeps rows 16-B aligned and spreads random cameras over the 16 bank
+// groups of ds_read_b128
+constexpr int kTblRec = kLin + 2;
 struct CamLds {
   const double* r;
   const float* k;
-  __device__ double R(int i) const { return r[kRecR + i]; }
-  __device__ double dR(int i) const { return r[kRecdR + i]; }
-  __device__ double T(int i) const { return r[kRecT + i]; }
-  __device__ double E(int i) const { return r[i]; }
+  __device__ bool var() const { return r[kLin] != 0.0; }
+  __device__ void load(double (&t)[kLin]) const {
+    const double2* s = reinterpret_cast<const double2*>(r);
+#pragma unroll
+    for (int k = 0; k < kLin / 2; ++k) { const double2 u = s[k]; t[2 * k] = u.x; t[2 * k + 1] = u.y; }
+  }
+  __device__ double K(int i) const { return (double)k[i]; }
+};
+// same rows, read element-wise where used (the compiler schedules and pairs
+// the LDS reads; fewer live registers than the 40-double preload)
+struct CamLdsLazy {
+  const double* r;
+  const float* k;
+  struct Row {
+    const double* r;
+    __device__ double operator[](int i) const { return r[i]; }
+  };
+  __device__ bool var() const { return r[kLin] != 0.0; }
+  __device__ Row row() const { return Row{r}; }
   __device__ double K(int i) const { return (double)k[i]; }
 };
 
-// r, J (Huber-corrected) of one observation into out[20]; returns rho
+// camera row as an indexable value: a register copy (CamGlobal, CamLds) or
+// an LDS view (CamLdsLazy)
+struct RowRegs {
+  double t[kLin];
+  __device__ double operator[](int i) const { return t[i]; }
+};
+template <class Cam>
+__device__ inline RowRegs cam_row(const Cam& cr) { RowRegs R; cr.load(R.t); return R; }
+__device__ inline CamLdsLazy::Row cam_row(const CamLdsLazy& cr) { return cr.row(); }
+
+// r, J (Huber-corrected) of one observation into out[20]; returns rho.
+// AngleReprojectionError (Optimizer.h:54-76) / PointOnlyReprojectionError
+// (Optimizer.h:96-107) with the chain rule of their Jets:
+//   q = K (R X + t),  dq/dw_k = K dR_k X,  dq/dt = K,  dq/dX = K R
+//   fixed: q = K E(0:3) [X;1] / w,  w = E(3) [X;1],  dq/dX = (K E - q e3) / w
+//   r = q01 / q2 - uv,  dr/d* = (dq01 - r' dq2) / q2,  Huber corrector sqrt(rho')
 template <class Cam>
 __device__ inline double lin_obs(const DevProblem& P, const Cam& cr, bool cvar, bool pvar, double X0, double X1,
                                  double X2, float2 uv, double (&out)[kJR], bool& fin) {
-  double pc[3], dp[3][9];
+  const auto T = cam_row(cr);
+  double q[3], iw = 1.0;
   if (cvar) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      pc[i] = cr.R(i) * X0 + cr.R(3 + i) * X1 + cr.R(6 + i) * X2 + cr.T(i);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) dp[i][k] = cr.dR(k * 9 + i) * X0 + cr.dR(k * 9 + 3 + i) * X1 + cr.dR(k * 9 + 6 + i) * X2;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) dp[i][3 + k] = (i == k) ? 1.0 : 0.0;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) dp[i][6 + k] = cr.R(k * 3 + i);
-    }
+    for (int i = 0; i < 3; ++i)
+      q[i] = T[kLinKR + i] * X0 + T[kLinKR + 3 + i] * X1 + T[kLinKR + 6 + i] * X2 + T[kLinKt + i];
   } else {
-    double ph[4];
+    const double wv = T[kLinE3] * X0 + T[kLinE3 + 1] * X1 + T[kLinE3 + 2] * X2 + T[kLinE3 + 3];
+    iw = 1.0 / wv;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ph[i] = X0 * cr.E(i) + X1 * cr.E(4 + i) + X2 * cr.E(8 + i) + cr.E(12 + i);
-    const double inv = 1.0 / ph[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      pc[i] = ph[i] * inv;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) dp[i][k] = 0.0;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) dp[i][6 + k] = (cr.E(k * 4 + i) - pc[i] * cr.E(k * 4 + 3)) * inv;
-    }
-  }
-  double q[3], dq[3][9];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    q[i] = pc[0] * cr.K(i) + pc[1] * cr.K(3 + i) + pc[2] * cr.K(6 + i);
-#pragma unroll
-    for (int k = 0; k < 9; ++k) dq[i][k] = dp[0][k] * cr.K(i) + dp[1][k] * cr.K(3 + i) + dp[2][k] * cr.K(6 + i);
+    for (int i = 0; i < 3; ++i)
+      q[i] = (T[kLinKE + i] * X0 + T[kLinKE + 3 + i] * X1 + T[kLinKE + 6 + i] * X2 + T[kLinKE + 9 + i]) * iw;
   }
   const double iq = 1.0 / q[2];
   const double pr0 = q[0] * iq, pr1 = q[1] * iq;
   const double r0 = pr0 - (double)uv.x, r1 = pr1 - (double)uv.y;
   double scale;
   const double rho = huber(r0 * r0 + r1 * r1, P.huber_a, P.huber_b, &scale);
-  fin = isfinite(r0) && isfinite(r1);
+  const double f = iq * scale;
+  fin = isfinite(r0) && isfinite(r1) && isfinite(f);
+  if (cvar) {
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const bool live = (k < 6) ? cvar : pvar;
-    const double j0 = live ? (dq[0][k] - pr0 * dq[2][k]) * iq * scale : 0.0;
-    const double j1 = live ? (dq[1][k] - pr1 * dq[2][k]) * iq * scale : 0.0;
-    fin = fin && isfinite(j0) && isfinite(j1);
-    if (k < 6) { out[k] = j0; out[6 + k] = j1; }
-    else { out[12 + k - 6] = j0; out[15 + k - 6] = j1; }
+    for (int k = 0; k < 3; ++k) {
+      const int b = kLinKdR + 9 * k;
+      const double d0 = T[b] * X0 + T[b + 3] * X1 + T[b + 6] * X2;
+      const double d1 = T[b + 1] * X0 + T[b + 4] * X1 + T[b + 7] * X2;
+      const double d2 = T[b + 2] * X0 + T[b + 5] * X1 + T[b + 8] * X2;
+      out[k] = (d0 - pr0 * d2) * f;
+      out[6 + k] = (d1 - pr1 * d2) * f;
+      const double k2 = cr.K(3 * k + 2);
+      out[3 + k] = (cr.K(3 * k) - pr0 * k2) * f;
+      out[9 + k] = (cr.K(3 * k + 1) - pr1 * k2) * f;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) out[k] = 0.0;
+  }
+  if (pvar) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double d0, d1, d2;
+      if (cvar) {
+        d0 = T[kLinKR + 3 * k]; d1 = T[kLinKR + 3 * k + 1]; d2 = T[kLinKR + 3 * k + 2];
+      } else {
+        const double e = T[kLinE3 + k];
+        d0 = (T[kLinKE + 3 * k] - q[0] * e) * iw;
+        d1 = (T[kLinKE + 3 * k + 1] - q[1] * e) * iw;
+        d2 = (T[kLinKE + 3 * k + 2] - q[2] * e) * iw;
+      }
+      out[12 + k] = (d0 - pr0 * d2) * f;
+      out[15 + k] = (d1 - pr1 * d2) * f;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) out[12 + k] = 0.0;
   }
   out[18] = r0 * scale;
   out[19] = r1 * scale;
+#pragma unroll
+  for (int k = 0; k < 18; ++k) fin = fin && isfinite(out[k]);
   return rho;
 }
 
-// Block body: NT observations per chunk; records staged in LDS (row stride
-// 21 doubles) so the global stores are contiguous — a row-per-lane store of
-// 160-B records is store-issue bound.
-template <int NT, class CamOf>
-__device__ inline void lin_chunks(const DevProblem& P, const double* __restrict__ pts, double* __restrict__ JR,
-                                  double* stage, const CamOf& cam_of, double (&acc)[2]) {
-  for (int base = blockIdx.x * NT; base < P.no; base += gridDim.x * NT) {
-    const int o = base + threadIdx.x;
-    const int nrec = min(NT, P.no - base);
-    if (o < P.no) {
-      const int c = P.obs_cam[o], p = P.obs_pt[o];
-      const float2 uv = P.uv[o];
-      const bool cvar = P.vc[c] >= 0;
-      const bool pvar = P.pt_var[p] != 0;
-      double out[kJR];
-      bool fin;
-      acc[0] += 0.5 * lin_obs(P, cam_of(c), cvar, pvar, pts[3 * p], pts[3 * p + 1], pts[3 * p + 2], uv, out, fin);
-      double* row = stage + threadIdx.x * kStageLd;
+// Wave body: every wave owns chunks of 64 consecutive observations (grid
+// stride over chunks), computes one record per lane, stages the records in a
+// wave-private LDS slot of ROWS rows (row stride 21 doubles: conflict-free
+// b64 writes; ROWS = 32 stages the chunk in two rounds to leave LDS for more
+// waves) and stores them as contiguous 1 KiB wave stores.  No workgroup
+// barrier: waves drift apart, so one wave's store burst overlaps the others'
+// arithmetic (measured ceiling of this store shape: tools/hbm_probe.hip
+// write_stage, 6.4 TB/s; a row-per-lane 160-B record store: 3.3 TB/s).
+// Indices are loaded three chunks ahead, the gathered point data two chunks
+// ahead of the arithmetic.
+// LDS hand-off between the lanes of one wave: DS operations of a wave
+// execute in order, so a compiler barrier is enough (a wavefront-scope
+// fence made the waitcnt pass drain vmcnt before every LDS read)
+__device__ inline void wave_lds_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// MODE (diagnostics only, tools/lin_probe.hip): 0 product; 1 no global
+// stores; 2 no arithmetic (records = a sum of the camera row); 3 table fill
+// only; 4 loads only; 5 arithmetic only (no stage, no stores); 6 = 5 with
+// every lane on camera 1 (broadcast table reads)
+template <int WAVES, int ROWS, class CamOf, int MODE = 0>
+__device__ inline void lin_waves(const DevProblem& P, const double* __restrict__ pts, double* __restrict__ JR,
+                                 double* stage_all, const CamOf& cam_of, double (&acc)[2]) {
+  static_assert(ROWS == 64 || ROWS == 32, "stage rows");
+  if (P.no == 0) return;   // (the clamped prefetch indices need no >= 1)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* stage = stage_all + w * (ROWS * kStageLd);
+  const int step = gridDim.x * WAVES * 64;
+  int base = (blockIdx.x * WAVES + w) * 64;
+  // loads are unconditional (index clamped to the last observation): no
+  // branches around them, so the waitcnt pass can keep them in flight
+  auto load_idx = [&](int o, int& c, int& p, float2& uv) {
+    const int oc = min(o, P.no - 1);
+    c = P.obs_cam[oc]; p = P.obs_pt[oc]; uv = P.uv[oc];
+  };
+  auto load_pt = [&](int, int p, double (&X)[3], uint8_t& pv) {
+    X[0] = pts[3 * p]; X[1] = pts[3 * p + 1]; X[2] = pts[3 * p + 2]; pv = P.pt_var[p];
+  };
+  // pipeline: chunk i computes while the point data of chunk i+2 and the
+  // indices of chunk i+3 are in flight (loads queue behind the store bursts
+  // of all waves of the CU: several microseconds under load)
+  int c, p, c1, p1, c2, p2;
+  float2 uv, uv1, uv2;
+  double X[3], X1[3];
+  uint8_t pv, pv1;
+  load_idx(base + lane, c, p, uv);
+  load_idx(base + step + lane, c1, p1, uv1);
+  load_idx(base + 2 * step + lane, c2, p2, uv2);
+  load_pt(base + lane, p, X, pv);
+  load_pt(base + step + lane, p1, X1, pv1);
+  for (; base < P.no; base += step) {
+    const int o = base + lane;
+    double X2[3];
+    uint8_t pv2;
+    load_pt(o + 2 * step, p2, X2, pv2);
+    int c3, p3;
+    float2 uv3;
+    load_idx(o + 3 * step, c3, p3, uv3);
+    double out[kJR];
+    if (MODE == 4) {   // loads only
+      acc[0] += X[0] + X[1] + X[2] + uv.x + pv + c;
+      c = c1; p = p1; uv = uv1;
+      c1 = c2; p1 = p2; uv1 = uv2;
+      c2 = c3; p2 = p3; uv2 = uv3;
+      X[0] = X1[0]; X[1] = X1[1]; X[2] = X1[2]; pv = pv1;
+      X1[0] = X2[0]; X1[1] = X2[1]; X1[2] = X2[2]; pv1 = pv2;
+      continue;
+    }
+    {
+      const bool live = o < P.no;
+      const auto cam = cam_of(c);
+      if constexpr (MODE == 2) {
+        const auto T = cam_row(cam);
+        double sum = X[0] + uv.x;
 #pragma unroll
-      for (int k = 0; k < kJR; ++k) row[k] = out[k];
-      acc[1] += fin ? 0.0 : 1.0;
+        for (int k = 0; k < kLin; ++k) sum += T[k];
+#pragma unroll
+        for (int k = 0; k < kJR; ++k) out[k] = sum + k;
+      } else if constexpr (MODE >= 5) {   // arithmetic only: no stage, no stores
+        bool fin;
+        const auto cam2 = cam_of(MODE == 6 ? 1 : c);
+        const double rho = lin_obs(P, cam2, cam2.var(), pv != 0, X[0], X[1], X[2], uv, out, fin);
+        double sum = 0.0;
+#pragma unroll
+        for (int k = 0; k < kJR; ++k) sum += out[k];
+        if (live) { acc[0] += 0.5 * rho; acc[1] += sum; }
+      } else {
+        bool fin;
+        const double rho = lin_obs(P, cam, cam.var(), pv != 0, X[0], X[1], X[2], uv, out, fin);
+        if (live) { acc[0] += 0.5 * rho; acc[1] += fin ? 0.0 : 1.0; }
+      }
     }
-    __syncthreads();
+    if constexpr (MODE >= 5) {
+      c = c1; p = p1; uv = uv1;
+      c1 = c2; p1 = p2; uv1 = uv2;
+      c2 = c3; p2 = p3; uv2 = uv3;
+      X[0] = X1[0]; X[1] = X1[1]; X[2] = X1[2]; pv = pv1;
+      X1[0] = X2[0]; X1[1] = X2[1]; X1[2] = X2[2]; pv1 = pv2;
+      continue;
+    }
+    const int nrec = min(64, P.no - base);
     double2* dst = reinterpret_cast<double2*>(JR + (size_t)base * kJR);
-    for (int e = threadIdx.x; e < nrec * (kJR / 2); e += NT) {
-      const int r = e / (kJR / 2), f = 2 * (e - r * (kJR / 2));
-      dst[e] = make_double2(stage[r * kStageLd + f], stage[r * kStageLd + f + 1]);
+#pragma unroll
+    for (int h = 0; h < 64 / ROWS; ++h) {
+      // all LDS reads into distinct registers first, then the stores: a
+      // store's data registers may not be overwritten before it completes
+      // (the waitcnt pass inserts vmcnt(0)), so reusing one register
+      // quadruple per store serialises the stores
+      if (ROWS == 64 || (lane >= h * ROWS && lane < (h + 1) * ROWS)) {
+        double* row = stage + (lane - h * ROWS) * kStageLd;
+#pragma unroll
+        for (int k = 0; k < kJR; ++k) row[k] = out[k];
+      }
+      wave_lds_sync();
+      constexpr int NIT = ROWS * kJR / 2 / 64;
+      double2 v[NIT];
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int e = it * 64 + lane;
+        const int r = e / (kJR / 2), f = 2 * (e - r * (kJR / 2));
+        v[it] = make_double2(stage[r * kStageLd + f], stage[r * kStageLd + f + 1]);
+      }
+      wave_lds_sync();
+      if (MODE == 1) {
+#pragma unroll
+        for (int it = 0; it < NIT; ++it)
+          if (v[it].x == 1234.5678) dst[h * ROWS * (kJR / 2) + it * 64 + lane] = v[it];
+      } else if (h * ROWS + ROWS <= nrec) {   // full: unconditional stores
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) dst[h * ROWS * (kJR / 2) + it * 64 + lane] = v[it];
+      } else {
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          const int e = it * 64 + lane;
+          if (h * ROWS + e / (kJR / 2) < nrec) dst[h * ROWS * (kJR / 2) + e] = v[it];
+        }
+      }
     }
-    __syncthreads();
+    c = c1; p = p1; uv = uv1;
+    c1 = c2; p1 = p2; uv1 = uv2;
+    c2 = c3; p2 = p3; uv2 = uv3;
+    X[0] = X1[0]; X[1] = X1[1]; X[2] = X1[2]; pv = pv1;
+    X1[0] = X2[0]; X1[1] = X2[1]; X1[2] = X2[2]; pv1 = pv2;
   }
 }
 
@@ -299,9 +494,9 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem P, const double* _
                                                    const double* __restrict__ pts, double* __restrict__ JR,
                                                    double* __restrict__ part) {
   __shared__ double lds[2 * 16];
-  __shared__ double stage[kThreads * kStageLd];
+  __shared__ double stage[4 * 64 * kStageLd];
   double acc[2] = {0.0, 0.0};  // cost, bad
-  lin_chunks<kThreads>(P, pts, JR, stage, [&](int c) { return CamGlobal{rec + (size_t)c * kCamRec}; }, acc);
+  lin_waves<4, 64>(P, pts, JR, stage, [&](int c) { return CamGlobal{rec + (size_t)c * kCamRec, P.vc[c] >= 0}; }, acc);
   double tot[2];
   block_sum<2>(acc, lds, tot);
   if (threadIdx.x == 0) {
@@ -315,26 +510,63 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem P, const double* _
 // path (the gathers, 24 x 16 B per lane from random cameras, saturate the
 // TA: measured 46 % issue stalls).  One 512-thread block per CU.
 constexpr int kLinLdsThreads = 512;
-constexpr int kLinLdsCams = 212;
-__global__ __launch_bounds__(kLinLdsThreads) void k_linearize_lds(DevProblem P, const double* __restrict__ rec,
-                                                                  const double* __restrict__ pts,
-                                                                  double* __restrict__ JR, double* __restrict__ part) {
-  __shared__ double lds[2 * 16];
-  __shared__ double stage[kLinLdsThreads * kStageLd];
-  __shared__ double tbl[kLinLdsCams * kTblRec];
-  __shared__ float ktb[kLinLdsCams * 9];
-  for (int e = threadIdx.x; e < P.nc * kTblRec; e += kLinLdsThreads) {
-    const int c = e / kTblRec, k = e - c * kTblRec;
-    tbl[e] = rec[(size_t)c * kCamRec + k];
+constexpr int kLinLdsCams = 200;
+// Camera table -> LDS, every global load of the fill issued before the
+// first LDS store (one round trip; an element-wise loop serialises ~16 L2
+// round trips in the block prologue).
+template <int NT>
+__device__ inline void fill_lin_table(const DevProblem& P, const double* __restrict__ rec, double* tbl, float* ktb) {
+  constexpr int kPer2 = (kLinLdsCams * (kLin / 2) + NT - 1) / NT;
+  constexpr int kPerK = (kLinLdsCams * 9 + NT - 1) / NT;
+  const int n2 = P.nc * (kLin / 2), nk = P.nc * 9;
+  double2 v[kPer2];
+  float kv[kPerK];
+  // unconditional loads (clamped indices): a load under a branch gets its
+  // own vmcnt(0) wait
+#pragma unroll
+  for (int i = 0; i < kPer2; ++i) {
+    const int e = min((int)threadIdx.x + i * NT, n2 - 1);
+    const int c = e / (kLin / 2), k2 = e - c * (kLin / 2);
+    v[i] = reinterpret_cast<const double2*>(rec + (size_t)c * kCamRec + kRecL)[k2];
   }
-  for (int e = threadIdx.x; e < P.nc * 9; e += kLinLdsThreads) {
-    const int c = e / 9, k = e - c * 9;
-    ktb[e] = (float)rec[(size_t)c * kCamRec + kRecK + k];   // K is float-valued (Eigen Matrix3f)
+#pragma unroll
+  for (int i = 0; i < kPerK; ++i) kv[i] = P.K[min((int)threadIdx.x + i * NT, nk - 1)];   // float-valued (Matrix3f)
+  const int c0 = threadIdx.x;
+  const double flag = P.vc[min(c0, P.nc - 1)] >= 0 ? 1.0 : 0.0;
+#pragma unroll
+  for (int i = 0; i < kPer2; ++i) {
+    const int e = threadIdx.x + i * NT;
+    if (e < n2) {
+      const int c = e / (kLin / 2), k2 = e - c * (kLin / 2);
+      reinterpret_cast<double2*>(tbl + c * kTblRec)[k2] = v[i];
+    }
   }
+#pragma unroll
+  for (int i = 0; i < kPerK; ++i) {
+    const int e = threadIdx.x + i * NT;
+    if (e < nk) ktb[e] = kv[i];
+  }
+  if (c0 < P.nc) { tbl[c0 * kTblRec + kLin] = flag; tbl[c0 * kTblRec + kLin + 1] = 0.0; }
   __syncthreads();
+}
+
+// NT threads per block (one block per CU: the camera table fills most of
+// the LDS), stage rows ROWS per wave.
+template <int NT, int ROWS, int MODE = 0, bool LAZY = false>
+__global__ __launch_bounds__(NT) void k_linearize_lds_t(DevProblem P, const double* __restrict__ rec,
+                                                        const double* __restrict__ pts, double* __restrict__ JR,
+                                                        double* __restrict__ part) {
+  __shared__ double lds[2 * 16];
+  __shared__ double stage[(NT / 64) * ROWS * kStageLd];
+  __shared__ __attribute__((aligned(16))) double tbl[kLinLdsCams * kTblRec];
+  __shared__ float ktb[kLinLdsCams * 9];
+  fill_lin_table<NT>(P, rec, tbl, ktb);
   double acc[2] = {0.0, 0.0};
-  lin_chunks<kLinLdsThreads>(P, pts, JR, stage,
-                             [&](int c) { return CamLds{tbl + c * kTblRec, ktb + c * 9}; }, acc);
+  auto cam_of = [&](int c) {
+    if constexpr (LAZY) return CamLdsLazy{tbl + c * kTblRec, ktb + c * 9};
+    else return CamLds{tbl + c * kTblRec, ktb + c * 9};
+  };
+  if (MODE != 3) lin_waves<NT / 64, ROWS, decltype(cam_of), MODE>(P, pts, JR, stage, cam_of, acc);
   double tot[2];
   block_sum<2>(acc, lds, tot);
   if (threadIdx.x == 0) {
@@ -342,6 +574,7 @@ __global__ __launch_bounds__(kLinLdsThreads) void k_linearize_lds(DevProblem P, 
     part_of(part, SL_LIN_BAD)[blockIdx.x] = tot[1];
   }
 }
+constexpr int kLinNT = 512, kLinRows = 64;    // product configuration (tools/lin_probe.hip)
 
 __device__ inline void load_jr(const double* __restrict__ JR, int o, double (&v)[kJR]) {
   const double2* s = reinterpret_cast<const double2*>(JR + (size_t)o * kJR);
@@ -684,50 +917,101 @@ __global__ __launch_bounds__(kLinLdsThreads) void k_candidate_lds(DevProblem P, 
   __shared__ double stage[kLinLdsThreads * kStageLd];
   __shared__ double tbl[kLinLdsCams * kCandRec];
   __shared__ float ktb[kLinLdsCams * 9];
-  for (int e = threadIdx.x; e < P.nc * kCandRec; e += kLinLdsThreads) {
-    const int c = e / kCandRec, k = e - c * kCandRec;
-    double v;
-    if (k < 16) {
+  {  // camera table: every load issued before the first LDS store (clamped, unconditional)
+    constexpr int kPer = (kLinLdsCams * kCandRec + kLinLdsThreads - 1) / kLinLdsThreads;
+    constexpr int kPerK = (kLinLdsCams * 9 + kLinLdsThreads - 1) / kLinLdsThreads;
+    const int n = P.nc * kCandRec, nk = P.nc * 9;
+    double v[kPer];
+    float kv[kPerK];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = min((int)threadIdx.x + i * kLinLdsThreads, n - 1);
+      const int c = e / kCandRec, k = e - c * kCandRec;
       const bool fixed = P.cam_fixed && P.cam_fixed[c];
-      v = fixed ? rec_c[(size_t)c * kCamRec + k]
-                : (k < 9 ? rec_c[(size_t)c * kCamRec + kRecR + k] : (k < 12 ? rec_c[(size_t)c * kCamRec + kRecT + k - 9] : 0.0));
-    } else {
       const int vc = P.vc[c];
-      v = vc >= 0 ? delta_c[(size_t)vc * 6 + (k - 16)] : 0.0;
+      const double* src;
+      bool zero = false;
+      if (k < 16) {
+        src = rec_c + (size_t)c * kCamRec + (fixed ? k : (k < 9 ? kRecR + k : kRecT + min(k - 9, 2)));
+        zero = !fixed && k >= 12;
+      } else {
+        src = delta_c + (size_t)max(vc, 0) * 6 + (k - 16);
+        zero = vc < 0;
+      }
+      const double x = *src;
+      v[i] = zero ? 0.0 : x;
     }
-    tbl[e] = v;
+#pragma unroll
+    for (int i = 0; i < kPerK; ++i) kv[i] = P.K[min((int)threadIdx.x + i * kLinLdsThreads, nk - 1)];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = threadIdx.x + i * kLinLdsThreads;
+      if (e < n) tbl[e] = v[i];
+    }
+#pragma unroll
+    for (int i = 0; i < kPerK; ++i) {
+      const int e = threadIdx.x + i * kLinLdsThreads;
+      if (e < nk) ktb[e] = kv[i];
+    }
   }
-  for (int e = threadIdx.x; e < P.nc * 9; e += kLinLdsThreads) {
-    const int c = e / 9, k = e - c * 9;
-    ktb[e] = (float)rec_c[(size_t)c * kCamRec + kRecK + k];
-  }
+  __syncthreads();   // table ready
   double acc[3] = {0.0, 0.0, 0.0};  // mneg, ccost, cand_bad
-  for (int base = blockIdx.x * kLinLdsThreads; base < P.no; base += gridDim.x * kLinLdsThreads) {
-    const int nrec = min(kLinLdsThreads, P.no - base);
-    __syncthreads();   // table ready / previous chunk consumed
-    const double2* src = reinterpret_cast<const double2*>(JR + (size_t)base * kJR);
-    for (int e = threadIdx.x; e < nrec * (kJR / 2); e += kLinLdsThreads) {
+  // wave-private chunks of 64 observations: the chunk's 64 records are read
+  // as 10 contiguous 1 KiB wave loads (one chunk ahead) into the wave's LDS
+  // slot, then each lane consumes its own record (no workgroup barrier).
+  // Loads are unconditional with clamped indices (no waitcnt drains).
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr int WAVES = kLinLdsThreads / 64;
+  double* st = stage + w * (64 * kStageLd);
+  const int step = gridDim.x * WAVES * 64;
+  const int last2 = P.no * (kJR / 2) - 1;
+  const double2* JR2 = reinterpret_cast<const double2*>(JR);
+  int base = (blockIdx.x * WAVES + w) * 64;
+  if (P.no == 0) base = P.no;
+  double2 t[kJR / 2];
+  int c = 0, p = 0;
+  float2 uv = make_float2(0.f, 0.f);
+  if (base < P.no) {
+#pragma unroll
+    for (int it = 0; it < kJR / 2; ++it) t[it] = JR2[min(base * (kJR / 2) + it * 64 + lane, last2)];
+    const int oc = min(base + lane, P.no - 1);
+    c = P.obs_cam[oc]; p = P.obs_pt[oc]; uv = P.uv[oc];
+  }
+  for (; base < P.no; base += step) {
+    const int o = base + lane;
+    // stage this chunk's records
+#pragma unroll
+    for (int it = 0; it < kJR / 2; ++it) {
+      const int e = it * 64 + lane;
       const int r = e / (kJR / 2), f = 2 * (e - r * (kJR / 2));
-      const double2 t = src[e];
-      stage[r * kStageLd + f] = t.x;
-      stage[r * kStageLd + f + 1] = t.y;
+      st[r * kStageLd + f] = t[it].x;
+      st[r * kStageLd + f + 1] = t[it].y;
     }
-    __syncthreads();
-    const int o = base + threadIdx.x;
-    if (o < P.no) {
-      const int c = P.obs_cam[o], p = P.obs_pt[o];
-      const double* j = stage + threadIdx.x * kStageLd;
+    const double dp0 = delta_p[3 * p], dp1 = delta_p[3 * p + 1], dp2 = delta_p[3 * p + 2];
+    const double X0 = pts_c[3 * p], X1 = pts_c[3 * p + 1], X2 = pts_c[3 * p + 2];
+    const bool cfix = P.cam_fixed && P.cam_fixed[c];
+    // next chunk's records and indices (in flight during this chunk)
+    const int nb = base + step;
+    int cn = c, pn = p;
+    float2 uvn = uv;
+    if (nb < P.no) {
+#pragma unroll
+      for (int it = 0; it < kJR / 2; ++it) t[it] = JR2[min(nb * (kJR / 2) + it * 64 + lane, last2)];
+      const int oc = min(nb + lane, P.no - 1);
+      cn = P.obs_cam[oc]; pn = P.obs_pt[oc]; uvn = P.uv[oc];
+    }
+    wave_lds_sync();
+    {
+      const double* j = st + lane * kStageLd;
       const double* cr = tbl + c * kCandRec;
       double jd0 = 0.0, jd1 = 0.0;
 #pragma unroll
       for (int a2 = 0; a2 < 6; ++a2) { jd0 += j[a2] * cr[16 + a2]; jd1 += j[6 + a2] * cr[16 + a2]; }
-      const double dp0 = delta_p[3 * p], dp1 = delta_p[3 * p + 1], dp2 = delta_p[3 * p + 2];
       jd0 += j[12] * dp0 + j[13] * dp1 + j[14] * dp2;
       jd1 += j[15] * dp0 + j[16] * dp1 + j[17] * dp2;
-      acc[0] += jd0 * (j[18] + jd0 / 2.0) + jd1 * (j[19] + jd1 / 2.0);
-      const double X0 = pts_c[3 * p], X1 = pts_c[3 * p + 1], X2 = pts_c[3 * p + 2];
+      const double mneg = jd0 * (j[18] + jd0 / 2.0) + jd1 * (j[19] + jd1 / 2.0);
       double pc[3];
-      if (!(P.cam_fixed && P.cam_fixed[c])) {
+      if (!cfix) {
 #pragma unroll
         for (int i = 0; i < 3; ++i) pc[i] = cr[i] * X0 + cr[3 + i] * X1 + cr[6 + i] * X2 + cr[9 + i];
       } else {
@@ -740,12 +1024,17 @@ __global__ __launch_bounds__(kLinLdsThreads) void k_candidate_lds(DevProblem P, 
       double q[3];
 #pragma unroll
       for (int i = 0; i < 3; ++i) q[i] = pc[0] * (double)Kc[i] + pc[1] * (double)Kc[3 + i] + pc[2] * (double)Kc[6 + i];
-      const float2 uv = P.uv[o];
       const double rc0 = q[0] / q[2] - (double)uv.x, rc1 = q[1] / q[2] - (double)uv.y;
       double sc;
-      acc[1] += 0.5 * huber(rc0 * rc0 + rc1 * rc1, P.huber_a, P.huber_b, &sc);
-      if (!isfinite(rc0) || !isfinite(rc1)) acc[2] += 1.0;
+      const double rho = huber(rc0 * rc0 + rc1 * rc1, P.huber_a, P.huber_b, &sc);
+      if (o < P.no) {
+        acc[0] += mneg;
+        acc[1] += 0.5 * rho;
+        if (!isfinite(rc0) || !isfinite(rc1)) acc[2] += 1.0;
+      }
     }
+    wave_lds_sync();
+    c = cn; p = pn; uv = uvn;
   }
   double out[3];
   block_sum<3>(acc, lds, out);
@@ -979,8 +1268,8 @@ __global__ __launch_bounds__(1024) void k_reduce(double* __restrict__ part, doub
 // ---------------------------------------------------------------------------
 void launch_cam_prep(const DevProblem& P, const double* cams, double* rec, bool deriv, hipStream_t s) {
   if (P.nc == 0) return;
-  hipLaunchKernelGGL(k_cam_prep, dim3((P.nc + 255) / 256), dim3(256), 0, s, P.nc, cams, P.K, P.cam_fixed, P.extr,
-                     rec, deriv ? 1 : 0);
+  hipLaunchKernelGGL(k_cam_prep, dim3(P.nc), dim3(64), 0, s, P.nc, cams, P.K, P.cam_fixed, P.extr, rec,
+                     deriv ? 1 : 0);
 }
 // one 512-thread block per CU for the LDS-table kernels
 static int lds_grid(int n) {
@@ -996,9 +1285,10 @@ static int lds_grid(int n) {
 }
 
 void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s) {
-  if (P.nc <= kLinLdsCams) {
+  if (P.nc > 0 && P.nc <= kLinLdsCams) {
     const int g = lds_grid(P.no);
-    hipLaunchKernelGGL(k_linearize_lds, dim3(g), dim3(kLinLdsThreads), 0, s, P, W.rec, W.pts, W.JR, W.part);
+    hipLaunchKernelGGL((k_linearize_lds_t<kLinNT, kLinRows>), dim3(g), dim3(kLinNT), 0, s, P, W.rec, W.pts, W.JR,
+                       W.part);
     return;
   }
   hipLaunchKernelGGL(k_linearize, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.rec, W.pts, W.JR, W.part);
