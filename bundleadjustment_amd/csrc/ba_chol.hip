@@ -20,7 +20,7 @@
 namespace bahip {
 
 constexpr int CB = 64;           // block size
-constexpr int LDP = CB + 1;      // padded LDS row (doubles)
+constexpr int LDP = CB + 2;      // padded LDS row (doubles): conflict-free MFMA operand reads (16 rows x 4 k per wave)
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -209,6 +209,14 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // The pivots d_t end up on the diagonal (a_tt), so the scaling
 // 1/sqrt(d_t) is computed once per lane in parallel and broadcast.
 // Writes the scaled L columns c0..c0+15 (rows c0..m-1) into T.
+//
+// Per column the dependency chain is kept to: LDS read of the pivot ->
+// reciprocal -> f -> update of the NEXT column -> LDS publish; the next
+// column's reads are issued right after the publish and the remaining
+// column updates run under their latency (sched_barriers pin that order;
+// the default schedule sank the publish below all updates).  Measured per
+// 16 columns (tools/chol_bench.hip): ~5.7k cycles (default schedule ~7.7k;
+// readlane broadcasts instead of LDS ~7.1k, hazard-serialised).
 __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0, int b, int m) {
   const int r = threadIdx.x & 63;
   double a[16];
@@ -217,25 +225,34 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
     const int t = c0 + cc;
     a[cc] = (r >= c0 && r < m && t < b && (t <= r || r >= b)) ? T[r][t] : 0.0;
   }
-  // column jj travels through LDS (same wave: in-order, no barrier); the next
-  // column is updated and published first, the rest of the row afterwards
   W.colv[0][r] = a[0];
+  __builtin_amdgcn_sched_barrier(0);
+  double d = W.colv[0][c0];
+  double ct[16];
+#pragma unroll
+  for (int t = 1; t < 16; ++t) ct[t] = W.colv[0][c0 + t];
 #pragma unroll
   for (int jj = 0; jj < 16; ++jj) {
     const int j = c0 + jj;
     if (j >= b) break;                       // uniform
     const int buf = jj & 1;
-    const double d = W.colv[buf][j];
-    double ct[16];
-#pragma unroll
-    for (int t = jj + 1; t < 16; ++t) ct[t] = W.colv[buf][c0 + t];
-    const double f = (r > j && r < m) ? a[jj] * recip(d) : 0.0;
+    const double rd = recip(d);
+    const double f = (r > j && r < m) ? a[jj] * rd : 0.0;
     if (jj + 1 < 16) {
       a[jj + 1] -= f * ct[jj + 1];
       W.colv[buf ^ 1][r] = a[jj + 1];
-    }
+      __builtin_amdgcn_sched_barrier(0);
+      const double dn = W.colv[buf ^ 1][c0 + jj + 1];
+      double ctn[16];
 #pragma unroll
-    for (int t = jj + 2; t < 16; ++t) a[t] -= f * ct[t];
+      for (int t = jj + 2; t < 16; ++t) ctn[t] = W.colv[buf ^ 1][c0 + t];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = jj + 2; t < 16; ++t) a[t] -= f * ct[t];
+      d = dn;
+#pragma unroll
+      for (int t = jj + 2; t < 16; ++t) ct[t] = ctn[t];
+    }
   }
   // own pivot (lanes c0..c0+15): d_r = a_rr
   double d_own = 1.0;
@@ -286,6 +303,7 @@ __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z
     const int c0 = 16 * p;
     if (c0 >= b) break;                      // uniform
     if (w == 0) panel_sweep(T, W, c0, b, m);
+    CHOL_STAMP(10 + 2 * p);
     __syncthreads();
     // trailing update of the remaining sub-panels: tiles (i, s), p < s <= i
     {
@@ -302,6 +320,7 @@ __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z
       }
     }
     __syncthreads();
+    CHOL_STAMP(11 + 2 * p);
   }
   CHOL_STAMP(3);
   diag_inverse16(T, X, b);
@@ -355,13 +374,17 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
       stage64(S1, A, lds, s, kc, nrows, kc + kb);   // A_{k+1,k}
       stage64(S2, Vk, CB, 0, 0, CB, CB);
       __syncthreads();
+      CHOL_STAMP(20);
       d4 acc[2][2];
       mfma_xyT_64(S1, S2, acc);              // P = A_{k+1,k} V_k^T
       __syncthreads();
+      CHOL_STAMP(21);
       acc_to_lds(S1, acc, 0);
       __syncthreads();
       lds_to_global(S1, L, lds, s, kc, m, kb);       // L_{k+1,k}
+      CHOL_STAMP(22);
       mfma_xyT_64(S1, S1, acc);              // P P^T
+      CHOL_STAMP(23);
       acc_to_lds(S0, acc, 1);                // C = A - P P^T
     }
     if (threadIdx.x == 0) cw.bad = 0;
@@ -410,59 +433,99 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
 }
 
 // ---------------------------------------------------------------------------
-// back substitution L^T y = z (z = row n of L), one workgroup, right-looking
-// over 64-blocks from the bottom: y_K = V_K^T z_K ; z_J -= L_KJ^T y_K (J < K).
-// z is kept in LDS when it fits (n <= kBackLds), else updated in place.
+// back substitution L^T y = z (z = row n of L) as a dataflow over block
+// columns: workgroup K owns y_K = V_K^T (z_K - sum_{J>K} L_JK^T y_J).  It
+// folds in the contribution of every y_J (J = T-1 .. K+1) as soon as
+// workgroup J has published it, prefetching the L_JK tile before it polls,
+// so the serial chain per block is one hand-off plus two 64x64 GEMVs (the
+// single-workgroup sweep it replaces was bound by one CU pulling all of L:
+// 152 us at n = 1194).
+//
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): producer =
+// plain stores of y_K -> every storing wave s_waitcnt vmcnt(0) -> barrier ->
+// one lane: agent release fence -> vmcnt(0) -> relaxed agent flag store;
+// consumer = one lane polls the flag (relaxed, agent, s_sleep) -> agent
+// acquire fence -> vmcnt(0) -> barrier -> plain loads.  Flags are zeroed
+// by a memset node before every launch; spins are bounded (a missing
+// producer sets the failure slot instead of hanging the GPU).
 // ---------------------------------------------------------------------------
-constexpr int kBackLds = 12288;
-__global__ __launch_bounds__(512) void k_chol_back(double* __restrict__ Lm, int ld, int n,
-                                                    const double* __restrict__ Vall, double* __restrict__ y) {
-  __shared__ double Vs[CB][LDP];
-  __shared__ double yb[CB];
-  __shared__ double zl[kBackLds];
-  double* zg = Lm + (size_t)n * ld;
-  const bool in_lds = n <= kBackLds;
-  double* z = in_lds ? zl : zg;
-  const int tid = threadIdx.x;
-  if (in_lds)
-    for (int t = tid; t < n; t += blockDim.x) zl[t] = zg[t];
-  const int nblk = (n + CB - 1) / CB;
-  for (int K = nblk - 1; K >= 0; --K) {
-    const int s0 = K * CB, bsz = min(CB, n - s0);
-    const double* V = Vall + (size_t)K * CB * CB;
-    for (int e = tid; e < CB * CB; e += blockDim.x) Vs[e / CB][e % CB] = V[e];
-    __syncthreads();
-    {  // y_K[j] = sum_{i >= j} V[i][j] z[s0 + i]   (8 threads per j)
-      const int j = tid >> 3, h = tid & 7;
-      double t = 0.0;
-      if (j < bsz)
-        for (int i = j + h; i < bsz; i += 8) t += Vs[i][j] * z[s0 + i];
-      for (int off = 4; off > 0; off >>= 1) t += __shfl_down(t, off, 8);
-      if (h == 0 && j < CB) yb[j] = (j < bsz) ? t : 0.0;
+constexpr long kSpinMax = 1L << 26;
+
+__device__ inline void flag_publish(int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// returns false if the spin bound was hit
+__device__ inline bool flag_wait(int* flag, int* lds_ok) {
+  if (threadIdx.x == 0) {
+    long it = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && it < kSpinMax) {
+      __builtin_amdgcn_s_sleep(1);
+      ++it;
     }
-    __syncthreads();
-    if (tid < bsz) y[s0 + tid] = yb[tid];
-    for (int t = tid; t < s0; t += blockDim.x) {  // z[t] -= sum_j L[s0+j][t] y_K[j]
-      // two batches of 32 loads in flight (rows past a partial last block
-      // are clamped; yb is zero there)
-      const double* Lc = Lm + (size_t)s0 * ld + t;
-      double acc = 0.0;
+    *lds_ok = it < kSpinMax;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  return *lds_ok != 0;
+}
+
+__global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ Lm, int ld, int n,
+                                                   const double* __restrict__ Vall, double* __restrict__ y,
+                                                   int* __restrict__ flags, double* __restrict__ scal) {
+  __shared__ double zs[CB];
+  __shared__ double ys[CB];
+  __shared__ double part[4][CB];
+  __shared__ int ok;
+  const int K = blockIdx.x, tid = threadIdx.x;
+  const int T = (n + CB - 1) / CB;
+  const int s0 = K * CB, bsz = min(CB, n - s0);
+  const size_t lds = (size_t)ld;
+  // thread (j = tid & 63, h = tid >> 6) sums rows i = h, h + 4, ... of a tile
+  const int j = tid & 63, h = tid >> 6;
+  if (tid < CB) zs[tid] = tid < bsz ? Lm[(size_t)n * lds + s0 + tid] : 0.0;
+  double acc = 0.0;
+  bool good = true;
+  for (int J = T - 1; J > K; --J) {
+    const int sJ = J * CB, bJ = min(CB, n - sJ);
+    double lv[16];
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        double lv[CB / 2];
-        const double* Lh = Lc + (size_t)(half * (CB / 2)) * ld;
-#pragma unroll
-        for (int j = 0; j < CB / 2; ++j) {
-          const int jj = half * (CB / 2) + j;
-          lv[j] = Lh[(size_t)(jj < bsz ? j : -half * (CB / 2)) * ld];
-        }
-#pragma unroll
-        for (int j = 0; j < CB / 2; ++j) acc += lv[j] * yb[half * (CB / 2) + j];
-      }
-      z[t] -= acc;
+    for (int q = 0; q < 16; ++q) {   // L[sJ + i][s0 + j], i = h + 4 q (prefetched before the poll)
+      const int i = h + 4 * q;
+      lv[q] = (i < bJ && j < bsz) ? Lm[(size_t)(sJ + i) * lds + s0 + j] : 0.0;
     }
+    good = flag_wait(flags + J, &ok) && good;
+    if (tid < CB) ys[tid] = tid < bJ ? y[sJ + tid] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc += lv[q] * ys[h + 4 * q];
     __syncthreads();
   }
+  part[h][j] = acc;
+  __syncthreads();
+  if (tid < CB) zs[tid] -= (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+  __syncthreads();
+  // y_K[j] = sum_{i >= j} V[i][j] z[i]
+  {
+    const double* V = Vall + (size_t)K * CB * CB;
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = h + 4 * q;
+      t += V[(size_t)i * CB + j] * zs[i];
+    }
+    part[h][j] = t;
+  }
+  __syncthreads();
+  if (tid < CB && tid < bsz) y[s0 + tid] = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+  flag_publish(flags + K);
+  if (tid == 0 && !good) scal[SL_CHOL_BAD] += 1.0;
 }
 
 void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, hipStream_t s) {
@@ -476,7 +539,8 @@ void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, hipStream_t s
     const int tr = (nrows - st + CB - 1) / CB, tc = (n - st + CB - 1) / CB;
     hipLaunchKernelGGL(k_chol_step, dim3(tc, tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf, W.scal);
   }
-  hipLaunchKernelGGL(k_chol_back, dim3(1), dim3(512), 0, s, W.Lf, P.ld, n, W.Vbuf, W.y);
+  (void)hipMemsetAsync(W.flags, 0, sizeof(int) * T, s);
+  hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.Lf, P.ld, n, W.Vbuf, W.y, W.flags, W.scal);
 }
 
 }  // namespace bahip

@@ -10,6 +10,7 @@ namespace bahip {
 constexpr int kThreads = 256;
 constexpr int kMaxBlocks = 2048;        // grid cap of the streaming kernels
 constexpr int kCamSplit = 8;            // workgroups per camera in k_cam_schur_diag
+constexpr int kFlagWords = 4096;        // hand-off flag words (DevWork::flags)
 
 // Scalar reduction slots (device buffer d_scal[kNumSlots]).
 enum Slot {
@@ -66,6 +67,7 @@ struct DevWork {
   double* Lf;                        // [(n+1) x ld] Cholesky factor, row n = L^-1 rhs
   double* y;                         // [n] reduced solution
   double* Vbuf;                      // [ceil(n/64)][64][64] inverses of the diagonal Cholesky blocks
+  int* flags;                        // [kFlagWords] hand-off flags of the dataflow kernels (zeroed per call)
   const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}
   const int2* pairs;                 // observation pairs per block
   double* cpart;                     // [kCamSplit][nvc][27] per-slice camera sums

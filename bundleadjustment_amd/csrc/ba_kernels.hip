@@ -14,6 +14,8 @@
 // Every reduction is a fixed-order tree (wave shuffles + LDS, then a
 // fixed-order fold of per-block partials): results are bitwise reproducible
 // run to run.  No floating-point atomics anywhere.
+#include <cstdlib>
+
 #include "ba_kernels.h"
 #include "ba_device.h"
 
@@ -1108,12 +1110,19 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
                                                      const int2* __restrict__ pairs, const double* __restrict__ W,
                                                      double* __restrict__ S) {
   const int lane = threadIdx.x & 63, sl = lane & 15, sub = lane >> 4;
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  // XCD-aware order: workgroups b and b + 8 share an XCD (round-robin
+  // dispatch).  XCD x owns the contiguous block range [x R, (x+1) R) (a few
+  // rows I of S) and its workgroups sweep it in rounds, so the W rows of the
+  // few cameras I active on an XCD are re-read from its L2 by the ~9 blocks
+  // (I, J) each observation contributes to.  gridDim.x is a multiple of 8.
+  const int xcd = blockIdx.x & 7, wx = blockIdx.x >> 3, nwx = gridDim.x >> 3;
+  const int R = (nblocks + 7) / 8;
+  const int r0 = xcd * R, r1 = min(nblocks, r0 + R);
+  const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   const size_t ld = (size_t)P.ld;
-  for (int base = wave * 4; base < nblocks; base += nwaves * 4) {
+  for (int base = r0 + (wx * nwv + wv) * 4; base < r1; base += nwx * nwv * 4) {
     const int bi = base + sub;
-    const bool live = bi < nblocks;
+    const bool live = bi < r1;
     const int4 blk = live ? blocks[bi] : make_int4(0, 0, 0, 0);
     double acc[36];
 #pragma unroll
@@ -1318,9 +1327,16 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s)
 }
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (W.nblocks == 0) return;
+  static int grid_cap = 0;
+  if (grid_cap == 0) {
+    const char* e = getenv("BA_PAIRS_GRID");   // diagnostics: workgroups (multiple of 8)
+    grid_cap = e ? atoi(e) : 2048;
+    if (grid_cap < 8) grid_cap = 8;
+  }
   int waves = (W.nblocks + 3) / 4;
   int grid = (waves + 3) / 4;
-  if (grid > 4 * kMaxBlocks) grid = 4 * kMaxBlocks;
+  if (grid > grid_cap) grid = grid_cap;
+  grid = (grid + 7) / 8 * 8;   // k_schur_pairs' XCD ranges need a multiple of 8
   hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
 }
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {

@@ -292,6 +292,7 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.Lf = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
   W.y = ctx->dalloc<double>(std::max(ctx->n, 1));
   W.Vbuf = ctx->dalloc<double>((size_t)((ctx->n + 63) / 64 + 1) * 64 * 64);
+  W.flags = ctx->dalloc<int>(kFlagWords);
   W.blocks = ctx->upload(blocks);
   W.nblocks = (int)blocks.size();
   W.pairs = ctx->upload(pairs);

@@ -48,6 +48,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dV, sizeof(double) * (size_t)(T + 1) * CB * CB));
   CK(hipMalloc(&dS, sizeof(double) * 64));
   CK(hipMalloc(&dy, sizeof(double) * n));
+  int* dF;
+  CK(hipMalloc(&dF, sizeof(int) * (T + 1)));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -74,10 +76,18 @@ int main(int argc, char** argv) {
                "  write %6llu cycles\n",
                k, grid.x, grid.y, ms * 1e3, st_h[1] - st_h[0], st_h[2] - st_h[1], st_h[3] - st_h[2],
                st_h[4] - st_h[3], st_h[5] - st_h[4], st_h[6] - st_h[5]);
+      if (verbose && k >= 0 && (k < 1 || k == T / 2))
+        printf("    stage %llu  gemm1 %llu  store %llu  gemm2 %llu  rest %llu\n", st_h[20] - st_h[0], st_h[21] - st_h[20],
+               st_h[22] - st_h[21], st_h[23] - st_h[22], st_h[1] - st_h[23]);
+      if (verbose && (k < 1 || k == T / 2))
+        printf("    sub-panels (sweep / update cycles): %llu/%llu %llu/%llu %llu/%llu %llu/%llu\n", st_h[10] - st_h[2],
+               st_h[11] - st_h[10], st_h[12] - st_h[11], st_h[13] - st_h[12], st_h[14] - st_h[13], st_h[15] - st_h[14],
+               st_h[16] - st_h[15], st_h[17] - st_h[16]);
 
     }
+    CK(hipMemset(dF, 0, sizeof(int) * T));
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(k_chol_back, dim3(1), dim3(512), 0, 0, dL, ld, n, dV, dy);
+    hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dL, ld, n, dV, dy, dF, dS);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float mb;
