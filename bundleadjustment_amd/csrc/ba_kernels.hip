@@ -724,17 +724,15 @@ __global__ __launch_bounds__(256) void k_cam_norms(DevProblem P, const double* _
 }
 
 // ---------------------------------------------------------------------------
-// point elimination fused with W: per point (one thread)
+// point elimination: per point (one thread)
 //   A = s Hpp s + D^2 (D = sqrt(diag / radius), ceres lm_diagonal_), L L^T = A,
-//   store L^-1 and u = L^-1 (s g); then for each of its observations with a
-//   variable camera: W_o = diag(s_c) Jc^T Jp diag(s_p) L^-T  (6x3, AoS [no][18])
+//   store L^-1 and u = L^-1 (s g)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_point_elim_w(DevProblem P, const double* __restrict__ Hpp,
-                                                      const double* __restrict__ gp, const double* __restrict__ scale_p,
-                                                      const double* __restrict__ diag_p, double radius,
-                                                      const double* __restrict__ JR, const double* __restrict__ scale_c,
-                                                      double* __restrict__ Linv, double* __restrict__ u,
-                                                      double* __restrict__ W, double* __restrict__ part) {
+__global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* __restrict__ Hpp,
+                                                    const double* __restrict__ gp, const double* __restrict__ scale_p,
+                                                    const double* __restrict__ diag_p, double radius,
+                                                    double* __restrict__ Linv, double* __restrict__ u,
+                                                    double* __restrict__ part) {
   __shared__ double lds[16];
   double acc[1] = {0.0};
   const size_t np = (size_t)P.np;
@@ -774,35 +772,108 @@ __global__ __launch_bounds__(256) void k_point_elim_w(DevProblem P, const double
     u[1 * np + p] = i10 * gs[0] + i11 * gs[1];
     u[2 * np + p] = i20 * gs[0] + i21 * gs[1] + i22 * gs[2];
     acc[0] += ok ? 0.0 : 1.0;
-    const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
-    for (int o = o0; o < o1; ++o) {
-      const int v = P.vc[P.obs_cam[o]];
-      if (v < 0) continue;
-      double j[kJR];
-      load_jr(JR, o, j);
-      double jp0[3], jp1[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) { jp0[k] = j[12 + k] * s[k]; jp1[k] = j[15 + k] * s[k]; }
-      double w[18];
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        const double sc = scale_c[(size_t)v * 6 + a];
-        const double c0 = j[a] * sc, c1 = j[6 + a] * sc;
-        const double e0 = c0 * jp0[0] + c1 * jp1[0];
-        const double e1 = c0 * jp0[1] + c1 * jp1[1];
-        const double e2 = c0 * jp0[2] + c1 * jp1[2];
-        w[a * 3 + 0] = e0 * i00;
-        w[a * 3 + 1] = e0 * i10 + e1 * i11;
-        w[a * 3 + 2] = e0 * i20 + e1 * i21 + e2 * i22;
-      }
-      double2* dst = reinterpret_cast<double2*>(W + (size_t)o * 18);
-#pragma unroll
-      for (int k = 0; k < 9; ++k) dst[k] = make_double2(w[2 * k], w[2 * k + 1]);
-    }
   }
   double out[1];
   block_sum<1>(acc, lds, out);
   if (threadIdx.x == 0) part_of(part, SL_ELIM_BAD)[blockIdx.x] = out[0];
+}
+
+// ---------------------------------------------------------------------------
+// W per observation with a variable camera and a variable point:
+//   W_o = diag(s_c) Jc^T Jp diag(s_p) L_p^-T     (6x3, AoS [no][18])
+// Wave-private chunks of 64 observations: the chunk's JR records arrive as
+// 10 contiguous 1 KiB wave loads through the wave's LDS slot, the 64 W
+// records leave as 9 contiguous 1 KiB wave stores through the same slot
+// (row-per-lane 144-B stores are store-issue bound: tools/hbm_probe.hip).
+// Camera scales come from an LDS table (nc <= kLinLdsCams) or global.
+// ---------------------------------------------------------------------------
+constexpr int kWRec = 18;
+template <bool TBL>
+__global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __restrict__ JR,
+                                               const double* __restrict__ scale_c, const double* __restrict__ scale_p,
+                                               const double* __restrict__ Linv, double* __restrict__ W) {
+  constexpr int WAVES = 8;
+  __shared__ double stage[WAVES * 64 * kStageLd];
+  __shared__ double sct[TBL ? kLinLdsCams * 6 : 1];
+  if (TBL) {
+    for (int e = threadIdx.x; e < P.nc * 6; e += 512) {
+      const int c = e / 6, a = e - 6 * c;
+      const int v = P.vc[c];
+      sct[e] = v >= 0 ? scale_c[(size_t)v * 6 + a] : 0.0;
+    }
+    __syncthreads();
+  }
+  if (P.no == 0) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* st = stage + w * (64 * kStageLd);
+  const int step = gridDim.x * WAVES * 64;
+  const size_t np = (size_t)P.np;
+  const int last2 = P.no * (kJR / 2) - 1;
+  const double2* JR2 = reinterpret_cast<const double2*>(JR);
+  for (int base = (blockIdx.x * WAVES + w) * 64; base < P.no; base += step) {
+    const int o = base + lane, oc = min(o, P.no - 1);
+    double2 t[kJR / 2];
+#pragma unroll
+    for (int it = 0; it < kJR / 2; ++it) t[it] = JR2[min(base * (kJR / 2) + it * 64 + lane, last2)];
+    const int c = P.obs_cam[oc], p = P.obs_pt[oc];
+    const int v = P.vc[c];
+    const bool live = o < P.no && v >= 0 && P.pt_var[p];
+    double sc[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) sc[a] = TBL ? sct[c * 6 + a] : scale_c[(size_t)max(v, 0) * 6 + a];
+    const double s0 = scale_p[p], s1 = scale_p[np + p], s2 = scale_p[2 * np + p];
+    const double i00 = Linv[p], i10 = Linv[np + p], i11 = Linv[2 * np + p];
+    const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
+#pragma unroll
+    for (int it = 0; it < kJR / 2; ++it) {
+      const int e = it * 64 + lane;
+      const int r = e / (kJR / 2), f = 2 * (e - r * (kJR / 2));
+      st[r * kStageLd + f] = t[it].x;
+      st[r * kStageLd + f + 1] = t[it].y;
+    }
+    wave_lds_sync();
+    double j[18];
+#pragma unroll
+    for (int k = 0; k < 18; ++k) j[k] = st[lane * kStageLd + k];
+    wave_lds_sync();
+    const double jp0[3] = {j[12] * s0, j[13] * s1, j[14] * s2};
+    const double jp1[3] = {j[15] * s0, j[16] * s1, j[17] * s2};
+    double wv[18];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const double c0 = j[a] * sc[a], c1 = j[6 + a] * sc[a];
+      const double e0 = c0 * jp0[0] + c1 * jp1[0];
+      const double e1 = c0 * jp0[1] + c1 * jp1[1];
+      const double e2 = c0 * jp0[2] + c1 * jp1[2];
+      wv[a * 3 + 0] = live ? e0 * i00 : 0.0;
+      wv[a * 3 + 1] = live ? e0 * i10 + e1 * i11 : 0.0;
+      wv[a * 3 + 2] = live ? e0 * i20 + e1 * i21 + e2 * i22 : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kWRec; ++k) st[lane * kStageLd + k] = wv[k];
+    wave_lds_sync();
+    constexpr int NIT = kWRec / 2;   // 9 x 1 KiB
+    double2 ov[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int e = it * 64 + lane;
+      const int r = e / (kWRec / 2), f = 2 * (e - r * (kWRec / 2));
+      ov[it] = make_double2(st[r * kStageLd + f], st[r * kStageLd + f + 1]);
+    }
+    wave_lds_sync();
+    double2* dst = reinterpret_cast<double2*>(W + (size_t)base * kWRec);
+    const int nrec = min(64, P.no - base);
+    if (nrec == 64) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) dst[it * 64 + lane] = ov[it];
+    } else {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int e = it * 64 + lane;
+        if (e / (kWRec / 2) < nrec) dst[e] = ov[it];
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1317,8 +1388,14 @@ void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale,
                      W.diag_c, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
 }
 void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
-  hipLaunchKernelGGL(k_point_elim_w, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.Hpp, W.gp, W.scale_p, W.diag_p,
-                     radius, W.JR, W.scale_c, W.Linv, W.u, W.W, W.part);
+  hipLaunchKernelGGL(k_point_elim, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.Hpp, W.gp, W.scale_p, W.diag_p,
+                     radius, W.Linv, W.u, W.part);
+  if (P.no == 0) return;
+  const int g = lds_grid(P.no);
+  if (P.nc <= kLinLdsCams)
+    hipLaunchKernelGGL(k_obs_w<true>, dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.W);
+  else
+    hipLaunchKernelGGL(k_obs_w<false>, dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.W);
 }
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
