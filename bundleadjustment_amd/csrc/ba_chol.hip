@@ -141,7 +141,8 @@ __device__ inline void lds_to_global(const double (*Sx)[LDP], double* __restrict
 // saturate LDS bandwidth; this one reads 6 doubles per thread per column.)
 // On exit T holds L (b columns, rows < m) and X holds L^-1 (b x b).
 struct CholLds {
-  double colv[2][CB];      // column broadcast of the sub-panel sweep
+  double2 colp[2][CB];     // column-pair broadcast of the sub-panel sweep
+  double rsv[CB];          // 1/sqrt(pivot) broadcast for the final scaling
   int bad;
 };
 
@@ -210,50 +211,70 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // 1/sqrt(d_t) is computed once per lane in parallel and broadcast.
 // Writes the scaled L columns c0..c0+15 (rows c0..m-1) into T.
 //
-// Per column the dependency chain is kept to: LDS read of the pivot ->
-// reciprocal -> f -> update of the NEXT column -> LDS publish; the next
-// column's reads are issued right after the publish and the remaining
-// column updates run under their latency (sched_barriers pin that order;
-// the default schedule sank the publish below all updates).  Measured per
-// 16 columns (tools/chol_bench.hip): ~5.7k cycles (default schedule ~7.7k;
-// readlane broadcasts instead of LDS ~7.1k, hazard-serialised).
+// Columns are eliminated in pairs (2 x 2 pivot block B of the updated
+// matrix): [f0, f1]_r = [a_rj, a_r,j+1] B^-1 and a_rt -= f0 a_tj + f1 a_t,j+1
+// for t > j+1 — the same Schur complement as two 1 x 1 steps, with one
+// reciprocal per pair on the chain.  Column j+1 is then brought to its 1 x 1
+// form (a_r,j+1 -= a_rj e / d_j) off the chain, so the final scaling and
+// the pivots on the diagonal are those of the column-by-column sweep.
+// Per pair the chain is: LDS read of B -> det, reciprocal -> f -> update of
+// the NEXT pair's two columns -> LDS publish (sched_barriers keep the publish
+// and the next reads ahead of the remaining updates).  Measured per 16
+// columns (tools/chol_bench.hip): 1 x 1 pivots ~5.7k cycles.
 __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0, int b, int m) {
   const int r = threadIdx.x & 63;
   double a[16];
+  {  // row r, columns c0..c0+15: 8 unconditional 16-B reads, then selects
+    const double2* src = reinterpret_cast<const double2*>(&T[r][c0]);
+    double2 v[8];
 #pragma unroll
-  for (int cc = 0; cc < 16; ++cc) {
-    const int t = c0 + cc;
-    a[cc] = (r >= c0 && r < m && t < b && (t <= r || r >= b)) ? T[r][t] : 0.0;
-  }
-  W.colv[0][r] = a[0];
-  __builtin_amdgcn_sched_barrier(0);
-  double d = W.colv[0][c0];
-  double ct[16];
+    for (int k = 0; k < 8; ++k) v[k] = src[k];
 #pragma unroll
-  for (int t = 1; t < 16; ++t) ct[t] = W.colv[0][c0 + t];
-#pragma unroll
-  for (int jj = 0; jj < 16; ++jj) {
-    const int j = c0 + jj;
-    if (j >= b) break;                       // uniform
-    const int buf = jj & 1;
-    const double rd = recip(d);
-    const double f = (r > j && r < m) ? a[jj] * rd : 0.0;
-    if (jj + 1 < 16) {
-      a[jj + 1] -= f * ct[jj + 1];
-      W.colv[buf ^ 1][r] = a[jj + 1];
-      __builtin_amdgcn_sched_barrier(0);
-      const double dn = W.colv[buf ^ 1][c0 + jj + 1];
-      double ctn[16];
-#pragma unroll
-      for (int t = jj + 2; t < 16; ++t) ctn[t] = W.colv[buf ^ 1][c0 + t];
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int t = jj + 2; t < 16; ++t) a[t] -= f * ct[t];
-      d = dn;
-#pragma unroll
-      for (int t = jj + 2; t < 16; ++t) ct[t] = ctn[t];
+    for (int cc = 0; cc < 16; ++cc) {
+      const int t = c0 + cc;
+      const double x = (cc & 1) ? v[cc >> 1].y : v[cc >> 1].x;
+      a[cc] = (r >= c0 && r < m && t < b && (t <= r || r >= b)) ? x : 0.0;
     }
   }
+  CHOL_STAMP(30 + c0 / 16 * 4);
+  W.colp[0][r] = make_double2(a[0], a[1]);
+  __builtin_amdgcn_sched_barrier(0);
+  double2 q0 = W.colp[0][c0], q1 = W.colp[0][c0 + 1];
+  double2 ct[16];
+#pragma unroll
+  for (int t = 2; t < 16; ++t) ct[t] = W.colp[0][c0 + t];
+#pragma unroll
+  for (int jj = 0; jj < 16; jj += 2) {
+    const int j = c0 + jj;
+    if (j + 1 >= b) break;                   // uniform: a last single column needs no update
+    const int buf = (jj >> 1) & 1;
+    const double d0 = q0.x, e = q1.x, d1 = q1.y;
+    const double rdet = recip(d0 * d1 - e * e);
+    const bool row = r > j + 1 && r < m;
+    const double u0 = a[jj], u1 = a[jj + 1];
+    const double f0 = row ? fma(u0, d1, -u1 * e) * rdet : 0.0;
+    const double f1 = row ? fma(u1, d0, -u0 * e) * rdet : 0.0;
+    if (jj + 2 < 16) {
+      a[jj + 2] = fma(-f1, ct[jj + 2].y, fma(-f0, ct[jj + 2].x, a[jj + 2]));
+      a[jj + 3] = fma(-f1, ct[jj + 3].y, fma(-f0, ct[jj + 3].x, a[jj + 3]));
+      W.colp[buf ^ 1][r] = make_double2(a[jj + 2], a[jj + 3]);
+      __builtin_amdgcn_sched_barrier(0);
+      const double2 q0n = W.colp[buf ^ 1][c0 + jj + 2], q1n = W.colp[buf ^ 1][c0 + jj + 3];
+      double2 ctn[16];
+#pragma unroll
+      for (int t = jj + 4; t < 16; ++t) ctn[t] = W.colp[buf ^ 1][c0 + t];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = jj + 4; t < 16; ++t) a[t] = fma(-f1, ct[t].y, fma(-f0, ct[t].x, a[t]));
+      q0 = q0n;
+      q1 = q1n;
+#pragma unroll
+      for (int t = jj + 4; t < 16; ++t) ct[t] = ctn[t];
+    }
+    // column j+1 to its 1 x 1 form (rows r > j; lane j+1 gets the pivot d1 - e^2/d0)
+    if (r > j && r < m) a[jj + 1] -= u0 * (e * recip(d0));
+  }
+  CHOL_STAMP(31 + c0 / 16 * 4);
   // own pivot (lanes c0..c0+15): d_r = a_rr
   double d_own = 1.0;
 #pragma unroll
@@ -261,17 +282,26 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
     if (r == c0 + cc) d_own = a[cc];
   if (r >= c0 && r < c0 + 16 && r < b && !(d_own > 0.0 && isfinite(d_own))) W.bad = 1;
   const double rs_own = 1.0 / sqrt(d_own);
-  if (r >= c0 && r < m) {
+  // broadcast the 16 scalings through LDS (in order within the wave)
+  W.rsv[r] = rs_own;
+  __builtin_amdgcn_sched_barrier(0);
+  double rs[16];
+  {
+    const double2* src = reinterpret_cast<const double2*>(&W.rsv[c0]);
 #pragma unroll
-    for (int cc = 0; cc < 16; ++cc) {
-      const int t = c0 + cc;
-      const double rs = readlane_f64(rs_own, c0 + cc);
-      double lv = 0.0;
-      if (t < b) {
-        if (t < r) lv = a[cc] * rs;
-        else if (t == r) lv = a[cc] * rs;   // sqrt(d_t) = d_t / sqrt(d_t)
+    for (int k = 0; k < 8; ++k) { const double2 x = src[k]; rs[2 * k] = x.x; rs[2 * k + 1] = x.y; }
+  }
+  if (r >= c0 && r < m) {
+    double2* dst = reinterpret_cast<double2*>(&T[r][c0]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      double lv[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int cc = 2 * k + h, t = c0 + cc;
+        lv[h] = (t < b && t <= r) ? a[cc] * rs[cc] : 0.0;   // t == r: sqrt(d_t) = d_t / sqrt(d_t)
       }
-      T[r][t] = lv;
+      dst[k] = make_double2(lv[0], lv[1]);
     }
   }
 }
@@ -476,9 +506,10 @@ __device__ inline bool flag_wait(int* flag, int* lds_ok) {
   return *lds_ok != 0;
 }
 
-__global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ Lm, int ld, int n,
-                                                   const double* __restrict__ Vall, double* __restrict__ y,
-                                                   int* __restrict__ flags, double* __restrict__ scal) {
+__global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A, const double* __restrict__ Lm,
+                                                   int ld, int n, const double* __restrict__ Vall,
+                                                   double* __restrict__ y, int* __restrict__ flags,
+                                                   double* __restrict__ scal) {
   __shared__ double zs[CB];
   __shared__ double ys[CB];
   __shared__ double part[4][CB];
@@ -489,7 +520,25 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ Lm
   const size_t lds = (size_t)ld;
   // thread (j = tid & 63, h = tid >> 6) sums rows i = h, h + 4, ... of a tile
   const int j = tid & 63, h = tid >> 6;
-  if (tid < CB) zs[tid] = tid < bsz ? Lm[(size_t)n * lds + s0 + tid] : 0.0;
+  if (n % CB == 0 && K == T - 1) {
+    // the rhs row starts a tile row of its own: no step factored it into
+    // z_K, the last trailing update left A_{n,K}; z_K = V_K A_{n,K}^T
+    if (tid < CB) ys[tid] = A[(size_t)n * lds + s0 + tid];
+    __syncthreads();
+    const double* V = Vall + (size_t)K * CB * CB;
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = h + 4 * q;
+      t += V[(size_t)j * CB + i] * ys[i];
+    }
+    part[h][j] = t;
+    __syncthreads();
+    if (tid < CB) zs[tid] = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+    __syncthreads();
+  } else if (tid < CB) {
+    zs[tid] = tid < bsz ? Lm[(size_t)n * lds + s0 + tid] : 0.0;
+  }
   double acc = 0.0;
   bool good = true;
   for (int J = T - 1; J > K; --J) {
@@ -540,7 +589,7 @@ void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, hipStream_t s
     hipLaunchKernelGGL(k_chol_step, dim3(tc, tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf, W.scal);
   }
   (void)hipMemsetAsync(W.flags, 0, sizeof(int) * T, s);
-  hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.Lf, P.ld, n, W.Vbuf, W.y, W.flags, W.scal);
+  hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.flags, W.scal);
 }
 
 }  // namespace bahip

@@ -79,6 +79,9 @@ int main(int argc, char** argv) {
       if (verbose && k >= 0 && (k < 1 || k == T / 2))
         printf("    stage %llu  gemm1 %llu  store %llu  gemm2 %llu  rest %llu\n", st_h[20] - st_h[0], st_h[21] - st_h[20],
                st_h[22] - st_h[21], st_h[23] - st_h[22], st_h[1] - st_h[23]);
+      if (verbose && k >= 0 && (k < 1 || k == T / 2))
+        printf("    sub-panel 0: load %llu  columns %llu  scale+store %llu\n", st_h[30] - st_h[2], st_h[31] - st_h[30],
+               st_h[10] - st_h[31]);
       if (verbose && (k < 1 || k == T / 2))
         printf("    sub-panels (sweep / update cycles): %llu/%llu %llu/%llu %llu/%llu %llu/%llu\n", st_h[10] - st_h[2],
                st_h[11] - st_h[10], st_h[12] - st_h[11], st_h[13] - st_h[12], st_h[14] - st_h[13], st_h[15] - st_h[14],
@@ -87,7 +90,7 @@ int main(int argc, char** argv) {
     }
     CK(hipMemset(dF, 0, sizeof(int) * T));
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dL, ld, n, dV, dy, dF, dS);
+    hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dA, dL, ld, n, dV, dy, dF, dS);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float mb;
