@@ -41,10 +41,11 @@ __device__ unsigned long long g_stamps[64];
 #endif
 
 // Stage a 64x64 block M[r0 + i][c0 + j] (i < rmax - r0, j < cmax - c0, else
-// 0) into LDS; all 8 loads per thread are issued before any LDS store.
-__device__ inline void stage64(double (*D)[LDP], const double* __restrict__ M, size_t ld, int r0, int c0, int rmax,
-                               int cmax) {
-  double2 v[8];
+// 0) into LDS: tile_load issues the 8 16-B loads of a thread, tile_put
+// writes them to LDS — several tiles' loads go out before the first store.
+struct TileRegs { double2 v[8]; };
+__device__ inline TileRegs tile_fetch(const double* __restrict__ M, size_t ld, int r0, int c0, int rmax, int cmax) {
+  TileRegs t;
   const int tid = threadIdx.x;
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
@@ -53,19 +54,27 @@ __device__ inline void stage64(double (*D)[LDP], const double* __restrict__ M, s
     const int ri = r0 + i, cj = c0 + j;
     const double* src = M + (size_t)ri * ld + cj;
     if (ri < rmax && cj + 1 < cmax && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
-      v[it] = *reinterpret_cast<const double2*>(src);
+      t.v[it] = *reinterpret_cast<const double2*>(src);
     } else {
-      v[it].x = (ri < rmax && cj < cmax) ? src[0] : 0.0;
-      v[it].y = (ri < rmax && cj + 1 < cmax) ? src[1] : 0.0;
+      t.v[it].x = (ri < rmax && cj < cmax) ? src[0] : 0.0;
+      t.v[it].y = (ri < rmax && cj + 1 < cmax) ? src[1] : 0.0;
     }
   }
+  return t;
+}
+__device__ inline void tile_put(double (*D)[LDP], const TileRegs& t) {
+  const int tid = threadIdx.x;
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
     const int e = tid + 256 * it;
     const int i = e >> 5, j = (e & 31) * 2;
-    D[i][j] = v[it].x;
-    D[i][j + 1] = v[it].y;
+    D[i][j] = t.v[it].x;
+    D[i][j + 1] = t.v[it].y;
   }
+}
+__device__ inline void stage64(double (*D)[LDP], const double* __restrict__ M, size_t ld, int r0, int c0, int rmax,
+                               int cmax) {
+  tile_put(D, tile_fetch(M, ld, r0, c0, rmax, cmax));
 }
 
 // C (64x64, distributed as 4 waves x 2x2 MFMA tiles of 16x16) = sum_k Xs[i][k] Ys[j][k]
@@ -86,6 +95,41 @@ __device__ inline void mfma_xyT_64(const double (*Xs)[LDP], const double (*Ys)[L
     acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, y0, acc[1][0], 0, 0, 0);
     acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, y1, acc[1][1], 0, 0, 0);
   }
+}
+
+// Lower 16x16 tiles (ti >= tj) of C = sum_k Xs[i][k] Xs[j][k] (a symmetric
+// product): 10 tiles over 4 waves (3, 3, 2, 2) instead of 16 (4 each).
+__device__ inline int lower_tiles_of(int w, int (*tl)[2]) {
+  constexpr int T[10][2] = {{0, 0}, {1, 0}, {1, 1}, {2, 0}, {2, 1}, {2, 2}, {3, 0}, {3, 1}, {3, 2}, {3, 3}};
+  const int first = w == 0 ? 0 : (w == 1 ? 3 : (w == 2 ? 6 : 8));
+  const int cnt = w < 2 ? 3 : 2;
+  for (int q = 0; q < 3; ++q) { tl[q][0] = T[first + min(q, cnt - 1)][0]; tl[q][1] = T[first + min(q, cnt - 1)][1]; }
+  return cnt;
+}
+__device__ inline void mfma_xxT_lower_sub(const double (*Xs)[LDP], double (*D)[LDP]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  int tl[3][2];
+  const int cnt = lower_tiles_of(w, tl);
+  d4 acc[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int k0 = 0; k0 < CB; k0 += 4) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      if (q < cnt) {
+        const double x = Xs[16 * tl[q][0] + li][k0 + lk];
+        const double y = Xs[16 * tl[q][1] + li][k0 + lk];
+        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc[q], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    if (q < cnt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) D[16 * tl[q][0] + lk + 4 * g][16 * tl[q][1] + li] -= acc[q][g];
 }
 
 // accumulator element (a, b, reg) -> tile-local (row, col); v_mfma_f64_16x16x4
@@ -399,10 +443,14 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
     const int b = min(CB, n - s);             // its order
     const int m = min(CB, nrows - s);         // rows in the tile (b or b + 1 with the rhs row)
     CHOL_STAMP(0);
-    stage64(S0, A, lds, s, s, nrows, s + b);  // A_{k+1,k+1} (+ rhs row)
     if (k >= 0) {
-      stage64(S1, A, lds, s, kc, nrows, kc + kb);   // A_{k+1,k}
-      stage64(S2, Vk, CB, 0, 0, CB, CB);
+      // the three tiles' loads all in flight before the first LDS store
+      const TileRegs tA = tile_fetch(A, lds, s, s, nrows, s + b);      // A_{k+1,k+1} (+ rhs row)
+      const TileRegs tP = tile_fetch(A, lds, s, kc, nrows, kc + kb);   // A_{k+1,k}
+      const TileRegs tV = tile_fetch(Vk, CB, 0, 0, CB, CB);
+      tile_put(S0, tA);
+      tile_put(S1, tP);
+      tile_put(S2, tV);
       __syncthreads();
       CHOL_STAMP(20);
       d4 acc[2][2];
@@ -410,22 +458,44 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
       __syncthreads();
       CHOL_STAMP(21);
       acc_to_lds(S1, acc, 0);
+      // L_{k+1,k} straight from the accumulators (16 consecutive columns per
+      // 16 lanes); the stores drain while the factorization runs
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            int rr, cc;
+            acc_pos(a, bb, g, &rr, &cc);
+            if (rr < m && cc < kb) L[(size_t)(s + rr) * ld + kc + cc] = acc[a][bb][g];
+          }
       __syncthreads();
-      lds_to_global(S1, L, lds, s, kc, m, kb);       // L_{k+1,k}
       CHOL_STAMP(22);
-      mfma_xyT_64(S1, S1, acc);              // P P^T
+      mfma_xxT_lower_sub(S1, S0);            // C = A - P P^T (lower tiles)
       CHOL_STAMP(23);
-      acc_to_lds(S0, acc, 1);                // C = A - P P^T
+    } else {
+      stage64(S0, A, lds, s, s, nrows, s + b);
     }
     if (threadIdx.x == 0) cw.bad = 0;
     CHOL_STAMP(1);
     factor_invert_blk(S0, S2, S1, cw, b, m);   // rows b..m-1 (rhs) come out as L rows too
     CHOL_STAMP(5);
     __syncthreads();
-    for (int e = threadIdx.x; e < CB * CB; e += 256) {
-      const int i = e / CB, j = e % CB;
-      if (i < m && j < b && (j <= i)) L[(size_t)(s + i) * ld + s + j] = S0[i][j];
-      Vbuf[(size_t)(k + 1) * CB * CB + e] = (j <= i && i < b && j < b) ? S2[i][j] : (i == j ? 1.0 : 0.0);
+    // only V_{k+1} and the rhs row of L leave the workgroup: the diagonal L
+    // block itself is never read again (back substitution uses V)
+    {
+      double2* Vd = reinterpret_cast<double2*>(Vbuf + (size_t)(k + 1) * CB * CB);
+      for (int e2 = threadIdx.x; e2 < CB * CB / 2; e2 += 256) {
+        const int i = (2 * e2) / CB, j = (2 * e2) % CB;
+        double v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          v[h] = (j + h <= i && i < b && j + h < b) ? S2[i][j + h] : (i == j + h ? 1.0 : 0.0);
+        Vd[e2] = make_double2(v[0], v[1]);
+      }
+      if (m > b)
+        for (int j = threadIdx.x; j < b; j += 256) L[(size_t)(s + b) * ld + s + j] = S0[b][j];
     }
     CHOL_STAMP(6);
     if (threadIdx.x == 0 && cw.bad) scal[SL_CHOL_BAD] += 1.0;

@@ -1317,30 +1317,32 @@ __global__ __launch_bounds__(256) void k_residuals(DevProblem P, const double* _
   }
 }
 
-// Fold partials -> scalars (fixed order), then clear the partials.
-__global__ __launch_bounds__(1024) void k_reduce(double* __restrict__ part, double* __restrict__ scal,
-                                                 uint32_t sum_mask, uint32_t max_mask) {
-  __shared__ double lds[16];
-  for (int slot = 0; slot < kNumSlots; ++slot) {
-    const bool is_sum = (sum_mask >> slot) & 1u, is_max = (max_mask >> slot) & 1u;
-    if (!is_sum && !is_max) continue;
-    double* pp = part + (size_t)slot * kMaxBlocks;
-    double v = is_max ? 0.0 : 0.0;
-    for (int i = threadIdx.x; i < kMaxBlocks; i += blockDim.x) {
-      v = is_max ? fmax(v, pp[i]) : v + pp[i];
-      pp[i] = 0.0;
-    }
-    double res;
-    if (is_max) {
-      res = block_max1(v, lds);
-    } else {
-      double a[1] = {v}, o[1];
-      block_sum<1>(a, lds, o);
-      res = o[0];
-    }
-    if (threadIdx.x == 0) scal[slot] = res;
-    __syncthreads();
+// Fold partials -> scalars (fixed order), then clear the partials.  One
+// wave per slot (kNumSlots waves), no workgroup barrier: each lane folds a
+// fixed strided subset, then a fixed-order shuffle tree.
+__global__ __launch_bounds__(64 * kNumSlots) void k_reduce(double* __restrict__ part, double* __restrict__ scal,
+                                                           uint32_t sum_mask, uint32_t max_mask) {
+  const int slot = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool is_sum = (sum_mask >> slot) & 1u, is_max = (max_mask >> slot) & 1u;
+  if (!is_sum && !is_max) return;
+  double* pp = part + (size_t)slot * kMaxBlocks;
+  constexpr int PER = kMaxBlocks / 64;
+  double v[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) v[i] = pp[i * 64 + lane];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) pp[i * 64 + lane] = 0.0;
+  double x = 0.0;
+  if (is_max) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) x = fmax(x, v[i]);
+    x = wave_max(x);
+  } else {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) x += v[i];
+    x = wave_sum(x);
   }
+  if (lane == 0) scal[slot] = x;
 }
 
 // ---------------------------------------------------------------------------
@@ -1438,7 +1440,7 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
                      W.rec_c, W.pts_c, W.part);
 }
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, s, W.part, W.scal, sum_mask, max_mask);
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(64 * kNumSlots), 0, s, W.part, W.scal, sum_mask, max_mask);
 }
 void launch_residuals(const DevProblem& P, const double* rec, const double* pts, double* r_raw, hipStream_t s) {
   hipLaunchKernelGGL(k_residuals, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, rec, pts, r_raw);
