@@ -1236,64 +1236,75 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
 }
 
 // S_cc += s Hcc s + D^2 ;  b_c += s * g_c      (after any cross-rank reduction)
+// one thread per (camera, entry): 21 lower entries of the diagonal block and
+// 6 rhs entries (a thread per camera serialised ~50 dependent accesses)
 __global__ __launch_bounds__(256) void k_cam_add_diag(DevProblem P, const double* __restrict__ Hcc,
                                                       const double* __restrict__ gc, const double* __restrict__ scale_c,
                                                       const double* __restrict__ diag_c, double radius,
                                                       double* __restrict__ S) {
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= P.nvc) return;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.nvc * 27) return;
+  const int v = e / 27, k = e - v * 27;
   const size_t ld = (size_t)P.ld;
-  double s[6];
-  for (int a = 0; a < 6; ++a) s[a] = scale_c[(size_t)v * 6 + a];
-  for (int a = 0; a < 6; ++a) {
-    for (int b = 0; b <= a; ++b) {
-      double h = Hcc[(size_t)v * 21 + tri(a, b)] * s[a] * s[b];
-      if (a == b) {
-        const double D = sqrt(diag_c[(size_t)v * 6 + a] / radius);
-        h += D * D;
-      }
-      S[(size_t)(6 * v + a) * ld + 6 * v + b] += h;
+  if (k < 21) {
+    int a = 0;
+    while ((a + 1) * (a + 2) / 2 <= k) ++a;
+    const int b = k - a * (a + 1) / 2;
+    double h = Hcc[(size_t)v * 21 + k] * scale_c[(size_t)v * 6 + a] * scale_c[(size_t)v * 6 + b];
+    if (a == b) {
+      const double D = sqrt(diag_c[(size_t)v * 6 + a] / radius);
+      h += D * D;
     }
-    S[(size_t)P.n * ld + 6 * v + a] += gc[(size_t)v * 6 + a] * s[a];
+    S[(size_t)(6 * v + a) * ld + 6 * v + b] += h;
+  } else {
+    const int a = k - 21;
+    S[(size_t)P.n * ld + 6 * v + a] += gc[(size_t)v * 6 + a] * scale_c[(size_t)v * 6 + a];
   }
 }
 
 // ---------------------------------------------------------------------------
 // candidate cameras: x' = x + s * (-y), value-only records at x'
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_cam_candidate(DevProblem P, const double* __restrict__ cams,
-                                                       const double* __restrict__ y, const double* __restrict__ scale_c,
-                                                       double* __restrict__ cams_c, double* __restrict__ delta_c,
-                                                       double* __restrict__ rec_c, double* __restrict__ part) {
+// one 64-lane block per camera: lanes 0..5 form the step, every lane
+// evaluates the (cheap) Rodrigues and writes record entries lane, lane + 64
+__global__ __launch_bounds__(64) void k_cam_candidate(DevProblem P, const double* __restrict__ cams,
+                                                      const double* __restrict__ y, const double* __restrict__ scale_c,
+                                                      double* __restrict__ cams_c, double* __restrict__ delta_c,
+                                                      double* __restrict__ rec_c, double* __restrict__ part) {
   __shared__ double lds[2 * 16];
+  const int lane = threadIdx.x;
   double acc[2] = {0.0, 0.0};  // step2, bad
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < P.nc; c += gridDim.x * blockDim.x) {
+  for (int c = blockIdx.x; c < P.nc; c += gridDim.x) {
     const int v = P.vc[c];
-    double x[6], xc[6];
-    for (int a = 0; a < 6; ++a) x[a] = cams[6 * c + a];
-    if (v >= 0) {
-      for (int a = 0; a < 6; ++a) {
-        const double step = -y[6 * v + a];
-        const double d = step * scale_c[(size_t)v * 6 + a];
+    double xc[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const double x = cams[6 * c + a];
+      double d = 0.0;
+      if (v >= 0) d = (-y[6 * v + a]) * scale_c[(size_t)v * 6 + a];
+      xc[a] = v >= 0 ? x + d : x;
+      if (lane == a && v >= 0) {
         delta_c[(size_t)v * 6 + a] = d;
-        xc[a] = x[a] + d;
-        const double e = x[a] - xc[a];
+        const double e = x - xc[a];
         acc[0] += e * e;
         if (!isfinite(d)) acc[1] += 1.0;
       }
-    } else {
-      for (int a = 0; a < 6; ++a) xc[a] = x[a];
     }
-    for (int a = 0; a < 6; ++a) cams_c[6 * c + a] = xc[a];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+      if (lane == a) cams_c[6 * c + a] = xc[a];
     double* o = rec_c + (size_t)c * kCamRec;
-    for (int k = 0; k < 9; ++k) o[kRecK + k] = (double)P.K[9 * c + k];
-    if (P.cam_fixed && P.cam_fixed[c]) {
-      for (int k = 0; k < 16; ++k) o[k] = (double)P.extr[16 * c + k];
-    } else {
-      double R[9];
-      angle_axis_to_R(xc, R);
-      for (int i = 0; i < 9; ++i) o[kRecR + i] = R[i];
-      for (int k = 0; k < 3; ++k) o[kRecT + k] = xc[3 + k];
+    const bool fixed = P.cam_fixed && P.cam_fixed[c];
+    double R[9];
+    if (!fixed) angle_axis_to_R(xc, R);
+    for (int e = lane; e < kRecL; e += 64) {
+      double val = 0.0;
+      if (e >= kRecK && e < kRecK + 9) val = (double)P.K[9 * c + e - kRecK];
+      else if (fixed) val = e < 16 ? (double)P.extr[16 * c + e] : 0.0;
+      else if (e < 9) val = R[e];
+      else if (e >= kRecT && e < kRecT + 3) val = xc[3 + e - kRecT];
+      else if (e < kRecK) continue;   // dR/dw: not used at a candidate point
+      o[e] = val;
     }
   }
   double out[2];
@@ -1420,12 +1431,13 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
 }
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
   if (P.nvc == 0) return;
-  hipLaunchKernelGGL(k_cam_add_diag, dim3((P.nvc + 255) / 256), dim3(256), 0, s, P, W.Hcc, W.gc, W.scale_c, W.diag_c,
-                     radius, W.S);
+  hipLaunchKernelGGL(k_cam_add_diag, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.Hcc, W.gc, W.scale_c,
+                     W.diag_c, radius, W.S);
 }
 void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
-  hipLaunchKernelGGL(k_cam_candidate, dim3(grid_for(P.nc)), dim3(kThreads), 0, s, P, W.cams, W.y, W.scale_c,
-                     W.cams_c, W.delta_c, W.rec_c, W.part);
+  if (P.nc == 0) return;
+  hipLaunchKernelGGL(k_cam_candidate, dim3(P.nc < kMaxBlocks ? P.nc : kMaxBlocks), dim3(64), 0, s, P, W.cams, W.y,
+                     W.scale_c, W.cams_c, W.delta_c, W.rec_c, W.part);
 }
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
   hipLaunchKernelGGL(k_backsub, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p, W.W, W.u,
