@@ -215,6 +215,41 @@ __device__ inline void project_value(const double* __restrict__ cr, bool cvar, d
 // ---------------------------------------------------------------------------
 constexpr int kJR = 20;
 constexpr int kStageLd = kJR + 1;   // LDS row stride of staged records
+// Storage: the record is split in two arrays inside the JR buffer so that
+// readers of one half fetch only that half's cache lines:
+//   JA = JR           [no][12]  fields 0..11   (camera rows: 96 B)
+//   JB = JR + 12 no   [no][8]   fields 12..19  (point rows + residual: 64 B)
+constexpr int kJA = 12, kJB = 8;
+__device__ inline const double* jr_a(const double* JR, int o) { return JR + (size_t)o * kJA; }
+__device__ inline const double* jr_b(const double* JR, int no, int o) {
+  return JR + (size_t)kJA * no + (size_t)o * kJB;
+}
+// the 64 records of the chunk at `base` as 10 coalesced 1 KiB wave loads
+// (6 of JA, 4 of JB), indices clamped (unconditional loads)
+__device__ inline void jr_chunk_load(const double* __restrict__ JR, int no, int base, int lane, double2 (&t)[10]) {
+  const double2* A2 = reinterpret_cast<const double2*>(JR);
+  const double2* B2 = reinterpret_cast<const double2*>(JR + (size_t)kJA * no);
+  const int lastA = (kJA / 2) * no - 1, lastB = (kJB / 2) * no - 1;
+#pragma unroll
+  for (int it = 0; it < kJA / 2; ++it) t[it] = A2[min((kJA / 2) * base + it * 64 + lane, lastA)];
+#pragma unroll
+  for (int it = 0; it < kJB / 2; ++it) t[kJA / 2 + it] = B2[min((kJB / 2) * base + it * 64 + lane, lastB)];
+}
+// scatter them into the wave's LDS rows (record fields 0..19, stride kStageLd)
+__device__ inline void jr_chunk_stage(double* st, int lane, const double2 (&t)[10]) {
+#pragma unroll
+  for (int it = 0; it < kJA / 2; ++it) {
+    const int e = it * 64 + lane, r = e / (kJA / 2), f = 2 * (e - r * (kJA / 2));
+    st[r * kStageLd + f] = t[it].x;
+    st[r * kStageLd + f + 1] = t[it].y;
+  }
+#pragma unroll
+  for (int it = 0; it < kJB / 2; ++it) {
+    const int e = it * 64 + lane, r = e / (kJB / 2), f = kJA + 2 * (e - r * (kJB / 2));
+    st[r * kStageLd + f] = t[kJA / 2 + it].x;
+    st[r * kStageLd + f + 1] = t[kJA / 2 + it].y;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // linearisation: one thread per observation (sorted by point)
@@ -447,7 +482,8 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
       continue;
     }
     const int nrec = min(64, P.no - base);
-    double2* dst = reinterpret_cast<double2*>(JR + (size_t)base * kJR);
+    double2* dA = reinterpret_cast<double2*>(JR) + (size_t)(kJA / 2) * base;
+    double2* dB = reinterpret_cast<double2*>(JR + (size_t)kJA * P.no) + (size_t)(kJB / 2) * base;
 #pragma unroll
     for (int h = 0; h < 64 / ROWS; ++h) {
       // all LDS reads into distinct registers first, then the stores: a
@@ -460,27 +496,43 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
         for (int k = 0; k < kJR; ++k) row[k] = out[k];
       }
       wave_lds_sync();
-      constexpr int NIT = ROWS * kJR / 2 / 64;
-      double2 v[NIT];
+      constexpr int NA = ROWS * (kJA / 2) / 64, NB = ROWS * (kJB / 2) / 64;
+      double2 va[NA], vb[NB];
 #pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        const int e = it * 64 + lane;
-        const int r = e / (kJR / 2), f = 2 * (e - r * (kJR / 2));
-        v[it] = make_double2(stage[r * kStageLd + f], stage[r * kStageLd + f + 1]);
+      for (int it = 0; it < NA; ++it) {
+        const int e = it * 64 + lane, r = e / (kJA / 2), f = 2 * (e - r * (kJA / 2));
+        va[it] = make_double2(stage[r * kStageLd + f], stage[r * kStageLd + f + 1]);
+      }
+#pragma unroll
+      for (int it = 0; it < NB; ++it) {
+        const int e = it * 64 + lane, r = e / (kJB / 2), f = kJA + 2 * (e - r * (kJB / 2));
+        vb[it] = make_double2(stage[r * kStageLd + f], stage[r * kStageLd + f + 1]);
       }
       wave_lds_sync();
+      double2* dAh = dA + h * ROWS * (kJA / 2);
+      double2* dBh = dB + h * ROWS * (kJB / 2);
       if (MODE == 1) {
 #pragma unroll
-        for (int it = 0; it < NIT; ++it)
-          if (v[it].x == 1234.5678) dst[h * ROWS * (kJR / 2) + it * 64 + lane] = v[it];
+        for (int it = 0; it < NA; ++it)
+          if (va[it].x == 1234.5678) dAh[it * 64 + lane] = va[it];
+#pragma unroll
+        for (int it = 0; it < NB; ++it)
+          if (vb[it].x == 1234.5678) dBh[it * 64 + lane] = vb[it];
       } else if (h * ROWS + ROWS <= nrec) {   // full: unconditional stores
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) dst[h * ROWS * (kJR / 2) + it * 64 + lane] = v[it];
+        for (int it = 0; it < NA; ++it) dAh[it * 64 + lane] = va[it];
+#pragma unroll
+        for (int it = 0; it < NB; ++it) dBh[it * 64 + lane] = vb[it];
       } else {
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) {
+        for (int it = 0; it < NA; ++it) {
           const int e = it * 64 + lane;
-          if (h * ROWS + e / (kJR / 2) < nrec) dst[h * ROWS * (kJR / 2) + e] = v[it];
+          if (h * ROWS + e / (kJA / 2) < nrec) dAh[e] = va[it];
+        }
+#pragma unroll
+        for (int it = 0; it < NB; ++it) {
+          const int e = it * 64 + lane;
+          if (h * ROWS + e / (kJB / 2) < nrec) dBh[e] = vb[it];
         }
       }
     }
@@ -578,10 +630,13 @@ __global__ __launch_bounds__(NT) void k_linearize_lds_t(DevProblem P, const doub
 }
 constexpr int kLinNT = 512, kLinRows = 64;    // product configuration (tools/lin_probe.hip)
 
-__device__ inline void load_jr(const double* __restrict__ JR, int o, double (&v)[kJR]) {
-  const double2* s = reinterpret_cast<const double2*>(JR + (size_t)o * kJR);
+__device__ inline void load_jr(const double* __restrict__ JR, int no, int o, double (&v)[kJR]) {
+  const double2* a = reinterpret_cast<const double2*>(jr_a(JR, o));
+  const double2* b = reinterpret_cast<const double2*>(jr_b(JR, no, o));
 #pragma unroll
-  for (int k = 0; k < kJR / 2; ++k) { const double2 t = s[k]; v[2 * k] = t.x; v[2 * k + 1] = t.y; }
+  for (int k = 0; k < kJA / 2; ++k) { const double2 t = a[k]; v[2 * k] = t.x; v[2 * k + 1] = t.y; }
+#pragma unroll
+  for (int k = 0; k < kJB / 2; ++k) { const double2 t = b[k]; v[kJA + 2 * k] = t.x; v[kJA + 2 * k + 1] = t.y; }
 }
 
 // ---------------------------------------------------------------------------
@@ -601,7 +656,7 @@ __global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const doub
     double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
     const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
     for (int o = o0; o < o1; ++o) {
-      const double2* s = reinterpret_cast<const double2*>(JR + (size_t)o * kJR + 12);
+      const double2* s = reinterpret_cast<const double2*>(jr_b(JR, P.no, o));
       const double2 t0 = s[0], t1 = s[1], t2 = s[2], t3 = s[3];
       const double jp[2][3] = {{t0.x, t0.y, t1.x}, {t1.y, t2.x, t2.y}};
       const double rr[2] = {t3.x, t3.y};
@@ -659,11 +714,11 @@ __global__ __launch_bounds__(256) void k_cam_assemble(DevProblem P, const double
   const int i0 = P.cam_off[v], i1 = P.cam_off[v + 1];
   for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int o = P.cam_obs[i];
-    const double2* s = reinterpret_cast<const double2*>(JR + (size_t)o * kJR);
+    const double2* s = reinterpret_cast<const double2*>(jr_a(JR, o));
     double jc[12];
 #pragma unroll
     for (int k = 0; k < 6; ++k) { const double2 t = s[k]; jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
-    const double2 rt = s[9];
+    const double2 rt = reinterpret_cast<const double2*>(jr_b(JR, P.no, o))[3];
     const double rr[2] = {rt.x, rt.y};
 #pragma unroll
     for (int row = 0; row < 2; ++row) {
@@ -808,13 +863,10 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
   double* st = stage + w * (64 * kStageLd);
   const int step = gridDim.x * WAVES * 64;
   const size_t np = (size_t)P.np;
-  const int last2 = P.no * (kJR / 2) - 1;
-  const double2* JR2 = reinterpret_cast<const double2*>(JR);
   for (int base = (blockIdx.x * WAVES + w) * 64; base < P.no; base += step) {
     const int o = base + lane, oc = min(o, P.no - 1);
     double2 t[kJR / 2];
-#pragma unroll
-    for (int it = 0; it < kJR / 2; ++it) t[it] = JR2[min(base * (kJR / 2) + it * 64 + lane, last2)];
+    jr_chunk_load(JR, P.no, base, lane, t);
     const int c = P.obs_cam[oc], p = P.obs_pt[oc];
     const int v = P.vc[c];
     const bool live = o < P.no && v >= 0 && P.pt_var[p];
@@ -824,13 +876,7 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
     const double s0 = scale_p[p], s1 = scale_p[np + p], s2 = scale_p[2 * np + p];
     const double i00 = Linv[p], i10 = Linv[np + p], i11 = Linv[2 * np + p];
     const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
-#pragma unroll
-    for (int it = 0; it < kJR / 2; ++it) {
-      const int e = it * 64 + lane;
-      const int r = e / (kJR / 2), f = 2 * (e - r * (kJR / 2));
-      st[r * kStageLd + f] = t[it].x;
-      st[r * kStageLd + f + 1] = t[it].y;
-    }
+    jr_chunk_stage(st, lane, t);
     wave_lds_sync();
     double j[18];
 #pragma unroll
@@ -947,7 +993,7 @@ __global__ __launch_bounds__(256) void k_candidate(DevProblem P, const double* _
     const int c = P.obs_cam[o], p = P.obs_pt[o];
     const int v = P.vc[c];
     double j[kJR];
-    load_jr(JR, o, j);
+    load_jr(JR, P.no, o, j);
     double jd0 = 0.0, jd1 = 0.0;
     if (v >= 0) {
       const double* dc = delta_c + (size_t)v * 6;
@@ -1037,29 +1083,20 @@ __global__ __launch_bounds__(kLinLdsThreads) void k_candidate_lds(DevProblem P, 
   constexpr int WAVES = kLinLdsThreads / 64;
   double* st = stage + w * (64 * kStageLd);
   const int step = gridDim.x * WAVES * 64;
-  const int last2 = P.no * (kJR / 2) - 1;
-  const double2* JR2 = reinterpret_cast<const double2*>(JR);
   int base = (blockIdx.x * WAVES + w) * 64;
   if (P.no == 0) base = P.no;
   double2 t[kJR / 2];
   int c = 0, p = 0;
   float2 uv = make_float2(0.f, 0.f);
   if (base < P.no) {
-#pragma unroll
-    for (int it = 0; it < kJR / 2; ++it) t[it] = JR2[min(base * (kJR / 2) + it * 64 + lane, last2)];
+    jr_chunk_load(JR, P.no, base, lane, t);
     const int oc = min(base + lane, P.no - 1);
     c = P.obs_cam[oc]; p = P.obs_pt[oc]; uv = P.uv[oc];
   }
   for (; base < P.no; base += step) {
     const int o = base + lane;
     // stage this chunk's records
-#pragma unroll
-    for (int it = 0; it < kJR / 2; ++it) {
-      const int e = it * 64 + lane;
-      const int r = e / (kJR / 2), f = 2 * (e - r * (kJR / 2));
-      st[r * kStageLd + f] = t[it].x;
-      st[r * kStageLd + f + 1] = t[it].y;
-    }
+    jr_chunk_stage(st, lane, t);
     const double dp0 = delta_p[3 * p], dp1 = delta_p[3 * p + 1], dp2 = delta_p[3 * p + 2];
     const double X0 = pts_c[3 * p], X1 = pts_c[3 * p + 1], X2 = pts_c[3 * p + 2];
     const bool cfix = P.cam_fixed && P.cam_fixed[c];
@@ -1068,8 +1105,7 @@ __global__ __launch_bounds__(kLinLdsThreads) void k_candidate_lds(DevProblem P, 
     int cn = c, pn = p;
     float2 uvn = uv;
     if (nb < P.no) {
-#pragma unroll
-      for (int it = 0; it < kJR / 2; ++it) t[it] = JR2[min(nb * (kJR / 2) + it * 64 + lane, last2)];
+      jr_chunk_load(JR, P.no, nb, lane, t);
       const int oc = min(nb + lane, P.no - 1);
       cn = P.obs_cam[oc]; pn = P.obs_pt[oc]; uvn = P.uv[oc];
     }

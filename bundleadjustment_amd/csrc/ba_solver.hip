@@ -693,17 +693,18 @@ int ba_linearize(ba_ctx* ctx, double* r, double* J, double* cost) {
     ba_default_options(&o);
     LinResult L = linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
     const int no = ctx->no;
-    constexpr int kJR = 20;  // record layout of ba_kernels.hip
-    std::vector<double> rec(kJR * (size_t)no);
+    // record layout of ba_kernels.hip: JA [no][12] (Jc rows) then JB [no][8] (Jp rows, r)
+    std::vector<double> rec(20 * (size_t)no);
     HIP_OK(hipMemcpy(rec.data(), ctx->W.JR, sizeof(double) * rec.size(), hipMemcpyDeviceToHost));
     for (int s = 0; s < no; ++s) {
       const int o2 = ctx->perm[s];
-      const double* q = &rec[(size_t)s * kJR];
-      if (r) { r[2 * o2] = q[18]; r[2 * o2 + 1] = q[19]; }
+      const double* qa = &rec[(size_t)s * 12];
+      const double* qb = &rec[(size_t)12 * no + (size_t)s * 8];
+      if (r) { r[2 * o2] = qb[6]; r[2 * o2 + 1] = qb[7]; }
       if (J)
         for (int row = 0; row < 2; ++row) {
-          for (int k = 0; k < 6; ++k) J[(size_t)o2 * 18 + row * 9 + k] = q[row * 6 + k];
-          for (int k = 0; k < 3; ++k) J[(size_t)o2 * 18 + row * 9 + 6 + k] = q[12 + row * 3 + k];
+          for (int k = 0; k < 6; ++k) J[(size_t)o2 * 18 + row * 9 + k] = qa[row * 6 + k];
+          for (int k = 0; k < 3; ++k) J[(size_t)o2 * 18 + row * 9 + 6 + k] = qb[row * 3 + k];
         }
     }
     if (cost) *cost = L.cost;
