@@ -43,7 +43,14 @@ __device__ unsigned long long g_stamps[64];
 // Stage a 64x64 block M[r0 + i][c0 + j] (i < rmax - r0, j < cmax - c0, else
 // 0) into LDS: tile_load issues the 8 16-B loads of a thread, tile_put
 // writes them to LDS — several tiles' loads go out before the first store.
+// Branch-free (a load under a divergent branch gets its own vmcnt(0) wait,
+// which serialised the 24 loads of the critical stage): every lane loads a
+// 16-B pair from a clamped in-range address and zeroes what is outside the
+// tile.  LOWER: pairs strictly above the diagonal are redirected to the
+// row's diagonal pair (a line another lane fetches anyway) and zeroed.
+// Needs ld even and cmax - c0 >= 2 (n = 6 * cameras).
 struct TileRegs { double2 v[8]; };
+template <bool LOWER = false>
 __device__ inline TileRegs tile_fetch(const double* __restrict__ M, size_t ld, int r0, int c0, int rmax, int cmax) {
   TileRegs t;
   const int tid = threadIdx.x;
@@ -51,14 +58,13 @@ __device__ inline TileRegs tile_fetch(const double* __restrict__ M, size_t ld, i
   for (int it = 0; it < 8; ++it) {
     const int e = tid + 256 * it;          // 2048 double2
     const int i = e >> 5, j = (e & 31) * 2;
-    const int ri = r0 + i, cj = c0 + j;
-    const double* src = M + (size_t)ri * ld + cj;
-    if (ri < rmax && cj + 1 < cmax && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
-      t.v[it] = *reinterpret_cast<const double2*>(src);
-    } else {
-      t.v[it].x = (ri < rmax && cj < cmax) ? src[0] : 0.0;
-      t.v[it].y = (ri < rmax && cj + 1 < cmax) ? src[1] : 0.0;
-    }
+    const bool up = LOWER && j > i;
+    const int ri = r0 + i, cj = c0 + (up ? (i & ~1) : j);
+    const int ric = min(ri, rmax - 1), cjc = min(cj, cmax - 2) & ~1;
+    const double2 v = *reinterpret_cast<const double2*>(M + (size_t)ric * ld + cjc);
+    const bool rok = ri < rmax && !up;
+    t.v[it].x = (rok && cj < cmax) ? v.x : 0.0;
+    t.v[it].y = (rok && cj + 1 < cmax) ? v.y : 0.0;
   }
   return t;
 }
@@ -132,6 +138,24 @@ __device__ inline void mfma_xxT_lower_sub(const double (*Xs)[LDP], double (*D)[L
       for (int g = 0; g < 4; ++g) D[16 * tl[q][0] + lk + 4 * g][16 * tl[q][1] + li] -= acc[q][g];
 }
 
+// P = Xs V^T with V lower triangular (V[j][k] = 0 for k > j): wave w owns
+// the row strip 16w..16w+15, and output column tile bc needs only k <
+// 16 (bc + 1) -> 40 MFMAs per wave (the square product: 64).
+// acc[bc] element g: row 16w + (lane >> 4) + 4g, col 16bc + (lane & 15).
+__device__ inline void mfma_xVT_strip(const double (*Xs)[LDP], const double (*Vs)[LDP], d4 acc[4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int bc = 0; bc < 4; ++bc) acc[bc] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k0 = 0; k0 < CB; k0 += 4) {
+    const double x = Xs[16 * w + li][k0 + lk];
+#pragma unroll
+    for (int bc = 0; bc < 4; ++bc)
+      if (k0 < 16 * (bc + 1)) acc[bc] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, Vs[16 * bc + li][k0 + lk], acc[bc], 0, 0, 0);
+  }
+}
+
 // accumulator element (a, b, reg) -> tile-local (row, col); v_mfma_f64_16x16x4
 // D layout: col = lane & 15, row = (lane >> 4) + 4 * reg
 __device__ inline void acc_pos(int a, int b, int reg, int* row, int* col) {
@@ -197,6 +221,15 @@ __device__ __forceinline__ double recip(double d) {
   y = fma(y, e, y);
   e = fma(-d, y, 1.0);
   return fma(y, e, y);
+}
+
+// 1/sqrt(d) to ~1 ulp: hardware estimate + two Newton steps (IEEE sqrt and
+// division are long instruction sequences on the column chain)
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  double y = __builtin_amdgcn_rsq(d);
+  const double h = 0.5 * d;
+  y = fma(y, fma(-h * y, y, 0.5), y);
+  return fma(y, fma(-h * y, y, 0.5), y);
 }
 
 // D (16x16, MFMA accumulator layout) += sgn * sum_{k < K} Xs[xr + i][xc + k] * Ys[yr + j][yc + k]
@@ -324,10 +357,12 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
 #pragma unroll
   for (int cc = 0; cc < 16; ++cc)
     if (r == c0 + cc) d_own = a[cc];
-  if (r >= c0 && r < c0 + 16 && r < b && !(d_own > 0.0 && isfinite(d_own))) W.bad = 1;
-  const double rs_own = 1.0 / sqrt(d_own);
-  // broadcast the 16 scalings through LDS (in order within the wave)
-  W.rsv[r] = rs_own;
+  const bool own = r >= c0 && r < c0 + 16;
+  if (own && r < b && !(d_own > 0.0 && isfinite(d_own))) W.bad = 1;
+  const double rs_own = rsqrt_nr(d_own);
+  // broadcast the 16 scalings through LDS (in order within the wave); they
+  // stay there as 1 / L_tt for the diagonal-block inverse
+  if (own) W.rsv[r] = rs_own;
   __builtin_amdgcn_sched_barrier(0);
   double rs[16];
   {
@@ -352,8 +387,8 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
 
 // X_pp = L_pp^-1 for the four 16x16 diagonal blocks, one wave each (lane
 // c < 16 solves L_pp x = e_c by forward substitution; L values are uniform
-// LDS broadcasts, 1/L_ii = 1/L_ii computed once per row).
-__device__ __forceinline__ void diag_inverse16(const double (*T)[LDP], double (*X)[LDP], int b) {
+// LDS broadcasts; 1/L_ii is the sweep's 1/sqrt(d_i), no divisions).
+__device__ __forceinline__ void diag_inverse16(const double (*T)[LDP], const double* rinv, double (*X)[LDP], int b) {
   const int w = threadIdx.x >> 6, c = threadIdx.x & 15;
   const int c0 = 16 * w;
   if (c0 >= b || (threadIdx.x & 63) >= 16) return;
@@ -363,7 +398,7 @@ __device__ __forceinline__ void diag_inverse16(const double (*T)[LDP], double (*
     double s = (i == c) ? 1.0 : 0.0;
 #pragma unroll
     for (int k = 0; k < i; ++k) s -= T[c0 + i][c0 + k] * x[k];
-    x[i] = (c0 + i < b) ? s / T[c0 + i][c0 + i] : 0.0;
+    x[i] = (c0 + i < b) ? s * rinv[c0 + i] : 0.0;   // rinv = 1 / L_ii from the sweep
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) X[c0 + i][c0 + c] = x[i];
@@ -397,7 +432,7 @@ __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z
     CHOL_STAMP(11 + 2 * p);
   }
   CHOL_STAMP(3);
-  diag_inverse16(T, X, b);
+  diag_inverse16(T, W.rsv, X, b);
   __syncthreads();
   // off-diagonal blocks of X = L^-1, by block distance dd
   for (int dd = 1; dd < 4; ++dd) {
@@ -445,31 +480,32 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
     CHOL_STAMP(0);
     if (k >= 0) {
       // the three tiles' loads all in flight before the first LDS store
-      const TileRegs tA = tile_fetch(A, lds, s, s, nrows, s + b);      // A_{k+1,k+1} (+ rhs row)
-      const TileRegs tP = tile_fetch(A, lds, s, kc, nrows, kc + kb);   // A_{k+1,k}
-      const TileRegs tV = tile_fetch(Vk, CB, 0, 0, CB, CB);
+      const TileRegs tA = tile_fetch<true>(A, lds, s, s, nrows, s + b);   // A_{k+1,k+1} (+ rhs row)
+      const TileRegs tP = tile_fetch(A, lds, s, kc, nrows, kc + kb);      // A_{k+1,k}
+      const TileRegs tV = tile_fetch<true>(Vk, CB, 0, 0, CB, CB);         // V_k (lower triangular)
       tile_put(S0, tA);
       tile_put(S1, tP);
       tile_put(S2, tV);
       __syncthreads();
       CHOL_STAMP(20);
-      d4 acc[2][2];
-      mfma_xyT_64(S1, S2, acc);              // P = A_{k+1,k} V_k^T
+      d4 acc[4];
+      mfma_xVT_strip(S1, S2, acc);           // P = A_{k+1,k} V_k^T
       __syncthreads();
       CHOL_STAMP(21);
-      acc_to_lds(S1, acc, 0);
-      // L_{k+1,k} straight from the accumulators (16 consecutive columns per
-      // 16 lanes); the stores drain while the factorization runs
+      // P -> LDS, and L_{k+1,k} straight from the accumulators (16
+      // consecutive columns per 16 lanes); the stores drain while the
+      // factorization runs
+      {
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb)
+        for (int bc = 0; bc < 4; ++bc)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            int rr, cc;
-            acc_pos(a, bb, g, &rr, &cc);
-            if (rr < m && cc < kb) L[(size_t)(s + rr) * ld + kc + cc] = acc[a][bb][g];
+            const int rr = 16 * w + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
+            S1[rr][cc] = acc[bc][g];
+            if (rr < m && cc < kb) L[(size_t)(s + rr) * ld + kc + cc] = acc[bc][g];
           }
+      }
       __syncthreads();
       CHOL_STAMP(22);
       mfma_xxT_lower_sub(S1, S0);            // C = A - P P^T (lower tiles)
