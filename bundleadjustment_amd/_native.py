@@ -75,6 +75,13 @@ class ba_prune_problem(C.Structure):
     ]
 
 
+class ba_pose_batch(C.Structure):
+    _fields_ = [
+        ("n_problems", C.c_int32), ("reserved", C.c_int32), ("obs_offset", C.c_void_p), ("cams", C.c_void_p),
+        ("K", C.c_void_p), ("pts", C.c_void_p), ("obs_uv", C.c_void_p), ("huber_a", C.c_double),
+    ]
+
+
 PRUNE_NAMES = {0: "INLIER", 1: "OUTLIER_BEHIND", 2: "OUTLIER_DEPTH", 3: "OUTLIER_CHI2"}
 
 
@@ -96,6 +103,8 @@ SIGNATURES = [
     ("ba_eval_residuals", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]),
     ("ba_linearize", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]),
     ("ba_prune", C.c_int, [C.c_void_p, C.POINTER(ba_prune_problem), C.c_void_p]),
+    ("ba_solve_pose_batch", C.c_int, [C.c_void_p, C.POINTER(ba_pose_batch), C.POINTER(ba_options), C.c_void_p,
+                                      C.POINTER(ba_summary)]),
     ("ba_synchronize", C.c_int, [C.c_void_p]),
     ("ba_bench_iterations", C.c_int, [C.c_void_p, C.c_int, C.c_double, C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]),

@@ -99,6 +99,15 @@ void launch_residuals(const DevProblem& P, const double* rec, const double* pts,
 void launch_prune(int n, const float* extr, const float* center, const float* K, const int* obs_cam, const float* X,
                   const float* uv, const float* inv_sigma, const float* dist, uint8_t* out, hipStream_t s);
 
+// batched pose-only LM, one wavefront per problem (ba_kernels.hip)
+struct PoseOpts {
+  int max_iter, max_invalid, jacobi;
+  double ftol, gtol, ptol, r0, rmax, rmin, min_rel, min_diag, max_diag;
+};
+void launch_pose_batch(int nprob, const int* off, const double* cams_in, const float* K, const double* X,
+                       const float2* uv, double huber_a, const PoseOpts& o, double* cams_out, double* summ,
+                       hipStream_t s);
+
 int grid_for(int n);
 
 }  // namespace bahip

@@ -18,6 +18,7 @@
 
 #include "ba_kernels.h"
 #include "ba_device.h"
+#include "../../include/ba_hip.h"   // ba_termination codes (batched pose-only solve)
 
 namespace bahip {
 
@@ -1492,6 +1493,303 @@ void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipSt
 }
 void launch_residuals(const DevProblem& P, const double* rec, const double* pts, double* r_raw, hipStream_t s) {
   hipLaunchKernelGGL(k_residuals, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, rec, pts, r_raw);
+}
+
+}  // namespace bahip
+
+// ===========================================================================
+// Batched pose-only LM: the solve of
+// MotionOnlyBAOptimizerAngles::optimizeCameraPose (Optimizer.cpp:417-457)
+// for many frames per launch.  One problem = one camera, constant points
+// (PoseOnlyAngleReprojectionError, Optimizer.h:163-182), HuberLoss.
+//
+// One wavefront per problem runs the WHOLE trust-region loop in-kernel: the
+// 6x6 normal equations are wave reductions (xor butterfly: every lane holds
+// the bitwise-identical total, so the LM bookkeeping runs lane-uniform in
+// registers), the 6x6 Cholesky and the accept/reject logic are the host
+// loop of solve() (ba_solver.hip) restated per wave.  Per LM iteration ONE
+// pass over the observations: model cost change from J(x), candidate cost
+// at x', and the linearisation at x' (speculative: adopted when the step is
+// accepted, exactly what a separate linearize(x') pass would produce).
+// Latency-bound by design (10^2-10^3 observations per problem): no host
+// round trip, no launch per iteration.
+// ===========================================================================
+namespace bahip {
+
+__device__ inline double wave_allsum(double v) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// K-folded derivative table of camera x (lin table, kLin entries) into LDS;
+// every lane evaluates the dual Rodrigues (uniform) and writes its entries.
+__device__ inline void pose_table(const double x[6], const double Kd[9], double* tbl) {
+  D3 R[9];
+  angle_axis_to_R_d3(x, R);
+  const int lane = threadIdx.x & 63;
+  for (int e = lane; e < kLin; e += 64) tbl[e] = cam_rec_entry(kRecL + e, x, x + 3, Kd, R, nullptr, true);
+  if (lane == 0) { tbl[kLin] = 1.0; tbl[kLin + 1] = 0.0; }
+  wave_lds_sync();
+}
+
+// accumulate the 2x6 camera block of one observation: H (21 lower, row-major), g (6)
+__device__ inline void pose_acc(const double (&out)[kJR], double (&H)[21], double (&g)[6]) {
+#pragma unroll
+  for (int row = 0; row < 2; ++row) {
+    const double* j = out + 6 * row;
+    int t = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = 0; b <= a; ++b) H[t++] += j[a] * j[b];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) g[a] += j[a] * out[18 + row];
+  }
+}
+
+__global__ __launch_bounds__(64) void k_pose_batch(int nprob, const int* __restrict__ off,
+                                                   const double* __restrict__ cams_in, const float* __restrict__ Kf,
+                                                   const double* __restrict__ Xw, const float2* __restrict__ uvs,
+                                                   double huber_a, PoseOpts o, double* __restrict__ cams_out,
+                                                   double* __restrict__ summ) {
+  __shared__ double tb[2][kLin + 2];
+  __shared__ float ks[9];
+  const int prob = blockIdx.x, lane = threadIdx.x;
+  if (prob >= nprob) return;
+  const int o0 = off[prob], o1 = off[prob + 1];
+  DevProblem P{};
+  P.huber_a = huber_a;
+  P.huber_b = huber_a * huber_a;
+  double x[6], Kd[9];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) x[a] = cams_in[6 * prob + a];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Kd[k] = (double)Kf[9 * prob + k];
+  if (lane < 9) ks[lane] = Kf[9 * prob + lane];
+  int cur = 0;
+  pose_table(x, Kd, tb[cur]);
+
+  // ---- linearisation at x (iteration 0)
+  double H[21], g[6], cost = 0.0, bad = 0.0;
+#pragma unroll
+  for (int k = 0; k < 21; ++k) H[k] = 0.0;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) g[a] = 0.0;
+  for (int ob = o0 + lane; ob < o1; ob += 64) {
+    double out[kJR];
+    bool fin;
+    const double rho = lin_obs(P, CamLds{tb[cur], ks}, true, false, Xw[3 * ob], Xw[3 * ob + 1], Xw[3 * ob + 2],
+                               uvs[ob], out, fin);
+    cost += 0.5 * rho;
+    bad += fin ? 0.0 : 1.0;
+    pose_acc(out, H, g);
+  }
+#pragma unroll
+  for (int k = 0; k < 21; ++k) H[k] = wave_allsum(H[k]);
+#pragma unroll
+  for (int a = 0; a < 6; ++a) g[a] = wave_allsum(g[a]);
+  cost = wave_allsum(cost);
+  bad = wave_allsum(bad);
+  const bool empty = o1 <= o0;
+
+  double s[6], dg[6];
+  auto norms = [&](double& gmax, double& gnorm, double& xnorm) {
+    double gn2 = 0.0, xn2 = 0.0;
+    gmax = 0.0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const double h = H[tri(a, a)];
+      dg[a] = fmin(fmax(h * s[a] * s[a], o.min_diag), o.max_diag);
+      const double d = x[a] - (x[a] + (-g[a]));
+      gmax = fmax(gmax, fabs(d));
+      gn2 += d * d;
+      xn2 += x[a] * x[a];
+    }
+    gnorm = sqrt(gn2);
+    xnorm = sqrt(xn2);
+  };
+#pragma unroll
+  for (int a = 0; a < 6; ++a) s[a] = o.jacobi ? 1.0 / (1.0 + sqrt(H[tri(a, a)])) : 1.0;
+  double gmax = 0.0, gnorm = 0.0, xnorm = 0.0;
+  double x_cost = cost;
+  const double initial_cost = cost;
+  int iteration = 0, nsucc = 0, nunsucc = 0, termination = BA_NO_CONVERGENCE;
+  if (empty) {   // no residual block touches the camera: nothing to solve
+    gmax = 0.0;
+    xnorm = 0.0;
+  } else {
+    norms(gmax, gnorm, xnorm);
+  }
+  if (!(bad == 0.0 && isfinite(cost))) {
+    termination = BA_FAILURE;
+  } else {
+    double radius = o.r0, decrease = 2.0;
+    int consecutive_invalid = 0;
+    bool last_success = true;
+    while (true) {
+      if (iteration >= o.max_iter) { termination = BA_NO_CONVERGENCE; break; }
+      if (last_success && gmax <= o.gtol) { termination = BA_CONVERGENCE; break; }
+      if (radius <= o.rmin) { termination = BA_CONVERGENCE; break; }
+      ++iteration;
+      // ---- reduced system (the camera block itself): S = s H s + D^2, b = s g
+      double L[21], y[6];
+      bool chol_ok = true;
+      {
+        int t = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+          for (int b = 0; b <= a; ++b, ++t) {
+            double h = H[t] * s[a] * s[b];
+            if (a == b) {
+              const double D = sqrt(dg[a] / radius);
+              h += D * D;
+            }
+            L[t] = h;
+          }
+        // LL^T in place (row-major lower), then forward / back substitution
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          double d = L[tri(j, j)];
+#pragma unroll
+          for (int k = 0; k < j; ++k) d -= L[tri(j, k)] * L[tri(j, k)];
+          if (!(d > 0.0 && isfinite(d))) chol_ok = false;
+          const double lj = sqrt(d);
+          L[tri(j, j)] = lj;
+#pragma unroll
+          for (int i = j + 1; i < 6; ++i) {
+            double v = L[tri(i, j)];
+#pragma unroll
+            for (int k = 0; k < j; ++k) v -= L[tri(i, k)] * L[tri(j, k)];
+            L[tri(i, j)] = v / lj;
+          }
+        }
+        double z[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          double v = g[i] * s[i];
+#pragma unroll
+          for (int k = 0; k < i; ++k) v -= L[tri(i, k)] * z[k];
+          z[i] = v / L[tri(i, i)];
+        }
+#pragma unroll
+        for (int i = 5; i >= 0; --i) {
+          double v = z[i];
+#pragma unroll
+          for (int k = i + 1; k < 6; ++k) v -= L[tri(k, i)] * y[k];
+          y[i] = v / L[tri(i, i)];
+        }
+      }
+      double xc[6], dl[6], step2 = 0.0;
+      bool step_bad = false;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        dl[a] = (-y[a]) * s[a];
+        xc[a] = x[a] + dl[a];
+        const double e = x[a] - xc[a];
+        step2 += e * e;
+        if (!isfinite(dl[a])) step_bad = true;
+      }
+      // ---- one pass: model cost change (J at x), candidate cost, linearisation at x'
+      const int nxt = cur ^ 1;
+      pose_table(xc, Kd, tb[nxt]);
+      double Rc[9];
+      angle_axis_to_R(xc, Rc);
+      double mneg = 0.0, ccost = 0.0, cbad = 0.0, H2[21], g2[6], cost2 = 0.0, bad2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 21; ++k) H2[k] = 0.0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) g2[a] = 0.0;
+      for (int ob = o0 + lane; ob < o1; ob += 64) {
+        const double X0 = Xw[3 * ob], X1 = Xw[3 * ob + 1], X2 = Xw[3 * ob + 2];
+        const float2 uv = uvs[ob];
+        double out[kJR];
+        bool fin;
+        lin_obs(P, CamLds{tb[cur], ks}, true, false, X0, X1, X2, uv, out, fin);
+        double jd0 = 0.0, jd1 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) { jd0 += out[a] * dl[a]; jd1 += out[6 + a] * dl[a]; }
+        mneg += jd0 * (out[18] + jd0 / 2.0) + jd1 * (out[19] + jd1 / 2.0);
+        // candidate residual, value-only record at x' (k_candidate's arithmetic)
+        double pc[3], q[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) pc[i] = Rc[i] * X0 + Rc[3 + i] * X1 + Rc[6 + i] * X2 + xc[3 + i];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) q[i] = pc[0] * Kd[i] + pc[1] * Kd[3 + i] + pc[2] * Kd[6 + i];
+        const double rc0 = q[0] / q[2] - (double)uv.x, rc1 = q[1] / q[2] - (double)uv.y;
+        double sc;
+        ccost += 0.5 * huber(rc0 * rc0 + rc1 * rc1, P.huber_a, P.huber_b, &sc);
+        if (!isfinite(rc0) || !isfinite(rc1)) cbad += 1.0;
+        // linearisation at x' (used if the step is accepted)
+        const double rho2 = lin_obs(P, CamLds{tb[nxt], ks}, true, false, X0, X1, X2, uv, out, fin);
+        cost2 += 0.5 * rho2;
+        bad2 += fin ? 0.0 : 1.0;
+        pose_acc(out, H2, g2);
+      }
+      mneg = wave_allsum(mneg);
+      ccost = wave_allsum(ccost);
+      cbad = wave_allsum(cbad);
+      const double mcc = -mneg;
+      const bool valid = chol_ok && !step_bad && mcc > 0.0;
+      if (!valid) {
+        if (++consecutive_invalid >= o.max_invalid) { termination = BA_FAILURE; break; }
+        radius = radius / decrease;
+        decrease *= 2.0;
+        last_success = false;
+        ++nunsucc;
+        continue;
+      }
+      consecutive_invalid = 0;
+      if (sqrt(step2) <= o.ptol * (xnorm + o.ptol)) { termination = BA_CONVERGENCE; break; }
+      const double cand_cost = (cbad > 0.0 || !isfinite(ccost)) ? 1.7976931348623157e308 : ccost;
+      const double cost_change = x_cost - cand_cost;
+      if (fabs(cost_change) <= o.ftol * x_cost) { termination = BA_CONVERGENCE; break; }
+      const double rel = cand_cost >= 1.7976931348623157e308 ? -1.7976931348623157e308 : (x_cost - cand_cost) / mcc;
+      if (rel > o.min_rel) {
+#pragma unroll
+        for (int k = 0; k < 21; ++k) H[k] = wave_allsum(H2[k]);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) { g[a] = wave_allsum(g2[a]); x[a] = xc[a]; }
+        cost = wave_allsum(cost2);
+        bad = wave_allsum(bad2);
+        cur = nxt;
+        if (!(bad == 0.0 && isfinite(cost))) { termination = BA_FAILURE; x_cost = cost; break; }
+        x_cost = cost;
+        norms(gmax, gnorm, xnorm);
+        const double t3 = 2.0 * rel - 1.0;
+        radius = fmin(o.rmax, radius / fmax(1.0 / 3.0, 1.0 - t3 * t3 * t3));
+        decrease = 2.0;
+        last_success = true;
+        ++nsucc;
+      } else {
+        radius = radius / decrease;
+        decrease *= 2.0;
+        last_success = false;
+        ++nunsucc;
+      }
+    }
+  }
+  if (lane < 6) cams_out[6 * prob + lane] = x[lane];
+  if (lane == 0) {
+    double* sm = summ + 8 * prob;
+    sm[0] = initial_cost;
+    sm[1] = x_cost;
+    sm[2] = iteration;
+    sm[3] = nsucc;
+    sm[4] = nunsucc;
+    sm[5] = termination;
+    sm[6] = gmax;
+    sm[7] = 0.0;
+  }
+}
+
+void launch_pose_batch(int nprob, const int* off, const double* cams_in, const float* K, const double* X,
+                       const float2* uv, double huber_a, const PoseOpts& o, double* cams_out, double* summ,
+                       hipStream_t s) {
+  if (nprob <= 0) return;
+  hipLaunchKernelGGL(k_pose_batch, dim3(nprob), dim3(64), 0, s, nprob, off, cams_in, K, X, uv, huber_a, o, cams_out,
+                     summ);
 }
 
 }  // namespace bahip

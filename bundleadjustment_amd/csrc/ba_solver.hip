@@ -81,6 +81,9 @@ struct ba_ctx {
   DevWork W{};
   std::vector<void*> allocs;     // device buffers of the current problem
   double* h_scal = nullptr;      // pinned scalar record
+  char* pose_buf = nullptr;      // ba_solve_pose_batch device staging (grown on demand)
+  size_t pose_cap = 0;
+  std::vector<char> pose_host;
 
   // solver state
   std::vector<ba_iteration> log;
@@ -579,6 +582,7 @@ int ba_destroy(ba_ctx* ctx) {
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
   if (ctx->h_scal) (void)hipHostFree(ctx->h_scal);
+  if (ctx->pose_buf) (void)hipFree(ctx->pose_buf);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return BA_OK;
@@ -751,6 +755,83 @@ int ba_prune(ba_ctx* ctx, const ba_prune_problem* p, uint8_t* result) {
     HIP_OK(hipMemcpyAsync(result, d + oR, (size_t)no, hipMemcpyDeviceToHost, ctx->stream));
     HIP_OK(hipStreamSynchronize(ctx->stream));
     (void)hipFree(d);
+  });
+}
+
+int ba_solve_pose_batch(ba_ctx* ctx, const ba_pose_batch* b, const ba_options* opt, double* cams_out,
+                        ba_summary* summaries) {
+  if (!ctx) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] {
+    if (!b || b->n_problems < 0) throw BaError{BA_ERR_INVALID_ARGUMENT, "ba_solve_pose_batch: bad batch"};
+    const int n = b->n_problems;
+    if (n == 0) return;
+    if (!b->obs_offset || !b->cams || !b->K || !cams_out)
+      throw BaError{BA_ERR_INVALID_ARGUMENT, "ba_solve_pose_batch: null array"};
+    if (b->obs_offset[0] != 0) throw BaError{BA_ERR_INVALID_ARGUMENT, "ba_solve_pose_batch: obs_offset[0] != 0"};
+    for (int i = 0; i < n; ++i)
+      if (b->obs_offset[i + 1] < b->obs_offset[i])
+        throw BaError{BA_ERR_INVALID_ARGUMENT, "ba_solve_pose_batch: obs_offset decreases at " + std::to_string(i)};
+    const int no = b->obs_offset[n];
+    if (no > 0 && (!b->pts || !b->obs_uv)) throw BaError{BA_ERR_INVALID_ARGUMENT, "ba_solve_pose_batch: null array"};
+    ba_options o;
+    if (opt) o = *opt; else ba_default_options(&o);
+    PoseOpts po{o.max_num_iterations, o.max_num_consecutive_invalid_steps, o.jacobi_scaling,
+                o.function_tolerance, o.gradient_tolerance, o.parameter_tolerance, o.initial_trust_region_radius,
+                o.max_trust_region_radius, o.min_trust_region_radius, o.min_relative_decrease, o.min_lm_diagonal,
+                o.max_lm_diagonal};
+    const double t0 = now_s();
+    HIP_OK(hipSetDevice(ctx->device));
+    // one staging buffer, 16-B aligned sections: inputs (uploaded), then outputs
+    auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
+    const size_t s_off = al(sizeof(int) * (n + 1)), s_cam = al(sizeof(double) * 6 * n), s_K = al(sizeof(float) * 9 * n),
+                 s_X = al(sizeof(double) * 3 * (size_t)no), s_uv = al(sizeof(float) * 2 * (size_t)no);
+    const size_t in_b = s_off + s_cam + s_K + s_X + s_uv;
+    const size_t out_b = s_cam + al(sizeof(double) * 8 * n);
+    if (in_b + out_b > ctx->pose_cap) {
+      if (ctx->pose_buf) (void)hipFree(ctx->pose_buf);
+      ctx->pose_buf = nullptr;
+      ctx->pose_cap = 0;
+      HIP_OK(hipMalloc(&ctx->pose_buf, in_b + out_b));
+      ctx->pose_cap = in_b + out_b;
+    }
+    std::vector<char>& h = ctx->pose_host;
+    h.assign(in_b + out_b, 0);
+    size_t at = 0;
+    auto put = [&](const void* src, size_t nb, size_t sec) { if (nb) std::memcpy(h.data() + at, src, nb); at += sec; };
+    put(b->obs_offset, sizeof(int) * (n + 1), s_off);
+    put(b->cams, sizeof(double) * 6 * n, s_cam);
+    put(b->K, sizeof(float) * 9 * n, s_K);
+    put(b->pts, sizeof(double) * 3 * (size_t)no, s_X);
+    put(b->obs_uv, sizeof(float) * 2 * (size_t)no, s_uv);
+    char* d = ctx->pose_buf;
+    HIP_OK(hipMemcpyAsync(d, h.data(), in_b, hipMemcpyHostToDevice, ctx->stream));
+    const int* d_off = reinterpret_cast<const int*>(d);
+    const double* d_cam = reinterpret_cast<const double*>(d + s_off);
+    const float* d_K = reinterpret_cast<const float*>(d + s_off + s_cam);
+    const double* d_X = reinterpret_cast<const double*>(d + s_off + s_cam + s_K);
+    const float2* d_uv = reinterpret_cast<const float2*>(d + s_off + s_cam + s_K + s_X);
+    double* d_out = reinterpret_cast<double*>(d + in_b);
+    double* d_sum = reinterpret_cast<double*>(d + in_b + s_cam);
+    launch_pose_batch(n, d_off, d_cam, d_K, d_X, d_uv, b->huber_a, po, d_out, d_sum, ctx->stream);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(h.data() + in_b, d + in_b, out_b, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    std::memcpy(cams_out, h.data() + in_b, sizeof(double) * 6 * n);
+    if (summaries) {
+      const double* sm = reinterpret_cast<const double*>(h.data() + in_b + s_cam);
+      const double wall = now_s() - t0;
+      for (int i = 0; i < n; ++i) {
+        ba_summary S{};
+        S.initial_cost = sm[8 * i];
+        S.final_cost = sm[8 * i + 1];
+        S.num_iterations = (int)sm[8 * i + 2];
+        S.num_successful_steps = (int)sm[8 * i + 3];
+        S.num_unsuccessful_steps = (int)sm[8 * i + 4];
+        S.termination_type = (int)sm[8 * i + 5];
+        S.total_time_s = wall;
+        summaries[i] = S;
+      }
+    }
   });
 }
 

@@ -13,7 +13,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _native as N
-from .problem import Problem
+from .problem import HUBER_A, Problem
 
 
 def _ptr(a):
@@ -189,6 +189,30 @@ class Solver:
         out = np.empty(n_obs, np.uint8)
         self._check(self.lib.ba_prune(self.h, C.byref(pp), _ptr(out)), "ba_prune")
         return out
+
+    def solve_pose_batch(self, obs_offset, cams, K, pts, obs_uv, options: Options | None = None,
+                         huber_a: float = HUBER_A) -> tuple[np.ndarray, list[Summary]]:
+        """Batched pose-only solves (MotionOnlyBAOptimizerAngles' Ceres solve,
+        Optimizer.cpp:417-442, for many frames in one launch).  Problem i owns
+        observations [obs_offset[i], obs_offset[i+1]) of constant points
+        pts[o] with pixels obs_uv[o]; returns (cams (n, 6), summaries)."""
+        off = np.ascontiguousarray(obs_offset, dtype=np.int32)
+        n = off.size - 1
+        c = np.ascontiguousarray(cams, dtype=np.float64).reshape(n, 6)
+        k = np.ascontiguousarray(K, dtype=np.float32).reshape(n, 9)
+        x = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 3)
+        uv = np.ascontiguousarray(obs_uv, dtype=np.float32).reshape(-1, 2)
+        b = N.ba_pose_batch(n_problems=n, reserved=0, obs_offset=_ptr(off), cams=_ptr(c), K=_ptr(k), pts=_ptr(x),
+                            obs_uv=_ptr(uv), huber_a=float(huber_a))
+        o = (options or Options()).to_c()
+        out = np.empty((n, 6))
+        sums = (N.ba_summary * max(n, 1))()
+        self._check(self.lib.ba_solve_pose_batch(self.h, C.byref(b), C.byref(o), _ptr(out), sums),
+                    "ba_solve_pose_batch")
+        res = [Summary(s.initial_cost, s.final_cost, s.num_iterations, s.num_successful_steps,
+                       s.num_unsuccessful_steps, N.TERMINATION_NAMES.get(s.termination_type, str(s.termination_type)),
+                       s.total_time_s, s.linearize_time_s, s.solve_time_s) for s in list(sums)[:n]]
+        return out, res
 
     def synchronize(self):
         self._check(self.lib.ba_synchronize(self.h), "ba_synchronize")

@@ -212,6 +212,35 @@ enum ba_prune_result {
 /* result[n_obs] receives a ba_prune_result per pair (runs on the device). */
 int ba_prune(ba_ctx* ctx, const ba_prune_problem* problem, uint8_t* result);
 
+/* Batched frame-to-frame pose-only solves.
+ * Replaces, per frame, the ceres::Problem + ceres::Solve of
+ * MotionOnlyBAOptimizerAngles::optimizeCameraPose (Optimizer.cpp:417-442;
+ * residuals from MotionOnlyBAOptimizerAngles::prepareConstraints,
+ * Optimizer.cpp:459-498: PoseOnlyAngleReprojectionError, Optimizer.h:163-182,
+ * with HuberLoss(huber_a)).  Problem i owns observations
+ * [obs_offset[i], obs_offset[i+1]) against its own camera; the points are
+ * constant.  Same Levenberg-Marquardt semantics as ba_solve on the
+ * equivalent one-camera problem (options and termination rules included),
+ * but the whole trust-region loop of every problem runs in one kernel
+ * launch (one wavefront per problem), so a frame costs one host round trip
+ * instead of two per LM iteration.  cams_out[6*i] receives the solution
+ * (may alias cams); summaries[i] (may be NULL) the per-problem summary
+ * (time fields: the batch's wall time). */
+typedef struct {
+  int32_t n_problems;
+  int32_t reserved;
+  const int32_t* obs_offset;      /* [n_problems + 1], obs_offset[0] = 0, non-decreasing */
+  const double*  cams;            /* [6*n_problems] initial [w, t] (world->camera)      */
+  const float*   K;               /* [9*n_problems] col-major                           */
+  const double*  pts;             /* [3*obs_offset[n]] constant world points (float values
+                                     of MapPoint::getPosition in the reference)          */
+  const float*   obs_uv;          /* [2*obs_offset[n]]                                  */
+  double huber_a;                 /* sqrt(5.991); <= 0: no loss                         */
+} ba_pose_batch;
+
+int ba_solve_pose_batch(ba_ctx* ctx, const ba_pose_batch* batch, const ba_options* opt, double* cams_out,
+                        ba_summary* summaries);
+
 /* Blocks until all device work of the context is done. */
 int ba_synchronize(ba_ctx* ctx);
 

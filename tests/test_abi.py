@@ -61,6 +61,8 @@ int main(void) {
   F(ba_iteration, cost) F(ba_iteration, model_cost_change) F(ba_iteration, iteration_time_s)
   printf("ba_prune_problem %zu\n", sizeof(ba_prune_problem));
   F(ba_prune_problem, extr) F(ba_prune_problem, obs_cam) F(ba_prune_problem, obs_dist)
+  printf("ba_pose_batch %zu\n", sizeof(ba_pose_batch));
+  F(ba_pose_batch, obs_offset) F(ba_pose_batch, pts) F(ba_pose_batch, obs_uv) F(ba_pose_batch, huber_a)
   return 0;
 }
 """
@@ -74,7 +76,8 @@ def test_ctypes_layout_matches_c_compiler(tmp_path):
     vals = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True,
                                                           check=True).stdout.splitlines())
     types = {"ba_problem": N.ba_problem, "ba_options": N.ba_options, "ba_summary": N.ba_summary,
-             "ba_iteration": N.ba_iteration, "ba_prune_problem": N.ba_prune_problem}
+             "ba_iteration": N.ba_iteration, "ba_prune_problem": N.ba_prune_problem,
+             "ba_pose_batch": N.ba_pose_batch}
     for k, v in vals.items():
         if "." in k:
             t, f = k.split(".")
