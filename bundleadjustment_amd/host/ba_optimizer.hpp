@@ -72,12 +72,40 @@ class HipBackend {
   HipBackend& operator=(const HipBackend&) = delete;
 
   int solve(const ba_problem& p, const ba_options& o, double* cams, double* pts, ba_summary* s) {
+    if (pose_only(p)) return solve_pose(p, o, cams, pts, s);
     int st = ba_set_problem(ctx_, &p);
     if (st == BA_OK) st = ba_solve(ctx_, &o, s);
     if (st == BA_OK) st = ba_get_params(ctx_, cams, pts);
     return st;
   }
   int prune(const ba_prune_problem& p, uint8_t* result) { return ba_prune(ctx_, &p, result); }
+
+  // The motion-only problem (one variable camera, every point constant:
+  // MotionOnlyBAOptimizerAngles::prepareConstraints, Optimizer.cpp:459-498)
+  // goes through the batched pose solver: the whole LM loop in one launch.
+  static bool pose_only(const ba_problem& p) {
+    if (p.n_cams != 1 || (p.cam_fixed && p.cam_fixed[0]) || !p.pt_fixed) return false;
+    for (int32_t i = 0; i < p.n_pts; ++i)
+      if (!p.pt_fixed[i]) return false;
+    return true;
+  }
+  int solve_pose(const ba_problem& p, const ba_options& o, double* cams, double* pts, ba_summary* s) {
+    const int32_t off[2] = {0, p.n_obs};
+    std::vector<double> X(3 * static_cast<size_t>(p.n_obs));
+    for (int32_t k = 0; k < p.n_obs; ++k)
+      for (int i = 0; i < 3; ++i) X[3 * k + i] = p.pts[3 * static_cast<size_t>(p.obs_pt[k]) + i];
+    ba_pose_batch b{};
+    b.n_problems = 1;
+    b.obs_offset = off;
+    b.cams = p.cams;
+    b.K = p.K;
+    b.pts = X.data();
+    b.obs_uv = p.obs_uv;
+    b.huber_a = p.huber_a;
+    const int st = ba_solve_pose_batch(ctx_, &b, &o, cams, s);
+    if (st == BA_OK && pts && p.n_pts > 0) std::copy(p.pts, p.pts + 3 * static_cast<size_t>(p.n_pts), pts);
+    return st;
+  }
   std::string last_error() const { return ba_last_error(ctx_); }
 
  private:
