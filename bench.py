@@ -86,6 +86,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3")
+    ap.add_argument("--scale", type=float, default=1.0, help="point-count scale of the config (per-GPU shard size)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--comm", action="store_true", help="use an RCCL communicator even at one rank (tests)")
@@ -105,7 +106,7 @@ def main():
     cfg = args.config
     seed = 0xBA5E0000 + CONFIG_INDEX[cfg]
     t = time.time()
-    problem = make_config(cfg, point_seed=None if rank == 0 else seed + 7919 * rank)
+    problem = make_config(cfg, scale=args.scale, point_seed=None if rank == 0 else seed + 7919 * rank)
     log(f"[rank {rank}] problem {cfg}: {problem.n_cams} cams x {problem.n_pts} pts x {problem.n_obs} obs "
         f"(generated in {time.time() - t:.1f}s)")
 

@@ -458,6 +458,12 @@ __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z
 //   A    working matrix ((n+1) x ld), trailing part updated in place
 //   L    output factor ((n+1) x ld)
 //   Vbuf [T][64][64] inverses of the diagonal blocks
+// SPLIT (large systems): the panel L_{I,k} = A_{I,k} V_k^T was formed and
+// stored by k_chol_panel just before; every tile reads it from L, so a tile
+// does one GEMM instead of three (the fused form recomputes P_I, P_J per
+// tile: 3x the flops and ~2.5x the bytes, which dominate once the trailing
+// matrix has thousands of tiles).
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, double* __restrict__ L, int ld, int n,
                                                    int k, double* __restrict__ Vbuf, double* __restrict__ scal) {
   const int I = blockIdx.y, J = blockIdx.x;
@@ -478,7 +484,14 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
     const int b = min(CB, n - s);             // its order
     const int m = min(CB, nrows - s);         // rows in the tile (b or b + 1 with the rhs row)
     CHOL_STAMP(0);
-    if (k >= 0) {
+    if (SPLIT && k >= 0) {
+      const TileRegs tA = tile_fetch<true>(A, lds, s, s, nrows, s + b);   // A_{k+1,k+1} (+ rhs row)
+      const TileRegs tP = tile_fetch(L, lds, s, kc, nrows, kc + kb);      // L_{k+1,k} (k_chol_panel)
+      tile_put(S0, tA);
+      tile_put(S1, tP);
+      __syncthreads();
+      mfma_xxT_lower_sub(S1, S0);            // C = A - P P^T (lower tiles)
+    } else if (k >= 0) {
       // the three tiles' loads all in flight before the first LDS store
       const TileRegs tA = tile_fetch<true>(A, lds, s, s, nrows, s + b);   // A_{k+1,k+1} (+ rhs row)
       const TileRegs tP = tile_fetch(A, lds, s, kc, nrows, kc + kb);      // A_{k+1,k}
@@ -540,6 +553,29 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
   // ---- trailing tile (I, J) != (0, 0)
   if (k < 0) return;
   if (r0 >= nrows || c0 >= n) return;
+  if (SPLIT) {
+    const TileRegs tI = tile_fetch(L, lds, r0, kc, nrows, kc + kb);   // L_{I,k}
+    if (I != J) {
+      const TileRegs tJ = tile_fetch(L, lds, c0, kc, n, kc + kb);     // L_{J,k}
+      tile_put(S1, tJ);
+    }
+    tile_put(S0, tI);
+    __syncthreads();
+    d4 acc[2][2];
+    mfma_xyT_64(S0, I != J ? S1 : S0, acc);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          int rr, cc;
+          acc_pos(a, b, g, &rr, &cc);
+          const int ri = r0 + rr, cj = c0 + cc;
+          if (ri < nrows && cj < n && cj <= ri) A[(size_t)ri * ld + cj] -= acc[a][b][g];
+        }
+    return;
+  }
   stage64(S2, Vk, CB, 0, 0, CB, CB);
   stage64(S0, A, lds, r0, kc, nrows, kc + kb);   // A_{I,k}
   if (I != J) stage64(S1, A, lds, c0, kc, n, kc + kb);  // A_{J,k}
@@ -683,16 +719,56 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
   if (tid == 0 && !good) scal[SL_CHOL_BAD] += 1.0;
 }
 
+// Panel of block step k (SPLIT mode): L_{I,k} = A_{I,k} V_k^T for every tile
+// row I > k (the rhs row included), one workgroup per tile row.
+__global__ __launch_bounds__(256) void k_chol_panel(const double* __restrict__ A, double* __restrict__ L, int ld,
+                                                    int n, int k, const double* __restrict__ Vbuf) {
+  __shared__ double S0[CB][LDP];
+  __shared__ double S2[CB][LDP];
+  const int nrows = n + 1;
+  const size_t lds = (size_t)ld;
+  const int kc = k * CB, kb = min(CB, n - kc);
+  const int r0 = (k + 1) * CB + blockIdx.x * CB;
+  if (r0 >= nrows) return;
+  const TileRegs tA = tile_fetch(A, lds, r0, kc, nrows, kc + kb);
+  const TileRegs tV = tile_fetch<true>(Vbuf + (size_t)k * CB * CB, CB, 0, 0, CB, CB);
+  tile_put(S0, tA);
+  tile_put(S2, tV);
+  __syncthreads();
+  d4 acc[4];
+  mfma_xVT_strip(S0, S2, acc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, m = min(CB, nrows - r0);
+#pragma unroll
+  for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int rr = 16 * w + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
+      if (rr < m && cc < kb) L[(size_t)(r0 + rr) * ld + kc + cc] = acc[bc][g];
+    }
+}
+
+// Block columns from which the split (panel + update) form is used: below it
+// the fused step's trailing tiles hide behind the critical workgroup and one
+// launch per step is cheaper (C3: 19 block columns); above it the trailing
+// GEMMs dominate (C4: 94).
+constexpr int kCholSplitBlocks = 24;
+
 void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, hipStream_t s) {
   const int n = P.n;
   if (n == 0) return;
   const int nrows = n + 1;
   const int T = (n + CB - 1) / CB;
-  hipLaunchKernelGGL(k_chol_step, dim3(1, 1), dim3(256), 0, s, W.S, W.Lf, P.ld, n, -1, W.Vbuf, W.scal);
+  const bool split = T >= kCholSplitBlocks;
+  hipLaunchKernelGGL(k_chol_step<false>, dim3(1, 1), dim3(256), 0, s, W.S, W.Lf, P.ld, n, -1, W.Vbuf, W.scal);
   for (int k = 0; k + 1 < T; ++k) {
     const int st = (k + 1) * CB;
     const int tr = (nrows - st + CB - 1) / CB, tc = (n - st + CB - 1) / CB;
-    hipLaunchKernelGGL(k_chol_step, dim3(tc, tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf, W.scal);
+    if (split) {
+      hipLaunchKernelGGL(k_chol_panel, dim3(tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf);
+      hipLaunchKernelGGL(k_chol_step<true>, dim3(tc, tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf, W.scal);
+    } else {
+      hipLaunchKernelGGL(k_chol_step<false>, dim3(tc, tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf, W.scal);
+    }
   }
   (void)hipMemsetAsync(W.flags, 0, sizeof(int) * T, s);
   hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.flags, W.scal);

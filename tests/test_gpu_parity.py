@@ -137,6 +137,19 @@ def test_solve_c3_first_iterations(solver, oracle_lib):
     assert_close(pts, op, 1e-8, 1e-10, "points")
 
 
+def test_many_cameras_global_table_path(solver, oracle_lib):
+    """More cameras than the LDS camera table holds (kLinLdsCams = 200): the
+    global-record linearisation / W / candidate kernels and a 1794-row
+    reduced system (29 Cholesky block steps, n % 64 != 0)."""
+    p = make_synthetic(300, 12_000, 6, seed=0xBA5E0003)
+    bp.fix_camera(p, 1)
+    cams, pts, summ, glog = run_gpu(solver, p, Options(max_num_iterations=4))
+    oc, op, osum, olog = oracle_lib.solve(p, oracle_lib.default_options(max_num_iterations=4))
+    compare_logs(glog, olog, rtol_cost=1e-10)
+    assert_close(cams, oc, 1e-8, 1e-10, "cameras")
+    assert_close(pts, op, 1e-8, 1e-10, "points")
+
+
 def test_solve_is_bitwise_deterministic(solver):
     p = make_config("c2")
     a = run_gpu(solver, p, Options(max_num_iterations=10))

@@ -63,7 +63,12 @@ int main(int argc, char** argv) {
       const int tr = (nrows - st + CB - 1) / CB, tc = (n - st + CB - 1) / CB;
       dim3 grid = k < 0 ? dim3(1, 1) : dim3(tc, tr);
       CK(hipEventRecord(e0));
-      hipLaunchKernelGGL(k_chol_step, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS);
+      if (k >= 0 && T >= kCholSplitBlocks) {
+        hipLaunchKernelGGL(k_chol_panel, dim3(grid.y), dim3(256), 0, 0, dA, dL, ld, n, k, dV);
+        hipLaunchKernelGGL(k_chol_step<true>, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS);
+      } else {
+        hipLaunchKernelGGL(k_chol_step<false>, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS);
+      }
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
