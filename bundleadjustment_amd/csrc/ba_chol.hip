@@ -433,7 +433,9 @@ __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z
   }
   CHOL_STAMP(3);
   diag_inverse16(T, W.rsv, X, b);
+  CHOL_STAMP(40);
   __syncthreads();
+  CHOL_STAMP(41);
   // off-diagonal blocks of X = L^-1, by block distance dd
   for (int dd = 1; dd < 4; ++dd) {
     const int i = dd + w, pp = w;            // wave w: block (dd + w, w)
