@@ -13,6 +13,7 @@ PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libba_hip.so"
 
 BA_OK = 0
+BA_ABI_VERSION = 2          # include/ba_hip.h
 STATUS_NAMES = {0: "BA_OK", 1: "BA_ERR_INVALID_ARGUMENT", 2: "BA_ERR_DEVICE", 3: "BA_ERR_OUT_OF_MEMORY",
                 4: "BA_ERR_NO_PROBLEM", 5: "BA_ERR_COMM"}
 TERMINATION_NAMES = {0: "CONVERGENCE", 1: "NO_CONVERGENCE", 2: "FAILURE"}
@@ -45,6 +46,8 @@ class ba_options(C.Structure):
         ("parameter_tolerance", C.c_double), ("initial_trust_region_radius", C.c_double),
         ("max_trust_region_radius", C.c_double), ("min_trust_region_radius", C.c_double),
         ("min_relative_decrease", C.c_double), ("min_lm_diagonal", C.c_double), ("max_lm_diagonal", C.c_double),
+        ("preconditioner_type", C.c_int32), ("max_linear_solver_iterations", C.c_int32),
+        ("min_linear_solver_iterations", C.c_int32), ("precision", C.c_int32), ("eta", C.c_double),
     ]
 
 
@@ -60,7 +63,7 @@ class ba_summary(C.Structure):
 class ba_iteration(C.Structure):
     _fields_ = [
         ("iteration", C.c_int32), ("step_is_valid", C.c_int32), ("step_is_successful", C.c_int32),
-        ("reserved", C.c_int32), ("cost", C.c_double), ("cost_change", C.c_double),
+        ("linear_solver_iterations", C.c_int32), ("cost", C.c_double), ("cost_change", C.c_double),
         ("gradient_max_norm", C.c_double), ("gradient_norm", C.c_double), ("step_norm", C.c_double),
         ("relative_decrease", C.c_double), ("trust_region_radius", C.c_double),
         ("model_cost_change", C.c_double), ("iteration_time_s", C.c_double),
@@ -106,8 +109,8 @@ SIGNATURES = [
     ("ba_solve_pose_batch", C.c_int, [C.c_void_p, C.POINTER(ba_pose_batch), C.POINTER(ba_options), C.c_void_p,
                                       C.POINTER(ba_summary)]),
     ("ba_synchronize", C.c_int, [C.c_void_p]),
-    ("ba_bench_iterations", C.c_int, [C.c_void_p, C.c_int, C.c_double, C.POINTER(C.c_double),
-                                      C.POINTER(C.c_double)]),
+    ("ba_bench_iterations", C.c_int, [C.c_void_p, C.POINTER(ba_options), C.c_int, C.c_double,
+                                      C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
 ]
 
 _LIB = None
@@ -131,7 +134,7 @@ def load_library(path: str | os.PathLike | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.ba_abi_version() != 1:
+    if lib.ba_abi_version() != BA_ABI_VERSION:
         raise NativeLibraryError("ABI version mismatch")
     if path is None:
         _LIB = lib

@@ -72,8 +72,23 @@ struct DevWork {
   const int2* pairs;                 // observation pairs per block
   double* cpart;                     // [kCamSplit][nvc][27] per-slice camera sums
   double* part;                      // [kNumSlots][kMaxBlocks]
-  double* scal;                      // [kNumSlots]
+  double* scal;                      // [kNumSlots + kPcgState]: scalar slots, then the PCG state record
+  // ITERATIVE_SCHUR (allocated on first use; x of the CG is y above)
+  double* Sd;                        // [nvc][27] diagonal Schur blocks (lower 21) + reduced rhs (6)
+  double* Adiag;                     // [nvc][21] s Hcc s + D^2 (lower)
+  double* Minv;                      // [nvc][36] preconditioner block inverses
+  double* pb; double* pr; double* pz; double* pp; double* pq;   // [n] CG vectors
+  double* vpt;                       // [np][3] point-side products of one implicit matvec
+  double* tpart;                     // [pcg_G][nvc][6] camera-side slices of one implicit matvec
+  int pcg_G;
+  const int* dup_off;                // [nvc+1] per variable camera: pairs of observations of one
+  const int2* dup_pairs;             //   point by that camera (Schur-Jacobi diagonal cross terms)
 };
+
+// PCG state record at scal + kNumSlots (doubles)
+enum PcgState { PS_RHO = 0, PS_Q0, PS_ALPHA, PS_NORM_B, PS_ITER, PS_DONE, PS_TERM, PS_PAD, kPcgState };
+enum PcgTerm { PCG_SUCCESS = 0, PCG_NO_CONVERGENCE = 1, PCG_FAILURE = 2 };
+struct PcgOpts { double q_tolerance; int min_iter, max_iter, schur_jacobi; };
 
 // --- launchers (all asynchronous on `s`) ---
 void launch_cam_prep(const DevProblem& P, const double* cams, double* rec, bool deriv, hipStream_t s);
@@ -84,12 +99,22 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
                       hipStream_t s);
 void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);  // + W = E L^-T
-void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s);
+// compact != nullptr: write the diagonal blocks + rhs to compact[nvc][27]
+// instead of the dense S (ITERATIVE_SCHUR)
+void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact = nullptr);
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
 void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, hipStream_t s);  // ba_chol.hip
 void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s);
+// ITERATIVE_SCHUR (ba_pcg.hip): implicit Schur complement + PCG
+void launch_pcg_setup(const DevProblem& P, const DevWork& W, double radius, const PcgOpts& o, hipStream_t s);
+void launch_pcg_dup(const DevProblem& P, const DevWork& W, hipStream_t s);   // Schur-Jacobi cross terms
+// one implicit matvec (point pass + camera pass) of vec into W.tpart
+void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s);
+// mode 0: full CG iteration; 1: up to the x update; 2: residual reset from W.tpart = matvec(x)
+void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, const PcgOpts& o, hipStream_t s);
+
 // Fold the partials of `slots` (bitmask) into d_scal; kernels producing
 // partials always use grid = nblocks_of(...)
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s);

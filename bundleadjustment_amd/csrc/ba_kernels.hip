@@ -18,6 +18,7 @@
 
 #include "ba_kernels.h"
 #include "ba_device.h"
+#include "ba_reduce.h"
 #include "../../include/ba_hip.h"   // ba_termination codes (batched pose-only solve)
 
 namespace bahip {
@@ -28,52 +29,6 @@ int grid_for(int n) {
   return g > kMaxBlocks ? kMaxBlocks : g;
 }
 
-// ---------------------------------------------------------------------------
-// reductions
-// ---------------------------------------------------------------------------
-__device__ inline double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-  return v;
-}
-__device__ inline double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_down(v, off, 64));
-  return v;
-}
-// Block-wide sum of NV values per thread (fixed order).  Result valid in
-// thread 0: out[k].  lds must hold NV * (blockDim/64) doubles.
-template <int NV>
-__device__ inline void block_sum(double (&v)[NV], double* lds, double (&out)[NV]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const double s = wave_sum(v[k]);
-    if (lane == 0) lds[k * 16 + w] = s;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      double s = 0.0;
-      for (int i = 0; i < nw; ++i) s += lds[k * 16 + i];
-      out[k] = s;
-    }
-  }
-  __syncthreads();
-}
-__device__ inline double block_max1(double v, double* lds) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  v = wave_max(v);
-  if (lane == 0) lds[w] = v;
-  __syncthreads();
-  double m = 0.0;
-  if (threadIdx.x == 0) for (int i = 0; i < nw; ++i) m = fmax(m, lds[i]);
-  __syncthreads();
-  return m;
-}
-
-__device__ inline double* part_of(double* part, int slot) { return part + (size_t)slot * kMaxBlocks; }
 
 // Per-camera work is split over kCamSplit workgroups (one workgroup per
 // camera leaves CUs idle and is latency bound).  Each slice stores its 27
@@ -90,7 +45,8 @@ __device__ inline void cam_slice_store(const double (&tot)[27], double* __restri
 }
 
 // fold the slices: mode 0 -> Hcc (21) / gc (6); mode 1 -> S diagonal block
-// (-sum W W^T, lower) and rhs row (-sum W u)
+// (-sum W W^T, lower) and rhs row (-sum W u); mode 2 -> the same 27 values
+// into a compact per-camera array (ITERATIVE_SCHUR)
 __global__ __launch_bounds__(256) void k_cam_fold(DevProblem P, const double* __restrict__ cpart, int mode,
                                                   double* __restrict__ Hcc, double* __restrict__ gc,
                                                   double* __restrict__ S) {
@@ -102,6 +58,8 @@ __global__ __launch_bounds__(256) void k_cam_fold(DevProblem P, const double* __
   if (mode == 0) {
     if (k < 21) Hcc[(size_t)v * 21 + k] = acc;
     else gc[(size_t)v * 6 + (k - 21)] = acc;
+  } else if (mode == 2) {   // compact [nvc][27] (ITERATIVE_SCHUR: diagonal Schur blocks + rhs, no dense S)
+    S[(size_t)v * 27 + k] = -acc;
   } else {
     const size_t ld = (size_t)P.ld;
     if (k < 21) {
@@ -1447,10 +1405,11 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
   else
     hipLaunchKernelGGL(k_obs_w<false>, dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.W);
 }
-void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s) {
+void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact) {
   if (P.nvc == 0) return;
   hipLaunchKernelGGL(k_cam_schur_diag, dim3(P.nvc, kCamSplit), dim3(kThreads), 0, s, P, W.W, W.u, W.S, W.cpart);
-  hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, 1, W.Hcc, W.gc, W.S);
+  hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, compact ? 2 : 1, W.Hcc,
+                     W.gc, compact ? compact : W.S);
 }
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (W.nblocks == 0) return;

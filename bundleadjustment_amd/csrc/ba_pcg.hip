@@ -1,0 +1,400 @@
+// ba_pcg.hip — ITERATIVE_SCHUR on gfx950: preconditioned conjugate gradients
+// on the implicit reduced camera system.
+//
+// Ceres semantics restated (iterative_schur_complement_solver.cc,
+// implicit_schur_complement.cc, conjugate_gradients_solver.cc; the oracle's
+// iterative_schur_solve is the CPU statement of the same algorithm):
+//
+//   (S x)_c = A_c x_c - sum_{o in c} W_o v_{p(o)},   v_p = sum_{o in p} W_o^T x_{c(o)},
+//   A_c = s_c Hcc_c s_c + D_c^2
+//
+// with W_o = diag(s_c) Jc^T Jp diag(s_p) L_p^-T (6x3, the same per-observation
+// blocks the DENSE_SCHUR path builds) — never forming S.  One matvec is two
+// HBM passes over W: a point pass (observations contiguous per point) and a
+// camera pass (observations gathered per camera, sliced over workgroups).
+// Everything on the camera side (6 nvc entries: A x, preconditioner,
+// dot products, the CG recurrences and Ceres' termination tests) is one
+// 1024-thread workgroup: the vectors are small, and a single workgroup
+// gives fixed-order reductions without grid barriers.  Multi-GPU: each rank
+// holds a point shard; the camera slices of every matvec are summed with one
+// RCCL all-reduce of 6 nvc x slices doubles (ba_solver.hip); all other CG
+// state is replicated and evolves identically on every rank.
+//
+// All reductions are fixed-order: results are bitwise reproducible.
+#include "ba_kernels.h"
+#include "ba_device.h"
+#include "ba_reduce.h"
+
+namespace bahip {
+
+constexpr int kPcgThreads = 1024;   // camera-side workgroup
+
+__device__ inline bool zero_or_inf(double x) { return x == 0.0 || isinf(x); }   // ceres IsZeroOrInfinity
+
+// lower-triangle index of (a, b), a >= b
+__device__ inline int tri(int a, int b) { return a * (a + 1) / 2 + b; }
+
+// y = A x for a symmetric 6x6 block stored as its lower 21 entries
+__device__ inline void sym6_mul(const double* __restrict__ A, const double (&x)[6], double (&y)[6]) {
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    double v = 0.0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) v += A[a >= b ? tri(a, b) : tri(b, a)] * x[b];
+    y[a] = v;
+  }
+}
+
+// Inverse of an SPD 6x6 block (lower 21) by LLT + two triangular solves
+// against I (Eigen selfadjointView().llt().solve(Identity), as Ceres'
+// BlockRandomAccessDiagonalMatrix::Invert).  Returns false if not PD.
+__device__ inline bool spd6_inverse(const double (&M)[21], double* __restrict__ out /*36, row-major*/) {
+  double L[21];
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double d = M[tri(j, j)];
+#pragma unroll
+    for (int t = 0; t < j; ++t) d -= L[tri(j, t)] * L[tri(j, t)];
+    ok = ok && d > 0.0;
+    d = sqrt(d);
+    L[tri(j, j)] = d;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double v = M[tri(i, j)];
+#pragma unroll
+      for (int t = 0; t < j; ++t) v -= L[tri(i, t)] * L[tri(j, t)];
+      L[tri(i, j)] = v / d;
+    }
+  }
+#pragma unroll
+  for (int col = 0; col < 6; ++col) {
+    double z[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      double v = i == col ? 1.0 : 0.0;
+#pragma unroll
+      for (int t = 0; t < i; ++t) v -= L[tri(i, t)] * z[t];
+      z[i] = v / L[tri(i, i)];
+    }
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {
+      double v = z[i];
+#pragma unroll
+      for (int t = i + 1; t < 6; ++t) v -= L[tri(t, i)] * z[t];
+      z[i] = v / L[tri(i, i)];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) out[i * 6 + col] = z[i];
+  }
+  return ok;
+}
+
+__device__ inline void mat6_mul(const double* __restrict__ M, const double (&x)[6], double (&y)[6]) {
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    double v = 0.0;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) v += M[a * 6 + b] * x[b];
+    y[a] = v;
+  }
+}
+
+__device__ inline void load6(const double* __restrict__ p, double (&v)[6]) {
+#pragma unroll
+  for (int a = 0; a < 6; ++a) v[a] = p[a];
+}
+__device__ inline void store6(double* __restrict__ p, const double (&v)[6]) {
+#pragma unroll
+  for (int a = 0; a < 6; ++a) p[a] = v[a];
+}
+
+__device__ inline void pcg_stop(double* st, double* scal, int term, int iters) {
+  if (threadIdx.x == 0) {
+    st[PS_DONE] = 1.0;
+    st[PS_TERM] = term;
+    st[PS_ITER] = iters;
+    if (term == PCG_FAILURE) scal[SL_CHOL_BAD] = 1.0;   // linear solver failure -> invalid step
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Schur-Jacobi cross terms of a point observed twice by one camera:
+// Sd_c -= W_a W_b^T + W_b W_a^T (lower), one thread per camera (fixed order)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pcg_dup(DevProblem P, const int* __restrict__ dup_off,
+                                                 const int2* __restrict__ dup_pairs, const double* __restrict__ Wm,
+                                                 double* __restrict__ Sd) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= P.nvc) return;
+  for (int i = dup_off[v]; i < dup_off[v + 1]; ++i) {
+    const int2 pr = dup_pairs[i];
+    const double* wa = Wm + (size_t)pr.x * 18;
+    const double* wb = Wm + (size_t)pr.y * 18;
+    for (int a = 0; a < 6; ++a)
+      for (int b = 0; b <= a; ++b) {
+        double s = 0.0;
+        for (int t = 0; t < 3; ++t) s += wa[a * 3 + t] * wb[b * 3 + t] + wb[a * 3 + t] * wa[b * 3 + t];
+        Sd[(size_t)v * 27 + tri(a, b)] -= s;
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// setup (one workgroup): A_c = s Hcc s + D^2, preconditioner block
+// M_c = A_c (JACOBI) or A_c + Sd_c (SCHUR_JACOBI) inverted, rhs
+// b_c = Sd_c[rhs] + s g_c; x = 0, r = b, z = M r, p = z; rho = r.z;
+// ceres' norm_b == 0 exit and the first iteration's rho test.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_setup(DevProblem P, const double* __restrict__ Sd,
+                                                           const double* __restrict__ Hcc,
+                                                           const double* __restrict__ gc,
+                                                           const double* __restrict__ scale_c,
+                                                           const double* __restrict__ diag_c, double radius,
+                                                           int schur_jacobi, double* __restrict__ Adiag,
+                                                           double* __restrict__ Minv, double* __restrict__ b,
+                                                           double* __restrict__ x, double* __restrict__ r,
+                                                           double* __restrict__ z, double* __restrict__ p,
+                                                           double* __restrict__ scal) {
+  __shared__ double lds[3 * 16];
+  double* st = scal + kNumSlots;
+  double acc[3] = {0.0, 0.0, 0.0};   // |b|^2, r.z, bad blocks
+  for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) {
+    double s[6], D2[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      s[a] = scale_c[(size_t)v * 6 + a];
+      const double D = sqrt(diag_c[(size_t)v * 6 + a] / radius);
+      D2[a] = D * D;
+    }
+    double A[21], M[21];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int c = 0; c <= a; ++c) {
+        const int k = tri(a, c);
+        double h = Hcc[(size_t)v * 21 + k] * s[a] * s[c];   // same arithmetic as k_cam_add_diag
+        if (a == c) h += D2[a];
+        A[k] = h;
+        M[k] = schur_jacobi ? Sd[(size_t)v * 27 + k] + h : h;
+      }
+#pragma unroll
+    for (int k = 0; k < 21; ++k) Adiag[(size_t)v * 21 + k] = A[k];
+    double* mi = Minv + (size_t)v * 36;
+    if (!spd6_inverse(M, mi)) acc[2] += 1.0;
+    double bv[6], zv[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) bv[a] = Sd[(size_t)v * 27 + 21 + a] + gc[(size_t)v * 6 + a] * s[a];
+    mat6_mul(mi, bv, zv);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const size_t i = (size_t)v * 6 + a;
+      b[i] = bv[a]; r[i] = bv[a]; x[i] = 0.0; z[i] = zv[a]; p[i] = zv[a];
+      acc[0] += bv[a] * bv[a];
+      acc[1] += bv[a] * zv[a];
+    }
+  }
+  block_allsum<3>(acc, lds);
+  if (threadIdx.x == 0) {
+    st[PS_RHO] = 1.0; st[PS_Q0] = -0.0; st[PS_ALPHA] = 0.0; st[PS_NORM_B] = sqrt(acc[0]);
+    st[PS_ITER] = 0.0; st[PS_DONE] = 0.0; st[PS_TERM] = PCG_NO_CONVERGENCE;
+  }
+  if (sqrt(acc[0]) == 0.0) { pcg_stop(st, scal, PCG_SUCCESS, 0); return; }   // x = 0
+  // iteration 1 starts: rho = r.z (an indefinite / singular preconditioner
+  // block yields a non-finite rho: stop as a failure, the step is invalid
+  // either way)
+  if (zero_or_inf(acc[1]) || isnan(acc[1]) || acc[2] != 0.0) { pcg_stop(st, scal, PCG_FAILURE, 1); return; }
+  if (threadIdx.x == 0) st[PS_RHO] = acc[1];
+}
+
+// ---------------------------------------------------------------------------
+// matvec, point pass: v_p = sum_{o in p} W_o^T x_{c(o)}  (thread per point)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pcg_point(DevProblem P, const double* __restrict__ Wm,
+                                                   const double* __restrict__ xv, double* __restrict__ vpt,
+                                                   const double* __restrict__ st) {
+  if (st[PS_DONE] != 0.0) return;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
+    double w0 = 0.0, w1 = 0.0, w2 = 0.0;
+    if (P.pt_var[p]) {
+      const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+      for (int o = o0; o < o1; ++o) {
+        const int v = P.vc[P.obs_cam[o]];
+        if (v < 0) continue;
+        const double2* wo = reinterpret_cast<const double2*>(Wm + (size_t)o * 18);
+        double wv[18];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) { const double2 t = wo[k]; wv[2 * k] = t.x; wv[2 * k + 1] = t.y; }
+        const double* xc = xv + 6 * v;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          const double xa = xc[a];
+          w0 += wv[a * 3] * xa; w1 += wv[a * 3 + 1] * xa; w2 += wv[a * 3 + 2] * xa;
+        }
+      }
+    }
+    vpt[3 * (size_t)p] = w0; vpt[3 * (size_t)p + 1] = w1; vpt[3 * (size_t)p + 2] = w2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// matvec, camera pass: slice g of camera v: sum_{o in slice} W_o v_{p(o)}
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pcg_cam(DevProblem P, const double* __restrict__ Wm,
+                                                 const double* __restrict__ vpt, double* __restrict__ tpart,
+                                                 const double* __restrict__ st) {
+  if (st[PS_DONE] != 0.0) return;
+  __shared__ double lds[6 * 16];
+  const int v = blockIdx.x, g = blockIdx.y, G = gridDim.y;
+  const int a0 = P.cam_off[v], a1 = P.cam_off[v + 1];
+  const int len = (a1 - a0 + G - 1) / G;
+  const int i0 = min(a1, a0 + g * len), i1 = min(a1, i0 + len);
+  double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int o = P.cam_obs[i];
+    const int p = P.obs_pt[o];
+    if (!P.pt_var[p]) continue;
+    const double2* wo = reinterpret_cast<const double2*>(Wm + (size_t)o * 18);
+    double wv[18];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) { const double2 t = wo[k]; wv[2 * k] = t.x; wv[2 * k + 1] = t.y; }
+    const double u0 = vpt[3 * (size_t)p], u1 = vpt[3 * (size_t)p + 1], u2 = vpt[3 * (size_t)p + 2];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[a] += wv[a * 3] * u0 + wv[a * 3 + 1] * u1 + wv[a * 3 + 2] * u2;
+  }
+  double tot[6];
+  block_sum<6>(acc, lds, tot);
+  if (threadIdx.x == 0) {
+    double* dst = tpart + ((size_t)g * P.nvc + v) * 6;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) dst[a] = tot[a];
+  }
+}
+
+// S y for camera v from its A block and the matvec slices of y
+__device__ inline void schur_row(const double* __restrict__ Adiag, const double* __restrict__ tpart, int G, int nvc,
+                                 int v, const double (&y)[6], double (&out)[6]) {
+  sym6_mul(Adiag + (size_t)v * 21, y, out);
+  for (int g = 0; g < G; ++g) {
+    const double* t = tpart + ((size_t)g * nvc + v) * 6;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) out[a] -= t[a];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// camera-side CG iteration (one workgroup), ceres ConjugateGradientsSolver:
+//   q = S p; pq = p.q (<= 0 or inf: NO_CONVERGENCE, stop); alpha = rho / pq
+//   (inf: FAILURE); x += alpha p; r -= alpha q  (every 10th: r = b - S x);
+//   Q1 = -x.(b + r); zeta = it (Q1 - Q0) / Q1 < q_tol: SUCCESS; it >= max:
+//   NO_CONVERGENCE; then iteration it+1 begins: z = M r, rho' = r.z,
+//   beta = rho' / rho (zero or inf: FAILURE), p = z + beta p.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kPcgThreads) void k_pcg_update(DevProblem P, int mode, int it, PcgOpts o, int G,
+                                                            const double* __restrict__ Adiag,
+                                                            const double* __restrict__ Minv,
+                                                            const double* __restrict__ b, double* __restrict__ x,
+                                                            double* __restrict__ r, double* __restrict__ z,
+                                                            double* __restrict__ p, double* __restrict__ q,
+                                                            const double* __restrict__ tpart,
+                                                            double* __restrict__ scal) {
+  __shared__ double lds[2 * 16];
+  double* st = scal + kNumSlots;
+  if (st[PS_DONE] != 0.0) return;
+  const int nvc = P.nvc;
+  double alpha;
+  if (mode != 2) {
+    double acc[1] = {0.0};
+    for (int v = threadIdx.x; v < nvc; v += blockDim.x) {
+      double pv[6], qv[6];
+      load6(p + 6 * (size_t)v, pv);
+      schur_row(Adiag, tpart, G, nvc, v, pv, qv);
+      store6(q + 6 * (size_t)v, qv);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) acc[0] += pv[a] * qv[a];
+    }
+    block_allsum<1>(acc, lds);
+    const double pq = acc[0], rho = st[PS_RHO];
+    if (pq <= 0.0 || isinf(pq)) { pcg_stop(st, scal, PCG_NO_CONVERGENCE, it); return; }
+    alpha = rho / pq;
+    if (isinf(alpha) || isnan(alpha)) { pcg_stop(st, scal, PCG_FAILURE, it); return; }
+    for (int v = threadIdx.x; v < nvc; v += blockDim.x)
+#pragma unroll
+      for (int a = 0; a < 6; ++a) x[6 * (size_t)v + a] = x[6 * (size_t)v + a] + alpha * p[6 * (size_t)v + a];
+    if (mode == 1) {
+      if (threadIdx.x == 0) st[PS_ALPHA] = alpha;
+      return;
+    }
+  } else {
+    alpha = st[PS_ALPHA];
+  }
+  double acc[1] = {0.0};
+  for (int v = threadIdx.x; v < nvc; v += blockDim.x) {
+    double rv[6], xv[6];
+    load6(x + 6 * (size_t)v, xv);
+    if (mode == 2) {
+      double sx[6];
+      schur_row(Adiag, tpart, G, nvc, v, xv, sx);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) rv[a] = b[6 * (size_t)v + a] - sx[a];
+    } else {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) rv[a] = r[6 * (size_t)v + a] - alpha * q[6 * (size_t)v + a];
+    }
+    store6(r + 6 * (size_t)v, rv);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[0] += xv[a] * (b[6 * (size_t)v + a] + rv[a]);
+  }
+  block_allsum<1>(acc, lds);
+  const double Q1 = -1.0 * acc[0];
+  const double Q0 = st[PS_Q0];
+  const double zeta = it * (Q1 - Q0) / Q1;
+  if (zeta < o.q_tolerance && it >= o.min_iter) { pcg_stop(st, scal, PCG_SUCCESS, it); return; }
+  if (it >= o.max_iter) { pcg_stop(st, scal, PCG_NO_CONVERGENCE, it); return; }
+  // iteration it + 1
+  double racc[1] = {0.0};
+  for (int v = threadIdx.x; v < nvc; v += blockDim.x) {
+    double rv[6], zv[6];
+    load6(r + 6 * (size_t)v, rv);
+    mat6_mul(Minv + (size_t)v * 36, rv, zv);
+    store6(z + 6 * (size_t)v, zv);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) racc[0] += rv[a] * zv[a];
+  }
+  block_allsum<1>(racc, lds);
+  const double rho_new = racc[0], rho = st[PS_RHO];
+  if (zero_or_inf(rho_new) || isnan(rho_new)) { pcg_stop(st, scal, PCG_FAILURE, it + 1); return; }
+  const double beta = rho_new / rho;
+  if (zero_or_inf(beta)) { pcg_stop(st, scal, PCG_FAILURE, it + 1); return; }
+  for (int v = threadIdx.x; v < nvc; v += blockDim.x)
+#pragma unroll
+    for (int a = 0; a < 6; ++a) p[6 * (size_t)v + a] = z[6 * (size_t)v + a] + beta * p[6 * (size_t)v + a];
+  if (threadIdx.x == 0) {
+    st[PS_RHO] = rho_new;
+    st[PS_Q0] = Q1;
+    st[PS_ITER] = it;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+void launch_pcg_dup(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  if (P.nvc == 0) return;
+  hipLaunchKernelGGL(k_pcg_dup, dim3((P.nvc + 255) / 256), dim3(256), 0, s, P, W.dup_off, W.dup_pairs, W.W, W.Sd);
+}
+void launch_pcg_setup(const DevProblem& P, const DevWork& W, double radius, const PcgOpts& o, hipStream_t s) {
+  hipLaunchKernelGGL(k_pcg_setup, dim3(1), dim3(kPcgThreads), 0, s, P, W.Sd, W.Hcc, W.gc, W.scale_c, W.diag_c, radius,
+                     o.schur_jacobi, W.Adiag, W.Minv, W.pb, W.y, W.pr, W.pz, W.pp, W.scal);
+}
+void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s) {
+  const double* st = W.scal + kNumSlots;
+  hipLaunchKernelGGL(k_pcg_point, dim3(grid_for(P.np)), dim3(256), 0, s, P, W.W, vec, W.vpt, st);
+  hipLaunchKernelGGL(k_pcg_cam, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.W, W.vpt, W.tpart, st);
+}
+void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, const PcgOpts& o, hipStream_t s) {
+  hipLaunchKernelGGL(k_pcg_update, dim3(1), dim3(kPcgThreads), 0, s, P, mode, it, o, W.pcg_G, W.Adiag, W.Minv, W.pb,
+                     W.y, W.pr, W.pz, W.pp, W.pq, W.tpart, W.scal);
+}
+
+}  // namespace bahip

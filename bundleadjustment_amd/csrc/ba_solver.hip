@@ -85,6 +85,12 @@ struct ba_ctx {
   size_t pose_cap = 0;
   std::vector<char> pose_host;
 
+  // host copies of the sorted structure, kept for the lazily built
+  // linear-solver structures (Schur pair lists / PCG duplicate pairs)
+  std::vector<int> h_pt_off, h_obs_cam, h_vc;
+  std::vector<uint8_t> h_pt_var;
+  bool have_dense = false, have_pcg = false;
+
   // solver state
   std::vector<ba_iteration> log;
   bool scale_valid = false;
@@ -108,7 +114,7 @@ struct ba_ctx {
     if (stream) (void)hipStreamSynchronize(stream);
     for (void* p : allocs) (void)hipFree(p);
     allocs.clear();
-    have_problem = false;
+    have_problem = have_dense = have_pcg = false;
     scale_valid = false;
     log.clear();
   }
@@ -118,7 +124,7 @@ struct ba_ctx {
     NCCL_OK(ncclAllReduce(d, d, count, ncclDouble, op, comm, stream));
   }
   void read_scalars() {
-    HIP_OK(hipMemcpyAsync(h_scal, W.scal, sizeof(double) * kNumSlots, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipMemcpyAsync(h_scal, W.scal, sizeof(double) * (kNumSlots + kPcgState), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
   }
 };
@@ -208,43 +214,6 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
     std::vector<int> fill(cam_off.begin(), cam_off.end() - 1);
     for (int s = 0; s < no; ++s) if (vc[obs_cam[s]] >= 0) cam_obs[fill[vc[obs_cam[s]]]++] = s;
   }
-  // Schur pair lists: for every variable point, every pair of its observations
-  // by variable cameras contributes W_a W_b^T to block (vc_a, vc_b), vc_a >= vc_b.
-  std::vector<int4> blocks;
-  std::vector<int2> pairs;
-  {
-    struct PE { int64_t key; int a, b; };
-    std::vector<PE> pe;
-    size_t est = 0;
-    for (int p = 0; p < np; ++p) if (pt_var[p]) { const size_t k = pt_off[p + 1] - pt_off[p]; est += k * (k - 1) / 2; }
-    pe.reserve(est);
-    std::vector<int> lst;
-    for (int p = 0; p < np; ++p) {
-      if (!pt_var[p]) continue;
-      lst.clear();
-      for (int s = pt_off[p]; s < pt_off[p + 1]; ++s) if (vc[obs_cam[s]] >= 0) lst.push_back(s);
-      for (size_t i = 0; i < lst.size(); ++i)
-        for (size_t j = 0; j < i; ++j) {
-          const int a = lst[i], b = lst[j];        // vc[a] >= vc[b] (sorted by camera)
-          const int I = vc[obs_cam[a]], J = vc[obs_cam[b]];
-          const int64_t key = (int64_t)I * nvc + J;
-          pe.push_back({key, a, b});
-          if (I == J) pe.push_back({key, b, a});    // duplicate camera on one point
-        }
-    }
-    // stable counting/radix by key keeps point order inside a block
-    std::stable_sort(pe.begin(), pe.end(), [](const PE& x, const PE& y) { return x.key < y.key; });
-    pairs.resize(pe.size());
-    for (size_t i = 0; i < pe.size(); ++i) {
-      pairs[i] = make_int2(pe[i].a, pe[i].b);
-      if (i == 0 || pe[i].key != pe[i - 1].key) {
-        if (!blocks.empty()) blocks.back().w = (int)i;
-        blocks.push_back(make_int4((int)(pe[i].key / nvc), (int)(pe[i].key % nvc), (int)i, 0));
-      }
-    }
-    if (!blocks.empty()) blocks.back().w = (int)pe.size();
-  }
-
   // ---- device upload
   DevProblem& P = ctx->P;
   P = DevProblem{};
@@ -291,23 +260,121 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.diag_c = ctx->dalloc<double>(6 * (size_t)nvc);
   W.delta_c = ctx->dalloc<double>(6 * (size_t)nvc);
   W.W = ctx->dalloc<double>(18 * (size_t)no);
+  W.y = ctx->dalloc<double>(std::max(ctx->n, 1));
+  W.part = ctx->dalloc<double>((size_t)kNumSlots * kMaxBlocks);
+  W.scal = ctx->dalloc<double>(kNumSlots + kPcgState);
+  W.cpart = ctx->dalloc<double>((size_t)kCamSplit * 27 * std::max(nvc, 1));
+
+  HIP_OK(hipMemsetAsync(W.part, 0, sizeof(double) * kNumSlots * kMaxBlocks, ctx->stream));
+  HIP_OK(hipMemsetAsync(W.scal, 0, sizeof(double) * (kNumSlots + kPcgState), ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  ctx->perm.swap(perm);
+  ctx->h_pt_off.swap(pt_off);
+  ctx->h_obs_cam.swap(obs_cam);
+  ctx->h_vc.swap(vc);
+  ctx->h_pt_var.swap(pt_var);
+  ctx->have_problem = true;
+}
+
+// DENSE_SCHUR structures (built on the first dense solve): the dense reduced
+// system S / factor Lf (16 n^2 bytes), Cholesky block inverses, and the Schur
+// pair lists.
+void ensure_dense(ba_ctx* ctx) {
+  if (ctx->have_dense) return;
+  const int np = ctx->np, nvc = ctx->nvc;
+  const std::vector<int>& pt_off = ctx->h_pt_off;
+  const std::vector<int>& obs_cam = ctx->h_obs_cam;
+  const std::vector<int>& vc = ctx->h_vc;
+  const std::vector<uint8_t>& pt_var = ctx->h_pt_var;
+  // Schur pair lists: for every variable point, every pair of its observations
+  // by variable cameras contributes W_a W_b^T to block (vc_a, vc_b), vc_a >= vc_b.
+  std::vector<int4> blocks;
+  std::vector<int2> pairs;
+  {
+    struct PE { int64_t key; int a, b; };
+    std::vector<PE> pe;
+    size_t est = 0;
+    for (int p = 0; p < np; ++p) if (pt_var[p]) { const size_t k = pt_off[p + 1] - pt_off[p]; est += k * (k - 1) / 2; }
+    pe.reserve(est);
+    std::vector<int> lst;
+    for (int p = 0; p < np; ++p) {
+      if (!pt_var[p]) continue;
+      lst.clear();
+      for (int s = pt_off[p]; s < pt_off[p + 1]; ++s) if (vc[obs_cam[s]] >= 0) lst.push_back(s);
+      for (size_t i = 0; i < lst.size(); ++i)
+        for (size_t j = 0; j < i; ++j) {
+          const int a = lst[i], b = lst[j];        // vc[a] >= vc[b] (sorted by camera)
+          const int I = vc[obs_cam[a]], J = vc[obs_cam[b]];
+          const int64_t key = (int64_t)I * nvc + J;
+          pe.push_back({key, a, b});
+          if (I == J) pe.push_back({key, b, a});    // duplicate camera on one point
+        }
+    }
+    // stable counting/radix by key keeps point order inside a block
+    std::stable_sort(pe.begin(), pe.end(), [](const PE& x, const PE& y) { return x.key < y.key; });
+    pairs.resize(pe.size());
+    for (size_t i = 0; i < pe.size(); ++i) {
+      pairs[i] = make_int2(pe[i].a, pe[i].b);
+      if (i == 0 || pe[i].key != pe[i - 1].key) {
+        if (!blocks.empty()) blocks.back().w = (int)i;
+        blocks.push_back(make_int4((int)(pe[i].key / nvc), (int)(pe[i].key % nvc), (int)i, 0));
+      }
+    }
+    if (!blocks.empty()) blocks.back().w = (int)pe.size();
+  }
+
+  DevWork& W = ctx->W;
   W.S = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
   W.Lf = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
-  W.y = ctx->dalloc<double>(std::max(ctx->n, 1));
   W.Vbuf = ctx->dalloc<double>((size_t)((ctx->n + 63) / 64 + 1) * 64 * 64);
   W.flags = ctx->dalloc<int>(kFlagWords);
   W.blocks = ctx->upload(blocks);
   W.nblocks = (int)blocks.size();
   W.pairs = ctx->upload(pairs);
-  W.part = ctx->dalloc<double>((size_t)kNumSlots * kMaxBlocks);
-  W.scal = ctx->dalloc<double>(kNumSlots);
-  W.cpart = ctx->dalloc<double>((size_t)kCamSplit * 27 * std::max(nvc, 1));
-
-  HIP_OK(hipMemsetAsync(W.part, 0, sizeof(double) * kNumSlots * kMaxBlocks, ctx->stream));
-  HIP_OK(hipMemsetAsync(W.scal, 0, sizeof(double) * kNumSlots, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
-  ctx->perm.swap(perm);
-  ctx->have_problem = true;
+  ctx->have_dense = true;
+}
+
+// ITERATIVE_SCHUR structures: compact diagonal blocks, preconditioner, CG
+// vectors, matvec scratch, and the (rare) pairs of observations of one point
+// by one camera, whose cross terms belong to the Schur-Jacobi diagonal block.
+void ensure_pcg(ba_ctx* ctx) {
+  if (ctx->have_pcg) return;
+  const int np = ctx->np, nvc = ctx->nvc;
+  const size_t n = (size_t)std::max(ctx->n, 1);
+  DevWork& W = ctx->W;
+  W.pcg_G = nvc > 0 ? std::min(kCamSplit, std::max(1, 2048 / nvc)) : 1;
+  W.Sd = ctx->dalloc<double>(27 * (size_t)std::max(nvc, 1));
+  W.Adiag = ctx->dalloc<double>(21 * (size_t)std::max(nvc, 1));
+  W.Minv = ctx->dalloc<double>(36 * (size_t)std::max(nvc, 1));
+  W.pb = ctx->dalloc<double>(n);
+  W.pr = ctx->dalloc<double>(n);
+  W.pz = ctx->dalloc<double>(n);
+  W.pp = ctx->dalloc<double>(n);
+  W.pq = ctx->dalloc<double>(n);
+  W.vpt = ctx->dalloc<double>(3 * (size_t)std::max(np, 1));
+  W.tpart = ctx->dalloc<double>((size_t)W.pcg_G * 6 * std::max(nvc, 1));
+  std::vector<int> dup_off(nvc + 1, 0);
+  std::vector<int2> dup;
+  {
+    std::vector<std::vector<int2>> per(nvc);
+    for (int p = 0; p < np; ++p) {
+      if (!ctx->h_pt_var[p]) continue;
+      for (int a = ctx->h_pt_off[p]; a < ctx->h_pt_off[p + 1]; ++a)
+        for (int b = a + 1; b < ctx->h_pt_off[p + 1] && ctx->h_obs_cam[b] == ctx->h_obs_cam[a]; ++b) {
+          const int v = ctx->h_vc[ctx->h_obs_cam[a]];
+          if (v >= 0) per[v].push_back(make_int2(a, b));
+        }
+    }
+    for (int v = 0; v < nvc; ++v) {
+      dup_off[v + 1] = dup_off[v] + (int)per[v].size();
+      dup.insert(dup.end(), per[v].begin(), per[v].end());
+    }
+  }
+  W.dup_off = ctx->upload(dup_off);
+  W.dup_pairs = ctx->upload(dup);
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  ctx->have_pcg = true;
 }
 
 // ---------------------------------------------------------------------------
@@ -350,14 +417,15 @@ LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max
   return r;
 }
 
-struct StepResult { bool linear_ok; double mcc, cand_cost, step_norm; };
+struct StepResult { bool linear_ok; double mcc, cand_cost, step_norm; int ls_iters; };
 
-StepResult solve_step(ba_ctx* ctx, double radius) {
+// DENSE_SCHUR: explicit reduced camera system + dense Cholesky
+void reduced_solve_dense(ba_ctx* ctx, double radius) {
   const hipStream_t s = ctx->stream;
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
+  ensure_dense(ctx);
   if (ctx->n > 0) HIP_OK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)(ctx->n + 1) * ctx->ld, s));
-  HIP_OK(hipMemsetAsync(W.scal + SL_CHOL_BAD, 0, sizeof(double), s));
   launch_point_elim(P, W, radius, s);
   launch_cam_schur_diag(P, W, s);
   launch_schur_pairs(P, W, s);
@@ -368,6 +436,61 @@ StepResult solve_step(ba_ctx* ctx, double radius) {
   }
   launch_cam_add_diag(P, W, radius, s);
   launch_cholesky_solve2(P, W, s);
+}
+
+// ITERATIVE_SCHUR: implicit Schur complement + PCG (ba_pcg.hip).  The host
+// enqueues CG iterations in batches and reads the device-side state record
+// between batches (the kernels of iterations past termination return at
+// once); every rank enqueues the same sequence, so the RCCL all-reduce of
+// each matvec's camera slices stays matched.  Returns the CG iteration count.
+int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
+  const hipStream_t s = ctx->stream;
+  DevProblem& P = ctx->P;
+  DevWork& W = ctx->W;
+  ensure_pcg(ctx);
+  PcgOpts po{o.eta, o.min_linear_solver_iterations, std::max(1, o.max_linear_solver_iterations),
+             o.preconditioner_type == BA_SCHUR_JACOBI ? 1 : 0};
+  launch_point_elim(P, W, radius, s);
+  launch_cam_schur_diag(P, W, s, W.Sd);
+  if (po.schur_jacobi) launch_pcg_dup(P, W, s);
+  launch_reduce(W, bit(SL_ELIM_BAD), 0, s);
+  const size_t tcount = (size_t)W.pcg_G * 6 * ctx->nvc;
+  if (ctx->nranks > 1) {
+    ctx->allreduce(W.Sd, 27 * (size_t)ctx->nvc);
+    ctx->allreduce(W.scal + SL_ELIM_BAD, 1);
+  }
+  if (ctx->nvc == 0) return 0;
+  launch_pcg_setup(P, W, radius, po, s);
+  int it = 0, batch = 4;
+  for (;;) {
+    for (int k = 0; k < batch && it < po.max_iter; ++k) {
+      ++it;
+      launch_pcg_matvec(P, W, W.pp, s);
+      if (ctx->nranks > 1) ctx->allreduce(W.tpart, tcount);
+      if (it % 10 == 0) {   // ceres residual_reset_period: r = b - S x
+        launch_pcg_update(P, W, 1, it, po, s);
+        launch_pcg_matvec(P, W, W.y, s);
+        if (ctx->nranks > 1) ctx->allreduce(W.tpart, tcount);
+        launch_pcg_update(P, W, 2, it, po, s);
+      } else {
+        launch_pcg_update(P, W, 0, it, po, s);
+      }
+    }
+    ctx->read_scalars();
+    if (ctx->h_scal[kNumSlots + PS_DONE] != 0.0 || it >= po.max_iter) break;
+    batch = std::min(2 * batch, 32);
+  }
+  return (int)ctx->h_scal[kNumSlots + PS_ITER];
+}
+
+StepResult solve_step(ba_ctx* ctx, double radius, const ba_options& o) {
+  const hipStream_t s = ctx->stream;
+  DevProblem& P = ctx->P;
+  DevWork& W = ctx->W;
+  HIP_OK(hipMemsetAsync(W.scal + SL_CHOL_BAD, 0, sizeof(double), s));
+  int ls_iters = 1;
+  if (o.linear_solver == BA_ITERATIVE_SCHUR) ls_iters = reduced_solve_pcg(ctx, radius, o);
+  else reduced_solve_dense(ctx, radius);
   launch_cam_candidate(P, W, s);
   launch_backsub_candidate(P, W, s);
   launch_reduce(W, bit(SL_MCC_NEG) | bit(SL_CCOST) | bit(SL_STEP2_P) | bit(SL_CAND_BAD) | bit(SL_STEP_BAD) |
@@ -382,12 +505,24 @@ StepResult solve_step(ba_ctx* ctx, double radius) {
   r.mcc = -h[SL_MCC_NEG];
   r.cand_cost = h[SL_CAND_BAD] > 0.0 || !std::isfinite(h[SL_CCOST]) ? std::numeric_limits<double>::max() : h[SL_CCOST];
   r.step_norm = std::sqrt(h[SL_STEP2_P] + h[SL_STEP2_C]);
+  r.ls_iters = ls_iters;
   return r;
 }
 
 void accept_candidate(ba_ctx* ctx) {
   std::swap(ctx->W.cams, ctx->W.cams_c);
   std::swap(ctx->W.pts, ctx->W.pts_c);
+}
+
+void check_options(const ba_options& o) {
+  if (o.linear_solver != BA_DENSE_SCHUR && o.linear_solver != BA_ITERATIVE_SCHUR)
+    throw BaError{BA_ERR_INVALID_ARGUMENT, "unknown linear_solver " + std::to_string(o.linear_solver)};
+  if (o.linear_solver == BA_ITERATIVE_SCHUR &&
+      ((o.preconditioner_type != BA_JACOBI && o.preconditioner_type != BA_SCHUR_JACOBI) ||
+       o.max_linear_solver_iterations < 1 || o.min_linear_solver_iterations < 0 || !(o.eta > 0.0)))
+    throw BaError{BA_ERR_INVALID_ARGUMENT, "invalid ITERATIVE_SCHUR options"};
+  if (o.precision != BA_FP64)
+    throw BaError{BA_ERR_INVALID_ARGUMENT, "precision " + std::to_string(o.precision) + " not supported"};
 }
 
 // ---------------------------------------------------------------------------
@@ -397,6 +532,7 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
   if (!ctx->have_problem) throw BaError{BA_ERR_NO_PROBLEM, "ba_solve before ba_set_problem"};
   ba_options o;
   if (opt) o = *opt; else ba_default_options(&o);
+  check_options(o);
   const double t0 = now_s();
   ctx->log.clear();
   ctx->t_lin = ctx->t_solve = 0.0;
@@ -447,8 +583,9 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
     ba_iteration it{};
     it.iteration = iteration;
     double ts = now_s();
-    StepResult st = solve_step(ctx, radius);
+    StepResult st = solve_step(ctx, radius, o);
     ctx->t_solve += now_s() - ts;
+    it.linear_solver_iterations = st.ls_iters;
     const bool valid = st.linear_ok && st.mcc > 0.0;
     it.model_cost_change = st.mcc;
     if (!valid) {
@@ -551,6 +688,11 @@ void ba_default_options(ba_options* o) {
   o->min_relative_decrease = 1e-3;
   o->min_lm_diagonal = 1e-6;
   o->max_lm_diagonal = 1e32;
+  o->preconditioner_type = BA_JACOBI;
+  o->max_linear_solver_iterations = 500;
+  o->min_linear_solver_iterations = 0;
+  o->precision = BA_FP64;
+  o->eta = 1e-1;
 }
 
 int ba_create(ba_ctx** out, int device) {
@@ -565,7 +707,7 @@ int ba_create(ba_ctx** out, int device) {
     HIP_OK(hipSetDevice(device));
     HIP_OK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     for (auto& e : ctx->ev) HIP_OK(hipEventCreate(&e));
-    HIP_OK(hipHostMalloc(&ctx->h_scal, sizeof(double) * kNumSlots, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc(&ctx->h_scal, sizeof(double) * (kNumSlots + kPcgState), hipHostMallocDefault));
   } catch (const BaError& e) {
     std::fprintf(stderr, "ba_create: %s\n", e.msg.c_str());
     delete ctx;
@@ -840,21 +982,25 @@ int ba_synchronize(ba_ctx* ctx) {
   return guarded(ctx, [&] { HIP_OK(hipStreamSynchronize(ctx->stream)); });
 }
 
-int ba_bench_iterations(ba_ctx* ctx, int iters, double radius, double* ms_per_iter, double* ms_rj_kernel) {
+int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double radius, double* ms_per_iter,
+                        double* ms_rj_kernel, double* linear_iters) {
   if (!ctx || iters < 1) return BA_ERR_INVALID_ARGUMENT;
   return guarded(ctx, [&] {
     if (!ctx->have_problem) throw BaError{BA_ERR_NO_PROBLEM, "no problem"};
     HIP_OK(hipSetDevice(ctx->device));
     ba_options o;
-    ba_default_options(&o);
+    if (opt) o = *opt; else ba_default_options(&o);
+    check_options(o);
     if (!ctx->scale_valid) linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
     double rj_total = 0.0;
+    long ls_total = 0;
     HIP_OK(hipEventRecord(ctx->ev[0], ctx->stream));
     for (int i = 0; i < iters; ++i) {
       float rj = 0.0f;
       linearize(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, &rj);
       rj_total += rj;
-      solve_step(ctx, radius);
+      const StepResult st = solve_step(ctx, radius, o);
+      ls_total += st.ls_iters;
     }
     HIP_OK(hipEventRecord(ctx->ev[1], ctx->stream));
     HIP_OK(hipEventSynchronize(ctx->ev[1]));
@@ -862,6 +1008,7 @@ int ba_bench_iterations(ba_ctx* ctx, int iters, double radius, double* ms_per_it
     HIP_OK(hipEventElapsedTime(&total, ctx->ev[0], ctx->ev[1]));
     if (ms_per_iter) *ms_per_iter = total / iters;
     if (ms_rj_kernel) *ms_rj_kernel = rj_total / iters;
+    if (linear_iters) *linear_iters = (double)ls_total / iters;
   });
 }
 

@@ -35,13 +35,26 @@ class Options:
     min_relative_decrease: float = 1e-3
     min_lm_diagonal: float = 1e-6
     max_lm_diagonal: float = 1e32
+    # linear solver: "DENSE_SCHUR" (the reference's, Optimizer.cpp:85) or
+    # "ITERATIVE_SCHUR" (implicit Schur + PCG, for C5-scale camera counts)
+    linear_solver_type: str = "DENSE_SCHUR"
+    preconditioner_type: str = "JACOBI"        # ceres default; or "SCHUR_JACOBI"
+    max_linear_solver_iterations: int = 500
+    min_linear_solver_iterations: int = 0
+    eta: float = 1e-1
+    precision: str = "FP64"                    # or "MIXED_FP32" (ITERATIVE_SCHUR)
 
     def to_c(self) -> N.ba_options:
         o = N.ba_options()
         o.max_num_iterations = int(self.max_num_iterations)
         o.max_num_consecutive_invalid_steps = int(self.max_num_consecutive_invalid_steps)
         o.jacobi_scaling = int(bool(self.jacobi_scaling))
-        o.linear_solver = 0
+        o.linear_solver = {"DENSE_SCHUR": 0, "ITERATIVE_SCHUR": 1}[self.linear_solver_type]
+        o.preconditioner_type = {"JACOBI": 0, "SCHUR_JACOBI": 1}[self.preconditioner_type]
+        o.max_linear_solver_iterations = int(self.max_linear_solver_iterations)
+        o.min_linear_solver_iterations = int(self.min_linear_solver_iterations)
+        o.precision = {"FP64": 0, "MIXED_FP32": 1}[self.precision]
+        o.eta = float(self.eta)
         for f in ("function_tolerance", "gradient_tolerance", "parameter_tolerance",
                   "initial_trust_region_radius", "max_trust_region_radius", "min_trust_region_radius",
                   "min_relative_decrease", "min_lm_diagonal", "max_lm_diagonal"):
@@ -62,7 +75,7 @@ class Summary:
     solve_time_s: float
 
 
-ITER_FIELDS = [f for f, _ in N.ba_iteration._fields_ if f != "reserved"]
+ITER_FIELDS = [f for f, _ in N.ba_iteration._fields_]
 
 
 class Solver:
@@ -217,11 +230,19 @@ class Solver:
     def synchronize(self):
         self._check(self.lib.ba_synchronize(self.h), "ba_synchronize")
 
-    def bench_iterations(self, iters: int, radius: float = 1e4) -> tuple[float, float]:
+    def bench_iterations(self, iters: int, radius: float = 1e4, options: Options | None = None,
+                         with_linear_iters: bool = False):
+        """Device time of `iters` LM iterations at a fixed radius: returns
+        (ms per iteration, ms of the residual+Jacobian kernel[, mean linear
+        solver iterations per LM iteration])."""
         ms = C.c_double()
         rj = C.c_double()
-        self._check(self.lib.ba_bench_iterations(self.h, int(iters), float(radius), C.byref(ms), C.byref(rj)),
-                    "ba_bench_iterations")
+        li = C.c_double()
+        o = (options or Options()).to_c()
+        self._check(self.lib.ba_bench_iterations(self.h, C.byref(o), int(iters), float(radius), C.byref(ms),
+                                                 C.byref(rj), C.byref(li)), "ba_bench_iterations")
+        if with_linear_iters:
+            return ms.value, rj.value, li.value
         return ms.value, rj.value
 
 

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BA_ABI_VERSION 1
+#define BA_ABI_VERSION 2
 
 enum ba_status {
   BA_OK = 0,
@@ -61,7 +61,21 @@ enum ba_termination {          /* ceres::TerminationType subset */
 };
 
 enum ba_linear_solver {
-  BA_DENSE_SCHUR = 0           /* ceres::DENSE_SCHUR (Optimizer.cpp:85) */
+  BA_DENSE_SCHUR = 0,          /* ceres::DENSE_SCHUR (Optimizer.cpp:85): explicit reduced camera
+                                  system, dense Cholesky (MFMA) */
+  BA_ITERATIVE_SCHUR = 1       /* ceres::ITERATIVE_SCHUR: implicit Schur complement + PCG
+                                  (C5 scale; one 6C all-reduce per CG step) */
+};
+
+enum ba_preconditioner {       /* ceres::PreconditionerType (ITERATIVE_SCHUR only) */
+  BA_JACOBI = 0,               /* ceres default: block diagonal of F'F + D^2 */
+  BA_SCHUR_JACOBI = 1          /* block diagonal of the Schur complement */
+};
+
+enum ba_precision {
+  BA_FP64 = 0,                 /* everything fp64 (the reference's Jets are double) */
+  BA_MIXED_FP32 = 1            /* ITERATIVE_SCHUR: fp32 storage of the per-observation Schur
+                                  blocks W read by every CG step; fp64 accumulation and CG vectors */
 };
 
 typedef struct ba_ctx ba_ctx;
@@ -98,6 +112,12 @@ typedef struct {
   double min_relative_decrease;               /* 1e-3  */
   double min_lm_diagonal;                     /* 1e-6  */
   double max_lm_diagonal;                     /* 1e32  */
+  /* ITERATIVE_SCHUR (ceres::Solver::Options defaults; unused by DENSE_SCHUR) */
+  int32_t preconditioner_type;                /* BA_JACOBI */
+  int32_t max_linear_solver_iterations;       /* 500 */
+  int32_t min_linear_solver_iterations;       /* 0   */
+  int32_t precision;                          /* BA_FP64 */
+  double eta;                                 /* 1e-1: CG q_tolerance (LevenbergMarquardtStrategy) */
 } ba_options;
 
 /* ceres::Solver::Summary subset */
@@ -119,7 +139,7 @@ typedef struct {
   int32_t iteration;
   int32_t step_is_valid;
   int32_t step_is_successful;
-  int32_t reserved;
+  int32_t linear_solver_iterations; /* CG iterations (ITERATIVE_SCHUR), 1 for DENSE_SCHUR */
   double cost;
   double cost_change;
   double gradient_max_norm;
@@ -160,7 +180,8 @@ int ba_set_problem(ba_ctx* ctx, const ba_problem* problem);
 /* Replace the parameter values of the current problem (same structure). */
 int ba_set_params(ba_ctx* ctx, const double* cams, const double* pts);
 
-/* Levenberg-Marquardt with DENSE_SCHUR (ceres::Solve semantics). */
+/* Levenberg-Marquardt with DENSE_SCHUR or ITERATIVE_SCHUR (ceres::Solve
+ * semantics; opt->linear_solver). */
 int ba_solve(ba_ctx* ctx, const ba_options* opt, ba_summary* summary);
 
 /* Current parameters (after ba_solve: the returned minimum). */
@@ -245,12 +266,14 @@ int ba_solve_pose_batch(ba_ctx* ctx, const ba_pose_batch* batch, const ba_option
 int ba_synchronize(ba_ctx* ctx);
 
 /* Timing hooks for bench.py: one LM iteration = linearise + assemble + Schur
- * + reduced solve + back-substitution + candidate evaluation at a fixed
- * trust-region radius (no accept/reject bookkeeping).  Runs `iters`
- * iterations on the context's stream and returns the device-measured
- * (HIP events) average milliseconds of the whole iteration and of the
- * residual+Jacobian kernel alone. */
-int ba_bench_iterations(ba_ctx* ctx, int iters, double radius, double* ms_per_iter, double* ms_rj_kernel);
+ * + reduced solve (opt->linear_solver; NULL = defaults) + back-substitution +
+ * candidate evaluation at a fixed trust-region radius (no accept/reject
+ * bookkeeping).  Runs `iters` iterations on the context's stream and returns
+ * the device-measured (HIP events) average milliseconds of the whole
+ * iteration and of the residual+Jacobian kernel alone, and the mean number
+ * of linear-solver iterations per LM iteration (may be NULL). */
+int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double radius, double* ms_per_iter,
+                        double* ms_rj_kernel, double* linear_iters);
 
 #ifdef __cplusplus
 }

@@ -19,7 +19,7 @@ HERE = Path(__file__).resolve().parent
 LIB = HERE / "liboracle.so"
 LOG_FIELDS = ["iteration", "cost", "cost_change", "gradient_max_norm", "gradient_norm", "step_norm",
               "relative_decrease", "trust_region_radius", "step_is_valid", "step_is_successful",
-              "model_cost_change", "_pad"]
+              "model_cost_change", "linear_solver_iterations"]
 TERMINATION = {0: "CONVERGENCE", 1: "NO_CONVERGENCE", 2: "FAILURE"}
 
 
@@ -32,12 +32,15 @@ class _Problem(C.Structure):
 
 class Options(C.Structure):
     _fields_ = [("max_num_iterations", C.c_int32), ("max_num_consecutive_invalid_steps", C.c_int32),
-                ("jacobi_scaling", C.c_int32), ("pad", C.c_int32),
+                ("jacobi_scaling", C.c_int32), ("linear_solver", C.c_int32),
                 ("function_tolerance", C.c_double), ("gradient_tolerance", C.c_double),
                 ("parameter_tolerance", C.c_double), ("initial_trust_region_radius", C.c_double),
                 ("max_trust_region_radius", C.c_double), ("min_trust_region_radius", C.c_double),
                 ("min_relative_decrease", C.c_double), ("min_lm_diagonal", C.c_double),
-                ("max_lm_diagonal", C.c_double)]
+                ("max_lm_diagonal", C.c_double),
+                # ITERATIVE_SCHUR (ceres defaults: JACOBI, 500, 0, fp64, eta 0.1)
+                ("preconditioner_type", C.c_int32), ("max_linear_solver_iterations", C.c_int32),
+                ("min_linear_solver_iterations", C.c_int32), ("precision", C.c_int32), ("eta", C.c_double)]
 
 
 def build(force: bool = False) -> Path:
@@ -130,8 +133,7 @@ def solve(problem, options: Options | None = None, max_log: int = 1024):
     n = lib().oracle_solve(C.byref(s), C.byref(o), _p(log), max_log, _p(summ))
     recs = [dict(zip(LOG_FIELDS, row)) for row in log[:min(n, max_log)]]
     for r in recs:
-        r.pop("_pad")
-        for k in ("iteration", "step_is_valid", "step_is_successful"):
+        for k in ("iteration", "step_is_valid", "step_is_successful", "linear_solver_iterations"):
             r[k] = int(r[k])
     summary = dict(initial_cost=summ[0], final_cost=summ[1], num_iterations=int(summ[2]),
                    num_successful_steps=int(summ[3]), num_unsuccessful_steps=int(summ[4]),

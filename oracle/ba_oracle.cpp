@@ -670,21 +670,326 @@ static bool dense_schur_solve(const Problem& P, const Schur& S, const std::vecto
   return true;
 }
 
-// ----------------------------------------------------------------------------
-// Ceres TrustRegionMinimizer + LevenbergMarquardtStrategy restated.
-// ----------------------------------------------------------------------------
+// ceres::Solver::Options fields used here (Ceres defaults: oracle_default_options)
 struct Options {
   int max_num_iterations;
   int max_num_consecutive_invalid_steps;
   int jacobi_scaling;
-  int pad;
+  int linear_solver;                  // 0 DENSE_SCHUR, 1 ITERATIVE_SCHUR
   double function_tolerance, gradient_tolerance, parameter_tolerance;
   double initial_trust_region_radius, max_trust_region_radius, min_trust_region_radius;
   double min_relative_decrease, min_lm_diagonal, max_lm_diagonal;
+  // ITERATIVE_SCHUR (ceres::Solver::Options defaults)
+  int preconditioner_type;            // 0 JACOBI (ceres default), 1 SCHUR_JACOBI
+  int max_linear_solver_iterations;   // 500
+  int min_linear_solver_iterations;   // 0
+  int precision;                      // 0 fp64 (the oracle always computes in fp64)
+  double eta;                         // 1e-1 (LM forcing sequence -> CG q_tolerance)
 };
+enum { LS_DENSE_SCHUR = 0, LS_ITERATIVE_SCHUR = 1 };
+enum { PC_JACOBI = 0, PC_SCHUR_JACOBI = 1 };
+
+// ----------------------------------------------------------------------------
+// ITERATIVE_SCHUR restated (Ceres 2.0/2.2: iterative_schur_complement_solver.cc,
+// implicit_schur_complement.cc, conjugate_gradients_solver.cc,
+// schur_jacobi_preconditioner.cc, block_random_access_diagonal_matrix.cc).
+// Not used by the reference (configureSolver picks DENSE_SCHUR,
+// Optimizer.cpp:85); it is the scalable linear solver SURVEY.md §8a-a7 / §8e
+// name for C5, restated so the GPU's implicit-Schur PCG has a checker.
+//
+//   S x = D_f^2 x + F'(F x - E (E'E + D_e^2)^-1 E'F x)     (RightMultiply)
+//   rhs = F'(b - E (E'E + D_e^2)^-1 E'b)                    (UpdateRhs)
+//   CG on S x = rhs from x = 0 with Ceres' termination rules
+//   (q_tolerance = eta, r_tolerance = -1: LevenbergMarquardtStrategy),
+//   preconditioner JACOBI = blockdiag(F'F + D_f^2)^-1 or SCHUR_JACOBI =
+//   blockdiag(S)^-1 (6x6 LLT solves against I);
+//   back substitution y_e = (E'E + D_e^2)^-1 E'(b - F x).
+// F holds the rows of residuals with a variable camera, E those with a
+// variable point, b = the corrected residuals (Ceres solves J step = r and
+// negates).  Returns false on LINEAR_SOLVER_FAILURE or a non-finite step.
+// ----------------------------------------------------------------------------
+static bool llt_inverse(const double* A, int n, double* Ai) {   // Eigen selfadjointView<Upper>().llt().solve(I)
+  std::vector<double> Lm((size_t)n * n, 0.0);
+  for (int j = 0; j < n; ++j) {
+    double d = A[j * n + j];
+    for (int t = 0; t < j; ++t) d -= Lm[j * n + t] * Lm[j * n + t];
+    if (!(d > 0.0)) return false;
+    d = std::sqrt(d);
+    Lm[j * n + j] = d;
+    for (int i = j + 1; i < n; ++i) {
+      double v = A[i * n + j];
+      for (int t = 0; t < j; ++t) v -= Lm[i * n + t] * Lm[j * n + t];
+      Lm[i * n + j] = v / d;
+    }
+  }
+  for (int col = 0; col < n; ++col) {
+    std::vector<double> z(n, 0.0);
+    for (int i = 0; i < n; ++i) {
+      double v = i == col ? 1.0 : 0.0;
+      for (int t = 0; t < i; ++t) v -= Lm[i * n + t] * z[t];
+      z[i] = v / Lm[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+      double v = z[i];
+      for (int t = i + 1; t < n; ++t) v -= Lm[t * n + i] * z[t];
+      z[i] = v / Lm[i * n + i];
+    }
+    for (int i = 0; i < n; ++i) Ai[i * n + col] = z[i];
+  }
+  return true;
+}
+
+static inline bool zero_or_inf(double x) { return x == 0.0 || std::isinf(x); }   // ceres IsZeroOrInfinity
+
+static bool iterative_schur_solve(const Problem& P, const Schur& S, const std::vector<Lin>& L,
+                                  const std::vector<double>& s, const std::vector<double>& D, const Options& opt,
+                                  std::vector<double>& y, int* cg_iterations) {
+  const int nf = S.nf, n = 6 * nf, npv = (int)P.var_pts.size();
+  y.assign(P.ncols, 0.0);
+  *cg_iterations = 0;
+  auto scJc = [&](int o, double* Jc) {
+    const int cc = P.cam_col[P.obs_cam[o]];
+    for (int i = 0; i < 2; ++i) for (int k = 0; k < 6; ++k) Jc[i * 6 + k] = L[o].Jc[i * 6 + k] * s[cc + k];
+  };
+  auto scJp = [&](int o, double* Jp) {
+    const int pc = P.pt_col[P.obs_pt[o]];
+    for (int i = 0; i < 2; ++i) for (int k = 0; k < 3; ++k) Jp[i * 3 + k] = L[o].Jp[i * 3 + k] * s[pc + k];
+  };
+  auto has_f = [&](int o) { return P.type[o] == RB_ANGLE || P.type[o] == RB_POSE_ONLY; };
+  auto has_e = [&](int o) { return P.type[o] == RB_ANGLE || P.type[o] == RB_POINT_ONLY; };
+  std::vector<int> vp(P.np, -1);
+  for (int i = 0; i < npv; ++i) vp[P.var_pts[i]] = i;
+  // (E'E + D_e^2)^-1 per point (ImplicitSchurComplement::AddDiagonalAndInvert)
+  std::vector<double> ete_inv((size_t)npv * 9);
+  for (int ip = 0; ip < npv; ++ip) {
+    const int pc = P.pt_col[P.var_pts[ip]];
+    double ete[9] = {0};
+    for (int o : S.pt_obs[ip]) {
+      double Jp[6];
+      scJp(o, Jp);
+      for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) ete[a * 3 + b] += Jp[a] * Jp[b] + Jp[3 + a] * Jp[3 + b];
+    }
+    for (int a = 0; a < 3; ++a) ete[a * 3 + a] += D[pc + a] * D[pc + a];
+    if (!inv3_spd(ete, &ete_inv[(size_t)ip * 9])) return false;
+  }
+  // rows: 2 per observation
+  auto F_mul = [&](const std::vector<double>& xf, std::vector<double>& rows) {   // rows += F xf
+    for (int o = 0; o < P.no; ++o) {
+      if (!has_f(o)) continue;
+      double Jc[12];
+      scJc(o, Jc);
+      const double* xc = &xf[6 * S.fidx[P.obs_cam[o]]];
+      for (int i = 0; i < 2; ++i) {
+        double v = 0;
+        for (int k = 0; k < 6; ++k) v += Jc[i * 6 + k] * xc[k];
+        rows[2 * o + i] += v;
+      }
+    }
+  };
+  auto Ft_mul = [&](const std::vector<double>& rows, std::vector<double>& yf) {   // yf += F' rows
+    for (int o = 0; o < P.no; ++o) {
+      if (!has_f(o)) continue;
+      double Jc[12];
+      scJc(o, Jc);
+      double* yc = &yf[6 * S.fidx[P.obs_cam[o]]];
+      for (int k = 0; k < 6; ++k) yc[k] += Jc[k] * rows[2 * o] + Jc[6 + k] * rows[2 * o + 1];
+    }
+  };
+  auto Et_mul = [&](const std::vector<double>& rows, std::vector<double>& ye) {   // ye += E' rows
+    for (int o = 0; o < P.no; ++o) {
+      if (!has_e(o)) continue;
+      double Jp[6];
+      scJp(o, Jp);
+      double* yp = &ye[3 * vp[P.obs_pt[o]]];
+      for (int k = 0; k < 3; ++k) yp[k] += Jp[k] * rows[2 * o] + Jp[3 + k] * rows[2 * o + 1];
+    }
+  };
+  auto E_mul = [&](const std::vector<double>& xe, std::vector<double>& rows) {   // rows += E xe
+    for (int o = 0; o < P.no; ++o) {
+      if (!has_e(o)) continue;
+      double Jp[6];
+      scJp(o, Jp);
+      const double* xp = &xe[3 * vp[P.obs_pt[o]]];
+      for (int i = 0; i < 2; ++i) rows[2 * o + i] += Jp[i * 3] * xp[0] + Jp[i * 3 + 1] * xp[1] + Jp[i * 3 + 2] * xp[2];
+    }
+  };
+  auto ete_mul = [&](const std::vector<double>& xe, std::vector<double>& ye, double sign) {
+    for (int ip = 0; ip < npv; ++ip) {
+      const double* m = &ete_inv[(size_t)ip * 9];
+      for (int a = 0; a < 3; ++a)
+        ye[3 * ip + a] += sign * (m[a * 3] * xe[3 * ip] + m[a * 3 + 1] * xe[3 * ip + 1] + m[a * 3 + 2] * xe[3 * ip + 2]);
+    }
+  };
+  std::vector<double> b(2 * (size_t)P.no, 0.0);
+  for (int o = 0; o < P.no; ++o) { b[2 * o] = L[o].r[0]; b[2 * o + 1] = L[o].r[1]; }
+  const std::vector<double> zf(n, 0.0), ze(3 * (size_t)npv, 0.0), zr(2 * (size_t)P.no, 0.0);
+  auto schur_mul = [&](const std::vector<double>& x, std::vector<double>& out) {   // ImplicitSchurComplement::RightMultiply
+    std::vector<double> rows = zr, te = ze, te2 = ze;
+    F_mul(x, rows);
+    Et_mul(rows, te);
+    ete_mul(te, te2, -1.0);
+    E_mul(te2, rows);
+    out.assign(n, 0.0);
+    for (int c : P.var_cams) {
+      const int f = S.fidx[c], cc = P.cam_col[c];
+      for (int a = 0; a < 6; ++a) out[6 * f + a] = D[cc + a] * D[cc + a] * x[6 * f + a];
+    }
+    Ft_mul(rows, out);
+  };
+  // rhs (UpdateRhs)
+  std::vector<double> rhs(n, 0.0);
+  {
+    std::vector<double> te = ze, y2 = ze, rows = zr;
+    Et_mul(b, te);
+    ete_mul(te, y2, 1.0);
+    E_mul(y2, rows);
+    for (size_t i = 0; i < rows.size(); ++i) rows[i] = b[i] - rows[i];
+    Ft_mul(rows, rhs);
+  }
+  // preconditioner blocks
+  std::vector<double> Minv((size_t)nf * 36, 0.0);
+  {
+    std::vector<double> blk((size_t)nf * 36, 0.0);
+    for (int o = 0; o < P.no; ++o) {
+      if (!has_f(o)) continue;
+      double Jc[12];
+      scJc(o, Jc);
+      double* B = &blk[(size_t)S.fidx[P.obs_cam[o]] * 36];
+      for (int a = 0; a < 6; ++a) for (int c = 0; c < 6; ++c) B[a * 6 + c] += Jc[a] * Jc[c] + Jc[6 + a] * Jc[6 + c];
+    }
+    for (int c : P.var_cams) {
+      const int f = S.fidx[c], cc = P.cam_col[c];
+      for (int a = 0; a < 6; ++a) blk[(size_t)f * 36 + a * 7] += D[cc + a] * D[cc + a];
+    }
+    if (opt.preconditioner_type == PC_SCHUR_JACOBI) {
+      // - sum_p (F_pf'E_p) (E_p'E_p + D^2)^-1 (E_p'F_pf) on the diagonal blocks
+      std::vector<int> fl;
+      std::vector<double> FtE;
+      for (int ip = 0; ip < npv; ++ip) {
+        fl.clear();
+        FtE.clear();
+        for (int o : S.pt_obs[ip]) {
+          if (P.type[o] != RB_ANGLE) continue;
+          const int f = S.fidx[P.obs_cam[o]];
+          int slot = -1;
+          for (size_t q = 0; q < fl.size(); ++q) if (fl[q] == f) slot = (int)q;
+          if (slot < 0) { slot = (int)fl.size(); fl.push_back(f); FtE.resize(FtE.size() + 18, 0.0); }
+          double Jc[12], Jp[6];
+          scJc(o, Jc);
+          scJp(o, Jp);
+          double* B = &FtE[(size_t)slot * 18];
+          for (int a = 0; a < 6; ++a) for (int c = 0; c < 3; ++c) B[a * 3 + c] += Jc[a] * Jp[c] + Jc[6 + a] * Jp[3 + c];
+        }
+        const double* m = &ete_inv[(size_t)ip * 9];
+        for (size_t q = 0; q < fl.size(); ++q) {
+          const double* B = &FtE[q * 18];
+          double T[18];
+          for (int a = 0; a < 6; ++a)
+            for (int c = 0; c < 3; ++c) T[a * 3 + c] = B[a * 3] * m[c] + B[a * 3 + 1] * m[3 + c] + B[a * 3 + 2] * m[6 + c];
+          double* M = &blk[(size_t)fl[q] * 36];
+          for (int a = 0; a < 6; ++a)
+            for (int c = 0; c < 6; ++c) M[a * 6 + c] -= T[a * 3] * B[c * 3] + T[a * 3 + 1] * B[c * 3 + 1] + T[a * 3 + 2] * B[c * 3 + 2];
+        }
+      }
+    }
+    for (int f = 0; f < nf; ++f)
+      if (!llt_inverse(&blk[(size_t)f * 36], 6, &Minv[(size_t)f * 36]))
+        for (int k = 0; k < 36; ++k) Minv[(size_t)f * 36 + k] = std::numeric_limits<double>::quiet_NaN();
+  }
+  auto precond = [&](const std::vector<double>& r, std::vector<double>& z) {
+    z.assign(n, 0.0);
+    for (int f = 0; f < nf; ++f)
+      for (int a = 0; a < 6; ++a) {
+        double v = 0;
+        for (int c = 0; c < 6; ++c) v += Minv[(size_t)f * 36 + a * 6 + c] * r[6 * f + c];
+        z[6 * f + a] = v;
+      }
+  };
+  auto dot = [](const std::vector<double>& u, const std::vector<double>& v) {
+    double d = 0;
+    for (size_t i = 0; i < u.size(); ++i) d += u[i] * v[i];
+    return d;
+  };
+  // ConjugateGradientsSolver::Solve
+  std::vector<double> x(n, 0.0);
+  bool failure = false;
+  if (nf > 0) {
+    const double norm_b = std::sqrt(dot(rhs, rhs));
+    if (norm_b != 0.0) {
+      const double r_tolerance = -1.0, q_tolerance = opt.eta;
+      const double tol_r = r_tolerance * norm_b;
+      std::vector<double> r = rhs, p(n), z, q, tmp;   // x = 0: r = b - A x = b
+      double norm_r = std::sqrt(dot(r, r));
+      if (!(opt.min_linear_solver_iterations == 0 && norm_r <= tol_r)) {
+        double rho = 1.0;
+        std::vector<double> bpr(n);
+        for (int i = 0; i < n; ++i) bpr[i] = rhs[i] + r[i];
+        double Q0 = -1.0 * dot(x, bpr);
+        for (int it = 1;; ++it) {
+          *cg_iterations = it;
+          precond(r, z);
+          const double last_rho = rho;
+          rho = dot(r, z);
+          if (zero_or_inf(rho)) { failure = true; break; }
+          if (it == 1) p = z;
+          else {
+            const double beta = rho / last_rho;
+            if (zero_or_inf(beta)) { failure = true; break; }
+            for (int i = 0; i < n; ++i) p[i] = z[i] + beta * p[i];
+          }
+          schur_mul(p, q);
+          const double pq = dot(p, q);
+          if (pq <= 0 || std::isinf(pq)) break;   // LINEAR_SOLVER_NO_CONVERGENCE: x is still used
+          const double alpha = rho / pq;
+          if (std::isinf(alpha)) { failure = true; break; }
+          for (int i = 0; i < n; ++i) x[i] = x[i] + alpha * p[i];
+          if (it % 10 == 0) {   // residual_reset_period
+            schur_mul(x, tmp);
+            for (int i = 0; i < n; ++i) r[i] = rhs[i] - tmp[i];
+          } else {
+            for (int i = 0; i < n; ++i) r[i] = r[i] - alpha * q[i];
+          }
+          for (int i = 0; i < n; ++i) bpr[i] = rhs[i] + r[i];
+          const double Q1 = -1.0 * dot(x, bpr);
+          const double zeta = it * (Q1 - Q0) / Q1;
+          if (zeta < q_tolerance && it >= opt.min_linear_solver_iterations) break;
+          Q0 = Q1;
+          norm_r = std::sqrt(dot(r, r));
+          if (norm_r <= tol_r && it >= opt.min_linear_solver_iterations) break;
+          if (it >= opt.max_linear_solver_iterations) break;
+        }
+      }
+    }
+  }
+  if (failure) return false;
+  // BackSubstitute
+  {
+    std::vector<double> rows = zr, te = ze, ye = ze;
+    F_mul(x, rows);
+    for (size_t i = 0; i < rows.size(); ++i) rows[i] = b[i] - rows[i];
+    Et_mul(rows, te);
+    ete_mul(te, ye, 1.0);
+    for (int ip = 0; ip < npv; ++ip)
+      for (int a = 0; a < 3; ++a) y[P.pt_col[P.var_pts[ip]] + a] = ye[3 * ip + a];
+    for (int c : P.var_cams) for (int a = 0; a < 6; ++a) y[P.cam_col[c] + a] = x[6 * S.fidx[c] + a];
+  }
+  for (double v : y) if (!std::isfinite(v)) return false;
+  return true;
+}
+
+static bool linear_solve(const Problem& P, const Schur& S, const std::vector<Lin>& L, const std::vector<double>& s,
+                         const std::vector<double>& D, const Options& opt, std::vector<double>& y, int* ls_iters) {
+  *ls_iters = 1;
+  if (opt.linear_solver == LS_ITERATIVE_SCHUR) return iterative_schur_solve(P, S, L, s, D, opt, y, ls_iters);
+  return dense_schur_solve(P, S, L, s, D, y);
+}
+
+// ----------------------------------------------------------------------------
+// Ceres TrustRegionMinimizer + LevenbergMarquardtStrategy restated.
+// ----------------------------------------------------------------------------
 
 enum { LOG_ITER = 0, LOG_COST, LOG_COST_CHANGE, LOG_GMAX, LOG_GNORM, LOG_STEP_NORM, LOG_REL_DEC,
-       LOG_RADIUS, LOG_VALID, LOG_SUCCESS, LOG_MCC, LOG_WIDTH = 12 };
+       LOG_RADIUS, LOG_VALID, LOG_SUCCESS, LOG_MCC, LOG_LS_ITERS, LOG_WIDTH = 12 };
 enum { TERM_CONVERGENCE = 0, TERM_NO_CONVERGENCE = 1, TERM_FAILURE = 2 };
 
 struct Summary {
@@ -850,7 +1155,9 @@ static int minimize(Problem& P, const Options& opt, double* log, int max_log, Su
       }
     }
     for (int i = 0; i < n; ++i) D[i] = std::sqrt(diag[i] / radius);
-    bool solved = dense_schur_solve(P, S, L, scale, D, y);
+    int ls_iters = 0;
+    bool solved = linear_solve(P, S, L, scale, D, opt, y, &ls_iters);
+    rec[LOG_LS_ITERS] = ls_iters;
     reuse_diagonal = true;
     bool valid = false;
     double mcc = 0.0;
@@ -1119,7 +1426,12 @@ void oracle_default_options(oracle::Options* o) {
   o->max_num_iterations = 50;
   o->max_num_consecutive_invalid_steps = 5;
   o->jacobi_scaling = 1;
-  o->pad = 0;
+  o->linear_solver = 0;
+  o->preconditioner_type = 0;
+  o->max_linear_solver_iterations = 500;
+  o->min_linear_solver_iterations = 0;
+  o->precision = 0;
+  o->eta = 1e-1;
   o->function_tolerance = 1e-6;
   o->gradient_tolerance = 1e-10;
   o->parameter_tolerance = 1e-8;

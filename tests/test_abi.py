@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
     for f in declared_functions():
         assert hasattr(lib, f)
     assert {name for name, _, _ in N.SIGNATURES} == set(declared_functions())
-    assert lib.ba_abi_version() == 1
+    assert lib.ba_abi_version() == N.BA_ABI_VERSION == 2
 
 
 def test_default_options_are_ceres_defaults():
@@ -56,7 +56,8 @@ int main(void) {
   printf("ba_problem %zu\nba_options %zu\nba_summary %zu\nba_iteration %zu\n", sizeof(ba_problem),
          sizeof(ba_options), sizeof(ba_summary), sizeof(ba_iteration));
   F(ba_problem, cams) F(ba_problem, obs_uv) F(ba_problem, huber_a)
-  F(ba_options, function_tolerance) F(ba_options, max_lm_diagonal)
+  F(ba_options, function_tolerance) F(ba_options, max_lm_diagonal) F(ba_options, preconditioner_type)
+  F(ba_options, eta) F(ba_iteration, linear_solver_iterations)
   F(ba_summary, num_iterations) F(ba_summary, termination_type) F(ba_summary, solve_time_s)
   F(ba_iteration, cost) F(ba_iteration, model_cost_change) F(ba_iteration, iteration_time_s)
   printf("ba_prune_problem %zu\n", sizeof(ba_prune_problem));
