@@ -90,6 +90,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--comm", action="store_true", help="use an RCCL communicator even at one rank (tests)")
+    ap.add_argument("--linear-solver", default="dense", choices=["dense", "iterative"],
+                    help="DENSE_SCHUR (the reference's) or ITERATIVE_SCHUR (implicit Schur + PCG)")
+    ap.add_argument("--preconditioner", default="SCHUR_JACOBI", choices=["JACOBI", "SCHUR_JACOBI"])
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -100,7 +103,7 @@ def main():
 
     import numpy as np
 
-    from bundleadjustment_amd import Solver, make_config
+    from bundleadjustment_amd import Options, Solver, make_config
     from bundleadjustment_amd.problem import CONFIG_INDEX, CONFIGS
 
     cfg = args.config
@@ -125,12 +128,15 @@ def main():
         if use_comm:
             solver.barrier()
 
+    iterative = args.linear_solver == "iterative"
+    opts = Options(linear_solver_type="ITERATIVE_SCHUR" if iterative else "DENSE_SCHUR",
+                   preconditioner_type=args.preconditioner)
     # warmup (first call also computes the Jacobi scaling, as LM iteration 0 does)
-    solver.bench_iterations(max(1, args.warmup))
+    solver.bench_iterations(max(1, args.warmup), options=opts)
     barrier()
     solver.synchronize()
     t0 = time.perf_counter()
-    ms_dev, ms_rj = solver.bench_iterations(args.steps)
+    ms_dev, ms_rj, cg_iters = solver.bench_iterations(args.steps, options=opts, with_linear_iters=True)
     solver.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -179,14 +185,18 @@ def main():
             "data": "synthetic (BAL-style, SURVEY.md §8d generator, seeded)",
             "config": {"workload": f"{cfg.upper()}: {CONFIGS[cfg]['n_cams']} cams x {problem.n_pts} pts x "
                                    f"{problem.n_obs} obs per GPU (point-sharded, cameras replicated)",
-                       "global_obs": n_obs_total, "solver": "LM + DENSE_SCHUR, fp64",
-                       "parallelism": f"points sharded x{world}, RCCL all-reduce of camera system"},
+                       "global_obs": n_obs_total,
+                       "solver": (f"LM + ITERATIVE_SCHUR (implicit Schur, PCG {args.preconditioner}, "
+                                  f"{cg_iters:.1f} CG iterations per LM iteration), fp64") if iterative
+                       else "LM + DENSE_SCHUR, fp64",
+                       "parallelism": f"points sharded x{world}, RCCL all-reduce of "
+                                      + ("camera blocks + one 6C vector per CG iteration" if iterative
+                                         else "camera system")},
             "device_ms_per_step": round(ms_dev, 4),
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    solver.close()
     solver.close()
 
 
