@@ -70,7 +70,8 @@ struct DevWork {
   int* flags;                        // [kFlagWords] hand-off flags of the dataflow kernels (zeroed per call)
   const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}
   const int2* pairs;                 // observation pairs per block
-  double* cpart;                     // [kCamSplit][nvc][27] per-slice camera sums
+  double* cpart;                     // [cam_split][nvc][27] per-slice camera sums
+  int cam_split;                     // workgroups per camera of the per-camera gathers (>= 2048 in total, <= kCamSplit)
   double* part;                      // [kNumSlots][kMaxBlocks]
   double* scal;                      // [kNumSlots + kPcgState]: scalar slots, then the PCG state record
   // ITERATIVE_SCHUR (allocated on first use; x of the CG is y above)
@@ -80,6 +81,7 @@ struct DevWork {
   double* pb; double* pr; double* pz; double* pp; double* pq;   // [n] CG vectors
   double* vpt;                       // [np][3] point-side products of one implicit matvec
   double* tpart;                     // [pcg_G][nvc][6] camera-side slices of one implicit matvec
+  double* ppart;                     // [3][kMaxBlocks] per-block partials of the camera-side kernels
   int pcg_G;
   const int* dup_off;                // [nvc+1] per variable camera: pairs of observations of one
   const int2* dup_pairs;             //   point by that camera (Schur-Jacobi diagonal cross terms)

@@ -30,7 +30,7 @@ int grid_for(int n) {
 }
 
 
-// Per-camera work is split over kCamSplit workgroups (one workgroup per
+// Per-camera work is split over W.cam_split <= kCamSplit workgroups (one workgroup per
 // camera leaves CUs idle and is latency bound).  Each slice stores its 27
 // block sums; a second kernel adds the slices in slice order (deterministic;
 // the kernel boundary makes the slices visible across XCDs — an in-kernel
@@ -47,14 +47,14 @@ __device__ inline void cam_slice_store(const double (&tot)[27], double* __restri
 // fold the slices: mode 0 -> Hcc (21) / gc (6); mode 1 -> S diagonal block
 // (-sum W W^T, lower) and rhs row (-sum W u); mode 2 -> the same 27 values
 // into a compact per-camera array (ITERATIVE_SCHUR)
-__global__ __launch_bounds__(256) void k_cam_fold(DevProblem P, const double* __restrict__ cpart, int mode,
+__global__ __launch_bounds__(256) void k_cam_fold(DevProblem P, const double* __restrict__ cpart, int nsl, int mode,
                                                   double* __restrict__ Hcc, double* __restrict__ gc,
                                                   double* __restrict__ S) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= P.nvc * 27) return;
   const int v = e / 27, k = e - v * 27;
   double acc = 0.0;
-  for (int sl = 0; sl < kCamSplit; ++sl) acc += cpart[((size_t)sl * P.nvc + v) * 27 + k];
+  for (int sl = 0; sl < nsl; ++sl) acc += cpart[((size_t)sl * P.nvc + v) * 27 + k];
   if (mode == 0) {
     if (k < 21) Hcc[(size_t)v * 21 + k] = acc;
     else gc[(size_t)v * 6 + (k - 21)] = acc;
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void k_cam_fold(DevProblem P, const double* __
 // observation range of slice blockIdx.y of camera v
 __device__ inline void cam_slice(const DevProblem& P, int v, int& i0, int& i1) {
   const int a = P.cam_off[v], b = P.cam_off[v + 1];
-  const int len = (b - a + kCamSplit - 1) / kCamSplit;
+  const int len = (b - a + (int)gridDim.y - 1) / (int)gridDim.y;
   i0 = min(b, a + (int)blockIdx.y * len);
   i1 = min(b, i0 + len);
 }
@@ -1407,8 +1407,9 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
 }
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact) {
   if (P.nvc == 0) return;
-  hipLaunchKernelGGL(k_cam_schur_diag, dim3(P.nvc, kCamSplit), dim3(kThreads), 0, s, P, W.W, W.u, W.S, W.cpart);
-  hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, compact ? 2 : 1, W.Hcc,
+  hipLaunchKernelGGL(k_cam_schur_diag, dim3(P.nvc, W.cam_split), dim3(kThreads), 0, s, P, W.W, W.u, W.S, W.cpart);
+  hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, W.cam_split,
+                     compact ? 2 : 1, W.Hcc,
                      W.gc, compact ? compact : W.S);
 }
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {

@@ -14,8 +14,9 @@
 // camera pass (observations gathered per camera, sliced over workgroups).
 // Everything on the camera side (6 nvc entries: A x, preconditioner,
 // dot products, the CG recurrences and Ceres' termination tests) is one
-// 1024-thread workgroup: the vectors are small, and a single workgroup
-// gives fixed-order reductions without grid barriers.  Multi-GPU: each rank
+// 1024-thread workgroup up to 1024 cameras (one launch per CG iteration,
+// fixed-order reductions without grid barriers) and three thread-per-camera
+// grid kernels beyond.  Multi-GPU: each rank
 // holds a point shard; the camera slices of every matvec are summed with one
 // RCCL all-reduce of 6 nvc x slices doubles (ba_solver.hip); all other CG
 // state is replicated and evolves identically on every rank.
@@ -140,26 +141,40 @@ __global__ __launch_bounds__(256) void k_pcg_dup(DevProblem P, const int* __rest
   }
 }
 
+// Sum of nb per-block partials, in a fixed order, returned to every thread
+// of the workgroup (wave 0 folds lane-strided, then the wave tree).
+__device__ inline double fold_part(const double* __restrict__ pp, int nb, double* lds1) {
+  if (threadIdx.x < 64) {
+    double v = 0.0;
+    for (int i = threadIdx.x; i < nb; i += 64) v += pp[i];
+    v = wave_sum(v);
+    if (threadIdx.x == 0) lds1[0] = v;
+  }
+  __syncthreads();
+  const double t = lds1[0];
+  __syncthreads();
+  return t;
+}
+
 // ---------------------------------------------------------------------------
-// setup (one workgroup): A_c = s Hcc s + D^2, preconditioner block
+// setup (thread per camera): A_c = s Hcc s + D^2, preconditioner block
 // M_c = A_c (JACOBI) or A_c + Sd_c (SCHUR_JACOBI) inverted, rhs
-// b_c = Sd_c[rhs] + s g_c; x = 0, r = b, z = M r, p = z; rho = r.z;
-// ceres' norm_b == 0 exit and the first iteration's rho test.
+// b_c = Sd_c[rhs] + s g_c; x = 0, r = b, z = M r, p = z; per-block partials
+// of |b|^2, r.z and non-PD blocks.  k_pcg_setup_fin then applies ceres'
+// norm_b == 0 exit and the first iteration's rho test.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_setup(DevProblem P, const double* __restrict__ Sd,
-                                                           const double* __restrict__ Hcc,
-                                                           const double* __restrict__ gc,
-                                                           const double* __restrict__ scale_c,
-                                                           const double* __restrict__ diag_c, double radius,
-                                                           int schur_jacobi, double* __restrict__ Adiag,
-                                                           double* __restrict__ Minv, double* __restrict__ b,
-                                                           double* __restrict__ x, double* __restrict__ r,
-                                                           double* __restrict__ z, double* __restrict__ p,
-                                                           double* __restrict__ scal) {
+__global__ __launch_bounds__(256) void k_pcg_setup(DevProblem P, const double* __restrict__ Sd,
+                                                   const double* __restrict__ Hcc, const double* __restrict__ gc,
+                                                   const double* __restrict__ scale_c,
+                                                   const double* __restrict__ diag_c, double radius, int schur_jacobi,
+                                                   double* __restrict__ Adiag, double* __restrict__ Minv,
+                                                   double* __restrict__ b, double* __restrict__ x,
+                                                   double* __restrict__ r, double* __restrict__ z,
+                                                   double* __restrict__ p, double* __restrict__ ppart) {
   __shared__ double lds[3 * 16];
-  double* st = scal + kNumSlots;
   double acc[3] = {0.0, 0.0, 0.0};   // |b|^2, r.z, bad blocks
-  for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < P.nvc) {
     double s[6], D2[6];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
@@ -194,17 +209,30 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_setup(DevProblem P, const d
       acc[1] += bv[a] * zv[a];
     }
   }
-  block_allsum<3>(acc, lds);
+  double tot[3];
+  block_sum<3>(acc, lds, tot);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ppart[k * kMaxBlocks + blockIdx.x] = tot[k];
+}
+
+__global__ __launch_bounds__(64) void k_pcg_setup_fin(const double* __restrict__ ppart, int nb,
+                                                      double* __restrict__ scal) {
+  __shared__ double lds[1];
+  double* st = scal + kNumSlots;
+  const double bb = fold_part(ppart, nb, lds);
+  const double rz = fold_part(ppart + kMaxBlocks, nb, lds);
+  const double bad = fold_part(ppart + 2 * kMaxBlocks, nb, lds);
   if (threadIdx.x == 0) {
-    st[PS_RHO] = 1.0; st[PS_Q0] = -0.0; st[PS_ALPHA] = 0.0; st[PS_NORM_B] = sqrt(acc[0]);
+    st[PS_RHO] = 1.0; st[PS_Q0] = -0.0; st[PS_ALPHA] = 0.0; st[PS_NORM_B] = sqrt(bb);
     st[PS_ITER] = 0.0; st[PS_DONE] = 0.0; st[PS_TERM] = PCG_NO_CONVERGENCE;
   }
-  if (sqrt(acc[0]) == 0.0) { pcg_stop(st, scal, PCG_SUCCESS, 0); return; }   // x = 0
+  if (sqrt(bb) == 0.0) { pcg_stop(st, scal, PCG_SUCCESS, 0); return; }   // x = 0
   // iteration 1 starts: rho = r.z (an indefinite / singular preconditioner
   // block yields a non-finite rho: stop as a failure, the step is invalid
   // either way)
-  if (zero_or_inf(acc[1]) || isnan(acc[1]) || acc[2] != 0.0) { pcg_stop(st, scal, PCG_FAILURE, 1); return; }
-  if (threadIdx.x == 0) st[PS_RHO] = acc[1];
+  if (zero_or_inf(rz) || isnan(rz) || bad != 0.0) { pcg_stop(st, scal, PCG_FAILURE, 1); return; }
+  if (threadIdx.x == 0) st[PS_RHO] = rz;
 }
 
 // ---------------------------------------------------------------------------
@@ -377,6 +405,124 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(DevProblem P, int mo
 }
 
 // ---------------------------------------------------------------------------
+// The same CG iteration for large camera counts (nvc > kPcgThreads): three
+// grid kernels, thread per camera; each block folds the previous kernel's
+// per-block partials itself (fixed order: every block reaches the same
+// decisions), block 0 records the state.
+//   k_pcg_q:  q = S p, partials p.q                              (modes 0, 1)
+//   k_pcg_xr: alpha, x += alpha p [mode 1 stops here], r update,
+//             z = M r, partials x.(b + r), r.z                  (modes 0, 1, 2)
+//   k_pcg_p:  termination tests, rho', beta, p = z + beta p
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pcg_q(DevProblem P, int G, const double* __restrict__ Adiag,
+                                               const double* __restrict__ p, double* __restrict__ q,
+                                               const double* __restrict__ tpart, double* __restrict__ ppart,
+                                               const double* __restrict__ st) {
+  if (st[PS_DONE] != 0.0) return;
+  __shared__ double lds[16];
+  double acc[1] = {0.0};
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < P.nvc) {
+    double pv[6], qv[6];
+    load6(p + 6 * (size_t)v, pv);
+    schur_row(Adiag, tpart, G, P.nvc, v, pv, qv);
+    store6(q + 6 * (size_t)v, qv);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[0] += pv[a] * qv[a];
+  }
+  double tot[1];
+  block_sum<1>(acc, lds, tot);
+  if (threadIdx.x == 0) ppart[blockIdx.x] = tot[0];
+}
+
+__global__ __launch_bounds__(256) void k_pcg_xr(DevProblem P, int mode, int it, int G,
+                                                const double* __restrict__ Adiag, const double* __restrict__ Minv,
+                                                const double* __restrict__ b, double* __restrict__ x,
+                                                double* __restrict__ r, double* __restrict__ z,
+                                                const double* __restrict__ p, const double* __restrict__ q,
+                                                const double* __restrict__ tpart, double* __restrict__ ppart,
+                                                double* __restrict__ scal) {
+  double* st = scal + kNumSlots;
+  if (st[PS_DONE] != 0.0) return;
+  __shared__ double lds[2 * 16];
+  const int nb = gridDim.x;
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = v < P.nvc;
+  double alpha;
+  if (mode != 2) {
+    const double pq = fold_part(ppart, nb, lds), rho = st[PS_RHO];
+    if (pq <= 0.0 || isinf(pq)) { if (blockIdx.x == 0) pcg_stop(st, scal, PCG_NO_CONVERGENCE, it); return; }
+    alpha = rho / pq;
+    if (isinf(alpha) || isnan(alpha)) { if (blockIdx.x == 0) pcg_stop(st, scal, PCG_FAILURE, it); return; }
+    if (live)
+#pragma unroll
+      for (int a = 0; a < 6; ++a) x[6 * (size_t)v + a] = x[6 * (size_t)v + a] + alpha * p[6 * (size_t)v + a];
+    if (mode == 1) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) st[PS_ALPHA] = alpha;
+      return;
+    }
+  } else {
+    alpha = st[PS_ALPHA];
+  }
+  double acc[2] = {0.0, 0.0};
+  if (live) {
+    double rv[6], xv[6], zv[6];
+    load6(x + 6 * (size_t)v, xv);
+    if (mode == 2) {
+      double sx[6];
+      schur_row(Adiag, tpart, G, P.nvc, v, xv, sx);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) rv[a] = b[6 * (size_t)v + a] - sx[a];
+    } else {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) rv[a] = r[6 * (size_t)v + a] - alpha * q[6 * (size_t)v + a];
+    }
+    store6(r + 6 * (size_t)v, rv);
+    mat6_mul(Minv + (size_t)v * 36, rv, zv);
+    store6(z + 6 * (size_t)v, zv);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      acc[0] += xv[a] * (b[6 * (size_t)v + a] + rv[a]);
+      acc[1] += rv[a] * zv[a];
+    }
+  }
+  double tot[2];
+  block_sum<2>(acc, lds, tot);
+  if (threadIdx.x == 0) {
+    ppart[kMaxBlocks + blockIdx.x] = tot[0];
+    ppart[2 * kMaxBlocks + blockIdx.x] = tot[1];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pcg_p(DevProblem P, int it, PcgOpts o, const double* __restrict__ z,
+                                               double* __restrict__ p, const double* __restrict__ ppart,
+                                               double* __restrict__ scal) {
+  double* st = scal + kNumSlots;
+  if (st[PS_DONE] != 0.0) return;
+  __shared__ double lds[1];
+  const int nb = gridDim.x;
+  const double Q1 = -1.0 * fold_part(ppart + kMaxBlocks, nb, lds);
+  const double rho_new = fold_part(ppart + 2 * kMaxBlocks, nb, lds);
+  const double Q0 = st[PS_Q0], rho = st[PS_RHO];
+  const double zeta = it * (Q1 - Q0) / Q1;
+  const bool lead = blockIdx.x == 0;
+  if (zeta < o.q_tolerance && it >= o.min_iter) { if (lead) pcg_stop(st, scal, PCG_SUCCESS, it); return; }
+  if (it >= o.max_iter) { if (lead) pcg_stop(st, scal, PCG_NO_CONVERGENCE, it); return; }
+  if (zero_or_inf(rho_new) || isnan(rho_new)) { if (lead) pcg_stop(st, scal, PCG_FAILURE, it + 1); return; }
+  const double beta = rho_new / rho;
+  if (zero_or_inf(beta)) { if (lead) pcg_stop(st, scal, PCG_FAILURE, it + 1); return; }
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < P.nvc)
+#pragma unroll
+    for (int a = 0; a < 6; ++a) p[6 * (size_t)v + a] = z[6 * (size_t)v + a] + beta * p[6 * (size_t)v + a];
+  if (lead && threadIdx.x == 0) {
+    st[PS_RHO] = rho_new;
+    st[PS_Q0] = Q1;
+    st[PS_ITER] = it;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 void launch_pcg_dup(const DevProblem& P, const DevWork& W, hipStream_t s) {
@@ -384,8 +530,10 @@ void launch_pcg_dup(const DevProblem& P, const DevWork& W, hipStream_t s) {
   hipLaunchKernelGGL(k_pcg_dup, dim3((P.nvc + 255) / 256), dim3(256), 0, s, P, W.dup_off, W.dup_pairs, W.W, W.Sd);
 }
 void launch_pcg_setup(const DevProblem& P, const DevWork& W, double radius, const PcgOpts& o, hipStream_t s) {
-  hipLaunchKernelGGL(k_pcg_setup, dim3(1), dim3(kPcgThreads), 0, s, P, W.Sd, W.Hcc, W.gc, W.scale_c, W.diag_c, radius,
-                     o.schur_jacobi, W.Adiag, W.Minv, W.pb, W.y, W.pr, W.pz, W.pp, W.scal);
+  const int nb = (P.nvc + 255) / 256;
+  hipLaunchKernelGGL(k_pcg_setup, dim3(nb), dim3(256), 0, s, P, W.Sd, W.Hcc, W.gc, W.scale_c, W.diag_c, radius,
+                     o.schur_jacobi, W.Adiag, W.Minv, W.pb, W.y, W.pr, W.pz, W.pp, W.ppart);
+  hipLaunchKernelGGL(k_pcg_setup_fin, dim3(1), dim3(64), 0, s, W.ppart, nb, W.scal);
 }
 void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s) {
   const double* st = W.scal + kNumSlots;
@@ -393,8 +541,18 @@ void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec,
   hipLaunchKernelGGL(k_pcg_cam, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.W, W.vpt, W.tpart, st);
 }
 void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, const PcgOpts& o, hipStream_t s) {
-  hipLaunchKernelGGL(k_pcg_update, dim3(1), dim3(kPcgThreads), 0, s, P, mode, it, o, W.pcg_G, W.Adiag, W.Minv, W.pb,
-                     W.y, W.pr, W.pz, W.pp, W.pq, W.tpart, W.scal);
+  if (P.nvc <= kPcgThreads) {   // one workgroup: one launch per CG iteration
+    hipLaunchKernelGGL(k_pcg_update, dim3(1), dim3(kPcgThreads), 0, s, P, mode, it, o, W.pcg_G, W.Adiag, W.Minv,
+                       W.pb, W.y, W.pr, W.pz, W.pp, W.pq, W.tpart, W.scal);
+    return;
+  }
+  const int nb = (P.nvc + 255) / 256;
+  const double* st = W.scal + kNumSlots;
+  if (mode != 2)
+    hipLaunchKernelGGL(k_pcg_q, dim3(nb), dim3(256), 0, s, P, W.pcg_G, W.Adiag, W.pp, W.pq, W.tpart, W.ppart, st);
+  hipLaunchKernelGGL(k_pcg_xr, dim3(nb), dim3(256), 0, s, P, mode, it, W.pcg_G, W.Adiag, W.Minv, W.pb, W.y, W.pr,
+                     W.pz, W.pp, W.pq, W.tpart, W.ppart, W.scal);
+  if (mode != 1) hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(256), 0, s, P, it, o, W.pz, W.pp, W.ppart, W.scal);
 }
 
 }  // namespace bahip

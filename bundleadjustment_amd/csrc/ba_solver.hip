@@ -263,7 +263,8 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.y = ctx->dalloc<double>(std::max(ctx->n, 1));
   W.part = ctx->dalloc<double>((size_t)kNumSlots * kMaxBlocks);
   W.scal = ctx->dalloc<double>(kNumSlots + kPcgState);
-  W.cpart = ctx->dalloc<double>((size_t)kCamSplit * 27 * std::max(nvc, 1));
+  W.cam_split = nvc > 0 ? std::min(kCamSplit, std::max(1, 2048 / nvc)) : 1;
+  W.cpart = ctx->dalloc<double>((size_t)W.cam_split * 27 * std::max(nvc, 1));
 
   HIP_OK(hipMemsetAsync(W.part, 0, sizeof(double) * kNumSlots * kMaxBlocks, ctx->stream));
   HIP_OK(hipMemsetAsync(W.scal, 0, sizeof(double) * (kNumSlots + kPcgState), ctx->stream));
@@ -343,7 +344,7 @@ void ensure_pcg(ba_ctx* ctx) {
   const int np = ctx->np, nvc = ctx->nvc;
   const size_t n = (size_t)std::max(ctx->n, 1);
   DevWork& W = ctx->W;
-  W.pcg_G = nvc > 0 ? std::min(kCamSplit, std::max(1, 2048 / nvc)) : 1;
+  W.pcg_G = W.cam_split;
   W.Sd = ctx->dalloc<double>(27 * (size_t)std::max(nvc, 1));
   W.Adiag = ctx->dalloc<double>(21 * (size_t)std::max(nvc, 1));
   W.Minv = ctx->dalloc<double>(36 * (size_t)std::max(nvc, 1));
@@ -354,6 +355,8 @@ void ensure_pcg(ba_ctx* ctx) {
   W.pq = ctx->dalloc<double>(n);
   W.vpt = ctx->dalloc<double>(3 * (size_t)std::max(np, 1));
   W.tpart = ctx->dalloc<double>((size_t)W.pcg_G * 6 * std::max(nvc, 1));
+  W.ppart = ctx->dalloc<double>(3 * (size_t)kMaxBlocks);
+  if ((nvc + 255) / 256 > kMaxBlocks) throw BaError{BA_ERR_INVALID_ARGUMENT, "too many cameras for ITERATIVE_SCHUR"};
   std::vector<int> dup_off(nvc + 1, 0);
   std::vector<int2> dup;
   {

@@ -188,3 +188,19 @@ def test_gpu_iterative_rejects_bad_options(solver):
     solver.set_problem(make_config("c1"))
     with pytest.raises(BAError):
         solver.solve(Options(linear_solver_type="ITERATIVE_SCHUR", max_linear_solver_iterations=0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pc", PRECONDITIONERS)
+def test_gpu_iterative_many_cameras(solver, oracle_lib, pc):
+    """> 1024 variable cameras: the camera side runs as thread-per-camera grid
+    kernels (k_pcg_q / k_pcg_xr / k_pcg_p) instead of one workgroup; the
+    per-camera gathers use one slice per camera."""
+    p = make_synthetic(1300, 4000, obs_per_pt=4, seed=21)
+    _, _, so, olog = oracle_lib.solve(p, oracle_opts(oracle_lib, pc, max_num_iterations=6))
+    _, _, sg, glog = gpu_solve(solver, p, preconditioner_type=pc, max_num_iterations=6)
+    compare(glog, olog, len(olog))
+    kw = dict(max_num_iterations=3, eta=1e-14, max_linear_solver_iterations=21)   # residual resets
+    _, _, so, olog = oracle_lib.solve(p, oracle_opts(oracle_lib, pc, **kw))
+    _, _, sg, glog = gpu_solve(solver, p, preconditioner_type=pc, **kw)
+    compare(glog, olog, len(olog), rtol=1e-8)
