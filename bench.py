@@ -93,6 +93,8 @@ def main():
     ap.add_argument("--linear-solver", default="dense", choices=["dense", "iterative"],
                     help="DENSE_SCHUR (the reference's) or ITERATIVE_SCHUR (implicit Schur + PCG)")
     ap.add_argument("--preconditioner", default="SCHUR_JACOBI", choices=["JACOBI", "SCHUR_JACOBI"])
+    ap.add_argument("--precision", default="FP64", choices=["FP64", "MIXED_FP32"],
+                    help="MIXED_FP32: fp32 storage of the per-observation Schur blocks (iterative only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -130,7 +132,7 @@ def main():
 
     iterative = args.linear_solver == "iterative"
     opts = Options(linear_solver_type="ITERATIVE_SCHUR" if iterative else "DENSE_SCHUR",
-                   preconditioner_type=args.preconditioner)
+                   preconditioner_type=args.preconditioner, precision=args.precision)
     # warmup (first call also computes the Jacobi scaling, as LM iteration 0 does)
     solver.bench_iterations(max(1, args.warmup), options=opts)
     barrier()
@@ -187,7 +189,8 @@ def main():
                                    f"{problem.n_obs} obs per GPU (point-sharded, cameras replicated)",
                        "global_obs": n_obs_total,
                        "solver": (f"LM + ITERATIVE_SCHUR (implicit Schur, PCG {args.preconditioner}, "
-                                  f"{cg_iters:.1f} CG iterations per LM iteration), fp64") if iterative
+                                  f"{cg_iters:.1f} CG iterations per LM iteration), fp64"
+                                  + (", W blocks stored fp32" if args.precision == "MIXED_FP32" else "")) if iterative
                        else "LM + DENSE_SCHUR, fp64",
                        "parallelism": f"points sharded x{world}, RCCL all-reduce of "
                                       + ("camera blocks + one 6C vector per CG iteration" if iterative

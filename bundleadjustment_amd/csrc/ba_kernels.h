@@ -62,7 +62,9 @@ struct DevWork {
   double* Hcc;   double* gc;         // [nvc][21], [nvc][6]
   double* scale_c; double* diag_c;   // [nvc][6]
   double* delta_c;                   // [nvc][6]
-  double* W;                         // [no][18]  (E L^-T per observation)
+  double* W;                         // [no][18]  (E L^-T per observation), fp64
+  float* Wf;                         // [no][18]  the same in fp32 (BA_MIXED_FP32)
+  bool w32;                          // W blocks stored in Wf
   double* S;                         // [(n+1) x ld] reduced system, row n = rhs (working matrix)
   double* Lf;                        // [(n+1) x ld] Cholesky factor, row n = L^-1 rhs
   double* y;                         // [n] reduced solution

@@ -15,6 +15,7 @@
 // fixed-order fold of per-block partials): results are bitwise reproducible
 // run to run.  No floating-point atomics anywhere.
 #include <cstdlib>
+#include <type_traits>
 
 #include "ba_kernels.h"
 #include "ba_device.h"
@@ -802,10 +803,11 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
 // Camera scales come from an LDS table (nc <= kLinLdsCams) or global.
 // ---------------------------------------------------------------------------
 constexpr int kWRec = 18;
-template <bool TBL>
+template <bool TBL, typename WT>
 __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __restrict__ JR,
                                                const double* __restrict__ scale_c, const double* __restrict__ scale_p,
-                                               const double* __restrict__ Linv, double* __restrict__ W) {
+                                               const double* __restrict__ Linv, WT* __restrict__ W) {
+  using V2 = typename std::conditional<sizeof(WT) == 8, double2, float2>::type;
   constexpr int WAVES = 8;
   __shared__ double stage[WAVES * 64 * kStageLd];
   __shared__ double sct[TBL ? kLinLdsCams * 6 : 1];
@@ -857,16 +859,17 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
 #pragma unroll
     for (int k = 0; k < kWRec; ++k) st[lane * kStageLd + k] = wv[k];
     wave_lds_sync();
-    constexpr int NIT = kWRec / 2;   // 9 x 1 KiB
-    double2 ov[NIT];
+    constexpr int NIT = kWRec / 2;   // 9 x 1 KiB (fp64) / 9 x 512 B (fp32)
+    V2 ov[NIT];
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int e = it * 64 + lane;
       const int r = e / (kWRec / 2), f = 2 * (e - r * (kWRec / 2));
-      ov[it] = make_double2(st[r * kStageLd + f], st[r * kStageLd + f + 1]);
+      ov[it].x = (WT)st[r * kStageLd + f];
+      ov[it].y = (WT)st[r * kStageLd + f + 1];
     }
     wave_lds_sync();
-    double2* dst = reinterpret_cast<double2*>(W + (size_t)base * kWRec);
+    V2* dst = reinterpret_cast<V2*>(W + (size_t)base * kWRec);
     const int nrec = min(64, P.no - base);
     if (nrec == 64) {
 #pragma unroll
@@ -885,9 +888,10 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
 // back-substitution, one thread per point (all points; fixed / unobserved
 // points keep x' = x):  y_p = L^-T (u_p - sum W_o^T y_c) ; d_p = s_p (-y_p)
 // ---------------------------------------------------------------------------
+template <typename WT>
 __global__ __launch_bounds__(256) void k_backsub(DevProblem P, const double* __restrict__ pts,
                                                  double* __restrict__ pts_c, double* __restrict__ delta_p,
-                                                 const double* __restrict__ W, const double* __restrict__ u,
+                                                 const WT* __restrict__ W, const double* __restrict__ u,
                                                  const double* __restrict__ Linv, const double* __restrict__ y,
                                                  const double* __restrict__ scale_p, double* __restrict__ part) {
   __shared__ double lds[2 * 16];
@@ -902,10 +906,8 @@ __global__ __launch_bounds__(256) void k_backsub(DevProblem P, const double* __r
       for (int o = o0; o < o1; ++o) {
         const int v = P.vc[P.obs_cam[o]];
         if (v < 0) continue;
-        const double2* wo = reinterpret_cast<const double2*>(W + (size_t)o * 18);
         double wv[18];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) { const double2 t = wo[k]; wv[2 * k] = t.x; wv[2 * k + 1] = t.y; }
+        load_w18(W, (size_t)o, wv);
         const double* yc = y + 6 * v;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
@@ -1117,7 +1119,8 @@ __global__ __launch_bounds__(kLinLdsThreads) void k_candidate_lds(DevProblem P, 
 // diagonal Schur blocks and rhs (local part): one workgroup per camera
 //   S_cc = -sum W W^T (lower 21) ; b_c = -sum W u_p
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const double* __restrict__ W,
+template <typename WT>
+__global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const WT* __restrict__ W,
                                                         const double* __restrict__ u, double* __restrict__ S,
                                                         double* __restrict__ cpart) {
   __shared__ double lds[27 * 16];
@@ -1133,9 +1136,7 @@ __global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const doub
     const int p = P.obs_pt[o];
     if (!P.pt_var[p]) continue;
     double w[18];
-    const double2* w2 = reinterpret_cast<const double2*>(W + (size_t)o * 18);
-#pragma unroll
-    for (int k = 0; k < 9; ++k) { const double2 t = w2[k]; w[2 * k] = t.x; w[2 * k + 1] = t.y; }
+    load_w18(W, (size_t)o, w);
     const double u0 = u[p], u1 = u[np + p], u2 = u[2 * np + p];
     int t = 0;
 #pragma unroll
@@ -1400,14 +1401,26 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
                      radius, W.Linv, W.u, W.part);
   if (P.no == 0) return;
   const int g = lds_grid(P.no);
-  if (P.nc <= kLinLdsCams)
-    hipLaunchKernelGGL(k_obs_w<true>, dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.W);
-  else
-    hipLaunchKernelGGL(k_obs_w<false>, dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.W);
+  if (W.w32) {
+    if (P.nc <= kLinLdsCams)
+      hipLaunchKernelGGL((k_obs_w<true, float>), dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.Wf);
+    else
+      hipLaunchKernelGGL((k_obs_w<false, float>), dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.Wf);
+  } else {
+    if (P.nc <= kLinLdsCams)
+      hipLaunchKernelGGL((k_obs_w<true, double>), dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.W);
+    else
+      hipLaunchKernelGGL((k_obs_w<false, double>), dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.W);
+  }
 }
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact) {
   if (P.nvc == 0) return;
-  hipLaunchKernelGGL(k_cam_schur_diag, dim3(P.nvc, W.cam_split), dim3(kThreads), 0, s, P, W.W, W.u, W.S, W.cpart);
+  if (W.w32)
+    hipLaunchKernelGGL(k_cam_schur_diag<float>, dim3(P.nvc, W.cam_split), dim3(kThreads), 0, s, P, W.Wf, W.u, W.S,
+                       W.cpart);
+  else
+    hipLaunchKernelGGL(k_cam_schur_diag<double>, dim3(P.nvc, W.cam_split), dim3(kThreads), 0, s, P, W.W, W.u, W.S,
+                       W.cpart);
   hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, W.cam_split,
                      compact ? 2 : 1, W.Hcc,
                      W.gc, compact ? compact : W.S);
@@ -1437,8 +1450,12 @@ void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) 
                      W.scale_c, W.cams_c, W.delta_c, W.rec_c, W.part);
 }
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
-  hipLaunchKernelGGL(k_backsub, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p, W.W, W.u,
-                     W.Linv, W.y, W.scale_p, W.part);
+  if (W.w32)
+    hipLaunchKernelGGL(k_backsub<float>, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p,
+                       W.Wf, W.u, W.Linv, W.y, W.scale_p, W.part);
+  else
+    hipLaunchKernelGGL(k_backsub<double>, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p,
+                       W.W, W.u, W.Linv, W.y, W.scale_p, W.part);
   if (P.nc <= kLinLdsCams) {
     const int g = lds_grid(P.no);
     hipLaunchKernelGGL(k_candidate_lds, dim3(g), dim3(kLinLdsThreads), 0, s, P, W.JR, W.delta_c, W.delta_p, W.rec_c,

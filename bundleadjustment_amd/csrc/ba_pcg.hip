@@ -123,15 +123,17 @@ __device__ inline void pcg_stop(double* st, double* scal, int term, int iters) {
 // Schur-Jacobi cross terms of a point observed twice by one camera:
 // Sd_c -= W_a W_b^T + W_b W_a^T (lower), one thread per camera (fixed order)
 // ---------------------------------------------------------------------------
+template <typename WT>
 __global__ __launch_bounds__(256) void k_pcg_dup(DevProblem P, const int* __restrict__ dup_off,
-                                                 const int2* __restrict__ dup_pairs, const double* __restrict__ Wm,
+                                                 const int2* __restrict__ dup_pairs, const WT* __restrict__ Wm,
                                                  double* __restrict__ Sd) {
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
   if (v >= P.nvc) return;
   for (int i = dup_off[v]; i < dup_off[v + 1]; ++i) {
     const int2 pr = dup_pairs[i];
-    const double* wa = Wm + (size_t)pr.x * 18;
-    const double* wb = Wm + (size_t)pr.y * 18;
+    double wa[18], wb[18];
+    load_w18(Wm, (size_t)pr.x, wa);
+    load_w18(Wm, (size_t)pr.y, wb);
     for (int a = 0; a < 6; ++a)
       for (int b = 0; b <= a; ++b) {
         double s = 0.0;
@@ -238,7 +240,8 @@ __global__ __launch_bounds__(64) void k_pcg_setup_fin(const double* __restrict__
 // ---------------------------------------------------------------------------
 // matvec, point pass: v_p = sum_{o in p} W_o^T x_{c(o)}  (thread per point)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pcg_point(DevProblem P, const double* __restrict__ Wm,
+template <typename WT>
+__global__ __launch_bounds__(256) void k_pcg_point(DevProblem P, const WT* __restrict__ Wm,
                                                    const double* __restrict__ xv, double* __restrict__ vpt,
                                                    const double* __restrict__ st) {
   if (st[PS_DONE] != 0.0) return;
@@ -249,10 +252,8 @@ __global__ __launch_bounds__(256) void k_pcg_point(DevProblem P, const double* _
       for (int o = o0; o < o1; ++o) {
         const int v = P.vc[P.obs_cam[o]];
         if (v < 0) continue;
-        const double2* wo = reinterpret_cast<const double2*>(Wm + (size_t)o * 18);
         double wv[18];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) { const double2 t = wo[k]; wv[2 * k] = t.x; wv[2 * k + 1] = t.y; }
+        load_w18(Wm, (size_t)o, wv);
         const double* xc = xv + 6 * v;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
@@ -268,7 +269,8 @@ __global__ __launch_bounds__(256) void k_pcg_point(DevProblem P, const double* _
 // ---------------------------------------------------------------------------
 // matvec, camera pass: slice g of camera v: sum_{o in slice} W_o v_{p(o)}
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pcg_cam(DevProblem P, const double* __restrict__ Wm,
+template <typename WT>
+__global__ __launch_bounds__(256) void k_pcg_cam(DevProblem P, const WT* __restrict__ Wm,
                                                  const double* __restrict__ vpt, double* __restrict__ tpart,
                                                  const double* __restrict__ st) {
   if (st[PS_DONE] != 0.0) return;
@@ -282,10 +284,8 @@ __global__ __launch_bounds__(256) void k_pcg_cam(DevProblem P, const double* __r
     const int o = P.cam_obs[i];
     const int p = P.obs_pt[o];
     if (!P.pt_var[p]) continue;
-    const double2* wo = reinterpret_cast<const double2*>(Wm + (size_t)o * 18);
     double wv[18];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) { const double2 t = wo[k]; wv[2 * k] = t.x; wv[2 * k + 1] = t.y; }
+    load_w18(Wm, (size_t)o, wv);
     const double u0 = vpt[3 * (size_t)p], u1 = vpt[3 * (size_t)p + 1], u2 = vpt[3 * (size_t)p + 2];
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[a] += wv[a * 3] * u0 + wv[a * 3 + 1] * u1 + wv[a * 3 + 2] * u2;
@@ -527,7 +527,12 @@ __global__ __launch_bounds__(256) void k_pcg_p(DevProblem P, int it, PcgOpts o, 
 // ---------------------------------------------------------------------------
 void launch_pcg_dup(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
-  hipLaunchKernelGGL(k_pcg_dup, dim3((P.nvc + 255) / 256), dim3(256), 0, s, P, W.dup_off, W.dup_pairs, W.W, W.Sd);
+  if (W.w32)
+    hipLaunchKernelGGL(k_pcg_dup<float>, dim3((P.nvc + 255) / 256), dim3(256), 0, s, P, W.dup_off, W.dup_pairs, W.Wf,
+                       W.Sd);
+  else
+    hipLaunchKernelGGL(k_pcg_dup<double>, dim3((P.nvc + 255) / 256), dim3(256), 0, s, P, W.dup_off, W.dup_pairs, W.W,
+                       W.Sd);
 }
 void launch_pcg_setup(const DevProblem& P, const DevWork& W, double radius, const PcgOpts& o, hipStream_t s) {
   const int nb = (P.nvc + 255) / 256;
@@ -537,8 +542,13 @@ void launch_pcg_setup(const DevProblem& P, const DevWork& W, double radius, cons
 }
 void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s) {
   const double* st = W.scal + kNumSlots;
-  hipLaunchKernelGGL(k_pcg_point, dim3(grid_for(P.np)), dim3(256), 0, s, P, W.W, vec, W.vpt, st);
-  hipLaunchKernelGGL(k_pcg_cam, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.W, W.vpt, W.tpart, st);
+  if (W.w32) {
+    hipLaunchKernelGGL(k_pcg_point<float>, dim3(grid_for(P.np)), dim3(256), 0, s, P, W.Wf, vec, W.vpt, st);
+    hipLaunchKernelGGL(k_pcg_cam<float>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wf, W.vpt, W.tpart, st);
+  } else {
+    hipLaunchKernelGGL(k_pcg_point<double>, dim3(grid_for(P.np)), dim3(256), 0, s, P, W.W, vec, W.vpt, st);
+    hipLaunchKernelGGL(k_pcg_cam<double>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.W, W.vpt, W.tpart, st);
+  }
 }
 void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, const PcgOpts& o, hipStream_t s) {
   if (P.nvc <= kPcgThreads) {   // one workgroup: one launch per CG iteration

@@ -75,4 +75,17 @@ __device__ inline void block_allsum(double (&v)[NV], double* lds) {
   __syncthreads();
 }
 
+// One per-observation Schur block W_o (6x3, 18 values) -> fp64 registers;
+// stored fp64 (144 B) or, with BA_MIXED_FP32, fp32 (72 B).
+__device__ inline void load_w18(const double* __restrict__ Wm, size_t o, double (&w)[18]) {
+  const double2* s = reinterpret_cast<const double2*>(Wm + o * 18);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) { const double2 t = s[k]; w[2 * k] = t.x; w[2 * k + 1] = t.y; }
+}
+__device__ inline void load_w18(const float* __restrict__ Wm, size_t o, double (&w)[18]) {
+  const float2* s = reinterpret_cast<const float2*>(Wm + o * 18);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) { const float2 t = s[k]; w[2 * k] = (double)t.x; w[2 * k + 1] = (double)t.y; }
+}
+
 }  // namespace bahip

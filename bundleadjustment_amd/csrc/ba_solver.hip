@@ -259,7 +259,8 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.scale_c = ctx->dalloc<double>(6 * (size_t)nvc);
   W.diag_c = ctx->dalloc<double>(6 * (size_t)nvc);
   W.delta_c = ctx->dalloc<double>(6 * (size_t)nvc);
-  W.W = ctx->dalloc<double>(18 * (size_t)no);
+  W.W = nullptr;   // per-observation Schur blocks: allocated by the first solve (fp64 or fp32)
+  W.Wf = nullptr;
   W.y = ctx->dalloc<double>(std::max(ctx->n, 1));
   W.part = ctx->dalloc<double>((size_t)kNumSlots * kMaxBlocks);
   W.scal = ctx->dalloc<double>(kNumSlots + kPcgState);
@@ -490,6 +491,9 @@ StepResult solve_step(ba_ctx* ctx, double radius, const ba_options& o) {
   const hipStream_t s = ctx->stream;
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
+  W.w32 = o.precision == BA_MIXED_FP32;
+  if (W.w32 && !W.Wf) W.Wf = ctx->dalloc<float>(18 * (size_t)ctx->no);
+  if (!W.w32 && !W.W) W.W = ctx->dalloc<double>(18 * (size_t)ctx->no);
   HIP_OK(hipMemsetAsync(W.scal + SL_CHOL_BAD, 0, sizeof(double), s));
   int ls_iters = 1;
   if (o.linear_solver == BA_ITERATIVE_SCHUR) ls_iters = reduced_solve_pcg(ctx, radius, o);
@@ -524,8 +528,10 @@ void check_options(const ba_options& o) {
       ((o.preconditioner_type != BA_JACOBI && o.preconditioner_type != BA_SCHUR_JACOBI) ||
        o.max_linear_solver_iterations < 1 || o.min_linear_solver_iterations < 0 || !(o.eta > 0.0)))
     throw BaError{BA_ERR_INVALID_ARGUMENT, "invalid ITERATIVE_SCHUR options"};
-  if (o.precision != BA_FP64)
-    throw BaError{BA_ERR_INVALID_ARGUMENT, "precision " + std::to_string(o.precision) + " not supported"};
+  if (o.precision != BA_FP64 && o.precision != BA_MIXED_FP32)
+    throw BaError{BA_ERR_INVALID_ARGUMENT, "unknown precision " + std::to_string(o.precision)};
+  if (o.precision == BA_MIXED_FP32 && o.linear_solver != BA_ITERATIVE_SCHUR)
+    throw BaError{BA_ERR_INVALID_ARGUMENT, "BA_MIXED_FP32 requires BA_ITERATIVE_SCHUR"};
 }
 
 // ---------------------------------------------------------------------------

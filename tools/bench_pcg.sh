@@ -13,4 +13,5 @@ run pcg_c3 --steps 10 --warmup 2 --linear-solver iterative &&
 run pcg_c3_jac --steps 10 --warmup 2 --linear-solver iterative --preconditioner JACOBI &&
 run pcg_c4 --config c4 --scale 0.125 --steps 5 --warmup 1 --linear-solver iterative &&
 run dense_c4 --config c4 --scale 0.125 --steps 5 --warmup 1 &&
-run pcg_c5 --config c5 --scale 0.125 --steps 3 --warmup 1 --linear-solver iterative
+run pcg_c5 --config c5 --scale 0.125 --steps 3 --warmup 1 --linear-solver iterative &&
+run pcg_c5_mixed --config c5 --scale 0.125 --steps 3 --warmup 1 --linear-solver iterative --precision MIXED_FP32
