@@ -267,6 +267,71 @@ template <class Cam>
 __device__ inline RowRegs cam_row(const Cam& cr) { RowRegs R; cr.load(R.t); return R; }
 __device__ inline CamLdsLazy::Row cam_row(const CamLdsLazy& cr) { return cr.row(); }
 
+// Many cameras (nc > kLinLdsCams): the 704-B camera records no longer fit the
+// LDS and, past ~5k cameras, not even one XCD's L2 (C5: 7 MB of records,
+// ~4.8 GB of per-observation record gathers served by the Infinity Cache).
+// Instead every observation gathers its camera's compact 128-B record
+// (w, t, K, flag: one cache line, the whole table L2-resident) and rebuilds
+// the K-folded table in registers: the dual-number Rodrigues of k_cam_prep
+// (same functions, same arithmetic) plus the 40 K-folds, ~400 fp64 VALU
+// operations per observation, cheap next to the HBM stream.
+constexpr int kCRec = 16;   // [0..5] w, t (variable) | camera index (fixed); [6..14] K; [15] variable flag
+struct CamRcPre {
+  double2 v[kCRec / 2];
+};
+struct CamRc {   // unpacked compact record; lin_obs(CamRc) forms the table terms itself
+  double w[3], t[3], Kd[9];
+  int cidx;
+  bool v;
+  __device__ bool var() const { return v; }
+  __device__ double K(int i) const { return Kd[i]; }
+};
+struct CamRcOf {
+  const double* crec;
+  const float* extr;
+};
+// prefetch / construct hooks of lin_waves: table-based camera accessors take
+// the camera index itself; CamRcOf prefetches the compact record one chunk
+// ahead and rebuilds the table at use
+template <class F>
+__device__ inline int cam_pre(const F&, int c) { return c; }
+template <class F>
+__device__ inline auto cam_make(const F& f, int c) { return f(c); }
+__device__ inline CamRcPre cam_pre(const CamRcOf& f, int c) {
+  CamRcPre q;
+  const double2* s = reinterpret_cast<const double2*>(f.crec + (size_t)c * kCRec);
+#pragma unroll
+  for (int k = 0; k < kCRec / 2; ++k) q.v[k] = s[k];
+  return q;
+}
+__device__ inline CamRc cam_make(const CamRcOf&, const CamRcPre& q) {
+  CamRc C;
+  double rv[kCRec];
+#pragma unroll
+  for (int k = 0; k < kCRec / 2; ++k) { rv[2 * k] = q.v[k].x; rv[2 * k + 1] = q.v[k].y; }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { C.w[k] = rv[k]; C.t[k] = rv[3 + k]; }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) C.Kd[k] = rv[6 + k];
+  C.cidx = (int)rv[0];
+  C.v = rv[15] != 0.0;
+  return C;
+}
+
+// compact camera records for CamRcOf (thread per camera)
+__global__ __launch_bounds__(256) void k_cam_compact(DevProblem P, const double* __restrict__ cams,
+                                                     double* __restrict__ crec) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= P.nc) return;
+  const bool var = P.vc[c] >= 0;
+  double* o = crec + (size_t)c * kCRec;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) o[k] = var ? cams[6 * c + k] : (k == 0 ? (double)c : 0.0);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) o[6 + k] = (double)P.K[9 * c + k];
+  o[15] = var ? 1.0 : 0.0;
+}
+
 // r, J (Huber-corrected) of one observation into out[20]; returns rho.
 // AngleReprojectionError (Optimizer.h:54-76) / PointOnlyReprojectionError
 // (Optimizer.h:96-107) with the chain rule of their Jets:
@@ -339,6 +404,89 @@ __device__ inline double lin_obs(const DevProblem& P, const Cam& cr, bool cvar, 
   return rho;
 }
 
+// The same record from a compact camera (CamRc): the Jets' evaluation order
+// itself — p = R X + t on duals of w, q = K p, dq/dX = K R — with R and its
+// w-derivatives from the dual Rodrigues of k_cam_prep.  Fixed cameras read
+// their float extrinsic.
+__device__ inline double lin_obs(const DevProblem& P, const CamRc& cr, bool cvar, bool pvar, double X0, double X1,
+                                 double X2, float2 uv, double (&out)[kJR], bool& fin) {
+  const double* Kd = cr.Kd;
+  double q[3], dq[3][3], dX[3][3], iw = 1.0;   // dq/dw_k [k][row], dq/dX_col [col][row]
+  if (cvar) {
+    D3 R[9];
+    angle_axis_to_R_d3(cr.w, R);
+    D3 p[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const D3 a = R[i], b = R[3 + i], c = R[6 + i];
+      p[i] = mk(a.a * X0 + b.a * X1 + c.a * X2 + cr.t[i], a.d[0] * X0 + b.d[0] * X1 + c.d[0] * X2,
+                a.d[1] * X0 + b.d[1] * X1 + c.d[1] * X2, a.d[2] * X0 + b.d[2] * X1 + c.d[2] * X2);
+    }
+#pragma unroll
+    for (int row = 0; row < 3; ++row) {
+      q[row] = Kd[row] * p[0].a + Kd[3 + row] * p[1].a + Kd[6 + row] * p[2].a;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dq[k][row] = Kd[row] * p[0].d[k] + Kd[3 + row] * p[1].d[k] + Kd[6 + row] * p[2].d[k];
+#pragma unroll
+      for (int col = 0; col < 3; ++col)
+        dX[col][row] = Kd[row] * R[col * 3].a + Kd[3 + row] * R[col * 3 + 1].a + Kd[6 + row] * R[col * 3 + 2].a;
+    }
+  } else {
+    const float* E = P.extr + 16 * cr.cidx;
+    double e3[4], KE[12];
+#pragma unroll
+    for (int l = 0; l < 12; ++l) {
+      const int col = l / 3, row = l % 3;
+      KE[l] = Kd[row] * (double)E[col * 4] + Kd[3 + row] * (double)E[col * 4 + 1] + Kd[6 + row] * (double)E[col * 4 + 2];
+    }
+#pragma unroll
+    for (int l = 0; l < 4; ++l) e3[l] = (double)E[l * 4 + 3];
+    const double wv = e3[0] * X0 + e3[1] * X1 + e3[2] * X2 + e3[3];
+    iw = 1.0 / wv;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) q[i] = (KE[i] * X0 + KE[3 + i] * X1 + KE[6 + i] * X2 + KE[9 + i]) * iw;
+#pragma unroll
+    for (int col = 0; col < 3; ++col)
+#pragma unroll
+      for (int row = 0; row < 3; ++row) dX[col][row] = (KE[3 * col + row] - q[row] * e3[col]) * iw;
+  }
+  const double iq = 1.0 / q[2];
+  const double pr0 = q[0] * iq, pr1 = q[1] * iq;
+  const double r0 = pr0 - (double)uv.x, r1 = pr1 - (double)uv.y;
+  double scale;
+  const double rho = huber(r0 * r0 + r1 * r1, P.huber_a, P.huber_b, &scale);
+  const double f = iq * scale;
+  fin = isfinite(r0) && isfinite(r1) && isfinite(f);
+  if (cvar) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      out[k] = (dq[k][0] - pr0 * dq[k][2]) * f;
+      out[6 + k] = (dq[k][1] - pr1 * dq[k][2]) * f;
+      const double k2 = Kd[3 * k + 2];
+      out[3 + k] = (Kd[3 * k] - pr0 * k2) * f;
+      out[9 + k] = (Kd[3 * k + 1] - pr1 * k2) * f;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) out[k] = 0.0;
+  }
+  if (pvar) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      out[12 + k] = (dX[k][0] - pr0 * dX[k][2]) * f;
+      out[15 + k] = (dX[k][1] - pr1 * dX[k][2]) * f;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) out[12 + k] = 0.0;
+  }
+  out[18] = r0 * scale;
+  out[19] = r1 * scale;
+#pragma unroll
+  for (int k = 0; k < 18; ++k) fin = fin && isfinite(out[k]);
+  return rho;
+}
+
 // Wave body: every wave owns chunks of 64 consecutive observations (grid
 // stride over chunks), computes one record per lane, stages the records in a
 // wave-private LDS slot of ROWS rows (row stride 21 doubles: conflict-free
@@ -391,6 +539,7 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
   load_idx(base + 2 * step + lane, c2, p2, uv2);
   load_pt(base + lane, p, X, pv);
   load_pt(base + step + lane, p1, X1, pv1);
+  auto q = cam_pre(cam_of, c);     // camera accessor of the current chunk (prefetched one chunk ahead)
   for (; base < P.no; base += step) {
     const int o = base + lane;
     double X2[3];
@@ -399,6 +548,7 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
     int c3, p3;
     float2 uv3;
     load_idx(o + 3 * step, c3, p3, uv3);
+    const auto qn = cam_pre(cam_of, c1);
     double out[kJR];
     if (MODE == 4) {   // loads only
       acc[0] += X[0] + X[1] + X[2] + uv.x + pv + c;
@@ -407,11 +557,12 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
       c2 = c3; p2 = p3; uv2 = uv3;
       X[0] = X1[0]; X[1] = X1[1]; X[2] = X1[2]; pv = pv1;
       X1[0] = X2[0]; X1[1] = X2[1]; X1[2] = X2[2]; pv1 = pv2;
+      q = qn;
       continue;
     }
     {
       const bool live = o < P.no;
-      const auto cam = cam_of(c);
+      const auto cam = cam_make(cam_of, q);
       if constexpr (MODE == 2) {
         const auto T = cam_row(cam);
         double sum = X[0] + uv.x;
@@ -439,6 +590,7 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
       c2 = c3; p2 = p3; uv2 = uv3;
       X[0] = X1[0]; X[1] = X1[1]; X[2] = X1[2]; pv = pv1;
       X1[0] = X2[0]; X1[1] = X2[1]; X1[2] = X2[2]; pv1 = pv2;
+      q = qn;
       continue;
     }
     const int nrec = min(64, P.no - base);
@@ -501,6 +653,7 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
     c2 = c3; p2 = p3; uv2 = uv3;
     X[0] = X1[0]; X[1] = X1[1]; X[2] = X1[2]; pv = pv1;
     X1[0] = X2[0]; X1[1] = X2[1]; X1[2] = X2[2]; pv1 = pv2;
+    q = qn;
   }
 }
 
@@ -511,6 +664,21 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem P, const double* _
   __shared__ double stage[4 * 64 * kStageLd];
   double acc[2] = {0.0, 0.0};  // cost, bad
   lin_waves<4, 64>(P, pts, JR, stage, [&](int c) { return CamGlobal{rec + (size_t)c * kCamRec, P.vc[c] >= 0}; }, acc);
+  double tot[2];
+  block_sum<2>(acc, lds, tot);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_COST)[blockIdx.x] = tot[0];
+    part_of(part, SL_LIN_BAD)[blockIdx.x] = tot[1];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_linearize_rc(DevProblem P, const double* __restrict__ crec,
+                                                      const double* __restrict__ pts, double* __restrict__ JR,
+                                                      double* __restrict__ part) {
+  __shared__ double lds[2 * 16];
+  __shared__ double stage[4 * 64 * kStageLd];
+  double acc[2] = {0.0, 0.0};  // cost, bad
+  lin_waves<4, 64>(P, pts, JR, stage, CamRcOf{crec, P.extr}, acc);
   double tot[2];
   block_sum<2>(acc, lds, tot);
   if (threadIdx.x == 0) {
@@ -939,100 +1107,80 @@ __global__ __launch_bounds__(256) void k_backsub(DevProblem P, const double* __r
 }
 
 // ---------------------------------------------------------------------------
-// model cost change + candidate cost, one thread per observation:
+// model cost change + candidate cost, one lane per observation:
 //   Jd = Jc d_c + Jp d_p ; m += Jd.(r + Jd/2)    (model_cost_change = -sum m)
 //   candidate residual at (camera', X') -> Huber cost
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_candidate(DevProblem P, const double* __restrict__ JR,
-                                                   const double* __restrict__ delta_c,
-                                                   const double* __restrict__ delta_p,
-                                                   const double* __restrict__ rec_c,
-                                                   const double* __restrict__ pts_c, double* __restrict__ part) {
-  __shared__ double lds[3 * 16];
-  double acc[3] = {0.0, 0.0, 0.0};  // mneg, ccost, cand_bad
-  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < P.no; o += gridDim.x * blockDim.x) {
-    const int c = P.obs_cam[o], p = P.obs_pt[o];
-    const int v = P.vc[c];
-    double j[kJR];
-    load_jr(JR, P.no, o, j);
-    double jd0 = 0.0, jd1 = 0.0;
-    if (v >= 0) {
-      const double* dc = delta_c + (size_t)v * 6;
-#pragma unroll
-      for (int a = 0; a < 6; ++a) { jd0 += j[a] * dc[a]; jd1 += j[6 + a] * dc[a]; }
-    }
-    const double dp0 = delta_p[3 * p], dp1 = delta_p[3 * p + 1], dp2 = delta_p[3 * p + 2];
-    jd0 += j[12] * dp0 + j[13] * dp1 + j[14] * dp2;
-    jd1 += j[15] * dp0 + j[16] * dp1 + j[17] * dp2;
-    acc[0] += jd0 * (j[18] + jd0 / 2.0) + jd1 * (j[19] + jd1 / 2.0);
-    double rc[2];
-    project_value(rec_c + (size_t)c * kCamRec, !(P.cam_fixed && P.cam_fixed[c]), pts_c[3 * p], pts_c[3 * p + 1],
-                  pts_c[3 * p + 2], P.uv[o], rc);
-    double sc;
-    const double rho = huber(rc[0] * rc[0] + rc[1] * rc[1], P.huber_a, P.huber_b, &sc);
-    acc[1] += 0.5 * rho;
-    if (!isfinite(rc[0]) || !isfinite(rc[1])) acc[2] += 1.0;
-  }
-  double out[3];
-  block_sum<3>(acc, lds, out);
-  if (threadIdx.x == 0) {
-    part_of(part, SL_MCC_NEG)[blockIdx.x] = out[0];
-    part_of(part, SL_CCOST)[blockIdx.x] = out[1];
-    part_of(part, SL_CAND_BAD)[blockIdx.x] = out[2];
-  }
-}
-
 // Same with the camera table (value-only candidate records + the camera
 // step) and the observation records staged in LDS: the JR records of a
 // chunk are read with contiguous 16-B-per-lane loads, the per-observation
 // camera data comes from LDS (nc <= kLinLdsCams).
 constexpr int kCandRec = 22;   // R (9) t (3) | extrinsic (16); camera step (6) at 16..21
-__global__ __launch_bounds__(kLinLdsThreads) void k_candidate_lds(DevProblem P, const double* __restrict__ JR,
-                                                                  const double* __restrict__ delta_c,
-                                                                  const double* __restrict__ delta_p,
-                                                                  const double* __restrict__ rec_c,
-                                                                  const double* __restrict__ pts_c,
-                                                                  double* __restrict__ part) {
+// entry e of the candidate camera table (value-only records + the step)
+__device__ inline double cand_entry(const DevProblem& P, const double* __restrict__ rec_c,
+                                    const double* __restrict__ delta_c, int e) {
+  const int c = e / kCandRec, k = e - c * kCandRec;
+  const bool fixed = P.cam_fixed && P.cam_fixed[c];
+  const int vc = P.vc[c];
+  const double* src;
+  bool zero = false;
+  if (k < 16) {
+    src = rec_c + (size_t)c * kCamRec + (fixed ? k : (k < 9 ? kRecR + k : kRecT + min(k - 9, 2)));
+    zero = !fixed && k >= 12;
+  } else {
+    src = delta_c + (size_t)max(vc, 0) * 6 + (k - 16);
+    zero = vc < 0;
+  }
+  const double x = *src;
+  return zero ? 0.0 : x;
+}
+// the same table in global memory for nc > kLinLdsCams (176 B per camera:
+// L2-resident up to ~20k cameras, where the 704-B records are not)
+__global__ __launch_bounds__(256) void k_cand_table(DevProblem P, const double* __restrict__ rec_c,
+                                                    const double* __restrict__ delta_c, double* __restrict__ tbl) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < P.nc * kCandRec) tbl[e] = cand_entry(P, rec_c, delta_c, e);
+}
+// NT threads per block; GTBL: camera table in global memory (gtbl, K = P.K),
+// else filled into LDS (nc <= kLinLdsCams)
+template <int NT, bool GTBL>
+__global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double* __restrict__ JR,
+                                                      const double* __restrict__ delta_c,
+                                                      const double* __restrict__ delta_p,
+                                                      const double* __restrict__ rec_c,
+                                                      const double* __restrict__ pts_c, const double* __restrict__ gtbl,
+                                                      double* __restrict__ part) {
   __shared__ double lds[3 * 16];
-  __shared__ double stage[kLinLdsThreads * kStageLd];
-  __shared__ double tbl[kLinLdsCams * kCandRec];
-  __shared__ float ktb[kLinLdsCams * 9];
-  {  // camera table: every load issued before the first LDS store (clamped, unconditional)
-    constexpr int kPer = (kLinLdsCams * kCandRec + kLinLdsThreads - 1) / kLinLdsThreads;
-    constexpr int kPerK = (kLinLdsCams * 9 + kLinLdsThreads - 1) / kLinLdsThreads;
+  __shared__ double stage[NT * kStageLd];
+  __shared__ double tbl_s[GTBL ? 1 : kLinLdsCams * kCandRec];
+  __shared__ float ktb_s[GTBL ? 1 : kLinLdsCams * 9];
+  const double* tbl;
+  const float* ktb;
+  if constexpr (GTBL) {
+    tbl = gtbl;
+    ktb = P.K;
+  } else {  // camera table: every load issued before the first LDS store (clamped, unconditional)
+    constexpr int kPer = (kLinLdsCams * kCandRec + NT - 1) / NT;
+    constexpr int kPerK = (kLinLdsCams * 9 + NT - 1) / NT;
     const int n = P.nc * kCandRec, nk = P.nc * 9;
     double v[kPer];
     float kv[kPerK];
 #pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = min((int)threadIdx.x + i * kLinLdsThreads, n - 1);
-      const int c = e / kCandRec, k = e - c * kCandRec;
-      const bool fixed = P.cam_fixed && P.cam_fixed[c];
-      const int vc = P.vc[c];
-      const double* src;
-      bool zero = false;
-      if (k < 16) {
-        src = rec_c + (size_t)c * kCamRec + (fixed ? k : (k < 9 ? kRecR + k : kRecT + min(k - 9, 2)));
-        zero = !fixed && k >= 12;
-      } else {
-        src = delta_c + (size_t)max(vc, 0) * 6 + (k - 16);
-        zero = vc < 0;
-      }
-      const double x = *src;
-      v[i] = zero ? 0.0 : x;
-    }
+    for (int i = 0; i < kPer; ++i) v[i] = cand_entry(P, rec_c, delta_c, min((int)threadIdx.x + i * NT, n - 1));
 #pragma unroll
-    for (int i = 0; i < kPerK; ++i) kv[i] = P.K[min((int)threadIdx.x + i * kLinLdsThreads, nk - 1)];
+    for (int i = 0; i < kPerK; ++i) kv[i] = P.K[min((int)threadIdx.x + i * NT, nk - 1)];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
-      const int e = threadIdx.x + i * kLinLdsThreads;
-      if (e < n) tbl[e] = v[i];
+      const int e = threadIdx.x + i * NT;
+      if (e < n) tbl_s[e] = v[i];
     }
 #pragma unroll
     for (int i = 0; i < kPerK; ++i) {
-      const int e = threadIdx.x + i * kLinLdsThreads;
-      if (e < nk) ktb[e] = kv[i];
+      const int e = threadIdx.x + i * NT;
+      if (e < nk) ktb_s[e] = kv[i];
     }
+    tbl = tbl_s;
+    ktb = ktb_s;
   }
   __syncthreads();   // table ready
   double acc[3] = {0.0, 0.0, 0.0};  // mneg, ccost, cand_bad
@@ -1041,7 +1189,7 @@ __global__ __launch_bounds__(kLinLdsThreads) void k_candidate_lds(DevProblem P, 
   // slot, then each lane consumes its own record (no workgroup barrier).
   // Loads are unconditional with clamped indices (no waitcnt drains).
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  constexpr int WAVES = kLinLdsThreads / 64;
+  constexpr int WAVES = NT / 64;
   double* st = stage + w * (64 * kStageLd);
   const int step = gridDim.x * WAVES * 64;
   int base = (blockIdx.x * WAVES + w) * 64;
@@ -1380,6 +1528,13 @@ void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s) {
                        W.part);
     return;
   }
+  static int rc = -1;
+  if (rc < 0) { const char* e = getenv("BA_LIN_TABLE"); rc = e && atoi(e) ? 0 : 1; }   // diagnostics: global-table kernel
+  if (rc) {
+    hipLaunchKernelGGL(k_cam_compact, dim3((P.nc + 255) / 256), dim3(256), 0, s, P, W.cams, W.crec);
+    hipLaunchKernelGGL(k_linearize_rc, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.crec, W.pts, W.JR, W.part);
+    return;
+  }
   hipLaunchKernelGGL(k_linearize, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.rec, W.pts, W.JR, W.part);
 }
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
@@ -1458,12 +1613,14 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
                        W.W, W.u, W.Linv, W.y, W.scale_p, W.part);
   if (P.nc <= kLinLdsCams) {
     const int g = lds_grid(P.no);
-    hipLaunchKernelGGL(k_candidate_lds, dim3(g), dim3(kLinLdsThreads), 0, s, P, W.JR, W.delta_c, W.delta_p, W.rec_c,
-                       W.pts_c, W.part);
+    hipLaunchKernelGGL((k_candidate_lds<kLinLdsThreads, false>), dim3(g), dim3(kLinLdsThreads), 0, s, P, W.JR,
+                       W.delta_c, W.delta_p, W.rec_c, W.pts_c, nullptr, W.part);
     return;
   }
-  hipLaunchKernelGGL(k_candidate, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.JR, W.delta_c, W.delta_p,
-                     W.rec_c, W.pts_c, W.part);
+  hipLaunchKernelGGL(k_cand_table, dim3((P.nc * kCandRec + 255) / 256), dim3(256), 0, s, P, W.rec_c, W.delta_c,
+                     W.ctbl);
+  hipLaunchKernelGGL((k_candidate_lds<256, true>), dim3(grid_for(P.no)), dim3(256), 0, s, P, W.JR, W.delta_c,
+                     W.delta_p, W.rec_c, W.pts_c, W.ctbl, W.part);
 }
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(64 * kNumSlots), 0, s, W.part, W.scal, sum_mask, max_mask);

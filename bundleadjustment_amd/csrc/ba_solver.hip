@@ -246,6 +246,8 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.pts_c = ctx->dalloc<double>(3 * (size_t)np);
   W.rec = ctx->dalloc<double>((size_t)kCamRec * nc);
   W.rec_c = ctx->dalloc<double>((size_t)kCamRec * nc);
+  W.crec = ctx->dalloc<double>((size_t)16 * nc);
+  W.ctbl = ctx->dalloc<double>((size_t)22 * nc);
   W.JR = ctx->dalloc<double>(20 * (size_t)no);
   W.delta_p = ctx->dalloc<double>(3 * (size_t)np);
   W.Hpp = ctx->dalloc<double>(6 * (size_t)np);

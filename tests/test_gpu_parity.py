@@ -137,6 +137,22 @@ def test_solve_c3_first_iterations(solver, oracle_lib):
     assert_close(pts, op, 1e-8, 1e-10, "points")
 
 
+def test_linearize_many_cameras_matches_oracle(solver, oracle_lib):
+    """> kLinLdsCams cameras: k_linearize_rc rebuilds each observation's camera
+    terms from the compact record (dual Rodrigues in the Jets' order), fixed
+    cameras from their float extrinsic."""
+    p = make_synthetic(300, 5000, 6, seed=0xBA5E0007)
+    for c in (1, 7, 150):
+        bp.fix_camera(p, c)
+    solver.set_problem(p)
+    r, J, cost = solver.linearize()
+    ro, Jo, costo, ok = oracle_lib.linearize(p)
+    assert ok
+    assert_close(r, ro, 1e-12, 1e-9, "corrected residual")
+    assert_close(J, Jo, 1e-11, 1e-9, "corrected jacobian")
+    assert cost == pytest.approx(costo, rel=1e-12)
+
+
 def test_many_cameras_global_table_path(solver, oracle_lib):
     """More cameras than the LDS camera table holds (kLinLdsCams = 200): the
     global-record linearisation / W / candidate kernels and a 1794-row
