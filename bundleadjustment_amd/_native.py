@@ -121,7 +121,8 @@ def load_library(path: str | os.PathLike | None = None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = Path(path) if path else LIB_PATH
+    # BA_HIP_LIB: load another build of the same ABI (A/B kernel comparisons)
+    p = Path(path) if path else Path(os.environ.get("BA_HIP_LIB", str(LIB_PATH)))
     if not p.exists():
         raise NativeLibraryError(
             f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

@@ -1,0 +1,132 @@
+// ba_chol_split.hip — split form of the dense Cholesky block step for large
+// reduced systems (>= kCholSplitBlocks block columns, e.g. C4's 6000 rows):
+// k_chol_panel forms L_{I,k} = A_{I,k} V_k^T once per tile row, then every
+// trailing tile does a single GEMM.  Its own translation unit, so the fused
+// step of ba_chol.hip keeps its code generation (a shared template changed
+// the inlining of the critical workgroup's factor_invert_blk).
+#include "ba_chol.h"
+
+namespace bahip {
+
+// One block step.  k < 0: factor block 0 only (grid 1x1).
+//   A    working matrix ((n+1) x ld), trailing part updated in place
+//   L    output factor ((n+1) x ld)
+//   Vbuf [T][64][64] inverses of the diagonal blocks
+// SPLIT (large systems): the panel L_{I,k} = A_{I,k} V_k^T was formed and
+// stored by k_chol_panel just before; every tile reads it from L, so a tile
+// does one GEMM instead of three (the fused form recomputes P_I, P_J per
+// tile: 3x the flops and ~2.5x the bytes, which dominate once the trailing
+// matrix has thousands of tiles).
+__global__ __launch_bounds__(256) void k_chol_step_split(double* __restrict__ A, double* __restrict__ L, int ld, int n,
+                                                   int k, double* __restrict__ Vbuf, double* __restrict__ scal) {
+  const int I = blockIdx.y, J = blockIdx.x;
+  if (J > I) return;
+  __shared__ double S0[CB][LDP];
+  __shared__ double S1[CB][LDP];
+  __shared__ double S2[CB][LDP];
+  __shared__ CholLds cw;
+  const int nrows = n + 1;
+  const size_t lds = (size_t)ld;
+  const int s = (k + 1) * CB;                 // first row/col of the trailing matrix
+  const int kc = k * CB;                      // column offset of block k
+  const int kb = k >= 0 ? min(CB, n - kc) : 0;
+  const int r0 = s + I * CB, c0 = s + J * CB;
+  if (I == 0 && J == 0) {
+    // ---- critical workgroup: next diagonal block
+    const int b = min(CB, n - s);             // its order
+    const int m = min(CB, nrows - s);         // rows in the tile (b or b + 1 with the rhs row)
+    CHOL_STAMP(0);
+    if (k >= 0) {
+      const TileRegs tA = tile_fetch<true>(A, lds, s, s, nrows, s + b);   // A_{k+1,k+1} (+ rhs row)
+      const TileRegs tP = tile_fetch(L, lds, s, kc, nrows, kc + kb);      // L_{k+1,k} (k_chol_panel)
+      tile_put(S0, tA);
+      tile_put(S1, tP);
+      __syncthreads();
+      mfma_xxT_lower_sub(S1, S0);            // C = A - P P^T (lower tiles)
+    } else {
+      stage64(S0, A, lds, s, s, nrows, s + b);
+    }
+    if (threadIdx.x == 0) cw.bad = 0;
+    CHOL_STAMP(1);
+    factor_invert_blk(S0, S2, S1, cw, b, m);   // rows b..m-1 (rhs) come out as L rows too
+    CHOL_STAMP(5);
+    __syncthreads();
+    // only V_{k+1} and the rhs row of L leave the workgroup: the diagonal L
+    // block itself is never read again (back substitution uses V)
+    {
+      double2* Vd = reinterpret_cast<double2*>(Vbuf + (size_t)(k + 1) * CB * CB);
+      for (int e2 = threadIdx.x; e2 < CB * CB / 2; e2 += 256) {
+        const int i = (2 * e2) / CB, j = (2 * e2) % CB;
+        double v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          v[h] = (j + h <= i && i < b && j + h < b) ? S2[i][j + h] : (i == j + h ? 1.0 : 0.0);
+        Vd[e2] = make_double2(v[0], v[1]);
+      }
+      if (m > b)
+        for (int j = threadIdx.x; j < b; j += 256) L[(size_t)(s + b) * ld + s + j] = S0[b][j];
+    }
+    CHOL_STAMP(6);
+    if (threadIdx.x == 0 && cw.bad) scal[SL_CHOL_BAD] += 1.0;
+    return;
+  }
+  // ---- trailing tile (I, J) != (0, 0)
+  if (k < 0) return;
+  if (r0 >= nrows || c0 >= n) return;
+  const TileRegs tI = tile_fetch(L, lds, r0, kc, nrows, kc + kb);   // L_{I,k}
+  if (I != J) {
+    const TileRegs tJ = tile_fetch(L, lds, c0, kc, n, kc + kb);     // L_{J,k}
+    tile_put(S1, tJ);
+  }
+  tile_put(S0, tI);
+  __syncthreads();
+  d4 acc[2][2];
+  mfma_xyT_64(S0, I != J ? S1 : S0, acc);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int rr, cc;
+        acc_pos(a, b, g, &rr, &cc);
+        const int ri = r0 + rr, cj = c0 + cc;
+        if (ri < nrows && cj < n && cj <= ri) A[(size_t)ri * ld + cj] -= acc[a][b][g];
+      }
+}
+
+// Panel of block step k (SPLIT mode): L_{I,k} = A_{I,k} V_k^T for every tile
+// row I > k (the rhs row included), one workgroup per tile row.
+__global__ __launch_bounds__(256) void k_chol_panel(const double* __restrict__ A, double* __restrict__ L, int ld,
+                                                    int n, int k, const double* __restrict__ Vbuf) {
+  __shared__ double S0[CB][LDP];
+  __shared__ double S2[CB][LDP];
+  const int nrows = n + 1;
+  const size_t lds = (size_t)ld;
+  const int kc = k * CB, kb = min(CB, n - kc);
+  const int r0 = (k + 1) * CB + blockIdx.x * CB;
+  if (r0 >= nrows) return;
+  const TileRegs tA = tile_fetch(A, lds, r0, kc, nrows, kc + kb);
+  const TileRegs tV = tile_fetch<true>(Vbuf + (size_t)k * CB * CB, CB, 0, 0, CB, CB);
+  tile_put(S0, tA);
+  tile_put(S2, tV);
+  __syncthreads();
+  d4 acc[4];
+  mfma_xVT_strip(S0, S2, acc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, m = min(CB, nrows - r0);
+#pragma unroll
+  for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int rr = 16 * w + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
+      if (rr < m && cc < kb) L[(size_t)(r0 + rr) * ld + kc + cc] = acc[bc][g];
+    }
+}
+
+void launch_chol_split_step(double* A, double* L, int ld, int n, int k, int tc, int tr, double* Vbuf, double* scal,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(k_chol_panel, dim3(tr), dim3(256), 0, s, A, L, ld, n, k, Vbuf);
+  hipLaunchKernelGGL(k_chol_step_split, dim3(tc, tr), dim3(256), 0, s, A, L, ld, n, k, Vbuf, scal);
+}
+
+}  // namespace bahip

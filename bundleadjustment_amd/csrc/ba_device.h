@@ -53,7 +53,7 @@ __host__ __device__ inline D3 dcos(D3 f) { const double s = -sin(f.a); return mk
 __host__ __device__ inline D3 dsin(D3 f) { const double c = cos(f.a); return mk(sin(f.a), c * f.d[0], c * f.d[1], c * f.d[2]); }
 
 // ceres::AngleAxisToRotationMatrix on duals; R column-major (R[c*3+r]).
-__host__ __device__ inline void angle_axis_to_R_d3(const double w[3], D3 R[9]) {
+__host__ __device__ __forceinline__ void angle_axis_to_R_d3(const double w[3], D3 R[9]) {
   const D3 a0 = mk(w[0], 1, 0, 0), a1 = mk(w[1], 0, 1, 0), a2 = mk(w[2], 0, 0, 1);
   const D3 theta2 = a0 * a0 + a1 * a1 + a2 * a2;
   if (theta2.a > 2.220446049250313080847e-16) {

@@ -98,6 +98,7 @@ struct PcgOpts { double q_tolerance; int min_iter, max_iter, schur_jacobi; };
 
 // --- launchers (all asynchronous on `s`) ---
 void launch_cam_prep(const DevProblem& P, const double* cams, double* rec, bool deriv, hipStream_t s);
+void launch_lin_prep(const DevProblem& P, const DevWork& W, hipStream_t s);   // camera tables for launch_linearize
 void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
                            double max_diag, hipStream_t s);

@@ -509,11 +509,16 @@ __device__ inline void wave_lds_sync() {
 // stores; 2 no arithmetic (records = a sum of the camera row); 3 table fill
 // only; 4 loads only; 5 arithmetic only (no stage, no stores); 6 = 5 with
 // every lane on camera 1 (broadcast table reads)
-template <int WAVES, int ROWS, class CamOf, int MODE = 0>
+struct NoInit {
+  __device__ void operator()() const {}
+};
+// init(): block-wide setup (e.g. building the LDS camera table) run by every
+// thread after the prologue loads are issued, so it overlaps their latency
+template <int WAVES, int ROWS, class CamOf, int MODE = 0, class Init = NoInit>
 __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__ pts, double* __restrict__ JR,
-                                 double* stage_all, const CamOf& cam_of, double (&acc)[2]) {
+                                 double* stage_all, const CamOf& cam_of, double (&acc)[2], const Init& init = Init{}) {
   static_assert(ROWS == 64 || ROWS == 32, "stage rows");
-  if (P.no == 0) return;   // (the clamped prefetch indices need no >= 1)
+  if (P.no == 0) { init(); return; }   // (the clamped prefetch indices need no >= 1)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double* stage = stage_all + w * (ROWS * kStageLd);
   const int step = gridDim.x * WAVES * 64;
@@ -539,7 +544,11 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
   load_idx(base + 2 * step + lane, c2, p2, uv2);
   load_pt(base + lane, p, X, pv);
   load_pt(base + step + lane, p1, X1, pv1);
-  auto q = cam_pre(cam_of, c);     // camera accessor of the current chunk (prefetched one chunk ahead)
+  init();
+  // compact-record cameras are prefetched one chunk ahead; table cameras are
+  // read at use (their index is all that travels)
+  constexpr bool kPre = std::is_same<CamOf, CamRcOf>::value;
+  auto q = cam_pre(cam_of, kPre ? c : 0);
   for (; base < P.no; base += step) {
     const int o = base + lane;
     double X2[3];
@@ -548,7 +557,7 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
     int c3, p3;
     float2 uv3;
     load_idx(o + 3 * step, c3, p3, uv3);
-    const auto qn = cam_pre(cam_of, c1);
+    const auto qn = cam_pre(cam_of, kPre ? c1 : 0);
     double out[kJR];
     if (MODE == 4) {   // loads only
       acc[0] += X[0] + X[1] + X[2] + uv.x + pv + c;
@@ -562,7 +571,10 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
     }
     {
       const bool live = o < P.no;
-      const auto cam = cam_make(cam_of, q);
+      const auto cam = [&] {
+        if constexpr (kPre) return cam_make(cam_of, q);
+        else return cam_of(c);
+      }();
       if constexpr (MODE == 2) {
         const auto T = cam_row(cam);
         double sum = X[0] + uv.x;
@@ -734,7 +746,8 @@ __device__ inline void fill_lin_table(const DevProblem& P, const double* __restr
 
 // NT threads per block (one block per CU: the camera table fills most of
 // the LDS), stage rows ROWS per wave.
-template <int NT, int ROWS, int MODE = 0, bool LAZY = false>
+// HOOK: the table fill runs after the first chunks' loads are issued
+template <int NT, int ROWS, int MODE = 0, bool LAZY = false, bool HOOK = false>
 __global__ __launch_bounds__(NT) void k_linearize_lds_t(DevProblem P, const double* __restrict__ rec,
                                                         const double* __restrict__ pts, double* __restrict__ JR,
                                                         double* __restrict__ part) {
@@ -742,13 +755,14 @@ __global__ __launch_bounds__(NT) void k_linearize_lds_t(DevProblem P, const doub
   __shared__ double stage[(NT / 64) * ROWS * kStageLd];
   __shared__ __attribute__((aligned(16))) double tbl[kLinLdsCams * kTblRec];
   __shared__ float ktb[kLinLdsCams * 9];
-  fill_lin_table<NT>(P, rec, tbl, ktb);
+  if (!HOOK) fill_lin_table<NT>(P, rec, tbl, ktb);
   double acc[2] = {0.0, 0.0};
   auto cam_of = [&](int c) {
     if constexpr (LAZY) return CamLdsLazy{tbl + c * kTblRec, ktb + c * 9};
     else return CamLds{tbl + c * kTblRec, ktb + c * 9};
   };
-  if (MODE != 3) lin_waves<NT / 64, ROWS, decltype(cam_of), MODE>(P, pts, JR, stage, cam_of, acc);
+  auto init = [&] { if (HOOK) fill_lin_table<NT>(P, rec, tbl, ktb); };
+  if (MODE != 3) lin_waves<NT / 64, ROWS, decltype(cam_of), MODE>(P, pts, JR, stage, cam_of, acc, init);
   double tot[2];
   block_sum<2>(acc, lds, tot);
   if (threadIdx.x == 0) {
@@ -1503,6 +1517,12 @@ __global__ __launch_bounds__(64 * kNumSlots) void k_reduce(double* __restrict__ 
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+// diagnostics: BA_LIN_LEGACY=1 -> the global-record linearisation beyond 200 cameras
+static bool lin_legacy() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("BA_LIN_LEGACY"); v = e && atoi(e) ? 1 : 0; }
+  return v != 0;
+}
 void launch_cam_prep(const DevProblem& P, const double* cams, double* rec, bool deriv, hipStream_t s) {
   if (P.nc == 0) return;
   hipLaunchKernelGGL(k_cam_prep, dim3(P.nc), dim3(64), 0, s, P.nc, cams, P.K, P.cam_fixed, P.extr, rec,
@@ -1521,17 +1541,19 @@ static int lds_grid(int n) {
   return g < 1 ? 1 : (g > n_cu ? n_cu : g);
 }
 
+void launch_lin_prep(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  if (P.nc <= kLinLdsCams || lin_legacy())
+    launch_cam_prep(P, W.cams, W.rec, true, s);
+  else
+    hipLaunchKernelGGL(k_cam_compact, dim3((P.nc + 255) / 256), dim3(256), 0, s, P, W.cams, W.crec);
+}
 void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nc > 0 && P.nc <= kLinLdsCams) {
-    const int g = lds_grid(P.no);
-    hipLaunchKernelGGL((k_linearize_lds_t<kLinNT, kLinRows>), dim3(g), dim3(kLinNT), 0, s, P, W.rec, W.pts, W.JR,
-                       W.part);
+    hipLaunchKernelGGL((k_linearize_lds_t<kLinNT, kLinRows>), dim3(lds_grid(P.no)), dim3(kLinNT), 0, s, P, W.rec,
+                       W.pts, W.JR, W.part);
     return;
   }
-  static int rc = -1;
-  if (rc < 0) { const char* e = getenv("BA_LIN_TABLE"); rc = e && atoi(e) ? 0 : 1; }   // diagnostics: global-table kernel
-  if (rc) {
-    hipLaunchKernelGGL(k_cam_compact, dim3((P.nc + 255) / 256), dim3(256), 0, s, P, W.cams, W.crec);
+  if (!lin_legacy()) {
     hipLaunchKernelGGL(k_linearize_rc, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.crec, W.pts, W.JR, W.part);
     return;
   }

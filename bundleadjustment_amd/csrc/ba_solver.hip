@@ -394,7 +394,7 @@ LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max
   const hipStream_t s = ctx->stream;
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
-  launch_cam_prep(P, W.cams, W.rec, true, s);
+  launch_lin_prep(P, W, s);
   if (rj_ms) HIP_OK(hipEventRecord(ctx->ev[2], s));
   launch_linearize(P, W, s);
   if (rj_ms) HIP_OK(hipEventRecord(ctx->ev[3], s));

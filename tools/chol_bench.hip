@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "ba_chol.hip"
+#include "ba_chol_split.hip"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 
@@ -65,9 +66,9 @@ int main(int argc, char** argv) {
       CK(hipEventRecord(e0));
       if (k >= 0 && T >= kCholSplitBlocks) {
         hipLaunchKernelGGL(k_chol_panel, dim3(grid.y), dim3(256), 0, 0, dA, dL, ld, n, k, dV);
-        hipLaunchKernelGGL(k_chol_step<true>, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS);
+        hipLaunchKernelGGL(k_chol_step_split, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS);
       } else {
-        hipLaunchKernelGGL(k_chol_step<false>, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS);
+        hipLaunchKernelGGL(k_chol_step, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS);
       }
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));

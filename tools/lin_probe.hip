@@ -171,6 +171,7 @@ int main() {
   };
   const int g = 256;
   run("k_linearize_lds_t<512,64>", [&] { hipLaunchKernelGGL((k_linearize_lds_t<512, 64>), dim3(g), dim3(512), 0, 0, P, rec, d_pts, JR, part); });
+  run("k_linearize_lds_t<512,64> fill hook", [&] { hipLaunchKernelGGL((k_linearize_lds_t<512, 64, 0, false, true>), dim3(g), dim3(512), 0, 0, P, rec, d_pts, JR, part); });
   run("var0 product body (no prefetch)", [&] { hipLaunchKernelGGL(k_lin_var<0>, dim3(g), dim3(512), 0, 0, P, rec, d_pts, JR, part); });
   run("var1 one camera", [&] { hipLaunchKernelGGL(k_lin_var<1>, dim3(g), dim3(512), 0, 0, P, rec, d_pts, JR, part); });
 
