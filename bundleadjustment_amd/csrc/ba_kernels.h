@@ -69,6 +69,7 @@ struct DevWork {
   bool w32;                          // W blocks stored in Wf
   double* S;                         // [(n+1) x ld] reduced system, row n = rhs (working matrix)
   double* Lf;                        // [(n+1) x ld] Cholesky factor, row n = L^-1 rhs
+  double* Spk;                       // [n(n+1)/2 + n] packed lower triangle + rhs of S (multi-rank exchange)
   double* y;                         // [n] reduced solution
   double* Vbuf;                      // [ceil(n/64)][64][64] inverses of the diagonal Cholesky blocks
   int* flags;                        // [kFlagWords] hand-off flags of the dataflow kernels (zeroed per call)
@@ -112,6 +113,8 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
 void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, hipStream_t s);  // ba_chol.hip
+// S <-> W.Spk: lower triangle row by row (offset i(i+1)/2), then the rhs row
+void launch_pack_lower(const DevProblem& P, const DevWork& W, bool pack, hipStream_t s);
 void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s);
 // ITERATIVE_SCHUR (ba_pcg.hip): implicit Schur complement + PCG

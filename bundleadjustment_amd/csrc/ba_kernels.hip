@@ -1616,6 +1616,23 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   grid = (grid + 7) / 8 * 8;   // k_schur_pairs' XCD ranges need a multiple of 8
   hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
 }
+// one workgroup per row of S: row i < n holds its lower part (j <= i), row n
+// the rhs (all n entries)
+__global__ __launch_bounds__(256) void k_pack_lower(int n, int ld, double* __restrict__ S, double* __restrict__ pk,
+                                                    int pack) {
+  const int i = blockIdx.x;
+  const size_t off = (size_t)i * (i + 1) / 2;   // row n: n(n+1)/2, the rhs
+  const int len = i < n ? i + 1 : n;
+  double* row = S + (size_t)i * ld;
+  for (int j = threadIdx.x; j < len; j += blockDim.x) {
+    if (pack) pk[off + j] = row[j];
+    else row[j] = pk[off + j];
+  }
+}
+void launch_pack_lower(const DevProblem& P, const DevWork& W, bool pack, hipStream_t s) {
+  if (P.n == 0) return;
+  hipLaunchKernelGGL(k_pack_lower, dim3(P.n + 1), dim3(256), 0, s, P.n, P.ld, W.S, W.Spk, pack ? 1 : 0);
+}
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
   if (P.nvc == 0) return;
   hipLaunchKernelGGL(k_cam_add_diag, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.Hcc, W.gc, W.scale_c,

@@ -119,6 +119,11 @@ struct ba_ctx {
     log.clear();
   }
 
+  // collectives on the data path: with more than one rank, or forced on a
+  // one-rank communicator (BA_FORCE_COLLECTIVES=1: tests of the exchange path
+  // on a single GPU, where the all-reduce is the identity)
+  bool force_coll = false;
+  bool coll() const { return comm && (nranks > 1 || force_coll); }
   void allreduce(double* d, size_t count, ncclRedOp_t op = ncclSum) {
     if (!comm || count == 0) return;   // a 1-rank communicator still runs the collectives (tests)
     NCCL_OK(ncclAllReduce(d, d, count, ncclDouble, op, comm, stream));
@@ -179,7 +184,7 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
     if (!ctx->cam_fixed_h[c]) cam_used[c] = 1;
     if (!pt_fixed[p]) pt_var[p] = 1;
   }
-  if (ctx->comm && ctx->nranks > 1 && nc > 0) {
+  if (ctx->coll() && nc > 0) {
     // the reduced system spans the union of the ranks' observed cameras
     uint8_t* d = nullptr;
     HIP_OK(hipMalloc(&d, nc));
@@ -332,6 +337,7 @@ void ensure_dense(ba_ctx* ctx) {
   W.Lf = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
   W.Vbuf = ctx->dalloc<double>((size_t)((ctx->n + 63) / 64 + 1) * 64 * 64);
   W.flags = ctx->dalloc<int>(kFlagWords);
+  W.Spk = nullptr;
   W.blocks = ctx->upload(blocks);
   W.nblocks = (int)blocks.size();
   W.pairs = ctx->upload(pairs);
@@ -401,7 +407,7 @@ LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max
   launch_point_assemble(P, W, compute_scale, min_diag, max_diag, s);
   launch_cam_assemble(P, W, s);
   launch_reduce(W, bit(SL_COST) | bit(SL_LIN_BAD) | bit(SL_GN2_P) | bit(SL_XN2_P), bit(SL_GMAX_P), s);
-  if (ctx->nranks > 1) {
+  if (ctx->coll()) {
     ctx->allreduce(W.Hcc, 21 * (size_t)ctx->nvc);
     ctx->allreduce(W.gc, 6 * (size_t)ctx->nvc);
     ctx->allreduce(W.scal + SL_COST, 2);          // COST, LIN_BAD
@@ -436,8 +442,14 @@ void reduced_solve_dense(ba_ctx* ctx, double radius) {
   launch_cam_schur_diag(P, W, s);
   launch_schur_pairs(P, W, s);
   launch_reduce(W, bit(SL_ELIM_BAD), 0, s);
-  if (ctx->nranks > 1) {
-    ctx->allreduce(W.S, (size_t)(ctx->n + 1) * ctx->ld);
+  if (ctx->coll()) {
+    // only the lower triangle and the rhs row of S carry data: all-reduce
+    // them packed (n(n+1)/2 + n doubles instead of (n+1) n)
+    const size_t npk = (size_t)ctx->n * (ctx->n + 1) / 2 + ctx->n;
+    if (!W.Spk) W.Spk = ctx->dalloc<double>(std::max<size_t>(npk, 1));
+    launch_pack_lower(P, W, true, s);
+    ctx->allreduce(W.Spk, npk);
+    launch_pack_lower(P, W, false, s);
     ctx->allreduce(W.scal + SL_ELIM_BAD, 1);
   }
   launch_cam_add_diag(P, W, radius, s);
@@ -461,7 +473,7 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
   if (po.schur_jacobi) launch_pcg_dup(P, W, s);
   launch_reduce(W, bit(SL_ELIM_BAD), 0, s);
   const size_t tcount = (size_t)W.pcg_G * 6 * ctx->nvc;
-  if (ctx->nranks > 1) {
+  if (ctx->coll()) {
     ctx->allreduce(W.Sd, 27 * (size_t)ctx->nvc);
     ctx->allreduce(W.scal + SL_ELIM_BAD, 1);
   }
@@ -472,11 +484,11 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
     for (int k = 0; k < batch && it < po.max_iter; ++k) {
       ++it;
       launch_pcg_matvec(P, W, W.pp, s);
-      if (ctx->nranks > 1) ctx->allreduce(W.tpart, tcount);
+      if (ctx->coll()) ctx->allreduce(W.tpart, tcount);
       if (it % 10 == 0) {   // ceres residual_reset_period: r = b - S x
         launch_pcg_update(P, W, 1, it, po, s);
         launch_pcg_matvec(P, W, W.y, s);
-        if (ctx->nranks > 1) ctx->allreduce(W.tpart, tcount);
+        if (ctx->coll()) ctx->allreduce(W.tpart, tcount);
         launch_pcg_update(P, W, 2, it, po, s);
       } else {
         launch_pcg_update(P, W, 0, it, po, s);
@@ -504,7 +516,7 @@ StepResult solve_step(ba_ctx* ctx, double radius, const ba_options& o) {
   launch_backsub_candidate(P, W, s);
   launch_reduce(W, bit(SL_MCC_NEG) | bit(SL_CCOST) | bit(SL_STEP2_P) | bit(SL_CAND_BAD) | bit(SL_STEP_BAD) |
                        bit(SL_STEP2_C), 0, s);
-  if (ctx->nranks > 1) {
+  if (ctx->coll()) {
     ctx->allreduce(W.scal + SL_MCC_NEG, 5);  // MCC_NEG, CCOST, STEP2_P, CAND_BAD, STEP_BAD
   }
   ctx->read_scalars();
@@ -762,6 +774,8 @@ int ba_comm_init(ba_ctx* ctx, const char id[128], int nranks, int rank) {
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
     NCCL_OK(ncclCommInitRank(&ctx->comm, nranks, uid, rank));
+    const char* fc = getenv("BA_FORCE_COLLECTIVES");
+    ctx->force_coll = fc && atoi(fc) != 0;
   });
 }
 

@@ -231,3 +231,27 @@ def test_gpu_mixed_fp32_requires_iterative(solver):
     solver.set_problem(make_config("c1"))
     with pytest.raises(BAError):
         solver.solve(Options(precision="MIXED_FP32"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("solver_type", ["DENSE_SCHUR", "ITERATIVE_SCHUR"])
+def test_gpu_exchange_path_on_one_rank(solver_type, monkeypatch):
+    """The multi-GPU exchange path (RCCL all-reduces of the camera blocks,
+    the packed lower triangle of S, the CG matvec slices, the step scalars)
+    forced on a one-rank communicator, where every all-reduce is the identity:
+    results are bitwise those of the communicator-free solve."""
+    from bundleadjustment_amd import Solver
+    p = make_config("c2", scale=0.2)
+    opts = Options(linear_solver_type=solver_type, preconditioner_type="SCHUR_JACOBI", max_num_iterations=6)
+    with Solver(0) as s0:
+        s0.set_problem(p)
+        r0 = s0.solve(opts)
+        c0, x0 = s0.params()
+    monkeypatch.setenv("BA_FORCE_COLLECTIVES", "1")
+    with Solver(0) as s1:
+        s1.comm_init(Solver.unique_id(), 1, 0)
+        s1.set_problem(p)
+        r1 = s1.solve(opts)
+        c1, x1 = s1.params()
+    assert r1.final_cost == r0.final_cost and r1.num_iterations == r0.num_iterations
+    assert np.array_equal(c0, c1) and np.array_equal(x0, x1)
