@@ -40,7 +40,7 @@ struct DevProblem {
   const float2* uv;          // [no]
   const int* pt_off;         // [np+1] CSR of observations by point
   const int* cam_off;        // [nvc+1] CSR of observations by active variable camera
-  const int* cam_obs;        // [..] sorted-observation indices grouped by camera
+  const int2* cam_op;        // [..] (sorted observation, its point) grouped by camera
   const int* vc;             // [nc] compact variable-camera index or -1
   const int* cam_of_vc;      // [nvc] camera id of a compact index
   const uint8_t* cam_fixed;  // [nc]

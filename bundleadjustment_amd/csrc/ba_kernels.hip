@@ -846,40 +846,47 @@ __global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const doub
 // ---------------------------------------------------------------------------
 // (one workgroup per camera: splitting it measured slower — the pass is
 // bound by the gathered record reads, 256 B fetched per 112 B used)
+// Hcc (lower 21) and gc per camera, slice blockIdx.y of its observations;
+// two observations in flight per thread (the camera-order index is one load
+// ahead of the record gathers)
+__device__ inline void cam_acc_jr(const double* __restrict__ JR, int no, int o, double (&acc)[27]) {
+  const double2* s = reinterpret_cast<const double2*>(jr_a(JR, o));
+  double jc[12];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { const double2 t = s[k]; jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
+  const double2 rt = reinterpret_cast<const double2*>(jr_b(JR, no, o))[3];
+  const double rr[2] = {rt.x, rt.y};
+#pragma unroll
+  for (int row = 0; row < 2; ++row) {
+    const double* j = jc + 6 * row;
+    int t = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = 0; b <= a; ++b) acc[t++] += j[a] * j[b];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] += j[a] * rr[row];
+  }
+}
 __global__ __launch_bounds__(256) void k_cam_assemble(DevProblem P, const double* __restrict__ JR,
-                                                      double* __restrict__ Hcc, double* __restrict__ gc) {
+                                                      double* __restrict__ cpart) {
   __shared__ double lds[27 * 16];
   const int v = blockIdx.x;
   double acc[27];
 #pragma unroll
   for (int k = 0; k < 27; ++k) acc[k] = 0.0;
-  const int i0 = P.cam_off[v], i1 = P.cam_off[v + 1];
-  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int o = P.cam_obs[i];
-    const double2* s = reinterpret_cast<const double2*>(jr_a(JR, o));
-    double jc[12];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) { const double2 t = s[k]; jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
-    const double2 rt = reinterpret_cast<const double2*>(jr_b(JR, P.no, o))[3];
-    const double rr[2] = {rt.x, rt.y};
-#pragma unroll
-    for (int row = 0; row < 2; ++row) {
-      const double* j = jc + 6 * row;
-      int t = 0;
-#pragma unroll
-      for (int a = 0; a < 6; ++a)
-#pragma unroll
-        for (int b = 0; b <= a; ++b) acc[t++] += j[a] * j[b];
-#pragma unroll
-      for (int a = 0; a < 6; ++a) acc[21 + a] += j[a] * rr[row];
-    }
+  int i0, i1;
+  cam_slice(P, v, i0, i1);
+  const int bd = blockDim.x;
+  for (int i = i0 + threadIdx.x; i < i1; i += 2 * bd) {
+    const bool two = i + bd < i1;
+    const int oa = P.cam_op[i].x, ob = P.cam_op[two ? i + bd : i].x;
+    cam_acc_jr(JR, P.no, oa, acc);
+    if (two) cam_acc_jr(JR, P.no, ob, acc);
   }
   double out[27];
   block_sum<27>(acc, lds, out);
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < 21; ++k) Hcc[(size_t)v * 21 + k] = out[k];
-    for (int k = 0; k < 6; ++k) gc[(size_t)v * 6 + k] = out[21 + k];
-  }
+  cam_slice_store(out, cpart, v, P.nvc);
 }
 
 __device__ inline int tri(int a, int b) { return a * (a + 1) / 2 + b; }  // a >= b
@@ -934,7 +941,13 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
   double acc[1] = {0.0};
   const size_t np = (size_t)P.np;
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
-    if (!P.pt_var[p]) continue;
+    if (!P.pt_var[p]) {   // zeros: the camera-side gathers then need no point flag (W_o = 0 there too)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) Linv[k * np + p] = 0.0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) u[k * np + p] = 0.0;
+      continue;
+    }
     double s[3], D2[3], gs[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -1293,13 +1306,9 @@ __global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const WT* 
   for (int k = 0; k < 27; ++k) acc[k] = 0.0;
   int i0, i1;
   cam_slice(P, v, i0, i1);
-  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int o = P.cam_obs[i];
-    const int p = P.obs_pt[o];
-    if (!P.pt_var[p]) continue;
-    double w[18];
-    load_w18(W, (size_t)o, w);
-    const double u0 = u[p], u1 = u[np + p], u2 = u[2 * np + p];
+  // observations of fixed points carry W = 0 and u = 0 (k_obs_w,
+  // k_point_elim): no flag needed; (o, p) pairs in camera order
+  auto add = [&](const double (&w)[18], double u0, double u1, double u2) {
     int t = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
@@ -1308,6 +1317,12 @@ __global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const WT* 
     }
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[21 + a] += w[a * 3] * u0 + w[a * 3 + 1] * u1 + w[a * 3 + 2] * u2;
+  };
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int2 op = P.cam_op[i];
+    double w[18];
+    load_w18(W, (size_t)op.x, w);
+    add(w, u[op.y], u[np + op.y], u[2 * np + op.y]);
   }
   double tot[27];
   block_sum<27>(acc, lds, tot);
@@ -1566,7 +1581,9 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
 }
 void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
-  hipLaunchKernelGGL(k_cam_assemble, dim3(P.nvc), dim3(kThreads), 0, s, P, W.JR, W.Hcc, W.gc);
+  hipLaunchKernelGGL(k_cam_assemble, dim3(P.nvc, W.cam_split), dim3(kThreads), 0, s, P, W.JR, W.cpart);
+  hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, W.cam_split, 0, W.Hcc,
+                     W.gc, nullptr);
 }
 void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
                       hipStream_t s) {

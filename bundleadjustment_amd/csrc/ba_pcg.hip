@@ -281,9 +281,8 @@ __global__ __launch_bounds__(256) void k_pcg_cam(DevProblem P, const WT* __restr
   const int i0 = min(a1, a0 + g * len), i1 = min(a1, i0 + len);
   double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int o = P.cam_obs[i];
-    const int p = P.obs_pt[o];
-    if (!P.pt_var[p]) continue;
+    const int2 op = P.cam_op[i];   // fixed points: W_o = 0, v_p = 0
+    const int o = op.x, p = op.y;
     double wv[18];
     load_w18(Wm, (size_t)o, wv);
     const double u0 = vpt[3 * (size_t)p], u1 = vpt[3 * (size_t)p + 1], u2 = vpt[3 * (size_t)p + 2];

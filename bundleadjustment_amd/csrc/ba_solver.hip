@@ -230,7 +230,11 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   P.uv = ctx->upload(uv);
   P.pt_off = ctx->upload(pt_off);
   P.cam_off = ctx->upload(cam_off);
-  P.cam_obs = ctx->upload(cam_obs);
+  {
+    std::vector<int2> cam_op(cam_obs.size());
+    for (size_t i = 0; i < cam_obs.size(); ++i) cam_op[i] = make_int2(cam_obs[i], obs_pt[cam_obs[i]]);
+    P.cam_op = ctx->upload(cam_op);
+  }
   P.vc = ctx->upload(vc);
   P.cam_of_vc = ctx->upload(ctx->cam_of_vc);
   P.cam_fixed = ctx->upload(ctx->cam_fixed_h);
