@@ -14,6 +14,7 @@
 // Every reduction is a fixed-order tree (wave shuffles + LDS, then a
 // fixed-order fold of per-block partials): results are bitwise reproducible
 // run to run.  No floating-point atomics anywhere.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -869,7 +870,8 @@ __device__ inline void cam_acc_jr(const double* __restrict__ JR, int no, int o, 
   }
 }
 __global__ __launch_bounds__(256) void k_cam_assemble(DevProblem P, const double* __restrict__ JR,
-                                                      double* __restrict__ cpart) {
+                                                      double* __restrict__ cpart, double* __restrict__ Hcc,
+                                                      double* __restrict__ gc) {
   __shared__ double lds[27 * 16];
   const int v = blockIdx.x;
   double acc[27];
@@ -886,6 +888,15 @@ __global__ __launch_bounds__(256) void k_cam_assemble(DevProblem P, const double
   }
   double out[27];
   block_sum<27>(acc, lds, out);
+  if (gridDim.y == 1) {   // one slice per camera: final sums
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int k = 0; k < 21; ++k) Hcc[(size_t)v * 21 + k] = out[k];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) gc[(size_t)v * 6 + k] = out[21 + k];
+    }
+    return;
+  }
   cam_slice_store(out, cpart, v, P.nvc);
 }
 
@@ -1581,9 +1592,16 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
 }
 void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
-  hipLaunchKernelGGL(k_cam_assemble, dim3(P.nvc, W.cam_split), dim3(kThreads), 0, s, P, W.JR, W.cpart);
-  hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, W.cam_split, 0, W.Hcc,
-                     W.gc, nullptr);
+  // one workgroup per camera: measured faster than slicing at C3 (57 vs
+  // 66 us at 8 slices) and at C5 (where 2048 / nvc < 1 anyway);
+  // BA_ASM_SPLIT (diagnostics) overrides
+  static int split = -1;
+  if (split < 0) { const char* e = getenv("BA_ASM_SPLIT"); split = e ? atoi(e) : 0; }
+  const int sl = split > 0 ? std::min(split, kCamSplit) : 1;
+  hipLaunchKernelGGL(k_cam_assemble, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
+  if (sl > 1)
+    hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
+                       nullptr);
 }
 void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
                       hipStream_t s) {
@@ -1609,13 +1627,14 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
 }
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact) {
   if (P.nvc == 0) return;
+  static int dsplit = -1;   // diagnostics: BA_DIAG_SPLIT overrides the slice count
+  if (dsplit < 0) { const char* e = getenv("BA_DIAG_SPLIT"); dsplit = e ? atoi(e) : 0; }
+  const int sl = dsplit > 0 ? std::min(dsplit, kCamSplit) : W.cam_split;
   if (W.w32)
-    hipLaunchKernelGGL(k_cam_schur_diag<float>, dim3(P.nvc, W.cam_split), dim3(kThreads), 0, s, P, W.Wf, W.u, W.S,
-                       W.cpart);
+    hipLaunchKernelGGL(k_cam_schur_diag<float>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wf, W.u, W.S, W.cpart);
   else
-    hipLaunchKernelGGL(k_cam_schur_diag<double>, dim3(P.nvc, W.cam_split), dim3(kThreads), 0, s, P, W.W, W.u, W.S,
-                       W.cpart);
-  hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, W.cam_split,
+    hipLaunchKernelGGL(k_cam_schur_diag<double>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.W, W.u, W.S, W.cpart);
+  hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl,
                      compact ? 2 : 1, W.Hcc,
                      W.gc, compact ? compact : W.S);
 }
