@@ -400,14 +400,18 @@ struct LinResult { double cost, gmax, gnorm, xnorm; bool ok; };
 
 constexpr uint32_t bit(int s) { return 1u << s; }
 
-LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max_diag, float* rj_ms = nullptr) {
+// Linearisation phase: enqueue (no host sync) / read back.  The solver
+// enqueues the next trust-region step right behind an accepted step's
+// linearisation and reads both records with one host sync (the step is
+// wasted only when the new gradient ends the solve).
+void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double max_diag, bool time_rj = false) {
   const hipStream_t s = ctx->stream;
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
   launch_lin_prep(P, W, s);
-  if (rj_ms) HIP_OK(hipEventRecord(ctx->ev[2], s));
+  if (time_rj) HIP_OK(hipEventRecord(ctx->ev[2], s));
   launch_linearize(P, W, s);
-  if (rj_ms) HIP_OK(hipEventRecord(ctx->ev[3], s));
+  if (time_rj) HIP_OK(hipEventRecord(ctx->ev[3], s));
   launch_point_assemble(P, W, compute_scale, min_diag, max_diag, s);
   launch_cam_assemble(P, W, s);
   launch_reduce(W, bit(SL_COST) | bit(SL_LIN_BAD) | bit(SL_GN2_P) | bit(SL_XN2_P), bit(SL_GMAX_P), s);
@@ -420,8 +424,11 @@ LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max
   }
   launch_cam_norms(P, W, compute_scale, min_diag, max_diag, s);
   launch_reduce(W, bit(SL_GN2_C) | bit(SL_XN2_C), bit(SL_GMAX_C), s);
-  ctx->read_scalars();
-  if (rj_ms) HIP_OK(hipEventElapsedTime(rj_ms, ctx->ev[2], ctx->ev[3]));
+  if (compute_scale) ctx->scale_valid = true;
+}
+
+// after ctx->read_scalars()
+LinResult lin_result(ba_ctx* ctx) {
   const double* h = ctx->h_scal;
   LinResult r;
   r.cost = h[SL_COST];
@@ -429,8 +436,13 @@ LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max
   r.gnorm = std::sqrt(h[SL_GN2_P] + h[SL_GN2_C]);
   r.xnorm = std::sqrt(h[SL_XN2_P] + h[SL_XN2_C]);
   r.ok = h[SL_LIN_BAD] == 0.0 && std::isfinite(r.cost);
-  if (compute_scale) ctx->scale_valid = true;
   return r;
+}
+
+LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max_diag) {
+  linearize_enqueue(ctx, compute_scale, min_diag, max_diag);
+  ctx->read_scalars();
+  return lin_result(ctx);
 }
 
 struct StepResult { bool linear_ok; double mcc, cand_cost, step_norm; int ls_iters; };
@@ -505,7 +517,9 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
   return (int)ctx->h_scal[kNumSlots + PS_ITER];
 }
 
-StepResult solve_step(ba_ctx* ctx, double radius, const ba_options& o) {
+// Trust-region step phase: enqueue (the PCG reads its state record between
+// batches of CG iterations) / read back.  Returns the linear-solver iterations.
+int step_enqueue(ba_ctx* ctx, double radius, const ba_options& o) {
   const hipStream_t s = ctx->stream;
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
@@ -523,7 +537,11 @@ StepResult solve_step(ba_ctx* ctx, double radius, const ba_options& o) {
   if (ctx->coll()) {
     ctx->allreduce(W.scal + SL_MCC_NEG, 5);  // MCC_NEG, CCOST, STEP2_P, CAND_BAD, STEP_BAD
   }
-  ctx->read_scalars();
+  return ls_iters;
+}
+
+// after ctx->read_scalars()
+StepResult step_result(ba_ctx* ctx, int ls_iters) {
   const double* h = ctx->h_scal;
   StepResult r;
   r.linear_ok = h[SL_ELIM_BAD] == 0.0 && h[SL_CHOL_BAD] == 0.0 && h[SL_STEP_BAD] == 0.0;
@@ -604,13 +622,23 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
     if (radius <= o.min_trust_region_radius) { termination = BA_CONVERGENCE; return false; }
     return true;
   };
+  // a step enqueued right behind the last accepted step's linearisation
+  // (its record arrived with the linearisation's): used if the solve goes on
+  bool have_step = false;
+  int spec_ls = 0;
   while (can_continue()) {
     const double ti = now_s();
     ++iteration;
     ba_iteration it{};
     it.iteration = iteration;
     double ts = now_s();
-    StepResult st = solve_step(ctx, radius, o);
+    int ls = spec_ls;
+    if (!have_step) {
+      ls = step_enqueue(ctx, radius, o);
+      ctx->read_scalars();
+    }
+    have_step = false;
+    StepResult st = step_result(ctx, ls);
     ctx->t_solve += now_s() - ts;
     it.linear_solver_iterations = st.ls_iters;
     const bool valid = st.linear_ok && st.mcc > 0.0;
@@ -638,13 +666,20 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
     it.relative_decrease = rel;
     if (rel > o.min_relative_decrease) {
       accept_candidate(ctx);
+      radius = std::min(o.max_trust_region_radius, radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3)));
+      decrease_factor = 2.0;
       tl = now_s();
-      L = linearize(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal);
+      linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal);
+      // speculate: the next step at the new radius, unless the loop ends on
+      // grounds already known (iteration cap, radius floor)
+      const bool spec = iteration < o.max_num_iterations && radius > o.min_trust_region_radius;
+      if (spec) spec_ls = step_enqueue(ctx, radius, o);
+      ctx->read_scalars();
+      L = lin_result(ctx);
+      have_step = spec;
       ctx->t_lin += now_s() - tl;
       if (!L.ok) { termination = BA_FAILURE; x_cost = L.cost; break; }
       x_cost = L.cost; x_norm = L.xnorm; gmax = L.gmax; gnorm = L.gnorm;
-      radius = std::min(o.max_trust_region_radius, radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3)));
-      decrease_factor = 2.0;
       last_success = true;
       S.num_successful_steps++;
       it.cost = x_cost; it.step_is_successful = 1;
@@ -1025,10 +1060,15 @@ int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double ra
     long ls_total = 0;
     HIP_OK(hipEventRecord(ctx->ev[0], ctx->stream));
     for (int i = 0; i < iters; ++i) {
+      // the solver's steady state after an accepted step: linearisation and
+      // the (speculative) next step enqueued back to back, one host read
+      linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, true);
+      const int ls = step_enqueue(ctx, radius, o);
+      ctx->read_scalars();
+      const StepResult st = step_result(ctx, ls);
       float rj = 0.0f;
-      linearize(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, &rj);
+      HIP_OK(hipEventElapsedTime(&rj, ctx->ev[2], ctx->ev[3]));
       rj_total += rj;
-      const StepResult st = solve_step(ctx, radius, o);
       ls_total += st.ls_iters;
     }
     HIP_OK(hipEventRecord(ctx->ev[1], ctx->stream));
