@@ -1425,8 +1425,9 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
 __global__ __launch_bounds__(256) void k_cam_add_diag(DevProblem P, const double* __restrict__ Hcc,
                                                       const double* __restrict__ gc, const double* __restrict__ scale_c,
                                                       const double* __restrict__ diag_c, double radius,
-                                                      double* __restrict__ S) {
+                                                      double* __restrict__ S, double* __restrict__ scal) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0) scal[SL_CHOL_BAD] = 0.0;   // the Cholesky that follows flags failures here
   if (e >= P.nvc * 27) return;
   const int v = e / 27, k = e - v * 27;
   const size_t ld = (size_t)P.ld;
@@ -1672,7 +1673,7 @@ void launch_pack_lower(const DevProblem& P, const DevWork& W, bool pack, hipStre
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
   if (P.nvc == 0) return;
   hipLaunchKernelGGL(k_cam_add_diag, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.Hcc, W.gc, W.scale_c,
-                     W.diag_c, radius, W.S);
+                     W.diag_c, radius, W.S, W.scal);
 }
 void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nc == 0) return;

@@ -414,7 +414,10 @@ void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double 
   if (time_rj) HIP_OK(hipEventRecord(ctx->ev[3], s));
   launch_point_assemble(P, W, compute_scale, min_diag, max_diag, s);
   launch_cam_assemble(P, W, s);
-  launch_reduce(W, bit(SL_COST) | bit(SL_LIN_BAD) | bit(SL_GN2_P) | bit(SL_XN2_P), bit(SL_GMAX_P), s);
+  // point-side scalars: folded here when they must be all-reduced before
+  // cam_norms, else together with the camera-side ones (one launch less)
+  const uint32_t lin_sum = bit(SL_COST) | bit(SL_LIN_BAD) | bit(SL_GN2_P) | bit(SL_XN2_P);
+  if (ctx->coll()) launch_reduce(W, lin_sum, bit(SL_GMAX_P), s);
   if (ctx->coll()) {
     ctx->allreduce(W.Hcc, 21 * (size_t)ctx->nvc);
     ctx->allreduce(W.gc, 6 * (size_t)ctx->nvc);
@@ -423,7 +426,8 @@ void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double 
     ctx->allreduce(W.scal + SL_GMAX_P, 1, ncclMax);
   }
   launch_cam_norms(P, W, compute_scale, min_diag, max_diag, s);
-  launch_reduce(W, bit(SL_GN2_C) | bit(SL_XN2_C), bit(SL_GMAX_C), s);
+  launch_reduce(W, bit(SL_GN2_C) | bit(SL_XN2_C) | (ctx->coll() ? 0u : lin_sum),
+                bit(SL_GMAX_C) | (ctx->coll() ? 0u : bit(SL_GMAX_P)), s);
   if (compute_scale) ctx->scale_valid = true;
 }
 
@@ -457,7 +461,7 @@ void reduced_solve_dense(ba_ctx* ctx, double radius) {
   launch_point_elim(P, W, radius, s);
   launch_cam_schur_diag(P, W, s);
   launch_schur_pairs(P, W, s);
-  launch_reduce(W, bit(SL_ELIM_BAD), 0, s);
+  if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
   if (ctx->coll()) {
     // only the lower triangle and the rhs row of S carry data: all-reduce
     // them packed (n(n+1)/2 + n doubles instead of (n+1) n)
@@ -487,7 +491,7 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
   launch_point_elim(P, W, radius, s);
   launch_cam_schur_diag(P, W, s, W.Sd);
   if (po.schur_jacobi) launch_pcg_dup(P, W, s);
-  launch_reduce(W, bit(SL_ELIM_BAD), 0, s);
+  if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
   const size_t tcount = (size_t)W.pcg_G * 6 * ctx->nvc;
   if (ctx->coll()) {
     ctx->allreduce(W.Sd, 27 * (size_t)ctx->nvc);
@@ -526,14 +530,15 @@ int step_enqueue(ba_ctx* ctx, double radius, const ba_options& o) {
   W.w32 = o.precision == BA_MIXED_FP32;
   if (W.w32 && !W.Wf) W.Wf = ctx->dalloc<float>(18 * (size_t)ctx->no);
   if (!W.w32 && !W.W) W.W = ctx->dalloc<double>(18 * (size_t)ctx->no);
-  HIP_OK(hipMemsetAsync(W.scal + SL_CHOL_BAD, 0, sizeof(double), s));
+  // (SL_CHOL_BAD is cleared by k_cam_add_diag / k_pcg_setup_fin, the first
+  // kernels that may set it, so no separate memset per step)
   int ls_iters = 1;
   if (o.linear_solver == BA_ITERATIVE_SCHUR) ls_iters = reduced_solve_pcg(ctx, radius, o);
   else reduced_solve_dense(ctx, radius);
   launch_cam_candidate(P, W, s);
   launch_backsub_candidate(P, W, s);
   launch_reduce(W, bit(SL_MCC_NEG) | bit(SL_CCOST) | bit(SL_STEP2_P) | bit(SL_CAND_BAD) | bit(SL_STEP_BAD) |
-                       bit(SL_STEP2_C), 0, s);
+                       bit(SL_STEP2_C) | (ctx->coll() ? 0u : bit(SL_ELIM_BAD)), 0, s);
   if (ctx->coll()) {
     ctx->allreduce(W.scal + SL_MCC_NEG, 5);  // MCC_NEG, CCOST, STEP2_P, CAND_BAD, STEP_BAD
   }
