@@ -869,9 +869,10 @@ __device__ inline void cam_acc_jr(const double* __restrict__ JR, int no, int o, 
     for (int a = 0; a < 6; ++a) acc[21 + a] += j[a] * rr[row];
   }
 }
-__global__ __launch_bounds__(256) void k_cam_assemble(DevProblem P, const double* __restrict__ JR,
-                                                      double* __restrict__ cpart, double* __restrict__ Hcc,
-                                                      double* __restrict__ gc) {
+template <int NT>
+__global__ __launch_bounds__(NT) void k_cam_assemble(DevProblem P, const double* __restrict__ JR,
+                                                     double* __restrict__ cpart, double* __restrict__ Hcc,
+                                                     double* __restrict__ gc) {
   __shared__ double lds[27 * 16];
   const int v = blockIdx.x;
   double acc[27];
@@ -1599,7 +1600,15 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
   static int split = -1;
   if (split < 0) { const char* e = getenv("BA_ASM_SPLIT"); split = e ? atoi(e) : 0; }
   const int sl = split > 0 ? std::min(split, kCamSplit) : 1;
-  hipLaunchKernelGGL(k_cam_assemble, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
+  static int nt = -1;   // diagnostics: BA_ASM_THREADS (256 / 512 / 1024)
+  if (nt < 0) { const char* e = getenv("BA_ASM_THREADS"); nt = e ? atoi(e) : 0; }
+  const int th = nt == 256 || nt == 512 || nt == 1024 ? nt : 512;   // C3: 54 us at 512, 57 at 256 / 1024
+  if (th == 1024)
+    hipLaunchKernelGGL(k_cam_assemble<1024>, dim3(P.nvc, sl), dim3(1024), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
+  else if (th == 512)
+    hipLaunchKernelGGL(k_cam_assemble<512>, dim3(P.nvc, sl), dim3(512), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
+  else
+    hipLaunchKernelGGL(k_cam_assemble<256>, dim3(P.nvc, sl), dim3(256), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
   if (sl > 1)
     hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
                        nullptr);
