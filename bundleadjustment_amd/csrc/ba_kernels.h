@@ -16,9 +16,11 @@ constexpr int kFlagWords = 4096;        // hand-off flag words (DevWork::flags)
 enum Slot {
   SL_COST = 0,      // robustified cost at x (linearisation)
   SL_LIN_BAD,       // non-finite residual / jacobian count
-  SL_GMAX_P,        // max |x - (x - g)| over point params
   SL_GN2_P,         // sum (x - (x - g))^2 over point params
   SL_XN2_P,         // sum x^2 over active point params
+  SL_GMAX_P,        // max |x - (x - g)| over point params
+  // (COST..XN2_P are contiguous and follow Hcc, gc in memory: one sum
+  // all-reduce carries all of them across ranks)
   SL_MCC_NEG,       // sum (J d)^T (r + J d / 2)  (model_cost_change = -this)
   SL_CCOST,         // robustified cost at the candidate point
   SL_STEP2_P,       // sum (x - x')^2 over point params

@@ -1688,8 +1688,13 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
 // one workgroup per row of S: row i < n holds its lower part (j <= i), row n
 // the rhs (all n entries)
 __global__ __launch_bounds__(256) void k_pack_lower(int n, int ld, double* __restrict__ S, double* __restrict__ pk,
-                                                    int pack) {
+                                                    double* __restrict__ scal, int pack) {
   const int i = blockIdx.x;
+  if (i == 0 && threadIdx.x == 0) {   // the elimination-failure count travels in the last slot
+    const size_t tail = (size_t)n * (n + 1) / 2 + n;
+    if (pack) pk[tail] = scal[SL_ELIM_BAD];
+    else scal[SL_ELIM_BAD] = pk[tail];
+  }
   const size_t off = (size_t)i * (i + 1) / 2;   // row n: n(n+1)/2, the rhs
   const int len = i < n ? i + 1 : n;
   double* row = S + (size_t)i * ld;
@@ -1700,7 +1705,7 @@ __global__ __launch_bounds__(256) void k_pack_lower(int n, int ld, double* __res
 }
 void launch_pack_lower(const DevProblem& P, const DevWork& W, bool pack, hipStream_t s) {
   if (P.n == 0) return;
-  hipLaunchKernelGGL(k_pack_lower, dim3(P.n + 1), dim3(256), 0, s, P.n, P.ld, W.S, W.Spk, pack ? 1 : 0);
+  hipLaunchKernelGGL(k_pack_lower, dim3(P.n + 1), dim3(256), 0, s, P.n, P.ld, W.S, W.Spk, W.scal, pack ? 1 : 0);
 }
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
   if (P.nvc == 0) return;

@@ -265,8 +265,14 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.diag_p = ctx->dalloc<double>(3 * (size_t)np);
   W.Linv = ctx->dalloc<double>(6 * (size_t)np);
   W.u = ctx->dalloc<double>(3 * (size_t)np);
-  W.Hcc = ctx->dalloc<double>(21 * (size_t)nvc);
-  W.gc = ctx->dalloc<double>(6 * (size_t)nvc);
+  // Hcc | gc | scalar slots | PCG state in one allocation: the camera blocks
+  // and the point-side sums cross ranks in one all-reduce
+  {
+    double* hx = ctx->dalloc<double>(27 * (size_t)nvc + kNumSlots + kPcgState);
+    W.Hcc = hx;
+    W.gc = hx + 21 * (size_t)nvc;
+    W.scal = hx + 27 * (size_t)nvc;
+  }
   W.scale_c = ctx->dalloc<double>(6 * (size_t)nvc);
   W.diag_c = ctx->dalloc<double>(6 * (size_t)nvc);
   W.delta_c = ctx->dalloc<double>(6 * (size_t)nvc);
@@ -274,7 +280,6 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.Wf = nullptr;
   W.y = ctx->dalloc<double>(std::max(ctx->n, 1));
   W.part = ctx->dalloc<double>((size_t)kNumSlots * kMaxBlocks);
-  W.scal = ctx->dalloc<double>(kNumSlots + kPcgState);
   W.cam_split = nvc > 0 ? std::min(kCamSplit, std::max(1, 2048 / nvc)) : 1;
   W.cpart = ctx->dalloc<double>((size_t)W.cam_split * 27 * std::max(nvc, 1));
 
@@ -419,10 +424,8 @@ void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double 
   const uint32_t lin_sum = bit(SL_COST) | bit(SL_LIN_BAD) | bit(SL_GN2_P) | bit(SL_XN2_P);
   if (ctx->coll()) launch_reduce(W, lin_sum, bit(SL_GMAX_P), s);
   if (ctx->coll()) {
-    ctx->allreduce(W.Hcc, 21 * (size_t)ctx->nvc);
-    ctx->allreduce(W.gc, 6 * (size_t)ctx->nvc);
-    ctx->allreduce(W.scal + SL_COST, 2);          // COST, LIN_BAD
-    ctx->allreduce(W.scal + SL_GN2_P, 2);         // GN2_P, XN2_P
+    // Hcc, gc, COST, LIN_BAD, GN2_P, XN2_P (contiguous), then the max
+    ctx->allreduce(W.Hcc, 27 * (size_t)ctx->nvc + SL_GMAX_P);
     ctx->allreduce(W.scal + SL_GMAX_P, 1, ncclMax);
   }
   launch_cam_norms(P, W, compute_scale, min_diag, max_diag, s);
@@ -465,12 +468,12 @@ void reduced_solve_dense(ba_ctx* ctx, double radius) {
   if (ctx->coll()) {
     // only the lower triangle and the rhs row of S carry data: all-reduce
     // them packed (n(n+1)/2 + n doubles instead of (n+1) n)
+    // (+1: the elimination-failure count rides along)
     const size_t npk = (size_t)ctx->n * (ctx->n + 1) / 2 + ctx->n;
-    if (!W.Spk) W.Spk = ctx->dalloc<double>(std::max<size_t>(npk, 1));
+    if (!W.Spk) W.Spk = ctx->dalloc<double>(npk + 1);
     launch_pack_lower(P, W, true, s);
-    ctx->allreduce(W.Spk, npk);
+    ctx->allreduce(W.Spk, npk + 1);
     launch_pack_lower(P, W, false, s);
-    ctx->allreduce(W.scal + SL_ELIM_BAD, 1);
   }
   launch_cam_add_diag(P, W, radius, s);
   launch_cholesky_solve2(P, W, s);
