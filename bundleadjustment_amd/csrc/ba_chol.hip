@@ -133,26 +133,27 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
 // plain stores of y_K -> every storing wave s_waitcnt vmcnt(0) -> barrier ->
 // one lane: agent release fence -> vmcnt(0) -> relaxed agent flag store;
 // consumer = one lane polls the flag (relaxed, agent, s_sleep) -> agent
-// acquire fence -> vmcnt(0) -> barrier -> plain loads.  Flags are zeroed
-// by a memset node before every launch; spins are bounded (a missing
-// producer sets the failure slot instead of hanging the GPU).
+// acquire fence -> vmcnt(0) -> barrier -> plain loads.  A flag holds the
+// epoch (launch counter, never 0) of its last publish, so no reset between
+// launches; spins are bounded (a missing producer sets the failure slot
+// instead of hanging the GPU).
 // ---------------------------------------------------------------------------
 constexpr long kSpinMax = 1L << 26;
 
-__device__ inline void flag_publish(int* flag) {
+__device__ inline void flag_publish(int* flag, int epoch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 // returns false if the spin bound was hit
-__device__ inline bool flag_wait(int* flag, int* lds_ok) {
+__device__ inline bool flag_wait(int* flag, int epoch, int* lds_ok) {
   if (threadIdx.x == 0) {
     long it = 0;
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && it < kSpinMax) {
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch && it < kSpinMax) {
       __builtin_amdgcn_s_sleep(1);
       ++it;
     }
@@ -166,7 +167,7 @@ __device__ inline bool flag_wait(int* flag, int* lds_ok) {
 
 __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A, const double* __restrict__ Lm,
                                                    int ld, int n, const double* __restrict__ Vall,
-                                                   double* __restrict__ y, int* __restrict__ flags,
+                                                   double* __restrict__ y, int* __restrict__ flags, int epoch,
                                                    double* __restrict__ scal) {
   __shared__ double zs[CB];
   __shared__ double ys[CB];
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
       const int i = h + 4 * q;
       lv[q] = (i < bJ && j < bsz) ? Lm[(size_t)(sJ + i) * lds + s0 + j] : 0.0;
     }
-    good = flag_wait(flags + J, &ok) && good;
+    good = flag_wait(flags + J, epoch, &ok) && good;
     if (tid < CB) ys[tid] = tid < bJ ? y[sJ + tid] : 0.0;
     __syncthreads();
 #pragma unroll
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
   }
   __syncthreads();
   if (tid < CB && tid < bsz) y[s0 + tid] = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
-  flag_publish(flags + K);
+  flag_publish(flags + K, epoch);
   if (tid == 0 && !good) scal[SL_CHOL_BAD] += 1.0;
 }
 
@@ -245,7 +246,7 @@ void launch_chol_split_step(double* A, double* L, int ld, int n, int k, int tc, 
 // GEMMs dominate (C4: 94).
 constexpr int kCholSplitBlocks = 24;
 
-void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, hipStream_t s) {
+void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hipStream_t s) {
   const int n = P.n;
   if (n == 0) return;
   const int nrows = n + 1;
@@ -261,8 +262,7 @@ void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, hipStream_t s
       hipLaunchKernelGGL(k_chol_step, dim3(tc, tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf, W.scal);
     }
   }
-  (void)hipMemsetAsync(W.flags, 0, sizeof(int) * T, s);
-  hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.flags, W.scal);
+  hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.flags, epoch, W.scal);
 }
 
 }  // namespace bahip

@@ -44,6 +44,7 @@ struct DevProblem {
   const int* cam_off;        // [nvc+1] CSR of observations by active variable camera
   const int2* cam_op;        // [..] (sorted observation, its point) grouped by camera
   const int* vc;             // [nc] compact variable-camera index or -1
+  const int* obs_vc;         // [no] vc of each observation's camera (one load instead of two dependent ones)
   const int* cam_of_vc;      // [nvc] camera id of a compact index
   const uint8_t* cam_fixed;  // [nc]
   const uint8_t* pt_var;     // [np] 1 = variable point with >=1 residual
@@ -76,6 +77,8 @@ struct DevWork {
   double* Vbuf;                      // [ceil(n/64)][64][64] inverses of the diagonal Cholesky blocks
   int* flags;                        // [kFlagWords] hand-off flags of the dataflow kernels (zeroed per call)
   const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}
+  const int2* eblocks; int neblocks; // lower off-diagonal blocks {I, J} with no observation pair
+  bool s_memset;                     // many empty blocks: memset S instead
   const int2* pairs;                 // observation pairs per block
   double* cpart;                     // [cam_split][nvc][27] per-slice camera sums
   int cam_split;                     // workgroups per camera of the per-camera gathers (>= 2048 in total, <= kCamSplit)
@@ -114,7 +117,12 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact = nullptr);
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
-void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, hipStream_t s);  // ba_chol.hip
+// ba_chol.hip; epoch: per-context launch counter (>= 1) tagging the
+// back substitution's hand-off flags
+void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hipStream_t s);
+// zero the lower Schur blocks no observation pair writes (the Cholesky
+// leaves its updates there)
+void launch_zero_blocks(const DevProblem& P, const DevWork& W, hipStream_t s);
 // S <-> W.Spk: lower triangle row by row (offset i(i+1)/2), then the rhs row
 void launch_pack_lower(const DevProblem& P, const DevWork& W, bool pack, hipStream_t s);
 void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s);

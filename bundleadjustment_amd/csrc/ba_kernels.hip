@@ -1133,9 +1133,8 @@ __global__ __launch_bounds__(256) void k_backsub(DevProblem P, const double* __r
     if (P.pt_var[p]) {
       double w[3] = {u[p], u[np + p], u[2 * np + p]};
       const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
-      for (int o = o0; o < o1; ++o) {
-        const int v = P.vc[P.obs_cam[o]];
-        if (v < 0) continue;
+      for (int o = o0; o < o1; ++o) {   // fixed cameras carry W_o = 0: no branch, loads stay in flight
+        const int v = max(P.obs_vc[o], 0);
         double wv[18];
         load_w18(W, (size_t)o, wv);
         const double* yc = y + 6 * v;
@@ -1706,6 +1705,19 @@ __global__ __launch_bounds__(256) void k_pack_lower(int n, int ld, double* __res
 void launch_pack_lower(const DevProblem& P, const DevWork& W, bool pack, hipStream_t s) {
   if (P.n == 0) return;
   hipLaunchKernelGGL(k_pack_lower, dim3(P.n + 1), dim3(256), 0, s, P.n, P.ld, W.S, W.Spk, W.scal, pack ? 1 : 0);
+}
+__global__ __launch_bounds__(256) void k_zero_blocks(int ld, const int2* __restrict__ eb, int nb,
+                                                     double* __restrict__ S) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nb * 36) return;
+  const int2 b = eb[e / 36];
+  const int k = e % 36;
+  S[(size_t)(6 * b.x + k / 6) * ld + 6 * b.y + k % 6] = 0.0;
+}
+void launch_zero_blocks(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  if (W.neblocks == 0) return;
+  hipLaunchKernelGGL(k_zero_blocks, dim3((W.neblocks * 36 + 255) / 256), dim3(256), 0, s, P.ld, W.eblocks, W.neblocks,
+                     W.S);
 }
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
   if (P.nvc == 0) return;

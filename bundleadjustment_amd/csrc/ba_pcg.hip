@@ -248,19 +248,18 @@ __global__ __launch_bounds__(256) void k_pcg_point(DevProblem P, const WT* __res
   if (st[PS_DONE] != 0.0) return;
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
     double w0 = 0.0, w1 = 0.0, w2 = 0.0;
-    if (P.pt_var[p]) {
-      const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
-      for (int o = o0; o < o1; ++o) {
-        const int v = P.vc[P.obs_cam[o]];
-        if (v < 0) continue;
-        double wv[18];
-        load_w18(Wm, (size_t)o, wv);
-        const double* xc = xv + 6 * v;
+    // fixed cameras and fixed points carry W_o = 0 (k_obs_w): no branches,
+    // so the loads of consecutive observations stay in flight
+    const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+    for (int o = o0; o < o1; ++o) {
+      const int v = max(P.obs_vc[o], 0);
+      double wv[18];
+      load_w18(Wm, (size_t)o, wv);
+      const double* xc = xv + 6 * v;
 #pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          const double xa = xc[a];
-          w0 += wv[a * 3] * xa; w1 += wv[a * 3 + 1] * xa; w2 += wv[a * 3 + 2] * xa;
-        }
+      for (int a = 0; a < 6; ++a) {
+        const double xa = xc[a];
+        w0 += wv[a * 3] * xa; w1 += wv[a * 3 + 1] * xa; w2 += wv[a * 3 + 2] * xa;
       }
     }
     vpt[3 * (size_t)p] = w0; vpt[3 * (size_t)p + 1] = w1; vpt[3 * (size_t)p + 2] = w2;

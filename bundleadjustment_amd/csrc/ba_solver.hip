@@ -90,6 +90,7 @@ struct ba_ctx {
   std::vector<int> h_pt_off, h_obs_cam, h_vc;
   std::vector<uint8_t> h_pt_var;
   bool have_dense = false, have_pcg = false;
+  int chol_epoch = 0;   // launches of the back substitution (hand-off flag values)
 
   // solver state
   std::vector<ba_iteration> log;
@@ -236,6 +237,11 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
     P.cam_op = ctx->upload(cam_op);
   }
   P.vc = ctx->upload(vc);
+  {
+    std::vector<int> obs_vc(no);
+    for (int o = 0; o < no; ++o) obs_vc[o] = vc[obs_cam[o]];
+    P.obs_vc = ctx->upload(obs_vc);
+  }
   P.cam_of_vc = ctx->upload(ctx->cam_of_vc);
   P.cam_fixed = ctx->upload(ctx->cam_fixed_h);
   P.pt_var = ctx->upload(pt_var);
@@ -350,6 +356,31 @@ void ensure_dense(ba_ctx* ctx) {
   W.blocks = ctx->upload(blocks);
   W.nblocks = (int)blocks.size();
   W.pairs = ctx->upload(pairs);
+  HIP_OK(hipMemsetAsync(W.flags, 0, sizeof(int) * kFlagWords, ctx->stream));
+  // S is rewritten every step (diagonal blocks, rhs and every co-observed
+  // block); the rest of the lower triangle must be re-zeroed (the Cholesky
+  // updates it in place): a list of those blocks, or a memset when they are
+  // the majority
+  {
+    const size_t nlow = (size_t)nvc * (nvc - (nvc > 0 ? 1 : 0)) / 2;
+    const size_t nfull = (size_t)std::count_if(blocks.begin(), blocks.end(), [](const int4& b) { return b.x != b.y; });
+    const size_t nempty = nlow - nfull;
+    W.s_memset = nempty > nfull || nempty > (size_t)(1 << 22);
+    W.neblocks = 0;
+    W.eblocks = nullptr;
+    if (!W.s_memset && nempty > 0) {
+      std::vector<uint8_t> used(nlow, 0);
+      auto lid = [](size_t I, size_t J) { return I * (I - 1) / 2 + J; };   // I > J
+      for (const int4& b : blocks) if (b.x != b.y) used[lid(b.x, b.y)] = 1;
+      std::vector<int2> eb;
+      eb.reserve(nempty);
+      for (int I = 1; I < nvc; ++I)
+        for (int J = 0; J < I; ++J) if (!used[lid(I, J)]) eb.push_back(make_int2(I, J));
+      W.eblocks = ctx->upload(eb);
+      W.neblocks = (int)eb.size();
+    }
+  }
+  HIP_OK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)(ctx->n + 1) * std::max(ctx->ld, 1), ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
   ctx->have_dense = true;
 }
@@ -460,7 +491,10 @@ void reduced_solve_dense(ba_ctx* ctx, double radius) {
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
   ensure_dense(ctx);
-  if (ctx->n > 0) HIP_OK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)(ctx->n + 1) * ctx->ld, s));
+  if (ctx->n > 0) {
+    if (W.s_memset) HIP_OK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)(ctx->n + 1) * ctx->ld, s));
+    else launch_zero_blocks(P, W, s);
+  }
   launch_point_elim(P, W, radius, s);
   launch_cam_schur_diag(P, W, s);
   launch_schur_pairs(P, W, s);
@@ -476,7 +510,7 @@ void reduced_solve_dense(ba_ctx* ctx, double radius) {
     launch_pack_lower(P, W, false, s);
   }
   launch_cam_add_diag(P, W, radius, s);
-  launch_cholesky_solve2(P, W, s);
+  launch_cholesky_solve2(P, W, ++ctx->chol_epoch, s);
 }
 
 // ITERATIVE_SCHUR: implicit Schur complement + PCG (ba_pcg.hip).  The host

@@ -99,7 +99,7 @@ int main(int argc, char** argv) {
     }
     CK(hipMemset(dF, 0, sizeof(int) * T));
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dA, dL, ld, n, dV, dy, dF, dS);
+    hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dA, dL, ld, n, dV, dy, dF, 1, dS);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float mb;
