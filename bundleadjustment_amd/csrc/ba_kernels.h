@@ -154,5 +154,6 @@ void launch_pose_batch(int nprob, const int* off, const double* cams_in, const f
                        hipStream_t s);
 
 int grid_for(int n);
+int pt_group_grid(int np);   // grid of the kPtLanes-lanes-per-point kernels
 
 }  // namespace bahip

@@ -46,6 +46,7 @@ int grid_for(int n) {
   if (g < 1) g = 1;
   return g > kMaxBlocks ? kMaxBlocks : g;
 }
+int pt_group_grid(int np) { return grid_for((int)std::min<long long>((long long)np * kPtLanes, 1LL << 30)); }
 
 
 // Per-camera work is split over W.cam_split <= kCamSplit workgroups (one workgroup per
@@ -1115,7 +1116,7 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
 }
 
 // ---------------------------------------------------------------------------
-// back-substitution, one thread per point (all points; fixed / unobserved
+// back-substitution, kPtLanes lanes per point (all points; fixed / unobserved
 // points keep x' = x):  y_p = L^-T (u_p - sum W_o^T y_c) ; d_p = s_p (-y_p)
 // ---------------------------------------------------------------------------
 template <typename WT>
@@ -1125,25 +1126,19 @@ __global__ __launch_bounds__(256) void k_backsub(DevProblem P, const double* __r
                                                  const double* __restrict__ Linv, const double* __restrict__ y,
                                                  const double* __restrict__ scale_p, double* __restrict__ part) {
   __shared__ double lds[2 * 16];
-  double acc[2] = {0.0, 0.0};  // step2, step_bad
+  double acc[2] = {0.0, 0.0};  // step2, step_bad (lane 0 of each point group)
   const size_t np = (size_t)P.np;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
+  const int gl = threadIdx.x & (kPtLanes - 1), gpb = blockDim.x / kPtLanes;
+  for (int p = blockIdx.x * gpb + threadIdx.x / kPtLanes; p < P.np; p += gridDim.x * gpb) {
+    // kPtLanes lanes per point (point_wtx); fixed cameras carry W_o = 0
+    double wy[3] = {0.0, 0.0, 0.0};
+    const bool var = P.pt_var[p];
+    if (var) point_wtx(W, P.obs_vc, y, P.pt_off[p], P.pt_off[p + 1], gl, wy);
+    if (gl != 0) continue;
     const double X[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
     double dX[3] = {0.0, 0.0, 0.0}, Xc[3] = {X[0], X[1], X[2]};
-    if (P.pt_var[p]) {
-      double w[3] = {u[p], u[np + p], u[2 * np + p]};
-      const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
-      for (int o = o0; o < o1; ++o) {   // fixed cameras carry W_o = 0: no branch, loads stay in flight
-        const int v = max(P.obs_vc[o], 0);
-        double wv[18];
-        load_w18(W, (size_t)o, wv);
-        const double* yc = y + 6 * v;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          const double ya = yc[a];
-          w[0] -= wv[a * 3] * ya; w[1] -= wv[a * 3 + 1] * ya; w[2] -= wv[a * 3 + 2] * ya;
-        }
-      }
+    if (var) {
+      const double w[3] = {u[p] - wy[0], u[np + p] - wy[1], u[2 * np + p] - wy[2]};
       const double i00 = Linv[0 * np + p], i10 = Linv[1 * np + p], i11 = Linv[2 * np + p];
       const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
       const double yp[3] = {i00 * w[0] + i10 * w[1] + i20 * w[2], i11 * w[1] + i21 * w[2], i22 * w[2]};
@@ -1731,10 +1726,10 @@ void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) 
 }
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (W.w32)
-    hipLaunchKernelGGL(k_backsub<float>, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p,
+    hipLaunchKernelGGL(k_backsub<float>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p,
                        W.Wf, W.u, W.Linv, W.y, W.scale_p, W.part);
   else
-    hipLaunchKernelGGL(k_backsub<double>, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p,
+    hipLaunchKernelGGL(k_backsub<double>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p,
                        W.W, W.u, W.Linv, W.y, W.scale_p, W.part);
   if (P.nc <= kLinLdsCams) {
     const int g = lds_grid(P.no);

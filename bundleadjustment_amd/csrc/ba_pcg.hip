@@ -246,23 +246,13 @@ __global__ __launch_bounds__(256) void k_pcg_point(DevProblem P, const WT* __res
                                                    const double* __restrict__ xv, double* __restrict__ vpt,
                                                    const double* __restrict__ st) {
   if (st[PS_DONE] != 0.0) return;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
-    double w0 = 0.0, w1 = 0.0, w2 = 0.0;
-    // fixed cameras and fixed points carry W_o = 0 (k_obs_w): no branches,
-    // so the loads of consecutive observations stay in flight
-    const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
-    for (int o = o0; o < o1; ++o) {
-      const int v = max(P.obs_vc[o], 0);
-      double wv[18];
-      load_w18(Wm, (size_t)o, wv);
-      const double* xc = xv + 6 * v;
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        const double xa = xc[a];
-        w0 += wv[a * 3] * xa; w1 += wv[a * 3 + 1] * xa; w2 += wv[a * 3 + 2] * xa;
-      }
-    }
-    vpt[3 * (size_t)p] = w0; vpt[3 * (size_t)p + 1] = w1; vpt[3 * (size_t)p + 2] = w2;
+  // kPtLanes lanes per point (point_wtx); fixed cameras and fixed points
+  // carry W_o = 0 (k_obs_w): no branches
+  const int gl = threadIdx.x & (kPtLanes - 1), gpb = blockDim.x / kPtLanes;
+  for (int p = blockIdx.x * gpb + threadIdx.x / kPtLanes; p < P.np; p += gridDim.x * gpb) {
+    double w[3];
+    point_wtx(Wm, P.obs_vc, xv, P.pt_off[p], P.pt_off[p + 1], gl, w);
+    if (gl < 3) vpt[3 * (size_t)p + gl] = gl == 0 ? w[0] : (gl == 1 ? w[1] : w[2]);
   }
 }
 
@@ -542,10 +532,10 @@ void launch_pcg_setup(const DevProblem& P, const DevWork& W, double radius, cons
 void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s) {
   const double* st = W.scal + kNumSlots;
   if (W.w32) {
-    hipLaunchKernelGGL(k_pcg_point<float>, dim3(grid_for(P.np)), dim3(256), 0, s, P, W.Wf, vec, W.vpt, st);
+    hipLaunchKernelGGL(k_pcg_point<float>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.Wf, vec, W.vpt, st);
     hipLaunchKernelGGL(k_pcg_cam<float>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wf, W.vpt, W.tpart, st);
   } else {
-    hipLaunchKernelGGL(k_pcg_point<double>, dim3(grid_for(P.np)), dim3(256), 0, s, P, W.W, vec, W.vpt, st);
+    hipLaunchKernelGGL(k_pcg_point<double>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.W, vec, W.vpt, st);
     hipLaunchKernelGGL(k_pcg_cam<double>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.W, W.vpt, W.tpart, st);
   }
 }

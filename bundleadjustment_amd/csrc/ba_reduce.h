@@ -88,4 +88,48 @@ __device__ inline void load_w18(const float* __restrict__ Wm, size_t o, double (
   for (int k = 0; k < 9; ++k) { const float2 t = s[k]; w[2 * k] = (double)t.x; w[2 * k + 1] = (double)t.y; }
 }
 
+// Value pair c (values 2c, 2c+1) of a run of contiguous W records.
+__device__ inline void w_pair(const double* __restrict__ base, int c, double& x, double& y) {
+  const double2 t = reinterpret_cast<const double2*>(base)[c]; x = t.x; y = t.y;
+}
+__device__ inline void w_pair(const float* __restrict__ base, int c, double& x, double& y) {
+  const float2 t = reinterpret_cast<const float2*>(base)[c]; x = (double)t.x; y = (double)t.y;
+}
+
+// Sum over the observations [o0, o1) of one point of W_o^T x_{vc(o)}
+// (3-vector), by a group of kPtLanes consecutive lanes.  Lane gl of the group
+// takes the value pairs gl, gl + kPtLanes, ... of the point's contiguous W
+// records (9 pairs per record), so one wavefront load instruction reads whole
+// 256-B (fp64) segments instead of 64 records 1.4 KB apart -- every cache
+// line is requested once.  Fixed-order xor reduction inside the group: all
+// lanes of the group get the same (deterministic) sum.
+constexpr int kPtLanes = 16;
+template <typename WT>
+__device__ inline void point_wtx(const WT* __restrict__ Wm, const int* __restrict__ obs_vc,
+                                 const double* __restrict__ xv, int o0, int o1, int gl, double (&s)[3]) {
+  const WT* base = Wm + (size_t)o0 * 18;
+  const int nch = 9 * (o1 - o0);
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int c = gl; c < nch; c += kPtLanes) {
+    double t0, t1;
+    w_pair(base, c, t0, t1);
+    const int k = c / 9, f = c - 9 * k;
+    const double* xc = xv + 6 * max(obs_vc[o0 + k], 0);   // fixed cameras: W_o = 0
+    // values i0 = 2f, i1 = 2f + 1 of W_o: row i / 3, column i % 3
+    const int i0 = 2 * f, i1 = i0 + 1;
+    const double p0 = t0 * xc[i0 / 3], p1 = t1 * xc[i1 / 3];
+    const int b0 = i0 % 3, b1 = i1 % 3;
+    s0 += b0 == 0 ? p0 : (b1 == 0 ? p1 : 0.0);
+    s1 += b0 == 1 ? p0 : (b1 == 1 ? p1 : 0.0);
+    s2 += b0 == 2 ? p0 : (b1 == 2 ? p1 : 0.0);
+  }
+#pragma unroll
+  for (int m = kPtLanes / 2; m > 0; m >>= 1) {
+    s0 += __shfl_xor(s0, m, kPtLanes);
+    s1 += __shfl_xor(s1, m, kPtLanes);
+    s2 += __shfl_xor(s2, m, kPtLanes);
+  }
+  s[0] = s0; s[1] = s1; s[2] = s2;
+}
+
 }  // namespace bahip
