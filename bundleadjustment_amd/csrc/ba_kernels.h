@@ -63,7 +63,7 @@ struct DevWork {
   double* delta_p;                   // [np][3] point step (scaled back)
   double* Hpp;   double* gp;         // [6][np], [3][np]
   double* scale_p; double* diag_p;   // [3][np]
-  double* Linv;  double* u;          // [6][np], [3][np]
+  double* Linv;  double* u;          // [6][np], [np][4] (AoS, last entry 0)
   double* Hcc;   double* gc;         // [nvc][21], [nvc][6]
   double* scale_c; double* diag_c;   // [nvc][6]
   double* delta_c;                   // [nvc][6]

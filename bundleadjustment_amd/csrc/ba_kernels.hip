@@ -981,7 +981,7 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
 #pragma unroll
       for (int k = 0; k < 6; ++k) Linv[k * np + p] = 0.0;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) u[k * np + p] = 0.0;
+      for (int k = 0; k < 4; ++k) u[4 * (size_t)p + k] = 0.0;
       continue;
     }
     double s[3], D2[3], gs[3];
@@ -1014,9 +1014,11 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
     const double i20 = -(l20 * i00 + l21 * i10) * i22;
     Linv[0 * np + p] = i00; Linv[1 * np + p] = i10; Linv[2 * np + p] = i11;
     Linv[3 * np + p] = i20; Linv[4 * np + p] = i21; Linv[5 * np + p] = i22;
-    u[0 * np + p] = i00 * gs[0];
-    u[1 * np + p] = i10 * gs[0] + i11 * gs[1];
-    u[2 * np + p] = i20 * gs[0] + i21 * gs[1] + i22 * gs[2];
+    // u AoS [np][4] (one 32-B sector per point for the camera-side gathers)
+    u[4 * (size_t)p + 0] = i00 * gs[0];
+    u[4 * (size_t)p + 1] = i10 * gs[0] + i11 * gs[1];
+    u[4 * (size_t)p + 2] = i20 * gs[0] + i21 * gs[1] + i22 * gs[2];
+    u[4 * (size_t)p + 3] = 0.0;
     acc[0] += ok ? 0.0 : 1.0;
   }
   double out[1];
@@ -1138,7 +1140,7 @@ __global__ __launch_bounds__(256) void k_backsub(DevProblem P, const double* __r
     const double X[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
     double dX[3] = {0.0, 0.0, 0.0}, Xc[3] = {X[0], X[1], X[2]};
     if (var) {
-      const double w[3] = {u[p] - wy[0], u[np + p] - wy[1], u[2 * np + p] - wy[2]};
+      const double w[3] = {u[4 * p] - wy[0], u[4 * p + 1] - wy[1], u[4 * p + 2] - wy[2]};
       const double i00 = Linv[0 * np + p], i10 = Linv[1 * np + p], i11 = Linv[2 * np + p];
       const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
       const double yp[3] = {i00 * w[0] + i10 * w[1] + i20 * w[2], i11 * w[1] + i21 * w[2], i22 * w[2]};
@@ -1329,7 +1331,6 @@ __global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const WT* 
                                                         double* __restrict__ cpart) {
   __shared__ double lds[27 * 16];
   const int v = blockIdx.x;
-  const size_t np = (size_t)P.np;
   double acc[27];
 #pragma unroll
   for (int k = 0; k < 27; ++k) acc[k] = 0.0;
@@ -1351,7 +1352,8 @@ __global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const WT* 
     const int2 op = P.cam_op[i];
     double w[18];
     load_w18(W, (size_t)op.x, w);
-    add(w, u[op.y], u[np + op.y], u[2 * np + op.y]);
+    const double2 u01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
+    add(w, u01.x, u01.y, u[4 * (size_t)op.y + 2]);
   }
   double tot[27];
   block_sum<27>(acc, lds, tot);

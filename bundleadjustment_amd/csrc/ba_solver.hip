@@ -270,7 +270,7 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.scale_p = ctx->dalloc<double>(3 * (size_t)np);
   W.diag_p = ctx->dalloc<double>(3 * (size_t)np);
   W.Linv = ctx->dalloc<double>(6 * (size_t)np);
-  W.u = ctx->dalloc<double>(3 * (size_t)np);
+  W.u = ctx->dalloc<double>(4 * (size_t)np);
   // Hcc | gc | scalar slots | PCG state in one allocation: the camera blocks
   // and the point-side sums cross ranks in one all-reduce
   {
