@@ -386,13 +386,16 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
   }
 }
 
-// X_pp = L_pp^-1 for the four 16x16 diagonal blocks, one wave each (lane
+// X_pp = L_pp^-1 for one 16x16 diagonal block p by the calling wave (lane
 // c < 16 solves L_pp x = e_c by forward substitution; L values are uniform
-// LDS broadcasts; 1/L_ii is the sweep's 1/sqrt(d_i), no divisions).
-__device__ __forceinline__ void diag_inverse16(const double (*T)[LDP], const double* rinv, double (*X)[LDP], int b) {
-  const int w = threadIdx.x >> 6, c = threadIdx.x & 15;
-  const int c0 = 16 * w;
-  if (c0 >= b || (threadIdx.x & 63) >= 16) return;
+// LDS broadcasts; 1/L_ii is the sweep's 1/sqrt(d_i), no divisions).  (A
+// recursive-doubling form, lane per entry and 8 LDS round trips, measured
+// slower in the pipeline.)
+__device__ __forceinline__ void diag_inverse16(const double (*T)[LDP], const double* rinv, double (*X)[LDP], int p,
+                                               int b) {
+  const int c = threadIdx.x & 63;
+  const int c0 = 16 * p;
+  if (c0 >= b || c >= 16) return;
   double x[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -405,14 +408,48 @@ __device__ __forceinline__ void diag_inverse16(const double (*T)[LDP], const dou
   for (int i = 0; i < 16; ++i) X[c0 + i][c0 + c] = x[i];
 }
 
+// Z_q (16x16, rows 16 zr.. of Z) = sum_{k=q}^{p-1} L_pk X_kq, by the calling wave
+__device__ __forceinline__ void inv_offdiag_sum(const double (*T)[LDP], const double (*X)[LDP], double (*Z)[LDP],
+                                                int p, int q, int zr) {
+  d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+  for (int k = q; k < p; ++k) acc = mfma_tile_n<16>(acc, T, 16 * p, 16 * k, X, 16 * k, 16 * q, 1.0);
+  tile_store(Z, zr, 0, acc);
+}
+// X_pq = -X_pp Z_q
+__device__ __forceinline__ void inv_offdiag_fin(double (*X)[LDP], const double (*Z)[LDP], int p, int q, int zr) {
+  d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+  acc = mfma_tile_n<16>(acc, X, 16 * p, 16 * p, Z, zr, 0, -1.0);
+  tile_store(X, 16 * p, 16 * q, acc);
+}
+
+// Row block p of X = L^-1 by ONE wave (diagonal block, then the blocks
+// (p, q < p) from the finished rows above); Z rows 16 zw.. are its scratch.
+// LDS operations of one wave complete in order, so no barrier inside.
+__device__ __forceinline__ void inverse_rowblock(const double (*T)[LDP], const double* rinv, double (*X)[LDP],
+                                                 double (*Z)[LDP], int p, int b, int zw) {
+  diag_inverse16(T, rinv, X, p, b);
+  for (int q = 0; q < p; ++q) {
+    inv_offdiag_sum(T, X, Z, p, q, 16 * zw);
+    inv_offdiag_fin(X, Z, p, q, 16 * zw);
+  }
+}
+
+// Factor the 64x64 block in four 16-column sub-panels (wave 0 sweeps, all
+// waves apply the trailing updates) and form X = L^-1 row block by row block:
+// row block p - 1 (wave 1) overlaps the sweep of sub-panel p, so only the
+// last row block follows the factorization (its off-diagonal sums spread
+// over waves 1..3).
 __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z)[LDP], CholLds& W, int b, int m) {
   const int w = threadIdx.x >> 6;
   __syncthreads();
   CHOL_STAMP(2);
+  int last = 0;
   for (int p = 0; p < 4; ++p) {
     const int c0 = 16 * p;
     if (c0 >= b) break;                      // uniform
+    last = p;
     if (w == 0) panel_sweep(T, W, c0, b, m);
+    else if (w == 1 && p > 0) inverse_rowblock(T, W.rsv, X, Z, p - 1, b, 1);
     CHOL_STAMP(10 + 2 * p);
     __syncthreads();
     // trailing update of the remaining sub-panels: tiles (i, s), p < s <= i
@@ -433,25 +470,12 @@ __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z
     CHOL_STAMP(11 + 2 * p);
   }
   CHOL_STAMP(3);
-  diag_inverse16(T, W.rsv, X, b);
+  // last row block: diagonal inverse (wave 0) beside the sums Z_q (wave q + 1)
+  if (w == 0) diag_inverse16(T, W.rsv, X, last, b);
+  else if (w - 1 < last) inv_offdiag_sum(T, X, Z, last, w - 1, 16 * w);
   __syncthreads();
-  // off-diagonal blocks of X = L^-1, by block distance dd
-  for (int dd = 1; dd < 4; ++dd) {
-    const int i = dd + w, pp = w;            // wave w: block (dd + w, w)
-    const bool act = i < 4 && 16 * i < b;
-    if (act) {
-      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-      for (int k = pp; k < i; ++k) acc = mfma_tile_n<16>(acc, T, 16 * i, 16 * k, X, 16 * k, 16 * pp, 1.0);
-      tile_store(Z, 16 * w, 0, acc);
-    }
-    __syncthreads();
-    if (act) {
-      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-      acc = mfma_tile_n<16>(acc, X, 16 * i, 16 * i, Z, 16 * w, 0, -1.0);
-      tile_store(X, 16 * i, 16 * pp, acc);
-    }
-    __syncthreads();
-  }
+  if (w >= 1 && w - 1 < last) inv_offdiag_fin(X, Z, last, w - 1, 16 * w);
+  __syncthreads();
   CHOL_STAMP(4);
 }
 
