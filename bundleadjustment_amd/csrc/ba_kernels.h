@@ -98,7 +98,10 @@ struct DevWork {
 };
 
 // PCG state record at scal + kNumSlots (doubles)
-enum PcgState { PS_RHO = 0, PS_Q0, PS_ALPHA, PS_NORM_B, PS_ITER, PS_DONE, PS_TERM, PS_PAD, kPcgState };
+// (PS_RHO1 / PS_Q01: the odd-iteration copies of rho and Q0 of the grid
+// kernels, whose lead block must not overwrite a value the other blocks of
+// the same launch still read)
+enum PcgState { PS_RHO = 0, PS_Q0, PS_ALPHA, PS_NORM_B, PS_ITER, PS_DONE, PS_TERM, PS_RHO1, PS_Q01, kPcgState };
 enum PcgTerm { PCG_SUCCESS = 0, PCG_NO_CONVERGENCE = 1, PCG_FAILURE = 2 };
 struct PcgOpts { double q_tolerance; int min_iter, max_iter, schur_jacobi; };
 

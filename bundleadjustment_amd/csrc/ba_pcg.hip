@@ -226,7 +226,7 @@ __global__ __launch_bounds__(64) void k_pcg_setup_fin(const double* __restrict__
   const double rz = fold_part(ppart + kMaxBlocks, nb, lds);
   const double bad = fold_part(ppart + 2 * kMaxBlocks, nb, lds);
   if (threadIdx.x == 0) {
-    st[PS_RHO] = 1.0; st[PS_Q0] = -0.0; st[PS_ALPHA] = 0.0; st[PS_NORM_B] = sqrt(bb);
+    st[PS_RHO] = st[PS_RHO1] = 1.0; st[PS_Q0] = st[PS_Q01] = -0.0; st[PS_ALPHA] = 0.0; st[PS_NORM_B] = sqrt(bb);
     st[PS_ITER] = 0.0; st[PS_DONE] = 0.0; st[PS_TERM] = PCG_NO_CONVERGENCE;
     scal[SL_CHOL_BAD] = 0.0;   // linear-solver failure flag of this step
   }
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(64) void k_pcg_setup_fin(const double* __restrict__
   // block yields a non-finite rho: stop as a failure, the step is invalid
   // either way)
   if (zero_or_inf(rz) || isnan(rz) || bad != 0.0) { pcg_stop(st, scal, PCG_FAILURE, 1); return; }
-  if (threadIdx.x == 0) st[PS_RHO] = rz;
+  if (threadIdx.x == 0) st[PS_RHO] = st[PS_RHO1] = rz;
 }
 
 // ---------------------------------------------------------------------------
@@ -403,6 +403,10 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(DevProblem P, int mo
 //             z = M r, partials x.(b + r), r.z                  (modes 0, 1, 2)
 //   k_pcg_p:  termination tests, rho', beta, p = z + beta p
 // ---------------------------------------------------------------------------
+// rho and Q0 of CG iteration it (grid kernels): parity slots
+__device__ inline int rho_slot(int it) { return (it & 1) ? PS_RHO1 : PS_RHO; }
+__device__ inline int q0_slot(int it) { return (it & 1) ? PS_Q01 : PS_Q0; }
+
 __global__ __launch_bounds__(256) void k_pcg_q(DevProblem P, int G, const double* __restrict__ Adiag,
                                                const double* __restrict__ p, double* __restrict__ q,
                                                const double* __restrict__ tpart, double* __restrict__ ppart,
@@ -439,7 +443,7 @@ __global__ __launch_bounds__(256) void k_pcg_xr(DevProblem P, int mode, int it, 
   const bool live = v < P.nvc;
   double alpha;
   if (mode != 2) {
-    const double pq = fold_part(ppart, nb, lds), rho = st[PS_RHO];
+    const double pq = fold_part(ppart, nb, lds), rho = st[rho_slot(it)];
     if (pq <= 0.0 || isinf(pq)) { if (blockIdx.x == 0) pcg_stop(st, scal, PCG_NO_CONVERGENCE, it); return; }
     alpha = rho / pq;
     if (isinf(alpha) || isnan(alpha)) { if (blockIdx.x == 0) pcg_stop(st, scal, PCG_FAILURE, it); return; }
@@ -492,7 +496,7 @@ __global__ __launch_bounds__(256) void k_pcg_p(DevProblem P, int it, PcgOpts o, 
   const int nb = gridDim.x;
   const double Q1 = -1.0 * fold_part(ppart + kMaxBlocks, nb, lds);
   const double rho_new = fold_part(ppart + 2 * kMaxBlocks, nb, lds);
-  const double Q0 = st[PS_Q0], rho = st[PS_RHO];
+  const double Q0 = st[q0_slot(it)], rho = st[rho_slot(it)];
   const double zeta = it * (Q1 - Q0) / Q1;
   const bool lead = blockIdx.x == 0;
   if (zeta < o.q_tolerance && it >= o.min_iter) { if (lead) pcg_stop(st, scal, PCG_SUCCESS, it); return; }
@@ -505,8 +509,8 @@ __global__ __launch_bounds__(256) void k_pcg_p(DevProblem P, int it, PcgOpts o, 
 #pragma unroll
     for (int a = 0; a < 6; ++a) p[6 * (size_t)v + a] = z[6 * (size_t)v + a] + beta * p[6 * (size_t)v + a];
   if (lead && threadIdx.x == 0) {
-    st[PS_RHO] = rho_new;
-    st[PS_Q0] = Q1;
+    st[rho_slot(it + 1)] = rho_new;   // the other parity: blocks of this launch still read rho, Q0
+    st[q0_slot(it + 1)] = Q1;
     st[PS_ITER] = it;
   }
 }

@@ -167,6 +167,24 @@ def test_gpu_iterative_is_deterministic(solver):
 
 
 @pytest.mark.gpu
+def test_gpu_iterative_grid_path_is_deterministic(solver):
+    """> 1024 cameras (thread-per-camera grid kernels, many workgroups per
+    CG step): repeated solves are bitwise identical.  Guards the hand-off of
+    rho / Q0 between CG iterations (the lead workgroup writes the next
+    iteration's values into the other parity slot while the other workgroups
+    of the same launch still read the current ones)."""
+    p = make_synthetic(6000, 6000, obs_per_pt=4, seed=5)
+    runs = [gpu_solve(solver, p, preconditioner_type="JACOBI", max_num_iterations=4,
+                      max_linear_solver_iterations=30, eta=1e-6) for _ in range(4)]
+    c0, x0, s0, l0 = runs[0]
+    assert any(r["linear_solver_iterations"] > 3 for r in l0[1:])
+    for c, x, s, l in runs[1:]:
+        assert s.final_cost == s0.final_cost
+        assert np.array_equal(c, c0) and np.array_equal(x, x0)
+        assert [r["linear_solver_iterations"] for r in l] == [r["linear_solver_iterations"] for r in l0]
+
+
+@pytest.mark.gpu
 def test_gpu_iterative_motion_only_and_no_cameras(solver, oracle_lib):
     """Edge cases: motion-only (no eliminated points: S = F'F + D^2) and
     structure-only (every camera fixed: empty reduced system)."""
