@@ -397,11 +397,23 @@ __device__ __forceinline__ void diag_inverse16(const double (*T)[LDP], const dou
   const int c0 = 16 * p;
   if (c0 >= b || c >= 16) return;
   double x[16];
+  // rows are read two ahead of the substitution (the LDS latency would
+  // otherwise sit on the chain of every row)
+  double Lr[3][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int k = 0; k < i; ++k) Lr[i][k] = T[c0 + i][c0 + k];
+  }
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
+    if (i + 2 < 16) {
+#pragma unroll
+      for (int k = 0; k < i + 2; ++k) Lr[(i + 2) % 3][k] = T[c0 + i + 2][c0 + k];
+    }
     double s = (i == c) ? 1.0 : 0.0;
 #pragma unroll
-    for (int k = 0; k < i; ++k) s -= T[c0 + i][c0 + k] * x[k];
+    for (int k = 0; k < i; ++k) s -= Lr[i % 3][k] * x[k];
     x[i] = (c0 + i < b) ? s * rinv[c0 + i] : 0.0;   // rinv = 1 / L_ii from the sweep
   }
 #pragma unroll
