@@ -12,7 +12,24 @@ namespace bahip {
 //   Vbuf [T][64][64] inverses of the diagonal blocks
 __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, double* __restrict__ L, int ld, int n,
                                                    int k, double* __restrict__ Vbuf, double* __restrict__ scal) {
-  const int I = blockIdx.y, J = blockIdx.x;
+  // XCD-aware tile order: workgroup b runs on XCD b % 8 (round-robin
+  // dispatch).  The tiles (1,0) and (1,1) produce A_{k+2,k+1} and
+  // A_{k+2,k+2}, the next launch's critical inputs; they take linear ids 8
+  // and 16 so they run on the critical workgroup's XCD (id 0) and the next
+  // critical workgroup stages them from that XCD's L2.
+  int I = blockIdx.y, J = blockIdx.x;
+  {
+    const int gx = gridDim.x, G = gx * gridDim.y;
+    if (k >= 0 && G > 16) {
+      const int a = gx, bb = gx + 1;                    // natural ids of (1,0), (1,1)
+      const int x = bb == 8 ? a : (bb == a ? 8 : bb);   // swap(8, a) applied to bb
+      int lin = blockIdx.y * gx + blockIdx.x;
+      lin = lin == 16 ? x : (lin == x ? 16 : lin);      // swap(16, x)
+      lin = lin == 8 ? a : (lin == a ? 8 : lin);        // swap(8, a)
+      I = lin / gx;
+      J = lin - I * gx;
+    }
+  }
   if (J > I) return;
   __shared__ double S0[CB][LDP];
   __shared__ double S1[CB][LDP];
