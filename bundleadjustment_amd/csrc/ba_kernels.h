@@ -108,7 +108,9 @@ struct PcgOpts { double q_tolerance; int min_iter, max_iter, schur_jacobi; };
 // --- launchers (all asynchronous on `s`) ---
 void launch_cam_prep(const DevProblem& P, const double* cams, double* rec, bool deriv, hipStream_t s);
 void launch_lin_prep(const DevProblem& P, const DevWork& W, hipStream_t s);   // camera tables for launch_linearize
-void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s);
+// t0 / t1: optional events stamped at the start / end of the kernel's execution
+void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s, hipEvent_t t0 = nullptr,
+                      hipEvent_t t1 = nullptr);
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
                            double max_diag, hipStream_t s);
 void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s);

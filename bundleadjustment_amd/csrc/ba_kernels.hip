@@ -18,6 +18,8 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include <hip/hip_ext.h>
+
 #include "ba_kernels.h"
 #include "ba_device.h"
 #include "ba_reduce.h"
@@ -1594,17 +1596,22 @@ void launch_lin_prep(const DevProblem& P, const DevWork& W, hipStream_t s) {
   else
     hipLaunchKernelGGL(k_cam_compact, dim3((P.nc + 255) / 256), dim3(256), 0, s, P, W.cams, W.crec);
 }
-void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s) {
+void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
+  // t0 / t1 (optional): start / stop of the kernel's execution, stamped by
+  // hipExtLaunchKernel itself (no separate event records around the launch)
   if (P.nc > 0 && P.nc <= kLinLdsCams) {
-    hipLaunchKernelGGL((k_linearize_lds_t<kLinNT, kLinRows>), dim3(lds_grid(P.no)), dim3(kLinNT), 0, s, P, W.rec,
-                       W.pts, W.JR, W.part);
+    hipExtLaunchKernelGGL((k_linearize_lds_t<kLinNT, kLinRows>), dim3(lds_grid(P.no)), dim3(kLinNT), 0, s, t0, t1, 0,
+                          P, (const double*)W.rec, (const double*)W.pts, W.JR, W.part);
     return;
   }
   if (!lin_legacy()) {
-    hipLaunchKernelGGL(k_linearize_rc, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.crec, W.pts, W.JR, W.part);
+    hipExtLaunchKernelGGL(k_linearize_rc, dim3(grid_for(P.no)), dim3(kThreads), 0, s, t0, t1, 0, P,
+                          (const double*)W.crec, (const double*)W.pts, W.JR, W.part);
     return;
   }
+  if (t0) (void)hipEventRecord(t0, s);
   hipLaunchKernelGGL(k_linearize, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.rec, W.pts, W.JR, W.part);
+  if (t1) (void)hipEventRecord(t1, s);
 }
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
                            double max_diag, hipStream_t s) {

@@ -445,9 +445,8 @@ void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double 
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
   launch_lin_prep(P, W, s);
-  if (time_rj) HIP_OK(hipEventRecord(ctx->ev[2], s));
-  launch_linearize(P, W, s);
-  if (time_rj) HIP_OK(hipEventRecord(ctx->ev[3], s));
+  // time_rj: kernel execution stamps from the launch itself (bench roofline)
+  launch_linearize(P, W, s, time_rj ? ctx->ev[2] : nullptr, time_rj ? ctx->ev[3] : nullptr);
   launch_point_assemble(P, W, compute_scale, min_diag, max_diag, s);
   launch_cam_assemble(P, W, s);
   // point-side scalars: folded here when they must be all-reduced before
