@@ -118,8 +118,10 @@ void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale,
                       hipStream_t s);
 void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);  // + W = E L^-T
 // compact != nullptr: write the diagonal blocks + rhs to compact[nvc][27]
-// instead of the dense S (ITERATIVE_SCHUR)
-void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact = nullptr);
+// instead of the dense S (ITERATIVE_SCHUR); radius > 0 (dense, single
+// rank): add s Hcc s + D^2 and s g_c in the same pass (no launch_cam_add_diag)
+void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact = nullptr,
+                           double radius = 0.0);
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
 // ba_chol.hip; epoch: per-context launch counter (>= 1) tagging the

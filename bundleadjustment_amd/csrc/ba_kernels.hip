@@ -1448,6 +1448,9 @@ __global__ __launch_bounds__(256) void k_cam_add_diag(DevProblem P, const double
                                                       const double* __restrict__ gc, const double* __restrict__ scale_c,
                                                       const double* __restrict__ diag_c, double radius,
                                                       double* __restrict__ S, double* __restrict__ scal) {
+  // no fma contraction: the fused and the exchange path (k_cam_fold +
+  // k_cam_add_diag) must round identically
+#pragma clang fp contract(off)
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e == 0) scal[SL_CHOL_BAD] = 0.0;   // the Cholesky that follows flags failures here
   if (e >= P.nvc * 27) return;
@@ -1466,6 +1469,40 @@ __global__ __launch_bounds__(256) void k_cam_add_diag(DevProblem P, const double
   } else {
     const int a = k - 21;
     S[(size_t)P.n * ld + 6 * v + a] += gc[(size_t)v * 6 + a] * scale_c[(size_t)v * 6 + a];
+  }
+}
+
+// single rank: k_cam_fold (mode 1) and k_cam_add_diag in one pass,
+//   S_cc = -sum_slices + s Hcc s + D^2 ;  b_c = -sum_slices + s g_c
+// (k_schur_pairs' duplicate-observation terms land on the diagonal after)
+__global__ __launch_bounds__(256) void k_cam_fold_diag(DevProblem P, const double* __restrict__ cpart, int nsl,
+                                                       const double* __restrict__ Hcc, const double* __restrict__ gc,
+                                                       const double* __restrict__ scale_c,
+                                                       const double* __restrict__ diag_c, double radius,
+                                                       double* __restrict__ S, double* __restrict__ scal) {
+  // no fma contraction: the fused and the exchange path (k_cam_fold +
+  // k_cam_add_diag) must round identically
+#pragma clang fp contract(off)
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0) scal[SL_CHOL_BAD] = 0.0;   // the Cholesky that follows flags failures here
+  if (e >= P.nvc * 27) return;
+  const int v = e / 27, k = e - v * 27;
+  double acc = 0.0;
+  for (int sl = 0; sl < nsl; ++sl) acc += cpart[((size_t)sl * P.nvc + v) * 27 + k];
+  const size_t ld = (size_t)P.ld;
+  if (k < 21) {
+    int a = 0;
+    while ((a + 1) * (a + 2) / 2 <= k) ++a;
+    const int b = k - a * (a + 1) / 2;
+    double h = Hcc[(size_t)v * 21 + k] * scale_c[(size_t)v * 6 + a] * scale_c[(size_t)v * 6 + b];
+    if (a == b) {
+      const double D = sqrt(diag_c[(size_t)v * 6 + a] / radius);
+      h += D * D;
+    }
+    S[(size_t)(6 * v + a) * ld + 6 * v + b] = -acc + h;
+  } else {
+    const int a = k - 21;
+    S[(size_t)P.n * ld + 6 * v + a] = -acc + gc[(size_t)v * 6 + a] * scale_c[(size_t)v * 6 + a];
   }
 }
 
@@ -1661,7 +1698,7 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
       hipLaunchKernelGGL((k_obs_w<false, double>), dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.W);
   }
 }
-void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact) {
+void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact, double radius) {
   if (P.nvc == 0) return;
   static int dsplit = -1;   // diagnostics: BA_DIAG_SPLIT overrides the slice count
   if (dsplit < 0) { const char* e = getenv("BA_DIAG_SPLIT"); dsplit = e ? atoi(e) : 0; }
@@ -1670,6 +1707,11 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
     hipLaunchKernelGGL(k_cam_schur_diag<float>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wf, W.u, W.S, W.cpart);
   else
     hipLaunchKernelGGL(k_cam_schur_diag<double>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.W, W.u, W.S, W.cpart);
+  if (!compact && radius > 0.0) {   // single rank: the LM diagonal goes in with the fold
+    hipLaunchKernelGGL(k_cam_fold_diag, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, W.Hcc,
+                       W.gc, W.scale_c, W.diag_c, radius, W.S, W.scal);
+    return;
+  }
   hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl,
                      compact ? 2 : 1, W.Hcc,
                      W.gc, compact ? compact : W.S);

@@ -91,6 +91,10 @@ struct ba_ctx {
   std::vector<uint8_t> h_pt_var;
   bool have_dense = false, have_pcg = false;
   int chol_epoch = 0;   // launches of the back substitution (hand-off flag values)
+  // scalar slots whose fold a linearisation left to the step enqueued right
+  // behind it (single rank: one k_reduce for both records)
+  uint32_t pend_sum = 0, pend_max = 0;
+  bool dup_diag = false;   // the dense pair list has diagonal blocks (duplicate observations)
 
   // solver state
   std::vector<ba_iteration> log;
@@ -355,6 +359,10 @@ void ensure_dense(ba_ctx* ctx) {
   W.Spk = nullptr;
   W.blocks = ctx->upload(blocks);
   W.nblocks = (int)blocks.size();
+  // diagonal pair blocks (a point observed twice by one camera) update the
+  // S diagonal after the fold: the LM diagonal is then added after them
+  // (separate k_cam_add_diag), in the order the exchange path uses
+  ctx->dup_diag = std::any_of(blocks.begin(), blocks.end(), [](const int4& b) { return b.x == b.y; });
   W.pairs = ctx->upload(pairs);
   HIP_OK(hipMemsetAsync(W.flags, 0, sizeof(int) * kFlagWords, ctx->stream));
   // S is rewritten every step (diagonal blocks, rhs and every co-observed
@@ -440,7 +448,10 @@ constexpr uint32_t bit(int s) { return 1u << s; }
 // enqueues the next trust-region step right behind an accepted step's
 // linearisation and reads both records with one host sync (the step is
 // wasted only when the new gradient ends the solve).
-void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double max_diag, bool time_rj = false) {
+// defer_reduce: a step_enqueue follows before the next read_scalars and
+// folds this linearisation's scalars with its own (single rank only)
+void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double max_diag, bool time_rj = false,
+                       bool defer_reduce = false) {
   const hipStream_t s = ctx->stream;
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
@@ -459,8 +470,14 @@ void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double 
     ctx->allreduce(W.scal + SL_GMAX_P, 1, ncclMax);
   }
   launch_cam_norms(P, W, compute_scale, min_diag, max_diag, s);
-  launch_reduce(W, bit(SL_GN2_C) | bit(SL_XN2_C) | (ctx->coll() ? 0u : lin_sum),
-                bit(SL_GMAX_C) | (ctx->coll() ? 0u : bit(SL_GMAX_P)), s);
+  const uint32_t sum_mask = bit(SL_GN2_C) | bit(SL_XN2_C) | (ctx->coll() ? 0u : lin_sum);
+  const uint32_t max_mask = bit(SL_GMAX_C) | (ctx->coll() ? 0u : bit(SL_GMAX_P));
+  if (defer_reduce && !ctx->coll()) {
+    ctx->pend_sum |= sum_mask;
+    ctx->pend_max |= max_mask;
+  } else {
+    launch_reduce(W, sum_mask, max_mask, s);
+  }
   if (compute_scale) ctx->scale_valid = true;
 }
 
@@ -495,7 +512,10 @@ void reduced_solve_dense(ba_ctx* ctx, double radius) {
     else launch_zero_blocks(P, W, s);
   }
   launch_point_elim(P, W, radius, s);
-  launch_cam_schur_diag(P, W, s);
+  // single rank, no diagonal pair blocks: the LM diagonal goes in with the
+  // fold (same operation order as the exchange path's, bitwise)
+  const bool fused_diag = !ctx->coll() && !ctx->dup_diag;
+  launch_cam_schur_diag(P, W, s, nullptr, fused_diag ? radius : 0.0);
   launch_schur_pairs(P, W, s);
   if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
   if (ctx->coll()) {
@@ -508,7 +528,7 @@ void reduced_solve_dense(ba_ctx* ctx, double radius) {
     ctx->allreduce(W.Spk, npk + 1);
     launch_pack_lower(P, W, false, s);
   }
-  launch_cam_add_diag(P, W, radius, s);
+  if (!fused_diag) launch_cam_add_diag(P, W, radius, s);   // (after the exchange)
   launch_cholesky_solve2(P, W, ++ctx->chol_epoch, s);
 }
 
@@ -574,7 +594,8 @@ int step_enqueue(ba_ctx* ctx, double radius, const ba_options& o) {
   launch_cam_candidate(P, W, s);
   launch_backsub_candidate(P, W, s);
   launch_reduce(W, bit(SL_MCC_NEG) | bit(SL_CCOST) | bit(SL_STEP2_P) | bit(SL_CAND_BAD) | bit(SL_STEP_BAD) |
-                       bit(SL_STEP2_C) | (ctx->coll() ? 0u : bit(SL_ELIM_BAD)), 0, s);
+                       bit(SL_STEP2_C) | (ctx->coll() ? 0u : bit(SL_ELIM_BAD)) | ctx->pend_sum, ctx->pend_max, s);
+  ctx->pend_sum = ctx->pend_max = 0;
   if (ctx->coll()) {
     ctx->allreduce(W.scal + SL_MCC_NEG, 5);  // MCC_NEG, CCOST, STEP2_P, CAND_BAD, STEP_BAD
   }
@@ -666,6 +687,7 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
   // a step enqueued right behind the last accepted step's linearisation
   // (its record arrived with the linearisation's): used if the solve goes on
   bool have_step = false;
+  ctx->pend_sum = ctx->pend_max = 0;   // (an earlier solve may have thrown between the two enqueues)
   int spec_ls = 0;
   while (can_continue()) {
     const double ti = now_s();
@@ -710,10 +732,10 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
       radius = std::min(o.max_trust_region_radius, radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3)));
       decrease_factor = 2.0;
       tl = now_s();
-      linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal);
       // speculate: the next step at the new radius, unless the loop ends on
       // grounds already known (iteration cap, radius floor)
       const bool spec = iteration < o.max_num_iterations && radius > o.min_trust_region_radius;
+      linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, false, spec);
       if (spec) spec_ls = step_enqueue(ctx, radius, o);
       ctx->read_scalars();
       L = lin_result(ctx);
@@ -1096,6 +1118,7 @@ int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double ra
     ba_options o;
     if (opt) o = *opt; else ba_default_options(&o);
     check_options(o);
+    ctx->pend_sum = ctx->pend_max = 0;
     if (!ctx->scale_valid) linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
     double rj_total = 0.0;
     long ls_total = 0;
@@ -1103,7 +1126,7 @@ int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double ra
     for (int i = 0; i < iters; ++i) {
       // the solver's steady state after an accepted step: linearisation and
       // the (speculative) next step enqueued back to back, one host read
-      linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, true);
+      linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, true, true);
       const int ls = step_enqueue(ctx, radius, o);
       ctx->read_scalars();
       const StepResult st = step_result(ctx, ls);
