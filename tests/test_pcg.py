@@ -253,13 +253,19 @@ def test_gpu_mixed_fp32_requires_iterative(solver):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("solver_type", ["DENSE_SCHUR", "ITERATIVE_SCHUR"])
-def test_gpu_exchange_path_on_one_rank(solver_type, monkeypatch):
+@pytest.mark.parametrize("dups", [False, True])
+def test_gpu_exchange_path_on_one_rank(solver_type, dups, monkeypatch):
     """The multi-GPU exchange path (RCCL all-reduces of the camera blocks,
     the packed lower triangle of S, the CG matvec slices, the step scalars)
     forced on a one-rank communicator, where every all-reduce is the identity:
-    results are bitwise those of the communicator-free solve."""
+    results are bitwise those of the communicator-free solve.  Without
+    duplicate observations the single-rank dense path adds the LM diagonal
+    inside the Schur-diagonal fold; with them (diagonal pair blocks) after
+    k_schur_pairs, as the exchange path does."""
     from bundleadjustment_amd import Solver
     p = make_config("c2", scale=0.2)
+    if dups:
+        p = with_duplicate_observations(p)
     opts = Options(linear_solver_type=solver_type, preconditioner_type="SCHUR_JACOBI", max_num_iterations=6)
     with Solver(0) as s0:
         s0.set_problem(p)
