@@ -90,6 +90,7 @@ struct DevWork {
   double* Minv;                      // [nvc][36] preconditioner block inverses
   double* pb; double* pr; double* pz; double* pp; double* pq;   // [n] CG vectors
   double* vpt;                       // [np][3] point-side products of one implicit matvec
+  double* tobs;                      // [no][6] per-observation products W_o v_p (null: gather W in the camera pass)
   double* tpart;                     // [pcg_G][nvc][6] camera-side slices of one implicit matvec
   double* ppart;                     // [3][kMaxBlocks] per-block partials of the camera-side kernels
   int pcg_G;

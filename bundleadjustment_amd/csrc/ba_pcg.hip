@@ -288,6 +288,55 @@ __global__ __launch_bounds__(256) void k_pcg_cam(DevProblem P, const WT* __restr
   }
 }
 
+// Matvec with per-observation products (point-major, coalesced): the point
+// pass also forms t_o = W_o v_p for the point's observations (the group has
+// just read those W records: the re-read hits the caches) and stores them
+// contiguously [no][6]; the camera pass then gathers 48-B t_o instead of the
+// 144-B W_o and the point's v_p.
+template <typename WT>
+__global__ __launch_bounds__(256) void k_pcg_point_t(DevProblem P, const WT* __restrict__ Wm,
+                                                     const double* __restrict__ xv, double* __restrict__ tobs,
+                                                     const double* __restrict__ st) {
+  if (st[PS_DONE] != 0.0) return;
+  const int gl = threadIdx.x & (kPtLanes - 1), gpb = blockDim.x / kPtLanes;
+  for (int p = blockIdx.x * gpb + threadIdx.x / kPtLanes; p < P.np; p += gridDim.x * gpb) {
+    const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+    double w[3];
+    point_wtx(Wm, P.obs_vc, xv, o0, o1, gl, w);
+    for (int o = o0 + gl; o < o1; o += kPtLanes) {
+      double wv[18];
+      load_w18(Wm, (size_t)o, wv);
+      double2* d = reinterpret_cast<double2*>(tobs + 6 * (size_t)o);
+#pragma unroll
+      for (int a = 0; a < 6; a += 2)
+        d[a / 2] = make_double2(wv[a * 3] * w[0] + wv[a * 3 + 1] * w[1] + wv[a * 3 + 2] * w[2],
+                                wv[a * 3 + 3] * w[0] + wv[a * 3 + 4] * w[1] + wv[a * 3 + 5] * w[2]);
+    }
+  }
+}
+__global__ __launch_bounds__(256) void k_pcg_cam_t(DevProblem P, const double* __restrict__ tobs,
+                                                   double* __restrict__ tpart, const double* __restrict__ st) {
+  if (st[PS_DONE] != 0.0) return;
+  __shared__ double lds[6 * 16];
+  const int v = blockIdx.x, g = blockIdx.y, G = gridDim.y;
+  const int a0 = P.cam_off[v], a1 = P.cam_off[v + 1];
+  const int len = (a1 - a0 + G - 1) / G;
+  const int i0 = min(a1, a0 + g * len), i1 = min(a1, i0 + len);
+  double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const double2* t = reinterpret_cast<const double2*>(tobs + 6 * (size_t)P.cam_op[i].x);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { const double2 x = t[k]; acc[2 * k] += x.x; acc[2 * k + 1] += x.y; }
+  }
+  double tot[6];
+  block_sum<6>(acc, lds, tot);
+  if (threadIdx.x == 0) {
+    double* dst = tpart + ((size_t)g * P.nvc + v) * 6;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) dst[a] = tot[a];
+  }
+}
+
 // S y for camera v from its A block and the matvec slices of y
 __device__ inline void schur_row(const double* __restrict__ Adiag, const double* __restrict__ tpart, int G, int nvc,
                                  int v, const double (&y)[6], double (&out)[6]) {
@@ -535,6 +584,14 @@ void launch_pcg_setup(const DevProblem& P, const DevWork& W, double radius, cons
 }
 void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s) {
   const double* st = W.scal + kNumSlots;
+  if (W.tobs) {
+    if (W.w32)
+      hipLaunchKernelGGL(k_pcg_point_t<float>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.Wf, vec, W.tobs, st);
+    else
+      hipLaunchKernelGGL(k_pcg_point_t<double>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.W, vec, W.tobs, st);
+    hipLaunchKernelGGL(k_pcg_cam_t, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
+    return;
+  }
   if (W.w32) {
     hipLaunchKernelGGL(k_pcg_point<float>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.Wf, vec, W.vpt, st);
     hipLaunchKernelGGL(k_pcg_cam<float>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wf, W.vpt, W.tpart, st);

@@ -95,6 +95,7 @@ struct ba_ctx {
   // behind it (single rank: one k_reduce for both records)
   uint32_t pend_sum = 0, pend_max = 0;
   bool dup_diag = false;   // the dense pair list has diagonal blocks (duplicate observations)
+  double* tobs_buf = nullptr;   // [no][6] ITERATIVE_SCHUR per-observation products (allocated on first use)
 
   // solver state
   std::vector<ba_iteration> log;
@@ -120,6 +121,7 @@ struct ba_ctx {
     for (void* p : allocs) (void)hipFree(p);
     allocs.clear();
     have_problem = have_dense = have_pcg = false;
+    tobs_buf = nullptr;
     scale_valid = false;
     log.clear();
   }
@@ -542,6 +544,19 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
   ensure_pcg(ctx);
+  {
+    // per-observation products (k_pcg_point_t / k_pcg_cam_t) when the fp64 W
+    // outgrows the 256-MiB Infinity Cache: the camera pass then gathers 48 B
+    // per observation from HBM instead of 144 + 24 B (C5 shard +2.7 %; below
+    // the cache, e.g. C3 and the C4 shard, the W gathers hit it and the extra
+    // pass loses ~0.7 %).  BA_PCG_T=0 / 1 (diagnostics) forces it off / on.
+    const char* fe = getenv("BA_PCG_T");   // (read per solve: tests switch it)
+    const int force = fe ? atoi(fe) : -1;
+    const bool big = 144.0 * (double)ctx->no > 256.0 * 1024 * 1024;
+    const bool use_t = force >= 0 ? force != 0 : (!W.w32 && big);
+    if (use_t && !ctx->tobs_buf) ctx->tobs_buf = ctx->dalloc<double>(6 * (size_t)std::max(ctx->no, 1));
+    W.tobs = use_t ? ctx->tobs_buf : nullptr;
+  }
   PcgOpts po{o.eta, o.min_linear_solver_iterations, std::max(1, o.max_linear_solver_iterations),
              o.preconditioner_type == BA_SCHUR_JACOBI ? 1 : 0};
   launch_point_elim(P, W, radius, s);

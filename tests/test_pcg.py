@@ -120,7 +120,13 @@ def compare(glog, olog, n, rtol=1e-9):
 @pytest.mark.gpu
 @pytest.mark.parametrize("pc", PRECONDITIONERS)
 @pytest.mark.parametrize("cfg,scale", [("c1", 1.0), ("c2", 0.2), ("c3", 0.01)])
-def test_gpu_iterative_matches_oracle(solver, oracle_lib, cfg, scale, pc):
+@pytest.mark.parametrize("pcg_t", ["auto", "1"])
+def test_gpu_iterative_matches_oracle(solver, oracle_lib, cfg, scale, pc, pcg_t, monkeypatch):
+    """pcg_t = "1" forces the per-observation product matvec (k_pcg_point_t /
+    k_pcg_cam_t), which the solver picks by itself only when the fp64 W
+    outgrows the Infinity Cache (C5-sized shards)."""
+    if pcg_t != "auto":
+        monkeypatch.setenv("BA_PCG_T", pcg_t)
     p = make_config(cfg, scale=scale)
     _, _, so, olog = oracle_lib.solve(p, oracle_opts(oracle_lib, pc, max_num_iterations=8))
     _, _, sg, glog = gpu_solve(solver, p, preconditioner_type=pc, max_num_iterations=8)
