@@ -190,8 +190,11 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
   __shared__ double ys[CB];
   __shared__ double part[4][CB];
   __shared__ int ok;
-  const int K = blockIdx.x, tid = threadIdx.x;
+  // producers first: workgroup K waits on every J > K, and low block ids are
+  // dispatched first, so block b takes K = T - 1 - b (if the grid cannot be
+  // resident at once, the waiting consumers are then the ones still queued)
   const int T = (n + CB - 1) / CB;
+  const int K = T - 1 - (int)blockIdx.x, tid = threadIdx.x;
   const int s0 = K * CB, bsz = min(CB, n - s0);
   const size_t lds = (size_t)ld;
   // thread (j = tid & 63, h = tid >> 6) sums rows i = h, h + 4, ... of a tile

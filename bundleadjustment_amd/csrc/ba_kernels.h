@@ -94,6 +94,7 @@ struct DevWork {
   double* tpart;                     // [pcg_G][nvc][6] camera-side slices of one implicit matvec
   double* ppart;                     // [3][kMaxBlocks] per-block partials of the camera-side kernels
   int pcg_G;
+  bool pcg_folded;                   // exchange path: slices folded into slice 0 before the all-reduce
   const int* dup_off;                // [nvc+1] per variable camera: pairs of observations of one
   const int2* dup_pairs;             //   point by that camera (Schur-Jacobi diagonal cross terms)
 };
@@ -140,6 +141,8 @@ void launch_pcg_setup(const DevProblem& P, const DevWork& W, double radius, cons
 void launch_pcg_dup(const DevProblem& P, const DevWork& W, hipStream_t s);   // Schur-Jacobi cross terms
 // one implicit matvec (point pass + camera pass) of vec into W.tpart
 void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s);
+// exchange path: fold the matvec's camera slices into slice 0 (one 6 nvc all-reduce)
+void launch_pcg_tfold(const DevProblem& P, const DevWork& W, hipStream_t s);
 // mode 0: full CG iteration; 1: up to the x update; 2: residual reset from W.tpart = matvec(x)
 void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, const PcgOpts& o, hipStream_t s);
 

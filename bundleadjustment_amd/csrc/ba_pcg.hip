@@ -337,15 +337,33 @@ __global__ __launch_bounds__(256) void k_pcg_cam_t(DevProblem P, const double* _
   }
 }
 
+// Sum of the G matvec slices of camera v entry a, in slice order (the same
+// order in k_pcg_tfold, so the exchange path, which folds the slices before
+// its all-reduce, rounds exactly like the single-rank path)
+__device__ inline double slice_sum(const double* __restrict__ tpart, int G, int nvc, int v, int a) {
+  double t = tpart[(size_t)v * 6 + a];
+  for (int g = 1; g < G; ++g) t += tpart[((size_t)g * nvc + v) * 6 + a];
+  return t;
+}
+
 // S y for camera v from its A block and the matvec slices of y
 __device__ inline void schur_row(const double* __restrict__ Adiag, const double* __restrict__ tpart, int G, int nvc,
                                  int v, const double (&y)[6], double (&out)[6]) {
   sym6_mul(Adiag + (size_t)v * 21, y, out);
-  for (int g = 0; g < G; ++g) {
-    const double* t = tpart + ((size_t)g * nvc + v) * 6;
 #pragma unroll
-    for (int a = 0; a < 6; ++a) out[a] -= t[a];
-  }
+  for (int a = 0; a < 6; ++a) out[a] -= slice_sum(tpart, G, nvc, v, a);
+}
+
+// Exchange path: fold the G slices into slice 0 before the all-reduce, so
+// every CG iteration sends one 6 nvc vector (not G of them).
+__global__ __launch_bounds__(256) void k_pcg_tfold(int nvc, int G, double* __restrict__ tpart,
+                                                   const double* __restrict__ st) {
+  if (st[PS_DONE] != 0.0) return;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 6 * nvc) return;
+  const int v = e / 6, a = e - 6 * v;
+  const double t = slice_sum(tpart, G, nvc, v, a);
+  tpart[e] = t;
 }
 
 // ---------------------------------------------------------------------------
@@ -600,17 +618,24 @@ void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec,
     hipLaunchKernelGGL(k_pcg_cam<double>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.W, W.vpt, W.tpart, st);
   }
 }
+void launch_pcg_tfold(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  if (W.pcg_G <= 1 || P.nvc == 0) return;
+  hipLaunchKernelGGL(k_pcg_tfold, dim3((6 * P.nvc + 255) / 256), dim3(256), 0, s, P.nvc, W.pcg_G, W.tpart,
+                     W.scal + kNumSlots);
+}
 void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, const PcgOpts& o, hipStream_t s) {
+  // (after launch_pcg_tfold the slices are folded into slice 0: G = 1)
+  const int G = W.pcg_folded ? 1 : W.pcg_G;
   if (P.nvc <= kPcgThreads) {   // one workgroup: one launch per CG iteration
-    hipLaunchKernelGGL(k_pcg_update, dim3(1), dim3(kPcgThreads), 0, s, P, mode, it, o, W.pcg_G, W.Adiag, W.Minv,
+    hipLaunchKernelGGL(k_pcg_update, dim3(1), dim3(kPcgThreads), 0, s, P, mode, it, o, G, W.Adiag, W.Minv,
                        W.pb, W.y, W.pr, W.pz, W.pp, W.pq, W.tpart, W.scal);
     return;
   }
   const int nb = (P.nvc + 255) / 256;
   const double* st = W.scal + kNumSlots;
   if (mode != 2)
-    hipLaunchKernelGGL(k_pcg_q, dim3(nb), dim3(256), 0, s, P, W.pcg_G, W.Adiag, W.pp, W.pq, W.tpart, W.ppart, st);
-  hipLaunchKernelGGL(k_pcg_xr, dim3(nb), dim3(256), 0, s, P, mode, it, W.pcg_G, W.Adiag, W.Minv, W.pb, W.y, W.pr,
+    hipLaunchKernelGGL(k_pcg_q, dim3(nb), dim3(256), 0, s, P, G, W.Adiag, W.pp, W.pq, W.tpart, W.ppart, st);
+  hipLaunchKernelGGL(k_pcg_xr, dim3(nb), dim3(256), 0, s, P, mode, it, G, W.Adiag, W.Minv, W.pb, W.y, W.pr,
                      W.pz, W.pp, W.pq, W.tpart, W.ppart, W.scal);
   if (mode != 1) hipLaunchKernelGGL(k_pcg_p, dim3(nb), dim3(256), 0, s, P, it, o, W.pz, W.pp, W.ppart, W.scal);
 }

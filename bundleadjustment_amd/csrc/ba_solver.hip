@@ -96,6 +96,7 @@ struct ba_ctx {
   uint32_t pend_sum = 0, pend_max = 0;
   bool dup_diag = false;   // the dense pair list has diagonal blocks (duplicate observations)
   double* tobs_buf = nullptr;   // [no][6] ITERATIVE_SCHUR per-observation products (allocated on first use)
+  int max_no = 0;               // largest observation count over the ranks (collective matvec-path choice)
 
   // solver state
   std::vector<ba_iteration> log;
@@ -109,6 +110,13 @@ struct ba_ctx {
     HIP_OK(hipMalloc(&p, count * sizeof(T)));
     allocs.push_back(p);
     return static_cast<T*>(p);
+  }
+  void dfree(void* p) {
+    if (!p) return;
+    auto it = std::find(allocs.begin(), allocs.end(), p);
+    if (it != allocs.end()) allocs.erase(it);
+    if (stream) (void)hipStreamSynchronize(stream);
+    (void)hipFree(p);
   }
   template <typename T>
   T* upload(const std::vector<T>& v) {
@@ -200,6 +208,21 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
     HIP_OK(hipMemcpyAsync(cam_used.data(), d, nc, hipMemcpyDeviceToHost, ctx->stream));
     HIP_OK(hipStreamSynchronize(ctx->stream));
     (void)hipFree(d);
+  }
+  ctx->max_no = no;
+  if (ctx->coll()) {
+    // every rank takes the same matvec path (ITERATIVE_SCHUR), chosen from the
+    // largest shard: identical kernels and rounding on every rank
+    double* d = nullptr;
+    const double h = (double)no;
+    HIP_OK(hipMalloc(&d, sizeof(double)));
+    HIP_OK(hipMemcpyAsync(d, &h, sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    NCCL_OK(ncclAllReduce(d, d, 1, ncclDouble, ncclMax, ctx->comm, ctx->stream));
+    double r = 0.0;
+    HIP_OK(hipMemcpyAsync(&r, d, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(d);
+    ctx->max_no = (int)r;
   }
   ctx->cam_of_vc.clear();
   for (int c = 0; c < nc; ++c)
@@ -552,9 +575,11 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
     // pass loses ~0.7 %).  BA_PCG_T=0 / 1 (diagnostics) forces it off / on.
     const char* fe = getenv("BA_PCG_T");   // (read per solve: tests switch it)
     const int force = fe ? atoi(fe) : -1;
-    const bool big = 144.0 * (double)ctx->no > 256.0 * 1024 * 1024;
+    // (decided from the largest rank's shard: every rank runs the same path)
+    const bool big = 144.0 * (double)ctx->max_no > 256.0 * 1024 * 1024;
     const bool use_t = force >= 0 ? force != 0 : (!W.w32 && big);
     if (use_t && !ctx->tobs_buf) ctx->tobs_buf = ctx->dalloc<double>(6 * (size_t)std::max(ctx->no, 1));
+    if (!use_t && ctx->tobs_buf) { ctx->dfree(ctx->tobs_buf); ctx->tobs_buf = nullptr; }   // 48 B/obs back
     W.tobs = use_t ? ctx->tobs_buf : nullptr;
   }
   PcgOpts po{o.eta, o.min_linear_solver_iterations, std::max(1, o.max_linear_solver_iterations),
@@ -563,7 +588,11 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
   launch_cam_schur_diag(P, W, s, W.Sd);
   if (po.schur_jacobi) launch_pcg_dup(P, W, s);
   if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
-  const size_t tcount = (size_t)W.pcg_G * 6 * ctx->nvc;
+  // exchange path: one 6 nvc vector per matvec crosses the ranks (the
+  // camera slices are folded first, in the order the single-rank update
+  // folds them, so both paths round identically)
+  const size_t tcount = (size_t)6 * ctx->nvc;
+  W.pcg_folded = ctx->coll();
   if (ctx->coll()) {
     ctx->allreduce(W.Sd, 27 * (size_t)ctx->nvc);
     ctx->allreduce(W.scal + SL_ELIM_BAD, 1);
@@ -575,11 +604,11 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
     for (int k = 0; k < batch && it < po.max_iter; ++k) {
       ++it;
       launch_pcg_matvec(P, W, W.pp, s);
-      if (ctx->coll()) ctx->allreduce(W.tpart, tcount);
+      if (ctx->coll()) { launch_pcg_tfold(P, W, s); ctx->allreduce(W.tpart, tcount); }
       if (it % 10 == 0) {   // ceres residual_reset_period: r = b - S x
         launch_pcg_update(P, W, 1, it, po, s);
         launch_pcg_matvec(P, W, W.y, s);
-        if (ctx->coll()) ctx->allreduce(W.tpart, tcount);
+        if (ctx->coll()) { launch_pcg_tfold(P, W, s); ctx->allreduce(W.tpart, tcount); }
         launch_pcg_update(P, W, 2, it, po, s);
       } else {
         launch_pcg_update(P, W, 0, it, po, s);
@@ -926,6 +955,9 @@ int ba_set_params(ba_ctx* ctx, const double* cams, const double* pts) {
     if (!ctx->have_problem) throw BaError{BA_ERR_NO_PROBLEM, "no problem"};
     if (cams && ctx->nc) HIP_OK(hipMemcpy(ctx->W.cams, cams, 6 * sizeof(double) * ctx->nc, hipMemcpyHostToDevice));
     if (pts && ctx->np) HIP_OK(hipMemcpy(ctx->W.pts, pts, 3 * sizeof(double) * ctx->np, hipMemcpyHostToDevice));
+    // the Jacobi scaling belongs to the old parameters (ceres evaluates it at
+    // the start of every solve): ba_bench_iterations must recompute it
+    ctx->scale_valid = false;
   });
 }
 
