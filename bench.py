@@ -8,13 +8,23 @@ factor the reduced camera system, back-substitute, evaluate the model cost
 change and the candidate cost — the accept/reject scalars read back to the
 host exactly as the solver does.  Inputs are resident in HBM before timing.
 
-Workload (N=1): BASELINE.json configs[2] = synthetic BAL-style 200 cams x
-100k points x 1M observations ("C3", the single-GPU config the metric is
-quoted on).  N>1: weak scaling — every rank owns a disjoint 100k-point shard
-(1M observations) of one scene with the same 200 replicated cameras; the
-camera-side system is all-reduced over RCCL each iteration.
+Workloads (--workload):
+  c3   (default) BASELINE.json configs[2], synthetic BAL-style 200 cams x 100k
+       points x 1M observations per GPU, DENSE_SCHUR (the reference's solver).
+       N = 1 is the single-GPU roofline config the metric is quoted on; N > 1
+       is weak scaling: every rank owns a disjoint 100k-point shard of one
+       scene with the same 200 replicated cameras, the camera-side system is
+       all-reduced over RCCL each iteration.
+  c4   BASELINE.json configs[3]: ONE fixed 1k cams x 1M points x 10M
+       observations problem split over the N ranks (strong scaling; the
+       points come in 8 fixed blocks of 125k, rank r holds blocks r, r + N,
+       ...), ITERATIVE_SCHUR (implicit Schur, no 6000^2 system per rank; one
+       6C all-reduce per CG iteration).
+  c5   BASELINE.json configs[4]: 10k cams x 10M points x 100M observations
+       (8 blocks of 1.25M points), ITERATIVE_SCHUR with the W blocks stored in
+       fp32 (BA_MIXED_FP32).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c4|c5]
        (N>1 via python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
 """
 from __future__ import annotations
@@ -80,20 +90,76 @@ def rendezvous_uid(rank: int, world: int, timeout_s: float = 300.0) -> bytes:
     raise RuntimeError(f"rank {rank}: no RCCL id at {path} after {timeout_s:.0f} s")
 
 
+STRONG = {   # global problems of the strong-scaling workloads: 8 fixed point blocks
+    "c4": dict(blocks=8, solver="ITERATIVE_SCHUR", precision="FP64"),
+    "c5": dict(blocks=8, solver="ITERATIVE_SCHUR", precision="MIXED_FP32"),
+}
+
+
+def strong_shard(cfg: str, rank: int, world: int):
+    """Rank `rank`'s part of the fixed global problem of `cfg`: point blocks
+    b = rank, rank + world, ... of 8 (block b drawn with point_seed
+    seed + 7919 b over the shared cameras), concatenated.  The union over the
+    ranks is the same problem for every N that divides 8."""
+    import numpy as np
+    from bundleadjustment_amd import make_config
+    from bundleadjustment_amd.problem import CONFIG_INDEX
+    nb = STRONG[cfg]["blocks"]
+    seed = 0xBA5E0000 + CONFIG_INDEX[cfg]
+    parts = [make_config(cfg, scale=1.0 / nb, point_seed=seed + 7919 * b) for b in range(rank, nb, world)]
+    p = parts[0].copy()
+    off = np.cumsum([0] + [q.n_pts for q in parts])
+    p.pts = np.concatenate([q.pts for q in parts])
+    p.obs_cam = np.concatenate([q.obs_cam for q in parts])
+    p.obs_pt = np.concatenate([q.obs_pt + o for q, o in zip(parts, off)]).astype(np.int32)
+    p.obs_uv = np.concatenate([q.obs_uv for q in parts])
+    p.gt_pts = None
+    return p.normalized()
+
+
+def cpu_baseline_leg(problem, cfg: str, target_s: float):
+    """The oracle (C++ restatement of Ceres LM + DENSE_SCHUR, not Ceres) on the
+    host cores: at the reference's num_threads = 4 (Optimizer.cpp:88) and at
+    every thread this process may use (OMP_NUM_THREADS, else os.cpu_count())."""
+    import oracle
+    oracle.build()
+    nproc = os.cpu_count() or 1
+    allowed = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or nproc
+
+    def leg(threads):
+        oracle.set_threads(threads)
+        first = oracle.bench_seconds_per_iteration(problem, 1)
+        iters = max(1, min(30, int(target_s / max(first, 1e-3))))
+        return oracle.bench_seconds_per_iteration(problem, iters), iters
+
+    spi4, it4 = leg(min(4, allowed))
+    spia, ita = leg(allowed) if allowed != min(4, allowed) else (spi4, it4)
+    return {"value": round(problem.n_obs / spia / 1e6, 3), "unit": "M-obs/s", "cores": allowed, "kind": "port",
+            "sample": f"full {cfg} problem ({problem.n_obs} obs), {ita} LM iterations of the C++ CPU restatement of "
+                      f"Ceres LM+DENSE_SCHUR (oracle/), not Ceres; {spia:.3f} s/iteration at {allowed} threads "
+                      f"(host nproc {nproc})",
+            "nproc": nproc,
+            "reference_threads": {"threads": min(4, allowed), "value": round(problem.n_obs / spi4 / 1e6, 3),
+                                  "s_per_iteration": round(spi4, 4), "iterations": it4,
+                                  "note": "num_threads = 4 as configureSolver sets it (Optimizer.cpp:88)"}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c3")
-    ap.add_argument("--scale", type=float, default=1.0, help="point-count scale of the config (per-GPU shard size)")
+    ap.add_argument("--workload", default="c3", choices=["c3", "c4", "c5"],
+                    help="c3: weak scaling of configs[2] (default); c4 / c5: strong scaling of configs[3] / [4]")
+    ap.add_argument("--config", default=None, help="weak mode: per-GPU config (default c3)")
+    ap.add_argument("--scale", type=float, default=1.0, help="weak mode: point-count scale of the per-GPU shard")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of each CPU-baseline sample")
     ap.add_argument("--comm", action="store_true", help="use an RCCL communicator even at one rank (tests)")
-    ap.add_argument("--linear-solver", default="dense", choices=["dense", "iterative"],
+    ap.add_argument("--linear-solver", default=None, choices=["dense", "iterative"],
                     help="DENSE_SCHUR (the reference's) or ITERATIVE_SCHUR (implicit Schur + PCG)")
     ap.add_argument("--preconditioner", default="SCHUR_JACOBI", choices=["JACOBI", "SCHUR_JACOBI"])
-    ap.add_argument("--precision", default="FP64", choices=["FP64", "MIXED_FP32"],
+    ap.add_argument("--precision", default=None, choices=["FP64", "MIXED_FP32"],
                     help="MIXED_FP32: fp32 storage of the per-observation Schur blocks (iterative only)")
     args = ap.parse_args()
 
@@ -103,15 +169,19 @@ def main():
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
-    import numpy as np
-
     from bundleadjustment_amd import Options, Solver, make_config
     from bundleadjustment_amd.problem import CONFIG_INDEX, CONFIGS
 
-    cfg = args.config
+    strong = args.workload in STRONG
+    cfg = args.workload if strong else (args.config or "c3")
+    if strong and 8 % world != 0:
+        raise SystemExit(f"--workload {cfg}: the 8 point blocks need a rank count dividing 8 (got {world})")
     seed = 0xBA5E0000 + CONFIG_INDEX[cfg]
     t = time.time()
-    problem = make_config(cfg, scale=args.scale, point_seed=None if rank == 0 else seed + 7919 * rank)
+    if strong:
+        problem = strong_shard(cfg, rank, world)
+    else:
+        problem = make_config(cfg, scale=args.scale, point_seed=None if rank == 0 else seed + 7919 * rank)
     log(f"[rank {rank}] problem {cfg}: {problem.n_cams} cams x {problem.n_pts} pts x {problem.n_obs} obs "
         f"(generated in {time.time() - t:.1f}s)")
 
@@ -130,9 +200,11 @@ def main():
         if use_comm:
             solver.barrier()
 
-    iterative = args.linear_solver == "iterative"
+    lin = args.linear_solver or ("iterative" if strong else "dense")
+    precision = args.precision or (STRONG[cfg]["precision"] if strong else "FP64")
+    iterative = lin == "iterative"
     opts = Options(linear_solver_type="ITERATIVE_SCHUR" if iterative else "DENSE_SCHUR",
-                   preconditioner_type=args.preconditioner, precision=args.precision)
+                   preconditioner_type=args.preconditioner, precision=precision)
     # warmup (first call also computes the Jacobi scaling, as LM iteration 0 does)
     solver.bench_iterations(max(1, args.warmup), options=opts)
     barrier()
@@ -144,34 +216,44 @@ def main():
     dt = time.perf_counter() - t0
 
     n_obs_total = problem.n_obs
+    n_pts_total = problem.n_pts
     if use_comm:   # max over ranks of the timed region, total observations
         dt = float(solver.allreduce_host([dt], "max")[0])
-        n_obs_total = int(solver.allreduce_host([float(problem.n_obs)], "sum")[0])
+        tot = solver.allreduce_host([float(problem.n_obs), float(problem.n_pts)], "sum")
+        n_obs_total, n_pts_total = int(tot[0]), int(tot[1])
 
     # algorithmic bytes of the residual+Jacobian kernel per launch:
     #   176 B/obs (uv 8 + two int32 idx 8 + r 16 + J 144) + 24 B/point + 48 B/camera
     B_rj = 176.0 * problem.n_obs + 24.0 * problem.n_pts + 48.0 * problem.n_cams
     achieved = B_rj / (ms_rj * 1e-3) / 1e9
-    traffic = pmc_traffic(cfg)
+    traffic = pmc_traffic(cfg) if not strong and args.scale == 1.0 else None
     roofline = {"kernel": "k_linearize (residual+Jacobian)", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "algorithmic_bytes": B_rj, "avg_launch_ms": round(ms_rj, 5)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import oracle
-        oracle.build()
-        threads = min(16, os.cpu_count() or 1)
-        oracle.set_threads(threads)
-        first = oracle.bench_seconds_per_iteration(problem, 1)
-        iters = max(1, min(30, int(args.cpu_seconds / max(first, 1e-3))))
-        spi = oracle.bench_seconds_per_iteration(problem, iters)
-        cpu = {"value": round(problem.n_obs / spi / 1e6, 3), "unit": "M-obs/s", "cores": threads, "kind": "port",
-               "sample": f"full {cfg} problem ({problem.n_obs} obs), {iters} LM iterations of the C++ CPU "
-                         f"restatement of Ceres LM+DENSE_SCHUR (oracle/), not Ceres; {spi:.3f} s/iteration"}
+        if problem.n_obs <= 20_000_000:
+            cpu = cpu_baseline_leg(problem, cfg, args.cpu_seconds)
+        else:   # one CPU LM iteration alone would take minutes: no bounded sample
+            log(f"cpu baseline skipped: {problem.n_obs} observations")
 
     if rank == 0:
         ms_step = dt / args.steps * 1e3
+        mixed = precision == "MIXED_FP32"
+        if strong:
+            workload = (f"{cfg.upper()}: one {CONFIGS[cfg]['n_cams']} cams x {n_pts_total} pts x {n_obs_total} obs "
+                        f"problem split over {world} GPU(s) (8 fixed point blocks, cameras replicated)")
+        else:
+            workload = (f"{cfg.upper()}: {CONFIGS[cfg]['n_cams']} cams x {problem.n_pts} pts x {problem.n_obs} obs "
+                        f"per GPU (point-sharded, cameras replicated)")
+        if iterative:
+            exchange = "one folded 6C-double vector per CG iteration + the camera blocks per LM iteration"
+            solver_s = (f"LM + ITERATIVE_SCHUR (implicit Schur, PCG {args.preconditioner}, {cg_iters:.1f} CG "
+                        f"iterations per LM iteration), fp64" + (", W blocks stored fp32" if mixed else ""))
+        else:
+            exchange = "the packed reduced camera system (n(n+1)/2 + n doubles) + the camera blocks per LM iteration"
+            solver_s = "LM + DENSE_SCHUR, fp64"
         out = {
             "metric": "M-obs/s per LM iteration (residual+Jacobian+Schur)",
             "value": round(n_obs_total * args.steps / dt / 1e6, 2),
@@ -181,20 +263,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f64 (W blocks f32)" if mixed else "f64",
             "data": "synthetic (BAL-style, SURVEY.md §8d generator, seeded)",
-            "config": {"workload": f"{cfg.upper()}: {CONFIGS[cfg]['n_cams']} cams x {problem.n_pts} pts x "
-                                   f"{problem.n_obs} obs per GPU (point-sharded, cameras replicated)",
+            "config": {"workload": workload,
                        "global_obs": n_obs_total,
-                       "solver": (f"LM + ITERATIVE_SCHUR (implicit Schur, PCG {args.preconditioner}, "
-                                  f"{cg_iters:.1f} CG iterations per LM iteration), fp64"
-                                  + (", W blocks stored fp32" if args.precision == "MIXED_FP32" else "")) if iterative
-                       else "LM + DENSE_SCHUR, fp64",
-                       "parallelism": f"points sharded x{world}, RCCL all-reduce of "
-                                      + ("camera blocks + one 6C vector per CG iteration" if iterative
-                                         else "camera system")},
+                       "solver": solver_s,
+                       "parallelism": f"points sharded x{world}, RCCL all-reduce of {exchange}"},
             "device_ms_per_step": round(ms_dev, 4),
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -683,7 +683,8 @@ struct Options {
   int preconditioner_type;            // 0 JACOBI (ceres default), 1 SCHUR_JACOBI
   int max_linear_solver_iterations;   // 500
   int min_linear_solver_iterations;   // 0
-  int precision;                      // 0 fp64 (the oracle always computes in fp64)
+  int precision;                      // 0 fp64; 1 MIXED_FP32: the Schur blocks W stored in float
+                                      // (iterative_schur_solve_w below); 2 the W form in fp64 (test hook)
   double eta;                         // 1e-1 (LM forcing sequence -> CG q_tolerance)
 };
 enum { LS_DENSE_SCHUR = 0, LS_ITERATIVE_SCHUR = 1 };
@@ -740,6 +741,81 @@ static bool llt_inverse(const double* A, int n, double* Ai) {   // Eigen selfadj
 }
 
 static inline bool zero_or_inf(double x) { return x == 0.0 || std::isinf(x); }   // ceres IsZeroOrInfinity
+
+// ceres ConjugateGradientsSolver::Solve (x = 0 start, r_tolerance = -1,
+// q_tolerance = eta, residual reset every 10 iterations) on S x = rhs with
+// the block-diagonal preconditioner Minv (nf blocks 6x6).  Returns false on
+// LINEAR_SOLVER_FAILURE (NO_CONVERGENCE keeps the iterate).
+template <class SchurMul>
+static bool pcg_solve(const std::vector<double>& rhs, SchurMul&& schur_mul, const std::vector<double>& Minv, int nf,
+                      const Options& opt, std::vector<double>& x, int* cg_iterations) {
+  const int n = 6 * nf;
+  auto precond = [&](const std::vector<double>& r, std::vector<double>& z) {
+    z.assign(n, 0.0);
+    for (int f = 0; f < nf; ++f)
+      for (int a = 0; a < 6; ++a) {
+        double v = 0;
+        for (int c = 0; c < 6; ++c) v += Minv[(size_t)f * 36 + a * 6 + c] * r[6 * f + c];
+        z[6 * f + a] = v;
+      }
+  };
+  auto dot = [](const std::vector<double>& u, const std::vector<double>& v) {
+    double d = 0;
+    for (size_t i = 0; i < u.size(); ++i) d += u[i] * v[i];
+    return d;
+  };
+  x.assign(n, 0.0);
+  bool failure = false;
+  if (nf > 0) {
+    const double norm_b = std::sqrt(dot(rhs, rhs));
+    if (norm_b != 0.0) {
+      const double r_tolerance = -1.0, q_tolerance = opt.eta;
+      const double tol_r = r_tolerance * norm_b;
+      std::vector<double> r = rhs, p(n), z, q, tmp;   // x = 0: r = b - A x = b
+      double norm_r = std::sqrt(dot(r, r));
+      if (!(opt.min_linear_solver_iterations == 0 && norm_r <= tol_r)) {
+        double rho = 1.0;
+        std::vector<double> bpr(n);
+        for (int i = 0; i < n; ++i) bpr[i] = rhs[i] + r[i];
+        double Q0 = -1.0 * dot(x, bpr);
+        for (int it = 1;; ++it) {
+          *cg_iterations = it;
+          precond(r, z);
+          const double last_rho = rho;
+          rho = dot(r, z);
+          if (zero_or_inf(rho)) { failure = true; break; }
+          if (it == 1) p = z;
+          else {
+            const double beta = rho / last_rho;
+            if (zero_or_inf(beta)) { failure = true; break; }
+            for (int i = 0; i < n; ++i) p[i] = z[i] + beta * p[i];
+          }
+          schur_mul(p, q);
+          const double pq = dot(p, q);
+          if (pq <= 0 || std::isinf(pq)) break;   // LINEAR_SOLVER_NO_CONVERGENCE: x is still used
+          const double alpha = rho / pq;
+          if (std::isinf(alpha)) { failure = true; break; }
+          for (int i = 0; i < n; ++i) x[i] = x[i] + alpha * p[i];
+          if (it % 10 == 0) {   // residual_reset_period
+            schur_mul(x, tmp);
+            for (int i = 0; i < n; ++i) r[i] = rhs[i] - tmp[i];
+          } else {
+            for (int i = 0; i < n; ++i) r[i] = r[i] - alpha * q[i];
+          }
+          for (int i = 0; i < n; ++i) bpr[i] = rhs[i] + r[i];
+          const double Q1 = -1.0 * dot(x, bpr);
+          const double zeta = it * (Q1 - Q0) / Q1;
+          if (zeta < q_tolerance && it >= opt.min_linear_solver_iterations) break;
+          Q0 = Q1;
+          norm_r = std::sqrt(dot(r, r));
+          if (norm_r <= tol_r && it >= opt.min_linear_solver_iterations) break;
+          if (it >= opt.max_linear_solver_iterations) break;
+        }
+      }
+    }
+  }
+  return !failure;
+}
 
 static bool iterative_schur_solve(const Problem& P, const Schur& S, const std::vector<Lin>& L,
                                   const std::vector<double>& s, const std::vector<double>& D, const Options& opt,
@@ -896,72 +972,8 @@ static bool iterative_schur_solve(const Problem& P, const Schur& S, const std::v
       if (!llt_inverse(&blk[(size_t)f * 36], 6, &Minv[(size_t)f * 36]))
         for (int k = 0; k < 36; ++k) Minv[(size_t)f * 36 + k] = std::numeric_limits<double>::quiet_NaN();
   }
-  auto precond = [&](const std::vector<double>& r, std::vector<double>& z) {
-    z.assign(n, 0.0);
-    for (int f = 0; f < nf; ++f)
-      for (int a = 0; a < 6; ++a) {
-        double v = 0;
-        for (int c = 0; c < 6; ++c) v += Minv[(size_t)f * 36 + a * 6 + c] * r[6 * f + c];
-        z[6 * f + a] = v;
-      }
-  };
-  auto dot = [](const std::vector<double>& u, const std::vector<double>& v) {
-    double d = 0;
-    for (size_t i = 0; i < u.size(); ++i) d += u[i] * v[i];
-    return d;
-  };
-  // ConjugateGradientsSolver::Solve
   std::vector<double> x(n, 0.0);
-  bool failure = false;
-  if (nf > 0) {
-    const double norm_b = std::sqrt(dot(rhs, rhs));
-    if (norm_b != 0.0) {
-      const double r_tolerance = -1.0, q_tolerance = opt.eta;
-      const double tol_r = r_tolerance * norm_b;
-      std::vector<double> r = rhs, p(n), z, q, tmp;   // x = 0: r = b - A x = b
-      double norm_r = std::sqrt(dot(r, r));
-      if (!(opt.min_linear_solver_iterations == 0 && norm_r <= tol_r)) {
-        double rho = 1.0;
-        std::vector<double> bpr(n);
-        for (int i = 0; i < n; ++i) bpr[i] = rhs[i] + r[i];
-        double Q0 = -1.0 * dot(x, bpr);
-        for (int it = 1;; ++it) {
-          *cg_iterations = it;
-          precond(r, z);
-          const double last_rho = rho;
-          rho = dot(r, z);
-          if (zero_or_inf(rho)) { failure = true; break; }
-          if (it == 1) p = z;
-          else {
-            const double beta = rho / last_rho;
-            if (zero_or_inf(beta)) { failure = true; break; }
-            for (int i = 0; i < n; ++i) p[i] = z[i] + beta * p[i];
-          }
-          schur_mul(p, q);
-          const double pq = dot(p, q);
-          if (pq <= 0 || std::isinf(pq)) break;   // LINEAR_SOLVER_NO_CONVERGENCE: x is still used
-          const double alpha = rho / pq;
-          if (std::isinf(alpha)) { failure = true; break; }
-          for (int i = 0; i < n; ++i) x[i] = x[i] + alpha * p[i];
-          if (it % 10 == 0) {   // residual_reset_period
-            schur_mul(x, tmp);
-            for (int i = 0; i < n; ++i) r[i] = rhs[i] - tmp[i];
-          } else {
-            for (int i = 0; i < n; ++i) r[i] = r[i] - alpha * q[i];
-          }
-          for (int i = 0; i < n; ++i) bpr[i] = rhs[i] + r[i];
-          const double Q1 = -1.0 * dot(x, bpr);
-          const double zeta = it * (Q1 - Q0) / Q1;
-          if (zeta < q_tolerance && it >= opt.min_linear_solver_iterations) break;
-          Q0 = Q1;
-          norm_r = std::sqrt(dot(r, r));
-          if (norm_r <= tol_r && it >= opt.min_linear_solver_iterations) break;
-          if (it >= opt.max_linear_solver_iterations) break;
-        }
-      }
-    }
-  }
-  if (failure) return false;
+  if (!pcg_solve(rhs, schur_mul, Minv, nf, opt, x, cg_iterations)) return false;
   // BackSubstitute
   {
     std::vector<double> rows = zr, te = ze, ye = ze;
@@ -977,10 +989,196 @@ static bool iterative_schur_solve(const Problem& P, const Schur& S, const std::v
   return true;
 }
 
+// ----------------------------------------------------------------------------
+// ITERATIVE_SCHUR with the per-observation Schur blocks stored in fp32
+// (BA_MIXED_FP32 of include/ba_hip.h; SURVEY.md §8a-a7 / §8c: C5 "fp32
+// mixed-precision Schur").  Restated from the definition, not from the
+// device code: with L_p L_p^T = E_p'E_p + D_e^2 (lower Cholesky) and
+//   W_o = F_o' E_o L_p^-T      (6x3, o = a residual with a variable camera
+//                               and a variable point),
+// the implicit reduced system of iterative_schur_solve is
+//   S x = (F'F + D_f^2) x - sum_p W_p W_p' x,   rhs = F'b - sum_o W_o u_p,
+//   u_p = L_p^-1 E_p' b,   back substitution y_e = L_p^-T (u_p - W_p' x),
+// and MIXED_FP32 means every W_o entry is rounded to float once and used
+// in that form in the matvec, the rhs, the SCHUR_JACOBI blocks and the back
+// substitution; all sums, the CG vectors and everything else stay fp64.
+// The CG (termination rules, preconditioner inversion) is the one above.
+// ----------------------------------------------------------------------------
+static bool iterative_schur_solve_w(const Problem& P, const Schur& S, const std::vector<Lin>& L,
+                                    const std::vector<double>& s, const std::vector<double>& D, const Options& opt,
+                                    std::vector<double>& y, int* cg_iterations) {
+  const int nf = S.nf, n = 6 * nf, npv = (int)P.var_pts.size();
+  y.assign(P.ncols, 0.0);
+  *cg_iterations = 0;
+  auto rnd = [&](double v) { return opt.precision == 1 ? (double)(float)v : v; };
+  auto scJc = [&](int o, double* Jc) {
+    const int cc = P.cam_col[P.obs_cam[o]];
+    for (int i = 0; i < 2; ++i) for (int k = 0; k < 6; ++k) Jc[i * 6 + k] = L[o].Jc[i * 6 + k] * s[cc + k];
+  };
+  auto scJp = [&](int o, double* Jp) {
+    const int pc = P.pt_col[P.obs_pt[o]];
+    for (int i = 0; i < 2; ++i) for (int k = 0; k < 3; ++k) Jp[i * 3 + k] = L[o].Jp[i * 3 + k] * s[pc + k];
+  };
+  auto has_f = [&](int o) { return P.type[o] == RB_ANGLE || P.type[o] == RB_POSE_ONLY; };
+  // per variable point: L_p^-1 (lower, row-major 3x3) and u_p
+  std::vector<double> Linv((size_t)npv * 9, 0.0), u((size_t)npv * 3, 0.0);
+  std::vector<int> vp(P.np, -1);
+  for (int i = 0; i < npv; ++i) vp[P.var_pts[i]] = i;
+  for (int ip = 0; ip < npv; ++ip) {
+    const int pc = P.pt_col[P.var_pts[ip]];
+    double A[9] = {0}, g[3] = {0};
+    for (int o : S.pt_obs[ip]) {
+      double Jp[6];
+      scJp(o, Jp);
+      for (int a = 0; a < 3; ++a) {
+        g[a] += Jp[a] * L[o].r[0] + Jp[3 + a] * L[o].r[1];
+        for (int b = 0; b < 3; ++b) A[a * 3 + b] += Jp[a] * Jp[b] + Jp[3 + a] * Jp[3 + b];
+      }
+    }
+    for (int a = 0; a < 3; ++a) A[a * 3 + a] += D[pc + a] * D[pc + a];
+    if (!(A[0] > 0.0)) return false;
+    const double l00 = std::sqrt(A[0]), l10 = A[3] / l00, l20 = A[6] / l00;
+    const double d11 = A[4] - l10 * l10;
+    if (!(d11 > 0.0)) return false;
+    const double l11 = std::sqrt(d11), l21 = (A[7] - l20 * l10) / l11;
+    const double d22 = A[8] - l20 * l20 - l21 * l21;
+    if (!(d22 > 0.0)) return false;
+    const double l22 = std::sqrt(d22);
+    double* M = &Linv[(size_t)ip * 9];   // inverse of [[l00,0,0],[l10,l11,0],[l20,l21,l22]]
+    M[0] = 1.0 / l00;
+    M[4] = 1.0 / l11;
+    M[8] = 1.0 / l22;
+    M[3] = -l10 * M[0] / l11;
+    M[7] = -l21 * M[4] / l22;
+    M[6] = -(l20 * M[0] + l21 * M[3]) / l22;
+    for (int a = 0; a < 3; ++a) u[(size_t)ip * 3 + a] = M[a * 3] * g[0] + M[a * 3 + 1] * g[1] + M[a * 3 + 2] * g[2];
+  }
+  // W_o (stored rounded) for residuals with a variable camera and point
+  std::vector<double> W((size_t)P.no * 18, 0.0);
+  for (int o = 0; o < P.no; ++o) {
+    if (P.type[o] != RB_ANGLE) continue;
+    const int ip = vp[P.obs_pt[o]];
+    double Jc[12], Jp[6];
+    scJc(o, Jc);
+    scJp(o, Jp);
+    const double* M = &Linv[(size_t)ip * 9];
+    for (int a = 0; a < 6; ++a) {
+      const double e[3] = {Jc[a] * Jp[0] + Jc[6 + a] * Jp[3], Jc[a] * Jp[1] + Jc[6 + a] * Jp[4],
+                           Jc[a] * Jp[2] + Jc[6 + a] * Jp[5]};
+      for (int k = 0; k < 3; ++k)   // (e L^-T)_k = sum_t e_t M[k][t]
+        W[(size_t)o * 18 + a * 3 + k] = rnd(e[0] * M[k * 3] + e[1] * M[k * 3 + 1] + e[2] * M[k * 3 + 2]);
+    }
+  }
+  // A_f = F'F + D_f^2 per camera block, rhs
+  std::vector<double> Af((size_t)nf * 36, 0.0), rhs(n, 0.0);
+  for (int o = 0; o < P.no; ++o) {
+    if (!has_f(o)) continue;
+    double Jc[12];
+    scJc(o, Jc);
+    const int f = S.fidx[P.obs_cam[o]];
+    double* B = &Af[(size_t)f * 36];
+    for (int a = 0; a < 6; ++a) {
+      rhs[6 * f + a] += Jc[a] * L[o].r[0] + Jc[6 + a] * L[o].r[1];
+      for (int c = 0; c < 6; ++c) B[a * 6 + c] += Jc[a] * Jc[c] + Jc[6 + a] * Jc[6 + c];
+    }
+  }
+  for (int c : P.var_cams) {
+    const int f = S.fidx[c], cc = P.cam_col[c];
+    for (int a = 0; a < 6; ++a) Af[(size_t)f * 36 + a * 7] += D[cc + a] * D[cc + a];
+  }
+  for (int o = 0; o < P.no; ++o) {
+    if (P.type[o] != RB_ANGLE) continue;
+    const int f = S.fidx[P.obs_cam[o]], ip = vp[P.obs_pt[o]];
+    const double* w = &W[(size_t)o * 18];
+    const double* up = &u[(size_t)ip * 3];
+    for (int a = 0; a < 6; ++a) rhs[6 * f + a] -= w[a * 3] * up[0] + w[a * 3 + 1] * up[1] + w[a * 3 + 2] * up[2];
+  }
+  auto schur_mul = [&](const std::vector<double>& x, std::vector<double>& out) {
+    std::vector<double> v((size_t)npv * 3, 0.0);
+    for (int o = 0; o < P.no; ++o) {
+      if (P.type[o] != RB_ANGLE) continue;
+      const double* w = &W[(size_t)o * 18];
+      const double* xc = &x[6 * S.fidx[P.obs_cam[o]]];
+      double* vv = &v[(size_t)vp[P.obs_pt[o]] * 3];
+      for (int k = 0; k < 3; ++k)
+        for (int a = 0; a < 6; ++a) vv[k] += w[a * 3 + k] * xc[a];
+    }
+    out.assign(n, 0.0);
+    for (int f = 0; f < nf; ++f)
+      for (int a = 0; a < 6; ++a) {
+        double t = 0.0;
+        for (int c = 0; c < 6; ++c) t += Af[(size_t)f * 36 + a * 6 + c] * x[6 * f + c];
+        out[6 * f + a] = t;
+      }
+    for (int o = 0; o < P.no; ++o) {
+      if (P.type[o] != RB_ANGLE) continue;
+      const double* w = &W[(size_t)o * 18];
+      const double* vv = &v[(size_t)vp[P.obs_pt[o]] * 3];
+      double* oc = &out[6 * S.fidx[P.obs_cam[o]]];
+      for (int a = 0; a < 6; ++a) oc[a] -= w[a * 3] * vv[0] + w[a * 3 + 1] * vv[1] + w[a * 3 + 2] * vv[2];
+    }
+  };
+  // preconditioner blocks: A_f (JACOBI) or A_f - sum_p B_pf B_pf' (SCHUR_JACOBI),
+  // B_pf = sum of the W_o of point p seen by camera f
+  std::vector<double> Minv((size_t)nf * 36, 0.0);
+  {
+    std::vector<double> blk(Af);
+    if (opt.preconditioner_type == PC_SCHUR_JACOBI) {
+      std::vector<int> fl;
+      std::vector<double> Bs;
+      for (int ip = 0; ip < npv; ++ip) {
+        fl.clear();
+        Bs.clear();
+        for (int o : S.pt_obs[ip]) {
+          if (P.type[o] != RB_ANGLE) continue;
+          const int f = S.fidx[P.obs_cam[o]];
+          int slot = -1;
+          for (size_t q = 0; q < fl.size(); ++q) if (fl[q] == f) slot = (int)q;
+          if (slot < 0) { slot = (int)fl.size(); fl.push_back(f); Bs.resize(Bs.size() + 18, 0.0); }
+          for (int k = 0; k < 18; ++k) Bs[(size_t)slot * 18 + k] += W[(size_t)o * 18 + k];
+        }
+        for (size_t q = 0; q < fl.size(); ++q) {
+          const double* B = &Bs[q * 18];
+          double* M = &blk[(size_t)fl[q] * 36];
+          for (int a = 0; a < 6; ++a)
+            for (int c = 0; c < 6; ++c) M[a * 6 + c] -= B[a * 3] * B[c * 3] + B[a * 3 + 1] * B[c * 3 + 1] + B[a * 3 + 2] * B[c * 3 + 2];
+        }
+      }
+    }
+    for (int f = 0; f < nf; ++f)
+      if (!llt_inverse(&blk[(size_t)f * 36], 6, &Minv[(size_t)f * 36]))
+        for (int k = 0; k < 36; ++k) Minv[(size_t)f * 36 + k] = std::numeric_limits<double>::quiet_NaN();
+  }
+  std::vector<double> x(n, 0.0);
+  if (!pcg_solve(rhs, schur_mul, Minv, nf, opt, x, cg_iterations)) return false;
+  // back substitution (scaled space), then the camera part
+  for (int ip = 0; ip < npv; ++ip) {
+    double w3[3] = {u[(size_t)ip * 3], u[(size_t)ip * 3 + 1], u[(size_t)ip * 3 + 2]};
+    for (int o : S.pt_obs[ip]) {
+      if (P.type[o] != RB_ANGLE) continue;
+      const double* w = &W[(size_t)o * 18];
+      const double* xc = &x[6 * S.fidx[P.obs_cam[o]]];
+      for (int k = 0; k < 3; ++k)
+        for (int a = 0; a < 6; ++a) w3[k] -= w[a * 3 + k] * xc[a];
+    }
+    const double* M = &Linv[(size_t)ip * 9];
+    const int pc = P.pt_col[P.var_pts[ip]];
+    for (int a = 0; a < 3; ++a) y[pc + a] = M[a] * w3[0] + M[3 + a] * w3[1] + M[6 + a] * w3[2];   // L^-T w
+  }
+  for (int c : P.var_cams) for (int a = 0; a < 6; ++a) y[P.cam_col[c] + a] = x[6 * S.fidx[c] + a];
+  for (double v : y) if (!std::isfinite(v)) return false;
+  return true;
+}
+
 static bool linear_solve(const Problem& P, const Schur& S, const std::vector<Lin>& L, const std::vector<double>& s,
                          const std::vector<double>& D, const Options& opt, std::vector<double>& y, int* ls_iters) {
   *ls_iters = 1;
-  if (opt.linear_solver == LS_ITERATIVE_SCHUR) return iterative_schur_solve(P, S, L, s, D, opt, y, ls_iters);
+  if (opt.linear_solver == LS_ITERATIVE_SCHUR) {
+    // precision 1: MIXED_FP32 (W in float); 2: the same W form in fp64 (test
+    // hook: checks the W-form restatement against the F/E form above)
+    if (opt.precision == 1 || opt.precision == 2) return iterative_schur_solve_w(P, S, L, s, D, opt, y, ls_iters);
+    return iterative_schur_solve(P, S, L, s, D, opt, y, ls_iters);
+  }
   return dense_schur_solve(P, S, L, s, D, y);
 }
 

@@ -13,7 +13,7 @@ import pytest
 from bundleadjustment_amd import Options, Solver, make_config, make_synthetic
 from bundleadjustment_amd import problem as bp
 from bundleadjustment_amd._native import BAError
-from conftest import assert_close
+from conftest import assert_close, compare_logs
 from golden_problems import golden_expected, golden_problem
 
 pytestmark = pytest.mark.gpu
@@ -31,29 +31,6 @@ def run_gpu(solver, p, opts=None):
     summ = solver.solve(opts)
     cams, pts = solver.params()
     return cams, pts, summ, solver.iteration_log()
-
-
-def compare_logs(glog, olog, rtol_cost=1e-10, n=None, strict_iters=None, late_rtol=1e-7):
-    """Iteration-by-iteration comparison of the ceres IterationSummary fields.
-    `strict_iters`: compare costs at rtol_cost only for the first iterations
-    and at late_rtol afterwards (problems with a free gauge: rounding
-    differences drift along the null space)."""
-    n = n or min(len(glog), len(olog))
-    assert len(glog) >= n and len(olog) >= n
-    for g, o in zip(glog[:n], olog[:n]):
-        tol = rtol_cost if strict_iters is None or g["iteration"] < strict_iters else late_rtol
-        assert g["iteration"] == o["iteration"]
-        assert g["step_is_valid"] == o["step_is_valid"], (g, o)
-        assert g["step_is_successful"] == o["step_is_successful"], (g, o)
-        assert g["cost"] == pytest.approx(o["cost"], rel=tol), (g["iteration"], g["cost"], o["cost"])
-        assert g["trust_region_radius"] == pytest.approx(o["trust_region_radius"], rel=1e-9)
-        if g["step_is_valid"] and g["iteration"] > 0:
-            # the model cost change is a small difference of quadratic-model
-            # terms near convergence: relative accuracy ~cond(S)*eps (observed
-            # <= 3e-8); it only enters the accept test rho > 1e-3.
-            mt = 1e-6 if tol == rtol_cost else 1e-3
-            assert g["model_cost_change"] == pytest.approx(o["model_cost_change"], rel=mt)
-            assert g["relative_decrease"] == pytest.approx(o["relative_decrease"], rel=mt, abs=1e-9)
 
 
 # ---------------------------------------------------------------------------
@@ -207,10 +184,18 @@ def test_unobserved_blocks_untouched_and_duplicates(solver, oracle_lib):
     # minimum, where the conditioning amplifies rounding; the final parameters
     # agree to ~1e-6
     compare_logs(glog, olog, strict_iters=10, late_rtol=1e-8)
+    # near the minimum the poorly conditioned rays amplify 1e-10 cost-level
+    # differences to ~1e-6 in the parameters (cond ~1e4 of the point blocks):
+    # the converged parameters are compared at 1e-5 ...
     assert_close(cams, oc, 1e-5, 1e-10, "cameras")
     assert_close(pts, op, 1e-5, 1e-10, "points")
     assert np.array_equal(cams[-1], p.cams[-1])
     assert np.array_equal(pts[-5:], p.pts[-5:])
+    # ... and at the stated 1e-8 while the trajectories are identical
+    c10, x10, _, _ = run_gpu(solver, p, Options(max_num_iterations=10))
+    oc10, ox10, _, _ = oracle_lib.solve(p, oracle_lib.default_options(max_num_iterations=10))
+    assert_close(c10, oc10, 1e-8, 1e-10, "cameras (10 iterations)")
+    assert_close(x10, ox10, 1e-8, 1e-10, "points (10 iterations)")
 
 
 def test_points_only_with_all_cameras_fixed(solver, oracle_lib):

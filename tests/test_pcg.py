@@ -88,6 +88,28 @@ def test_oracle_residual_reset_and_iteration_cap(oracle_lib):
     assert s["final_cost"] < s["initial_cost"]
 
 
+@pytest.mark.parametrize("pc", PRECONDITIONERS)
+def test_oracle_w_form_and_mixed_precision(oracle_lib, pc):
+    """precision 2 (oracle test hook): the per-observation W-block form of the
+    implicit reduced system, the form MIXED_FP32 rounds, restates Ceres' F/E
+    form — identical CG counts, costs to 1e-12.  precision 1 (MIXED_FP32, W
+    rounded to fp32): final cost within 1e-6 of fp64."""
+    p = gauge_fixed("c2", 0.5)
+    runs = {}
+    for prec in (0, 2, 1):
+        _, _, s, log = oracle_lib.solve(p, oracle_opts(oracle_lib, pc, max_num_iterations=12, precision=prec))
+        runs[prec] = (s, log)
+    s0, l0 = runs[0]
+    s2, l2 = runs[2]
+    assert [r["linear_solver_iterations"] for r in l2] == [r["linear_solver_iterations"] for r in l0]
+    for a, b in zip(l2, l0):
+        assert a["cost"] == pytest.approx(b["cost"], rel=1e-12)
+    s1, l1 = runs[1]
+    assert s1["termination_type"] != "FAILURE"
+    assert s1["final_cost"] == pytest.approx(s0["final_cost"], rel=1e-6)
+    assert s1["final_cost"] != s0["final_cost"]   # the rounding is really applied
+
+
 # ---------------------------------------------------------------------------
 # HIP path vs oracle (GPU)
 # ---------------------------------------------------------------------------
@@ -146,7 +168,12 @@ def test_gpu_iterative_reaches_dense_minimum(solver, pc):
 
 
 @pytest.mark.gpu
-def test_gpu_iterative_residual_reset_and_cap(solver, oracle_lib):
+@pytest.mark.parametrize("pcg_t", ["auto", "1"])
+def test_gpu_iterative_residual_reset_and_cap(solver, oracle_lib, pcg_t, monkeypatch):
+    """Residual resets (r = b - S x every 10 CG iterations: a matvec of the
+    iterate) and the iteration cap, on both matvec forms."""
+    if pcg_t != "auto":
+        monkeypatch.setenv("BA_PCG_T", pcg_t)
     p = make_config("c2", scale=0.2)
     kw = dict(max_num_iterations=4, eta=1e-14, max_linear_solver_iterations=23)
     _, _, so, olog = oracle_lib.solve(p, oracle_opts(oracle_lib, "JACOBI", **kw))
@@ -247,6 +274,41 @@ def test_gpu_mixed_fp32_matches_fp64(solver, pc):
     # deterministic as well
     c32b, x32b, s32b, _ = gpu_solve(solver, p, precision="MIXED_FP32", **kw)
     assert s32b.final_cost == s32.final_cost and np.array_equal(c32, c32b) and np.array_equal(x32, x32b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pc", PRECONDITIONERS)
+@pytest.mark.parametrize("cfg,scale", [("c2", 0.2), ("c3", 0.01)])
+@pytest.mark.parametrize("pcg_t", ["auto", "1"])
+def test_gpu_mixed_fp32_matches_oracle_mixed(solver, oracle_lib, cfg, scale, pc, pcg_t, monkeypatch):
+    """BA_MIXED_FP32 against the oracle's independent fp32-W restatement
+    (oracle precision 1): the same W entries rounded to float, so the
+    iterations match like the fp64 ones — cost 1e-9, identical decisions and
+    CG counts — on both matvec forms (BA_PCG_T=1 runs k_pcg_point_t<float>)."""
+    if pcg_t != "auto":
+        monkeypatch.setenv("BA_PCG_T", pcg_t)
+    p = make_config(cfg, scale=scale)
+    _, _, so, olog = oracle_lib.solve(p, oracle_opts(oracle_lib, pc, max_num_iterations=8, precision=1))
+    _, _, sg, glog = gpu_solve(solver, p, preconditioner_type=pc, max_num_iterations=8, precision="MIXED_FP32")
+    compare(glog, olog, min(len(glog), len(olog), 6))
+    assert sg.final_cost == pytest.approx(so["final_cost"], rel=1e-8)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_gpu_pcg_t_auto_threshold(solver, monkeypatch):
+    """2M observations: the fp64 W (144 B/obs = 288 MB) outgrows the 256-MiB
+    Infinity Cache, so the solver picks the per-observation product matvec by
+    itself; it must match the W-gather matvec (BA_PCG_T=0) on the same
+    problem: costs 1e-10, identical decisions and CG counts."""
+    p = make_config("c3", scale=2.0)
+    assert 144 * p.n_obs > 256 * 2 ** 20
+    kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=5)
+    _, _, sa, la = gpu_solve(solver, p, **kw)
+    monkeypatch.setenv("BA_PCG_T", "0")
+    _, _, sb, lb = gpu_solve(solver, p, **kw)
+    compare(la, lb, len(lb), rtol=1e-10)
+    assert sa.final_cost == pytest.approx(sb.final_cost, rel=1e-10)
 
 
 @pytest.mark.gpu
