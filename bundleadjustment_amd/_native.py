@@ -85,6 +85,9 @@ class ba_pose_batch(C.Structure):
     ]
 
 
+# int (*)(void* user, double* values, int64_t n, int op) of ba_comm_init_host
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.c_int)
+
 PRUNE_NAMES = {0: "INLIER", 1: "OUTLIER_BEHIND", 2: "OUTLIER_DEPTH", 3: "OUTLIER_CHI2"}
 
 
@@ -98,6 +101,7 @@ SIGNATURES = [
     ("ba_comm_unique_id", C.c_int, [C.c_char_p]),
     ("ba_comm_init", C.c_int, [C.c_void_p, C.c_char_p, C.c_int, C.c_int]),
     ("ba_comm_allreduce_host", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
+    ("ba_comm_init_host", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]),
     ("ba_set_problem", C.c_int, [C.c_void_p, C.POINTER(ba_problem)]),
     ("ba_set_params", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("ba_solve", C.c_int, [C.c_void_p, C.POINTER(ba_options), C.POINTER(ba_summary)]),

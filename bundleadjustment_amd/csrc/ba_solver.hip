@@ -69,6 +69,11 @@ struct ba_ctx {
   // multi-GPU
   int nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
+  // host-staged transport (ba_comm_init_host: tests of the multi-rank path
+  // with several ranks on one GPU, where RCCL refuses duplicate devices)
+  ba_host_allreduce_fn host_fn = nullptr;
+  void* host_user = nullptr;
+  std::vector<double> host_buf;
 
   // problem
   bool have_problem = false;
@@ -138,10 +143,31 @@ struct ba_ctx {
   // one-rank communicator (BA_FORCE_COLLECTIVES=1: tests of the exchange path
   // on a single GPU, where the all-reduce is the identity)
   bool force_coll = false;
-  bool coll() const { return comm && (nranks > 1 || force_coll); }
+  bool has_comm() const { return comm || host_fn; }
+  bool coll() const { return has_comm() && (nranks > 1 || force_coll); }
   void allreduce(double* d, size_t count, ncclRedOp_t op = ncclSum) {
-    if (!comm || count == 0) return;   // a 1-rank communicator still runs the collectives (tests)
+    if (!has_comm() || count == 0) return;   // a 1-rank communicator still runs the collectives (tests)
+    if (host_fn) {   // stage through the host and the caller's transport
+      host_buf.resize(count);
+      HIP_OK(hipMemcpyAsync(host_buf.data(), d, sizeof(double) * count, hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+      if (host_fn(host_user, host_buf.data(), (int64_t)count, op == ncclMax ? 1 : 0) != 0)
+        throw BaError{BA_ERR_COMM, "host all-reduce callback failed"};
+      HIP_OK(hipMemcpyAsync(d, host_buf.data(), sizeof(double) * count, hipMemcpyHostToDevice, stream));
+      return;
+    }
     NCCL_OK(ncclAllReduce(d, d, count, ncclDouble, op, comm, stream));
+  }
+  // host values (set_problem structure, bench timing)
+  void allreduce_host_values(double* v, size_t count, int op) {
+    if (!has_comm() || count == 0) return;
+    double* d = nullptr;
+    HIP_OK(hipMalloc(&d, sizeof(double) * count));
+    HIP_OK(hipMemcpyAsync(d, v, sizeof(double) * count, hipMemcpyHostToDevice, stream));
+    allreduce(d, count, op == 1 ? ncclMax : ncclSum);
+    HIP_OK(hipMemcpyAsync(v, d, sizeof(double) * count, hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    (void)hipFree(d);
   }
   void read_scalars() {
     HIP_OK(hipMemcpyAsync(h_scal, W.scal, sizeof(double) * (kNumSlots + kPcgState), hipMemcpyDeviceToHost, stream));
@@ -201,28 +227,18 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   }
   if (ctx->coll() && nc > 0) {
     // the reduced system spans the union of the ranks' observed cameras
-    uint8_t* d = nullptr;
-    HIP_OK(hipMalloc(&d, nc));
-    HIP_OK(hipMemcpyAsync(d, cam_used.data(), nc, hipMemcpyHostToDevice, ctx->stream));
-    NCCL_OK(ncclAllReduce(d, d, nc, ncclUint8, ncclMax, ctx->comm, ctx->stream));
-    HIP_OK(hipMemcpyAsync(cam_used.data(), d, nc, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_OK(hipStreamSynchronize(ctx->stream));
-    (void)hipFree(d);
+    std::vector<double> u(nc);
+    for (int c = 0; c < nc; ++c) u[c] = cam_used[c];
+    ctx->allreduce_host_values(u.data(), nc, 1);
+    for (int c = 0; c < nc; ++c) cam_used[c] = u[c] != 0.0;
   }
   ctx->max_no = no;
   if (ctx->coll()) {
     // every rank takes the same matvec path (ITERATIVE_SCHUR), chosen from the
     // largest shard: identical kernels and rounding on every rank
-    double* d = nullptr;
-    const double h = (double)no;
-    HIP_OK(hipMalloc(&d, sizeof(double)));
-    HIP_OK(hipMemcpyAsync(d, &h, sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-    NCCL_OK(ncclAllReduce(d, d, 1, ncclDouble, ncclMax, ctx->comm, ctx->stream));
-    double r = 0.0;
-    HIP_OK(hipMemcpyAsync(&r, d, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_OK(hipStreamSynchronize(ctx->stream));
-    (void)hipFree(d);
-    ctx->max_no = (int)r;
+    double h = (double)no;
+    ctx->allreduce_host_values(&h, 1, 1);
+    ctx->max_no = (int)h;
   }
   ctx->cam_of_vc.clear();
   for (int c = 0; c < nc; ++c)
@@ -915,6 +931,7 @@ int ba_comm_init(ba_ctx* ctx, const char id[128], int nranks, int rank) {
   return guarded(ctx, [&] {
     HIP_OK(hipSetDevice(ctx->device));
     if (ctx->comm) { ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+    ctx->host_fn = nullptr;
     ctx->nranks = nranks;
     ctx->rank = rank;
     ncclUniqueId uid;
@@ -928,19 +945,23 @@ int ba_comm_init(ba_ctx* ctx, const char id[128], int nranks, int rank) {
 int ba_comm_allreduce_host(ba_ctx* ctx, double* values, int n, int op) {
   if (!ctx || n < 0 || (n > 0 && !values) || (op != 0 && op != 1)) return BA_ERR_INVALID_ARGUMENT;
   return guarded(ctx, [&] {
-    if (!ctx->comm) return;
+    if (!ctx->has_comm()) return;
     HIP_OK(hipSetDevice(ctx->device));
-    const int m = n > 0 ? n : 1;
-    double* d = nullptr;
-    HIP_OK(hipMalloc(&d, sizeof(double) * m));
-    std::vector<double> h(m, 0.0);
-    if (n > 0) std::memcpy(h.data(), values, sizeof(double) * n);
-    HIP_OK(hipMemcpyAsync(d, h.data(), sizeof(double) * m, hipMemcpyHostToDevice, ctx->stream));
-    NCCL_OK(ncclAllReduce(d, d, m, ncclDouble, op == 0 ? ncclSum : ncclMax, ctx->comm, ctx->stream));
-    HIP_OK(hipMemcpyAsync(h.data(), d, sizeof(double) * m, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_OK(hipStreamSynchronize(ctx->stream));
-    (void)hipFree(d);
-    if (n > 0) std::memcpy(values, h.data(), sizeof(double) * n);
+    double zero = 0.0;
+    ctx->allreduce_host_values(n > 0 ? values : &zero, n > 0 ? (size_t)n : 1, op);   // n = 0: a barrier
+  });
+}
+
+int ba_comm_init_host(ba_ctx* ctx, ba_host_allreduce_fn fn, void* user, int nranks, int rank) {
+  if (!ctx || !fn || nranks < 1 || rank < 0 || rank >= nranks) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] {
+    if (ctx->comm) { ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+    ctx->host_fn = fn;
+    ctx->host_user = user;
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    const char* fc = getenv("BA_FORCE_COLLECTIVES");
+    ctx->force_coll = fc && atoi(fc) != 0;
   });
 }
 

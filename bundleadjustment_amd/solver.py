@@ -126,6 +126,20 @@ class Solver:
         assert len(uid) == 128
         self._check(self.lib.ba_comm_init(self.h, C.c_char_p(uid), int(nranks), int(rank)), "ba_comm_init")
 
+    def comm_init_host(self, allreduce, nranks: int, rank: int):
+        """Host-staged transport for the multi-rank exchange (test hook, see
+        ba_comm_init_host): `allreduce(values: np.ndarray, op: str)` reduces the
+        float64 array in place across the ranks ("sum" / "max")."""
+        def cb(_user, ptr, n, op):
+            try:
+                allreduce(np.ctypeslib.as_array(ptr, shape=(int(n),)), "max" if op == 1 else "sum")
+                return 0
+            except Exception:   # noqa: BLE001 - reported as BA_ERR_COMM
+                return 1
+        self._host_cb = N.HOST_ALLREDUCE_FN(cb)   # kept alive with the solver
+        self._check(self.lib.ba_comm_init_host(self.h, C.cast(self._host_cb, C.c_void_p), None, int(nranks),
+                                               int(rank)), "ba_comm_init_host")
+
     def allreduce_host(self, values, op: str = "sum") -> np.ndarray:
         """In-place RCCL reduction of a few host doubles across ranks (identity
         without a communicator)."""

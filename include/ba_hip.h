@@ -174,6 +174,16 @@ int ba_comm_init(ba_ctx* ctx, const char id[128], int nranks, int rank);
  * timing, so no second GPU runtime is needed for host-side rendezvous. */
 int ba_comm_allreduce_host(ba_ctx* ctx, double* values, int n, int op);
 
+/* Host-staged transport for the same exchange (test hook, not the product
+ * path): every all-reduce of the multi-rank LM iteration is copied to the
+ * host and handed to fn(user, values, n, op) (op 0 = sum, 1 = max; in place;
+ * return 0 on success), e.g. torch.distributed over gloo.  It lets several
+ * ranks share one GPU — RCCL refuses duplicate devices — so the multi-rank
+ * HIP path (packing, folding, replicated decisions) runs on a 1-GPU box.
+ * Replaces any RCCL communicator of the context. */
+typedef int (*ba_host_allreduce_fn)(void* user, double* values, int64_t n, int op);
+int ba_comm_init_host(ba_ctx* ctx, ba_host_allreduce_fn fn, void* user, int nranks, int rank);
+
 /* Copy a problem to the device and build its (fixed) structure. */
 int ba_set_problem(ba_ctx* ctx, const ba_problem* problem);
 
