@@ -139,6 +139,35 @@ __device__ inline void mfma_xxT_lower_sub(const double (*Xs)[LDP], double (*D)[L
       for (int g = 0; g < 4; ++g) D[16 * tl[q][0] + lk + 4 * g][16 * tl[q][1] + li] -= acc[q][g];
 }
 
+// The same product split for the critical path: the tiles (w, 0) of
+// column 0 first (one per wave: all the first sub-panel sweep reads), the
+// other six lower tiles (two per wave for waves 1..3) while wave 0 sweeps.
+// Each tile accumulates over k in the order of mfma_xxT_lower_sub (bitwise
+// the same C).
+__device__ inline void mfma_xxT_tile(const double (*Xs)[LDP], double (*D)[LDP], int ti, int tj) {
+  const int lane = threadIdx.x & 63;
+  const int li = lane & 15, lk = lane >> 4;
+  d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int k0 = 0; k0 < CB; k0 += 4) {
+    const double x = Xs[16 * ti + li][k0 + lk];
+    const double y = Xs[16 * tj + li][k0 + lk];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(x, y, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) D[16 * ti + lk + 4 * g][16 * tj + li] -= acc[g];
+}
+__device__ inline void mfma_xxT_col0(const double (*Xs)[LDP], double (*D)[LDP]) {
+  mfma_xxT_tile(Xs, D, threadIdx.x >> 6, 0);
+}
+__device__ inline void mfma_xxT_rest(const double (*Xs)[LDP], double (*D)[LDP]) {
+  constexpr int T[6][2] = {{1, 1}, {2, 1}, {2, 2}, {3, 1}, {3, 2}, {3, 3}};
+  const int w = threadIdx.x >> 6;
+  if (w == 0) return;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) mfma_xxT_tile(Xs, D, T[2 * (w - 1) + h][0], T[2 * (w - 1) + h][1]);
+}
+
 // P = Xs V^T with V lower triangular (V[j][k] = 0 for k > j): wave w owns
 // the row strip 16w..16w+15, and output column tile bc needs only k <
 // 16 (bc + 1) -> 40 MFMAs per wave (the square product: 64).
@@ -451,7 +480,12 @@ __device__ __forceinline__ void inverse_rowblock(const double (*T)[LDP], const d
 // row block p - 1 (wave 1) overlaps the sweep of sub-panel p, so only the
 // last row block follows the factorization (its off-diagonal sums spread
 // over waves 1..3).
-__device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z)[LDP], CholLds& W, int b, int m) {
+// Pc != nullptr: T is final in its column-0 tiles only; waves 1..3 apply
+// the rest of C = T - Pc Pc^T (mfma_xxT_rest) during the first sweep (Pc
+// must stay intact until the first sub-panel's barrier: Z aliases it only
+// from sub-panel 1 on).
+__device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z)[LDP], CholLds& W, int b, int m,
+                                  const double (*Pc)[LDP] = nullptr) {
   const int w = threadIdx.x >> 6;
   __syncthreads();
   CHOL_STAMP(2);
@@ -462,6 +496,7 @@ __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z
     last = p;
     if (w == 0) panel_sweep(T, W, c0, b, m);
     else if (w == 1 && p > 0) inverse_rowblock(T, W.rsv, X, Z, p - 1, b, 1);
+    else if (p == 0 && Pc != nullptr) mfma_xxT_rest(Pc, T);
     CHOL_STAMP(10 + 2 * p);
     __syncthreads();
     // trailing update of the remaining sub-panels: tiles (i, s), p < s <= i

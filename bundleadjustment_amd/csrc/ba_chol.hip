@@ -77,14 +77,14 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
       }
       __syncthreads();
       CHOL_STAMP(22);
-      mfma_xxT_lower_sub(S1, S0);            // C = A - P P^T (lower tiles)
+      mfma_xxT_col0(S1, S0);                 // C = A - P P^T: column 0 now, the rest beside the first sweep
       CHOL_STAMP(23);
     } else {
       stage64(S0, A, lds, s, s, nrows, s + b);
     }
     if (threadIdx.x == 0) cw.bad = 0;
     CHOL_STAMP(1);
-    factor_invert_blk(S0, S2, S1, cw, b, m);   // rows b..m-1 (rhs) come out as L rows too
+    factor_invert_blk(S0, S2, S1, cw, b, m, k >= 0 ? S1 : nullptr);   // rows b..m-1 (rhs) come out as L rows too
     CHOL_STAMP(5);
     __syncthreads();
     // only V_{k+1} and the rhs row of L leave the workgroup: the diagonal L
@@ -146,50 +146,47 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
 // single-workgroup sweep it replaces was bound by one CU pulling all of L:
 // 152 us at n = 1194).
 //
-// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): producer =
-// plain stores of y_K -> every storing wave s_waitcnt vmcnt(0) -> barrier ->
-// one lane: agent release fence -> vmcnt(0) -> relaxed agent flag store;
-// consumer = one lane polls the flag (relaxed, agent, s_sleep) -> agent
-// acquire fence -> vmcnt(0) -> barrier -> plain loads.  A flag holds the
-// epoch (launch counter, never 0) of its last publish, so no reset between
-// launches; spins are bounded (a missing producer sets the failure slot
-// instead of hanging the GPU).
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility: the
+// data-tagged granule form, its hand-off table's handoff-1to1 row): every
+// element of y_K travels as one 16-B granule {value, epoch} written by ONE
+// write-through store (global_store_dwordx4 sc1); each consumer lane polls
+// its element's granule with 16-B sc1 loads until the tag matches, so the
+// value arrives with its flag (one fabric round trip per hop, no separate
+// flag, no L2 write-back or L1 invalidate).  The epoch (launch counter,
+// never 0) tags the latest publish, so nothing is reset between launches;
+// spins are bounded (a missing producer sets the failure slot instead of
+// hanging the GPU).  The plain y (read by later kernels) is stored too.
 // ---------------------------------------------------------------------------
-constexpr long kSpinMax = 1L << 26;
+constexpr long kSpinMax = 1L << 24;
+typedef int gi4 __attribute__((ext_vector_type(4)));
 
-__device__ inline void flag_publish(int* flag, int epoch) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+__device__ inline void gran_store(double* g, double v, int epoch) {
+  const long long b = __double_as_longlong(v);
+  const gi4 d = {(int)b, (int)(b >> 32), epoch, 0};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(g), "v"(d) : "memory");
 }
-// returns false if the spin bound was hit
-__device__ inline bool flag_wait(int* flag, int epoch, int* lds_ok) {
-  if (threadIdx.x == 0) {
-    long it = 0;
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch && it < kSpinMax) {
-      __builtin_amdgcn_s_sleep(1);
-      ++it;
-    }
-    *lds_ok = it < kSpinMax;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// waits for the granule of `epoch`; false if the spin bound was hit
+__device__ inline bool gran_wait(const double* g, int epoch, double& v) {
+  gi4 d;
+  long it = 0;
+  while (true) {
+    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(d) : "v"(g) : "memory");
+    if (d.z == epoch || it >= kSpinMax) break;
+    __builtin_amdgcn_s_sleep(1);
+    ++it;
   }
-  __syncthreads();
-  return *lds_ok != 0;
+  v = __longlong_as_double(((long long)d.y << 32) | (unsigned)d.x);
+  return d.z == epoch;
 }
 
 __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A, const double* __restrict__ Lm,
                                                    int ld, int n, const double* __restrict__ Vall,
-                                                   double* __restrict__ y, int* __restrict__ flags, int epoch,
+                                                   double* __restrict__ y, double* __restrict__ yg, int epoch,
                                                    double* __restrict__ scal) {
   __shared__ double zs[CB];
   __shared__ double ys[CB];
   __shared__ double part[4][CB];
-  __shared__ int ok;
+  __shared__ int bad;
   // producers first: workgroup K waits on every J > K, and low block ids are
   // dispatched first, so block b takes K = T - 1 - b (if the grid cannot be
   // resident at once, the waiting consumers are then the ones still queued)
@@ -199,6 +196,7 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
   const size_t lds = (size_t)ld;
   // thread (j = tid & 63, h = tid >> 6) sums rows i = h, h + 4, ... of a tile
   const int j = tid & 63, h = tid >> 6;
+  if (tid == 0) bad = 0;
   if (n % CB == 0 && K == T - 1) {
     // the rhs row starts a tile row of its own: no step factored it into
     // z_K, the last trailing update left A_{n,K}; z_K = V_K A_{n,K}^T
@@ -219,7 +217,6 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
     zs[tid] = tid < bsz ? Lm[(size_t)n * lds + s0 + tid] : 0.0;
   }
   double acc = 0.0;
-  bool good = true;
   for (int J = T - 1; J > K; --J) {
     const int sJ = J * CB, bJ = min(CB, n - sJ);
     double lv[16];
@@ -228,8 +225,11 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
       const int i = h + 4 * q;
       lv[q] = (i < bJ && j < bsz) ? Lm[(size_t)(sJ + i) * lds + s0 + j] : 0.0;
     }
-    good = flag_wait(flags + J, epoch, &ok) && good;
-    if (tid < CB) ys[tid] = tid < bJ ? y[sJ + tid] : 0.0;
+    if (tid < CB) {
+      double v = 0.0;
+      if (tid < bJ && !gran_wait(yg + 2 * (size_t)(sJ + tid), epoch, v)) bad = 1;
+      ys[tid] = v;
+    }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc += lv[q] * ys[h + 4 * q];
@@ -251,9 +251,12 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
     part[h][j] = t;
   }
   __syncthreads();
-  if (tid < CB && tid < bsz) y[s0 + tid] = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
-  flag_publish(flags + K, epoch);
-  if (tid == 0 && !good) scal[SL_CHOL_BAD] += 1.0;
+  if (tid < CB && tid < bsz) {
+    const double val = (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]);
+    gran_store(yg + 2 * (size_t)(s0 + tid), val, epoch);
+    y[s0 + tid] = val;
+  }
+  if (tid == 0 && bad) scal[SL_CHOL_BAD] += 1.0;
 }
 
 // split-form block step (ba_chol_split.hip)
@@ -282,7 +285,7 @@ void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hi
       hipLaunchKernelGGL(k_chol_step, dim3(tc, tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf, W.scal);
     }
   }
-  hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.flags, epoch, W.scal);
+  hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.yg, epoch, W.scal);
 }
 
 }  // namespace bahip

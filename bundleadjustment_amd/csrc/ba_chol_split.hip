@@ -42,13 +42,13 @@ __global__ __launch_bounds__(256) void k_chol_step_split(double* __restrict__ A,
       tile_put(S0, tA);
       tile_put(S1, tP);
       __syncthreads();
-      mfma_xxT_lower_sub(S1, S0);            // C = A - P P^T (lower tiles)
+      mfma_xxT_col0(S1, S0);                 // C = A - P P^T: column 0 now, the rest beside the first sweep
     } else {
       stage64(S0, A, lds, s, s, nrows, s + b);
     }
     if (threadIdx.x == 0) cw.bad = 0;
     CHOL_STAMP(1);
-    factor_invert_blk(S0, S2, S1, cw, b, m);   // rows b..m-1 (rhs) come out as L rows too
+    factor_invert_blk(S0, S2, S1, cw, b, m, k >= 0 ? S1 : nullptr);   // rows b..m-1 (rhs) come out as L rows too
     CHOL_STAMP(5);
     __syncthreads();
     // only V_{k+1} and the rhs row of L leave the workgroup: the diagonal L

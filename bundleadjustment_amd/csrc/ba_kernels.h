@@ -10,7 +10,6 @@ namespace bahip {
 constexpr int kThreads = 256;
 constexpr int kMaxBlocks = 2048;        // grid cap of the streaming kernels
 constexpr int kCamSplit = 8;            // workgroups per camera in k_cam_schur_diag
-constexpr int kFlagWords = 4096;        // hand-off flag words (DevWork::flags)
 
 // Scalar reduction slots (device buffer d_scal[kNumSlots]).
 enum Slot {
@@ -75,7 +74,7 @@ struct DevWork {
   double* Spk;                       // [n(n+1)/2 + n] packed lower triangle + rhs of S (multi-rank exchange)
   double* y;                         // [n] reduced solution
   double* Vbuf;                      // [ceil(n/64)][64][64] inverses of the diagonal Cholesky blocks
-  int* flags;                        // [kFlagWords] hand-off flags of the dataflow kernels (zeroed per call)
+  double* yg;                        // [n][2] back-substitution hand-off granules {y, epoch} (zeroed once)
   const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}
   const int2* eblocks; int neblocks; // lower off-diagonal blocks {I, J} with no observation pair
   bool s_memset;                     // many empty blocks: memset S instead

@@ -797,7 +797,10 @@ __global__ __launch_bounds__(NT) void k_linearize_lds_t(DevProblem P, const doub
     part_of(part, SL_LIN_BAD)[blockIdx.x] = tot[1];
   }
 }
-constexpr int kLinNT = 512, kLinRows = 64;    // product configuration (tools/lin_probe.hip)
+#ifndef BA_LIN_ROWS
+#define BA_LIN_ROWS 64
+#endif
+constexpr int kLinNT = 512, kLinRows = BA_LIN_ROWS;    // product configuration (tools/lin_probe.hip)
 
 __device__ inline void load_jr(const double* __restrict__ JR, int no, int o, double (&v)[kJR]) {
   const double2* a = reinterpret_cast<const double2*>(jr_a(JR, o));

@@ -396,7 +396,7 @@ void ensure_dense(ba_ctx* ctx) {
   W.S = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
   W.Lf = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
   W.Vbuf = ctx->dalloc<double>((size_t)((ctx->n + 63) / 64 + 1) * 64 * 64);
-  W.flags = ctx->dalloc<int>(kFlagWords);
+  W.yg = ctx->dalloc<double>(2 * (size_t)std::max(ctx->n, 1));
   W.Spk = nullptr;
   W.blocks = ctx->upload(blocks);
   W.nblocks = (int)blocks.size();
@@ -405,7 +405,7 @@ void ensure_dense(ba_ctx* ctx) {
   // (separate k_cam_add_diag), in the order the exchange path uses
   ctx->dup_diag = std::any_of(blocks.begin(), blocks.end(), [](const int4& b) { return b.x == b.y; });
   W.pairs = ctx->upload(pairs);
-  HIP_OK(hipMemsetAsync(W.flags, 0, sizeof(int) * kFlagWords, ctx->stream));
+  HIP_OK(hipMemsetAsync(W.yg, 0, sizeof(double) * 2 * (size_t)std::max(ctx->n, 1), ctx->stream));
   // S is rewritten every step (diagonal blocks, rhs and every co-observed
   // block); the rest of the lower triangle must be re-zeroed (the Cholesky
   // updates it in place): a list of those blocks, or a memset when they are

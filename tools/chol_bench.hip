@@ -49,8 +49,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dV, sizeof(double) * (size_t)(T + 1) * CB * CB));
   CK(hipMalloc(&dS, sizeof(double) * 64));
   CK(hipMalloc(&dy, sizeof(double) * n));
-  int* dF;
-  CK(hipMalloc(&dF, sizeof(int) * (T + 1)));
+  double* dF;
+  CK(hipMalloc(&dF, sizeof(double) * 2 * n));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -97,7 +97,7 @@ int main(int argc, char** argv) {
                st_h[16] - st_h[15], st_h[17] - st_h[16]);
 
     }
-    CK(hipMemset(dF, 0, sizeof(int) * T));
+    CK(hipMemset(dF, 0, sizeof(double) * 2 * n));
     CK(hipEventRecord(e0));
     hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dA, dL, ld, n, dV, dy, dF, 1, dS);
     CK(hipEventRecord(e1));
