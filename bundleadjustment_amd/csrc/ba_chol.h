@@ -277,8 +277,8 @@ __device__ __forceinline__ d4 mfma_tile(d4 acc, const double (*Xs)[LDP], int xr,
 }
 
 // same with the second operand transposed: Ys[yr + k][yc + j]
-template <int K>
-__device__ __forceinline__ d4 mfma_tile_n(d4 acc, const double (*Xs)[LDP], int xr, int xc, const double (*Ys)[LDP],
+template <int K, int YLD = LDP>
+__device__ __forceinline__ d4 mfma_tile_n(d4 acc, const double (*Xs)[LDP], int xr, int xc, const double (*Ys)[YLD],
                                           int yr, int yc, double sgn) {
   const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
 #pragma unroll
@@ -298,7 +298,8 @@ __device__ __forceinline__ d4 tile_load(const double (*S)[LDP], int r0, int c0) 
   return v;
 }
 
-__device__ __forceinline__ void tile_store(double (*S)[LDP], int r0, int c0, d4 v) {
+template <int SLD = LDP>
+__device__ __forceinline__ void tile_store(double (*S)[SLD], int r0, int c0, d4 v) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int g = 0; g < 4; ++g) S[r0 + (lane >> 4) + 4 * g][c0 + (lane & 15)] = v[g];
@@ -449,25 +450,28 @@ __device__ __forceinline__ void diag_inverse16(const double (*T)[LDP], const dou
   for (int i = 0; i < 16; ++i) X[c0 + i][c0 + c] = x[i];
 }
 
-// Z_q (16x16, rows 16 zr.. of Z) = sum_{k=q}^{p-1} L_pk X_kq, by the calling wave
-__device__ __forceinline__ void inv_offdiag_sum(const double (*T)[LDP], const double (*X)[LDP], double (*Z)[LDP],
+// Z_q (16x16, rows zr.. of Z; Z's row stride ZLD) = sum_{k=q}^{p-1} L_pk X_kq, by the calling wave
+template <int ZLD>
+__device__ __forceinline__ void inv_offdiag_sum(const double (*T)[LDP], const double (*X)[LDP], double (*Z)[ZLD],
                                                 int p, int q, int zr) {
   d4 acc = d4{0.0, 0.0, 0.0, 0.0};
   for (int k = q; k < p; ++k) acc = mfma_tile_n<16>(acc, T, 16 * p, 16 * k, X, 16 * k, 16 * q, 1.0);
-  tile_store(Z, zr, 0, acc);
+  tile_store<ZLD>(Z, zr, 0, acc);
 }
 // X_pq = -X_pp Z_q
-__device__ __forceinline__ void inv_offdiag_fin(double (*X)[LDP], const double (*Z)[LDP], int p, int q, int zr) {
+template <int ZLD>
+__device__ __forceinline__ void inv_offdiag_fin(double (*X)[LDP], const double (*Z)[ZLD], int p, int q, int zr) {
   d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-  acc = mfma_tile_n<16>(acc, X, 16 * p, 16 * p, Z, zr, 0, -1.0);
+  acc = mfma_tile_n<16, ZLD>(acc, X, 16 * p, 16 * p, Z, zr, 0, -1.0);
   tile_store(X, 16 * p, 16 * q, acc);
 }
 
 // Row block p of X = L^-1 by ONE wave (diagonal block, then the blocks
 // (p, q < p) from the finished rows above); Z rows 16 zw.. are its scratch.
 // LDS operations of one wave complete in order, so no barrier inside.
+template <int ZLD>
 __device__ __forceinline__ void inverse_rowblock(const double (*T)[LDP], const double* rinv, double (*X)[LDP],
-                                                 double (*Z)[LDP], int p, int b, int zw) {
+                                                 double (*Z)[ZLD], int p, int b, int zw) {
   diag_inverse16(T, rinv, X, p, b);
   for (int q = 0; q < p; ++q) {
     inv_offdiag_sum(T, X, Z, p, q, 16 * zw);
@@ -484,7 +488,10 @@ __device__ __forceinline__ void inverse_rowblock(const double (*T)[LDP], const d
 // the rest of C = T - Pc Pc^T (mfma_xxT_rest) during the first sweep (Pc
 // must stay intact until the first sub-panel's barrier: Z aliases it only
 // from sub-panel 1 on).
-__device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z)[LDP], CholLds& W, int b, int m,
+// Z: inverse scratch, rows 16..63 used (row stride ZLD >= 16).  X may alias
+// Pc (written from the second sub-panel on).
+template <int ZLD = LDP>
+__device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z)[ZLD], CholLds& W, int b, int m,
                                   const double (*Pc)[LDP] = nullptr) {
   const int w = threadIdx.x >> 6;
   __syncthreads();

@@ -17,13 +17,27 @@ namespace bahip {
 // does one GEMM instead of three (the fused form recomputes P_I, P_J per
 // tile: 3x the flops and ~2.5x the bytes, which dominate once the trailing
 // matrix has thousands of tiles).
+// Grid: the lower tiles only, linear id -> (I, J <= I) (tile 0 = the
+// critical block); a rhs-only last tile row (n % 64 == 0) follows them.
+__device__ inline void split_tile_of(int lin, int tc, int& I, int& J) {
+  const int tri = tc * (tc + 1) / 2;
+  if (lin >= tri) { I = tc; J = lin - tri; return; }
+  int i = (int)((sqrt(8.0 * lin + 1.0) - 1.0) * 0.5);
+  while (i * (i + 1) / 2 > lin) --i;
+  while ((i + 1) * (i + 2) / 2 <= lin) ++i;
+  I = i;
+  J = lin - i * (i + 1) / 2;
+}
 __global__ __launch_bounds__(256) void k_chol_step_split(double* __restrict__ A, double* __restrict__ L, int ld, int n,
                                                    int k, double* __restrict__ Vbuf, double* __restrict__ scal) {
-  const int I = blockIdx.y, J = blockIdx.x;
-  if (J > I) return;
+  int I, J;
+  split_tile_of(blockIdx.x, (n - (k + 1) * CB + CB - 1) / CB, I, J);
+  // two tiles + a narrow inverse scratch (78 KB: two workgroups per CU, so
+  // one tile's operand loads overlap another's MFMAs); the critical
+  // workgroup forms the block inverse in S1 once C = A - P P^T consumed it
   __shared__ double S0[CB][LDP];
   __shared__ double S1[CB][LDP];
-  __shared__ double S2[CB][LDP];
+  __shared__ double Zs[CB][18];
   __shared__ CholLds cw;
   const int nrows = n + 1;
   const size_t lds = (size_t)ld;
@@ -48,7 +62,7 @@ __global__ __launch_bounds__(256) void k_chol_step_split(double* __restrict__ A,
     }
     if (threadIdx.x == 0) cw.bad = 0;
     CHOL_STAMP(1);
-    factor_invert_blk(S0, S2, S1, cw, b, m, k >= 0 ? S1 : nullptr);   // rows b..m-1 (rhs) come out as L rows too
+    factor_invert_blk<18>(S0, S1, Zs, cw, b, m, k >= 0 ? S1 : nullptr);   // rows b..m-1 (rhs) come out as L rows too
     CHOL_STAMP(5);
     __syncthreads();
     // only V_{k+1} and the rhs row of L leave the workgroup: the diagonal L
@@ -60,7 +74,7 @@ __global__ __launch_bounds__(256) void k_chol_step_split(double* __restrict__ A,
         double v[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-          v[h] = (j + h <= i && i < b && j + h < b) ? S2[i][j + h] : (i == j + h ? 1.0 : 0.0);
+          v[h] = (j + h <= i && i < b && j + h < b) ? S1[i][j + h] : (i == j + h ? 1.0 : 0.0);
         Vd[e2] = make_double2(v[0], v[1]);
       }
       if (m > b)
@@ -74,10 +88,23 @@ __global__ __launch_bounds__(256) void k_chol_step_split(double* __restrict__ A,
   if (k < 0) return;
   if (r0 >= nrows || c0 >= n) return;
   const TileRegs tI = tile_fetch(L, lds, r0, kc, nrows, kc + kb);   // L_{I,k}
-  if (I != J) {
-    const TileRegs tJ = tile_fetch(L, lds, c0, kc, n, kc + kb);     // L_{J,k}
-    tile_put(S1, tJ);
-  }
+  TileRegs tJ;
+  if (I != J) tJ = tile_fetch(L, lds, c0, kc, n, kc + kb);          // L_{J,k}
+  // the A tile (read-modify-write target) is loaded with the operands, so
+  // its latency hides behind the staging and the MFMAs (clamped addresses,
+  // unconditional loads)
+  double av[2][2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int rr, cc;
+        acc_pos(a, b, g, &rr, &cc);
+        av[a][b][g] = A[(size_t)min(r0 + rr, nrows - 1) * ld + min(c0 + cc, n - 1)];
+      }
+  if (I != J) tile_put(S1, tJ);
   tile_put(S0, tI);
   __syncthreads();
   d4 acc[2][2];
@@ -91,7 +118,7 @@ __global__ __launch_bounds__(256) void k_chol_step_split(double* __restrict__ A,
         int rr, cc;
         acc_pos(a, b, g, &rr, &cc);
         const int ri = r0 + rr, cj = c0 + cc;
-        if (ri < nrows && cj < n && cj <= ri) A[(size_t)ri * ld + cj] -= acc[a][b][g];
+        if (ri < nrows && cj < n && cj <= ri) A[(size_t)ri * ld + cj] = av[a][b][g] - acc[a][b][g];
       }
 }
 
@@ -126,7 +153,8 @@ __global__ __launch_bounds__(256) void k_chol_panel(const double* __restrict__ A
 void launch_chol_split_step(double* A, double* L, int ld, int n, int k, int tc, int tr, double* Vbuf, double* scal,
                             hipStream_t s) {
   hipLaunchKernelGGL(k_chol_panel, dim3(tr), dim3(256), 0, s, A, L, ld, n, k, Vbuf);
-  hipLaunchKernelGGL(k_chol_step_split, dim3(tc, tr), dim3(256), 0, s, A, L, ld, n, k, Vbuf, scal);
+  const int ntiles = tc * (tc + 1) / 2 + (tr > tc ? tc : 0);   // lower tiles (+ a rhs-only tile row)
+  hipLaunchKernelGGL(k_chol_step_split, dim3(ntiles), dim3(256), 0, s, A, L, ld, n, k, Vbuf, scal);
 }
 
 }  // namespace bahip

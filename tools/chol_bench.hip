@@ -65,8 +65,7 @@ int main(int argc, char** argv) {
       dim3 grid = k < 0 ? dim3(1, 1) : dim3(tc, tr);
       CK(hipEventRecord(e0));
       if (k >= 0 && T >= kCholSplitBlocks) {
-        hipLaunchKernelGGL(k_chol_panel, dim3(grid.y), dim3(256), 0, 0, dA, dL, ld, n, k, dV);
-        hipLaunchKernelGGL(k_chol_step_split, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS);
+        launch_chol_split_step(dA, dL, ld, n, k, grid.x, grid.y, dV, dS, 0);
       } else {
         hipLaunchKernelGGL(k_chol_step, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS);
       }
