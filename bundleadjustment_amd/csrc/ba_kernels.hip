@@ -1140,7 +1140,7 @@ __global__ __launch_bounds__(256) void k_backsub(DevProblem P, const double* __r
     // kPtLanes lanes per point (point_wtx); fixed cameras carry W_o = 0
     double wy[3] = {0.0, 0.0, 0.0};
     const bool var = P.pt_var[p];
-    if (var) point_wtx(W, P.obs_vc, y, P.pt_off[p], P.pt_off[p + 1], gl, wy);
+    if (var) point_wtx<false>(W, P.obs_vc, y, P.pt_off[p], P.pt_off[p + 1], gl, wy);
     if (gl != 0) continue;
     const double X[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
     double dX[3] = {0.0, 0.0, 0.0}, Xc[3] = {X[0], X[1], X[2]};

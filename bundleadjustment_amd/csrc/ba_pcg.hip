@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void k_pcg_point(DevProblem P, const WT* __res
   const int gl = threadIdx.x & (kPtLanes - 1), gpb = blockDim.x / kPtLanes;
   for (int p = blockIdx.x * gpb + threadIdx.x / kPtLanes; p < P.np; p += gridDim.x * gpb) {
     double w[3];
-    point_wtx(Wm, P.obs_vc, xv, P.pt_off[p], P.pt_off[p + 1], gl, w);
+    point_wtx<true>(Wm, P.obs_vc, xv, P.pt_off[p], P.pt_off[p + 1], gl, w);
     if (gl < 3) vpt[3 * (size_t)p + gl] = gl == 0 ? w[0] : (gl == 1 ? w[1] : w[2]);
   }
 }
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void k_pcg_point_t(DevProblem P, const WT* __r
   for (int p = blockIdx.x * gpb + threadIdx.x / kPtLanes; p < P.np; p += gridDim.x * gpb) {
     const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
     double w[3];
-    point_wtx(Wm, P.obs_vc, xv, o0, o1, gl, w);
+    point_wtx<true>(Wm, P.obs_vc, xv, o0, o1, gl, w);
     for (int o = o0 + gl; o < o1; o += kPtLanes) {
       double wv[18];
       load_w18(Wm, (size_t)o, wv);
