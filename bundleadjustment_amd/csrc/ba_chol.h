@@ -527,7 +527,9 @@ __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z
   // last row block: diagonal inverse (wave 0) beside the sums Z_q (wave q + 1)
   if (w == 0) diag_inverse16(T, W.rsv, X, last, b);
   else if (w - 1 < last) inv_offdiag_sum(T, X, Z, last, w - 1, 16 * w);
+  CHOL_STAMP(40);
   __syncthreads();
+  CHOL_STAMP(41);
   if (w >= 1 && w - 1 < last) inv_offdiag_fin(X, Z, last, w - 1, 16 * w);
   __syncthreads();
   CHOL_STAMP(4);

@@ -88,8 +88,8 @@ int main(int argc, char** argv) {
         printf("    sub-panel 0: load %llu  columns %llu  scale+store %llu\n", st_h[30] - st_h[2], st_h[31] - st_h[30],
                st_h[10] - st_h[31]);
       if (verbose && (k < 1 || k == T / 2))
-        printf("    inverse: diag16 (wave 0) %llu  barrier %llu  rounds %llu\n", st_h[40] - st_h[3], st_h[41] - st_h[40],
-               st_h[4] - st_h[41]);
+        printf("    inverse tail: diag16 (wave 0) %llu  wait for the sums %llu  fin + barrier %llu\n", st_h[40] - st_h[3],
+               st_h[41] - st_h[40], st_h[4] - st_h[41]);
       if (verbose && (k < 1 || k == T / 2))
         printf("    sub-panels (sweep / update cycles): %llu/%llu %llu/%llu %llu/%llu %llu/%llu\n", st_h[10] - st_h[2],
                st_h[11] - st_h[10], st_h[12] - st_h[11], st_h[13] - st_h[12], st_h[14] - st_h[13], st_h[15] - st_h[14],
