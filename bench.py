@@ -231,6 +231,23 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "algorithmic_bytes": B_rj, "avg_launch_ms": round(ms_rj, 5)}
 
+    # whole-iteration figure (reported beside the kernel line):
+    # B_iter = 176N (r+J) + 160N (r, J re-read for assembly) + 144N (W write)
+    # + 144N (W read, Schur) + 16N (candidate: uv + idx) + P (24 + 72 + 72)
+    # + C (48 + 216) + 16 (6C)^2 (dense S formed and factored) or 2 x 144N per
+    # CG iteration (implicit Schur); W terms 72N with fp32 W storage.  Per
+    # rank, over the rank's device time per LM iteration.
+    wb = 72.0 if precision == "MIXED_FP32" else 144.0
+    N, Pn, Cn = float(problem.n_obs), float(problem.n_pts), float(problem.n_cams)
+    B_iter = (176.0 + 160.0 + 2.0 * wb + 16.0) * N + 168.0 * Pn + 264.0 * Cn
+    B_iter += 2.0 * wb * N * cg_iters if iterative else 16.0 * (6.0 * Cn) ** 2
+    it_ach = B_iter / (ms_dev * 1e-3) / 1e9
+    iteration_roofline = {"bound": "hbm", "achieved": round(it_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(it_ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": round(B_iter),
+                          "note": "B_iter of SURVEY.md §8d over the device time per LM iteration (one rank); "
+                                  "the iteration is bound by the serial reduced-camera factorisation and the "
+                                  "Infinity-Cache Schur gathers, not by HBM"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if problem.n_obs <= 20_000_000:
@@ -273,6 +290,7 @@ def main():
                        "parallelism": f"points sharded x{world}, RCCL all-reduce of {exchange}"},
             "device_ms_per_step": round(ms_dev, 4),
             "roofline": roofline,
+            "iteration_roofline": iteration_roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
