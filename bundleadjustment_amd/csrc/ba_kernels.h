@@ -56,7 +56,7 @@ struct DevWork {
   double* cams;  double* pts;        // x
   double* cams_c; double* pts_c;     // candidate x'
   double* rec;   double* rec_c;      // camera records at x / x'
-  double* crec;                      // [nc][16] compact camera records (w, t, K, flag) for > kLinLdsCams cameras
+  double* crec;                      // [nc][16] compact camera records (w, t, K, flag, theta terms) for > kLinLdsCams cameras
   double* ctbl;                      // [nc][22] candidate camera table for > kLinLdsCams cameras
   double* JR;                        // [no][20] AoS: Jc row0 (6), Jc row1 (6), Jp rows (3+3), r (2)
   double* delta_p;                   // [np][3] point step (scaled back)

@@ -297,17 +297,24 @@ __device__ inline CamLdsLazy::Row cam_row(const CamLdsLazy& cr) { return cr.row(
 // Many cameras (nc > kLinLdsCams): the 704-B camera records no longer fit the
 // LDS and, past ~5k cameras, not even one XCD's L2 (C5: 7 MB of records,
 // ~4.8 GB of per-observation record gathers served by the Infinity Cache).
-// Instead every observation gathers its camera's compact 128-B record
-// (w, t, K, flag: one cache line, the whole table L2-resident) and rebuilds
-// the K-folded table in registers: the dual-number Rodrigues of k_cam_prep
-// (same functions, same arithmetic) plus the 40 K-folds, ~400 fp64 VALU
-// operations per observation, cheap next to the HBM stream.
-constexpr int kCRec = 16;   // [0..5] w, t (variable) | camera index (fixed); [6..14] K; [15] variable flag
+// Instead every observation gathers its camera's compact 128-B record (one
+// cache line, the whole table L2-resident) and rebuilds the K-folded terms in
+// registers: the dual-number Rodrigues of k_cam_prep (same functions, same
+// arithmetic), cheap next to the HBM stream.  The per-camera scalars of the
+// Rodrigues (theta = |w|, 1 / (2 theta), 1 / theta, cos, sin) are formed
+// once per camera by k_cam_compact and travel in the record, so the
+// per-observation work has no sqrt, divide or sin / cos on its chain.
+//   [0..2] w (variable) | camera index in [0] (fixed); [3..5] t;
+//   [6..10] K as 9 floats (float-valued Matrix3f) + the variable flag as
+//   float 9; [11..15] theta, 1/(2 theta), 1/theta, cos theta, sin theta
+//   (theta = 0: the small-angle branch)
+constexpr int kCRec = 16;
+constexpr int kCRecK = 6, kCRecTh = 11;
 struct CamRcPre {
   double2 v[kCRec / 2];
 };
 struct CamRc {   // unpacked compact record; lin_obs(CamRc) forms the table terms itself
-  double w[3], t[3], Kd[9];
+  double w[3], t[3], Kd[9], th[5];
   int cidx;
   bool v;
   __device__ bool var() const { return v; }
@@ -338,11 +345,55 @@ __device__ inline CamRc cam_make(const CamRcOf&, const CamRcPre& q) {
   for (int k = 0; k < kCRec / 2; ++k) { rv[2 * k] = q.v[k].x; rv[2 * k + 1] = q.v[k].y; }
 #pragma unroll
   for (int k = 0; k < 3; ++k) { C.w[k] = rv[k]; C.t[k] = rv[3 + k]; }
+  float kf[10];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) C.Kd[k] = rv[6 + k];
+  for (int k = 0; k < 5; ++k) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, rv[kCRecK + k]);
+    kf[2 * k] = __builtin_bit_cast(float, (unsigned)b);
+    kf[2 * k + 1] = __builtin_bit_cast(float, (unsigned)(b >> 32));
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) C.Kd[k] = (double)kf[k];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) C.th[k] = rv[kCRecTh + k];
   C.cidx = (int)rv[0];
-  C.v = rv[15] != 0.0;
+  C.v = kf[9] != 0.0f;
   return C;
+}
+
+// ceres::AngleAxisToRotationMatrix on duals (angle_axis_to_R_d3) with the
+// value-only scalars of theta taken from the record: theta, 1 / (2 theta)
+// (dsqrt), 1 / theta (the three quotients) and cos / sin (dcos, dsin) are the
+// same operations on the same operand, so the result is the same
+__device__ __forceinline__ void angle_axis_to_R_d3_pre(const double w[3], const double th[5], D3 R[9]) {
+  const D3 a0 = mk(w[0], 1, 0, 0), a1 = mk(w[1], 0, 1, 0), a2 = mk(w[2], 0, 0, 1);
+  if (th[0] > 0.0) {
+    const D3 theta2 = a0 * a0 + a1 * a1 + a2 * a2;
+    const double ti = th[1], gi = th[2], cs = th[3], sn = th[4];
+    const D3 theta = mk(th[0], theta2.d[0] * ti, theta2.d[1] * ti, theta2.d[2] * ti);
+    auto quot = [&](D3 f) {
+      const double fg = f.a * gi;
+      return mk(fg, (f.d[0] - fg * theta.d[0]) * gi, (f.d[1] - fg * theta.d[1]) * gi, (f.d[2] - fg * theta.d[2]) * gi);
+    };
+    const D3 wx = quot(a0), wy = quot(a1), wz = quot(a2);
+    const double ns = -sn;
+    const D3 c = mk(cs, ns * theta.d[0], ns * theta.d[1], ns * theta.d[2]);
+    const D3 s = mk(sn, cs * theta.d[0], cs * theta.d[1], cs * theta.d[2]);
+    const D3 oc = rsub(1.0, c);
+    R[0] = c + wx * wx * oc;
+    R[1] = wz * s + wx * wy * oc;
+    R[2] = -(wy * s) + wx * wz * oc;
+    R[3] = wx * wy * oc - wz * s;
+    R[4] = c + wy * wy * oc;
+    R[5] = wx * s + wy * wz * oc;
+    R[6] = wy * s + wx * wz * oc;
+    R[7] = -(wx * s) + wy * wz * oc;
+    R[8] = c + wz * wz * oc;
+  } else {
+    R[0] = mk(1, 0, 0, 0); R[1] = a2;             R[2] = -a1;
+    R[3] = -a2;            R[4] = mk(1, 0, 0, 0); R[5] = a0;
+    R[6] = a1;             R[7] = -a0;            R[8] = mk(1, 0, 0, 0);
+  }
 }
 
 // compact camera records for CamRcOf (thread per camera)
@@ -352,11 +403,33 @@ __global__ __launch_bounds__(256) void k_cam_compact(DevProblem P, const double*
   if (c >= P.nc) return;
   const bool var = P.vc[c] >= 0;
   double* o = crec + (size_t)c * kCRec;
+  double w[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) w[k] = var ? cams[6 * c + k] : 0.0;
 #pragma unroll
   for (int k = 0; k < 6; ++k) o[k] = var ? cams[6 * c + k] : (k == 0 ? (double)c : 0.0);
+  float kf[10];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) o[6 + k] = (double)P.K[9 * c + k];
-  o[15] = var ? 1.0 : 0.0;
+  for (int k = 0; k < 9; ++k) kf[k] = P.K[9 * c + k];
+  kf[9] = var ? 1.0f : 0.0f;
+#pragma unroll
+  for (int k = 0; k < 5; ++k)
+    o[kCRecK + k] = __builtin_bit_cast(double, ((unsigned long long)__builtin_bit_cast(unsigned, kf[2 * k + 1]) << 32) |
+                                                   __builtin_bit_cast(unsigned, kf[2 * k]));
+  // the scalars of angle_axis_to_R_d3: theta2.a of the duals is w.w
+  const D3 a0 = mk(w[0], 1, 0, 0), a1 = mk(w[1], 0, 1, 0), a2 = mk(w[2], 0, 0, 1);
+  const D3 theta2 = a0 * a0 + a1 * a1 + a2 * a2;
+  double th[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  if (var && theta2.a > 2.220446049250313080847e-16) {
+    const double t = sqrt(theta2.a);
+    th[0] = t;
+    th[1] = 1.0 / (2.0 * t);
+    th[2] = 1.0 / t;
+    th[3] = cos(t);
+    th[4] = sin(t);
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) o[kCRecTh + k] = th[k];
 }
 
 // r, J (Huber-corrected) of one observation into out[20]; returns rho.
@@ -441,7 +514,7 @@ __device__ inline double lin_obs(const DevProblem& P, const CamRc& cr, bool cvar
   double q[3], dq[3][3], dX[3][3], iw = 1.0;   // dq/dw_k [k][row], dq/dX_col [col][row]
   if (cvar) {
     D3 R[9];
-    angle_axis_to_R_d3(cr.w, R);
+    angle_axis_to_R_d3_pre(cr.w, cr.th, R);
     D3 p[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
