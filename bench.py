@@ -244,9 +244,12 @@ def main():
     it_ach = B_iter / (ms_dev * 1e-3) / 1e9
     iteration_roofline = {"bound": "hbm", "achieved": round(it_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(it_ach / HBM_PEAK_GBS, 4), "algorithmic_bytes": round(B_iter),
-                          "note": "B_iter of SURVEY.md §8d over the device time per LM iteration (one rank); "
-                                  "the iteration is bound by the serial reduced-camera factorisation and the "
-                                  "Infinity-Cache Schur gathers, not by HBM"}
+                          "note": "B_iter of SURVEY.md §8d over the device time per LM iteration (one rank); " +
+                                  ("the implicit-Schur iteration runs a chain of streaming kernels (W, "
+                                   "matvecs, camera-order gathers through the Infinity Cache) at 0.3-0.6 of "
+                                   "HBM each" if iterative else
+                                   "the iteration is bound by the serial reduced-camera factorisation and the "
+                                   "Infinity-Cache Schur gathers, not by HBM")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
