@@ -1333,10 +1333,28 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
   double2 t[kJR / 2];
   int c = 0, p = 0;
   float2 uv = make_float2(0.f, 0.f);
+  // GTBL: the lane's camera record (176 B, 16-B aligned) and K are gathered
+  // one chunk ahead into registers, beside the next chunk's JR loads (read at
+  // use, each chunk waited one L2 round trip for them)
+  struct CandCam {
+    double2 r[kCandRec / 2];
+    float k[9];
+  };
+  auto cam_load = [&](int cc, CandCam& q) {
+    if constexpr (GTBL) {
+      const double2* s2 = reinterpret_cast<const double2*>(tbl + (size_t)cc * kCandRec);
+#pragma unroll
+      for (int i = 0; i < kCandRec / 2; ++i) q.r[i] = s2[i];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) q.k[i] = ktb[(size_t)cc * 9 + i];
+    }
+  };
+  CandCam cq;
   if (base < P.no) {
     jr_chunk_load(JR, P.no, base, lane, t);
     const int oc = min(base + lane, P.no - 1);
     c = P.obs_cam[oc]; p = P.obs_pt[oc]; uv = P.uv[oc];
+    cam_load(c, cq);
   }
   for (; base < P.no; base += step) {
     const int o = base + lane;
@@ -1349,15 +1367,22 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
     const int nb = base + step;
     int cn = c, pn = p;
     float2 uvn = uv;
+    CandCam cqn;
     if (nb < P.no) {
       jr_chunk_load(JR, P.no, nb, lane, t);
       const int oc = min(nb + lane, P.no - 1);
       cn = P.obs_cam[oc]; pn = P.obs_pt[oc]; uvn = P.uv[oc];
+      cam_load(cn, cqn);
     }
     wave_lds_sync();
     {
       const double* j = st + lane * kStageLd;
-      const double* cr = tbl + c * kCandRec;
+      double crv[GTBL ? kCandRec : 1];
+      if constexpr (GTBL) {
+#pragma unroll
+        for (int i = 0; i < kCandRec / 2; ++i) { crv[2 * i] = cq.r[i].x; crv[2 * i + 1] = cq.r[i].y; }
+      }
+      const double* cr = GTBL ? crv : tbl + c * kCandRec;
       double jd0 = 0.0, jd1 = 0.0;
 #pragma unroll
       for (int a2 = 0; a2 < 6; ++a2) { jd0 += j[a2] * cr[16 + a2]; jd1 += j[6 + a2] * cr[16 + a2]; }
@@ -1374,7 +1399,7 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
         for (int i = 0; i < 4; ++i) ph[i] = X0 * cr[i] + X1 * cr[4 + i] + X2 * cr[8 + i] + cr[12 + i];
         pc[0] = ph[0] / ph[3]; pc[1] = ph[1] / ph[3]; pc[2] = ph[2] / ph[3];
       }
-      const float* Kc = ktb + c * 9;
+      const float* Kc = GTBL ? cq.k : ktb + c * 9;
       double q[3];
 #pragma unroll
       for (int i = 0; i < 3; ++i) q[i] = pc[0] * (double)Kc[i] + pc[1] * (double)Kc[3 + i] + pc[2] * (double)Kc[6 + i];
@@ -1389,6 +1414,7 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
     }
     wave_lds_sync();
     c = cn; p = pn; uv = uvn;
+    if constexpr (GTBL) cq = cqn;
   }
   double out[3];
   block_sum<3>(acc, lds, out);
