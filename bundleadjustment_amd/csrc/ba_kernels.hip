@@ -1135,19 +1135,51 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
   double* st = stage + w * (64 * kStageLd);
   const int step = gridDim.x * WAVES * 64;
   const size_t np = (size_t)P.np;
-  for (int base = (blockIdx.x * WAVES + w) * 64; base < P.no; base += step) {
-    const int o = base + lane, oc = min(o, P.no - 1);
-    double2 t[kJR / 2];
-    jr_chunk_load(JR, P.no, base, lane, t);
-    const int c = P.obs_cam[oc], p = P.obs_pt[oc];
+  // pipeline (every load unconditional, indices clamped): the indices of
+  // chunk i+2 and the JR records + per-camera / per-point factors of chunk
+  // i+1 are in flight while chunk i computes (issued at use, each chunk waited
+  // for its index -> camera -> scale chain)
+  struct Fac {
+    double sc[6], sp[3], li[6];
+    bool live;
+  };
+  auto load_idx = [&](int b, int& c, int& p) {
+    const int oc = min(b + lane, P.no - 1);
+    c = P.obs_cam[oc]; p = P.obs_pt[oc];
+  };
+  auto load_fac = [&](int b, int c, int p, Fac& f) {
     const int v = P.vc[c];
-    const bool live = o < P.no && v >= 0 && P.pt_var[p];
+    f.live = b + lane < P.no && v >= 0 && P.pt_var[p];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) f.sc[a] = TBL ? sct[c * 6 + a] : scale_c[(size_t)max(v, 0) * 6 + a];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) f.sp[k] = scale_p[k * np + p];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) f.li[k] = Linv[k * np + p];
+  };
+  int base = (blockIdx.x * WAVES + w) * 64;
+  int ci0, pi0, ci1, pi1;
+  load_idx(base, ci0, pi0);
+  load_idx(base + step, ci1, pi1);
+  double2 t[kJR / 2];
+  jr_chunk_load(JR, P.no, min(base, P.no - 1), lane, t);
+  Fac fc;
+  load_fac(base, ci0, pi0, fc);
+  for (; base < P.no; base += step) {
+    const int nb = base + step;
+    int ci2, pi2;
+    load_idx(nb + step, ci2, pi2);
+    double2 tn[kJR / 2];
+    jr_chunk_load(JR, P.no, min(nb, P.no - 1), lane, tn);
+    Fac fn;
+    load_fac(nb, ci1, pi1, fn);
+    const bool live = fc.live;
     double sc[6];
 #pragma unroll
-    for (int a = 0; a < 6; ++a) sc[a] = TBL ? sct[c * 6 + a] : scale_c[(size_t)max(v, 0) * 6 + a];
-    const double s0 = scale_p[p], s1 = scale_p[np + p], s2 = scale_p[2 * np + p];
-    const double i00 = Linv[p], i10 = Linv[np + p], i11 = Linv[2 * np + p];
-    const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
+    for (int a = 0; a < 6; ++a) sc[a] = fc.sc[a];
+    const double s0 = fc.sp[0], s1 = fc.sp[1], s2 = fc.sp[2];
+    const double i00 = fc.li[0], i10 = fc.li[1], i11 = fc.li[2];
+    const double i20 = fc.li[3], i21 = fc.li[4], i22 = fc.li[5];
     jr_chunk_stage(st, lane, t);
     wave_lds_sync();
     double j[18];
@@ -1192,6 +1224,10 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
         if (e / (kWRec / 2) < nrec) dst[e] = ov[it];
       }
     }
+#pragma unroll
+    for (int k = 0; k < kJR / 2; ++k) t[k] = tn[k];
+    fc = fn;
+    ci1 = ci2; pi1 = pi2;
   }
 }
 
