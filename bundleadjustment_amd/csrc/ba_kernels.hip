@@ -1713,9 +1713,11 @@ __global__ __launch_bounds__(256) void k_residuals(DevProblem P, const double* _
 // Fold partials -> scalars (fixed order), then clear the partials.  One
 // wave per slot (kNumSlots waves), no workgroup barrier: each lane folds a
 // fixed strided subset, then a fixed-order shuffle tree.
-__global__ __launch_bounds__(64 * kNumSlots) void k_reduce(double* __restrict__ part, double* __restrict__ scal,
-                                                           uint32_t sum_mask, uint32_t max_mask) {
-  const int slot = threadIdx.x >> 6, lane = threadIdx.x & 63;
+// one 64-lane workgroup per slot (the slots' 16-KB folds run on separate
+// CUs; as waves of one workgroup they all went through one CU)
+__global__ __launch_bounds__(64) void k_reduce(double* __restrict__ part, double* __restrict__ scal,
+                                               uint32_t sum_mask, uint32_t max_mask) {
+  const int slot = blockIdx.x, lane = threadIdx.x & 63;
   const bool is_sum = (sum_mask >> slot) & 1u, is_max = (max_mask >> slot) & 1u;
   if (!is_sum && !is_max) return;
   double* pp = part + (size_t)slot * kMaxBlocks;
@@ -1932,7 +1934,7 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
                      W.delta_p, W.rec_c, W.pts_c, W.ctbl, W.part);
 }
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(64 * kNumSlots), 0, s, W.part, W.scal, sum_mask, max_mask);
+  hipLaunchKernelGGL(k_reduce, dim3(kNumSlots), dim3(64), 0, s, W.part, W.scal, sum_mask, max_mask);
 }
 void launch_residuals(const DevProblem& P, const double* rec, const double* pts, double* r_raw, hipStream_t s) {
   hipLaunchKernelGGL(k_residuals, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, rec, pts, r_raw);
