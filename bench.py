@@ -227,9 +227,14 @@ def main():
     B_rj = 176.0 * problem.n_obs + 24.0 * problem.n_pts + 48.0 * problem.n_cams
     achieved = B_rj / (ms_rj * 1e-3) / 1e9
     traffic = pmc_traffic(cfg) if not strong and args.scale == 1.0 else None
+    # measured copy bandwidth of this GPU (reported beside the
+    # vendor peak, which stays the denominator of `frac`): 1 GiB non-temporal
+    # 16-B copy, 10 launches, after the timed region
+    copy_gbs = solver.stream_copy(1 << 30, 10)
     roofline = {"kernel": "k_linearize (residual+Jacobian)", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "algorithmic_bytes": B_rj, "avg_launch_ms": round(ms_rj, 5)}
+                "traffic": traffic, "algorithmic_bytes": B_rj, "avg_launch_ms": round(ms_rj, 5),
+                "measured_copy": round(copy_gbs, 1), "frac_of_copy": round(achieved / copy_gbs, 4)}
 
     # whole-iteration figure (reported beside the kernel line):
     # B_iter = 176N (r+J) + 160N (r, J re-read for assembly) + 144N (W write)

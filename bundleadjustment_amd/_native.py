@@ -115,6 +115,7 @@ SIGNATURES = [
     ("ba_synchronize", C.c_int, [C.c_void_p]),
     ("ba_bench_iterations", C.c_int, [C.c_void_p, C.POINTER(ba_options), C.c_int, C.c_double,
                                       C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    ("ba_stream_copy", C.c_int, [C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_double)]),
 ]
 
 _LIB = None

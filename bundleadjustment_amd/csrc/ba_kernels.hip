@@ -1933,6 +1933,22 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
   hipLaunchKernelGGL((k_candidate_lds<256, true>), dim3(grid_for(P.no)), dim3(256), 0, s, P, W.JR, W.delta_c,
                      W.delta_p, W.rec_c, W.pts_c, W.ctbl, W.part);
 }
+// STREAM-style copy for the measured bandwidth figure (ba_stream_copy):
+// non-temporal 16-B loads and stores, one per lane, grid up to one lane per
+// element (tools/copy_probe.hip, 1 GiB: 5.95 TB/s at 65536 workgroups vs
+// 5.1 with four per lane at 8192)
+__global__ __launch_bounds__(256) void k_stream_copy(const double2* __restrict__ a, double2* __restrict__ b, size_t n2) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const ntd2*>(a + i)),
+                                reinterpret_cast<ntd2*>(b + i));
+}
+void launch_stream_copy(const double* a, double* b, size_t n2, hipStream_t s) {
+  if (n2 == 0) return;
+  const size_t g = std::min<size_t>((n2 + 255) / 256, 262144);
+  hipLaunchKernelGGL(k_stream_copy, dim3((unsigned)g), dim3(256), 0, s, reinterpret_cast<const double2*>(a),
+                     reinterpret_cast<double2*>(b), n2);
+}
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce, dim3(kNumSlots), dim3(64), 0, s, W.part, W.scal, sum_mask, max_mask);
 }

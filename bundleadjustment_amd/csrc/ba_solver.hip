@@ -1177,6 +1177,34 @@ int ba_synchronize(ba_ctx* ctx) {
   return guarded(ctx, [&] { HIP_OK(hipStreamSynchronize(ctx->stream)); });
 }
 
+int ba_stream_copy(ba_ctx* ctx, size_t bytes, int reps, double* gbs) {
+  if (!ctx || reps < 1 || bytes < 16 || !gbs) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] {
+    HIP_OK(hipSetDevice(ctx->device));
+    const size_t n2 = bytes / 16;
+    double *a = nullptr, *b = nullptr;
+    HIP_OK(hipMalloc(&a, n2 * 16));
+    if (hipMalloc(&b, n2 * 16) != hipSuccess) {
+      (void)hipFree(a);
+      throw BaError{BA_ERR_OUT_OF_MEMORY, "ba_stream_copy: hipMalloc"};
+    }
+    struct Free {
+      double *a, *b;
+      ~Free() { (void)hipFree(a); (void)hipFree(b); }
+    } fr{a, b};
+    HIP_OK(hipMemsetAsync(a, 0, n2 * 16, ctx->stream));
+    bahip::launch_stream_copy(a, b, n2, ctx->stream);   // warm-up
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(ctx->ev[0], ctx->stream));
+    for (int r = 0; r < reps; ++r) bahip::launch_stream_copy(a, b, n2, ctx->stream);
+    HIP_OK(hipEventRecord(ctx->ev[1], ctx->stream));
+    HIP_OK(hipEventSynchronize(ctx->ev[1]));
+    float ms = 0.0f;
+    HIP_OK(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
+    *gbs = 2.0 * 16.0 * (double)n2 * reps / ((double)ms * 1e-3) / 1e9;
+  });
+}
+
 int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double radius, double* ms_per_iter,
                         double* ms_rj_kernel, double* linear_iters) {
   if (!ctx || iters < 1) return BA_ERR_INVALID_ARGUMENT;

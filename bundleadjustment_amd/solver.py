@@ -259,6 +259,13 @@ class Solver:
             return ms.value, rj.value, li.value
         return ms.value, rj.value
 
+    def stream_copy(self, nbytes: int = 1 << 30, reps: int = 10) -> float:
+        """Measured device copy bandwidth in GB/s (read + write bytes), the
+        STREAM-copy figure SURVEY.md §8d asks for beside the HBM peak."""
+        g = C.c_double()
+        self._check(self.lib.ba_stream_copy(self.h, C.c_size_t(int(nbytes)), int(reps), C.byref(g)), "ba_stream_copy")
+        return g.value
+
 
 def solve(problem: Problem, options: Options | None = None, device: int = 0):
     """One-shot convenience: returns (cams, pts, summary, iteration_log)."""

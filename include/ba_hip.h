@@ -285,6 +285,14 @@ int ba_synchronize(ba_ctx* ctx);
 int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double radius, double* ms_per_iter,
                         double* ms_rj_kernel, double* linear_iters);
 
+/* Measured copy bandwidth of the context's device ("also
+ * report a measured STREAM-copy figure" beside the 8 TB/s peak): a
+ * non-temporal 16-B load / store copy of `bytes` (rounded down to 16 B)
+ * between two device buffers, `reps` timed launches after one warm-up, HIP
+ * events on the context's stream.  *gbs = 2 * bytes * reps / time (read +
+ * write).  Diagnostic; no reference counterpart. */
+int ba_stream_copy(ba_ctx* ctx, size_t bytes, int reps, double* gbs);
+
 #ifdef __cplusplus
 }
 #endif

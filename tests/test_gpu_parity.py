@@ -262,3 +262,12 @@ def test_rccl_path_single_rank_is_identity(solver):
         s.barrier()
     assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
     assert [r["cost"] for r in got[3]] == [r["cost"] for r in ref[3]]
+
+
+def test_stream_copy_bandwidth(solver):
+    """The measured-copy diagnostic bench.py reports beside the HBM peak
+    (SURVEY.md §8d): a plausible positive GB/s, and bad arguments refused."""
+    g = solver.stream_copy(64 << 20, 3)
+    assert 100.0 < g < 20000.0
+    with pytest.raises(BAError):
+        solver.stream_copy(8, 1)
