@@ -197,44 +197,61 @@ constexpr int kJR = 20;
 constexpr int kStageLd = kJR + 1;   // LDS row stride of staged records
 // Storage: the record is split in two arrays inside the JR buffer so that
 // readers of one half fetch only that half's cache lines:
-//   JA = JR           [no][12]  fields 0..11   (camera rows: 96 B)
-//   JB = JR + 12 no   [no][8]   fields 12..19  (point rows + residual: 64 B)
-constexpr int kJA = 12, kJB = 8;
-__device__ inline const double* jr_a(const double* JR, int o) { return JR + (size_t)o * kJA; }
+//   JA = JR           [no][JA]  fields 0..11 (camera rows: 96 B)
+//                               (+ 18..19 when JA = 14: the residual again)
+//   JB = JR + JA no   [no][8]   fields 12..19 (point rows + residual: 64 B)
+// JA = 12 up to kLinLdsCams cameras.  Beyond, JA = 14: k_cam_assemble's
+// camera-order gathers then read one 112-B record (~1.75 lines) instead of
+// 96 B plus a JB line (~2.5 lines) — C5 shard +1.6 %; at C3 the 16 B/obs of
+// extra writes cost more than the gathers save (profiles/r02_v7_ab_jr_*).
+constexpr int kJB = 8;
+constexpr int kFJB = 12;   // record field of the first JB slot
+constexpr int jr_ja(bool many_cams) { return many_cams ? 14 : 12; }
+// JA slot k -> record field
+__device__ __forceinline__ int ja_field(int k) { return k < 12 ? k : k + 6; }
+template <int JA>
+__device__ inline const double* jr_a(const double* JR, int o) { return JR + (size_t)o * JA; }
+template <int JA>
 __device__ inline const double* jr_b(const double* JR, int no, int o) {
-  return JR + (size_t)kJA * no + (size_t)o * kJB;
+  return JR + (size_t)JA * no + (size_t)o * kJB;
 }
-// the 64 records of the chunk at `base` as 10 coalesced 1 KiB wave loads
-// (6 of JA, 4 of JB), indices clamped (unconditional loads); non-temporal:
-// each chunk is read once per kernel (measured +0.9 % per LM iteration)
-__device__ inline void jr_chunk_load(const double* __restrict__ JR, int no, int base, int lane, double2 (&t)[10]) {
+// the 64 records of the chunk at `base` as JA/2 + 4 coalesced 1 KiB wave
+// loads, indices clamped (unconditional loads); non-temporal: each chunk is
+// read once per kernel (measured +0.9 % per LM iteration)
+template <int JA>
+__device__ inline void jr_chunk_load(const double* __restrict__ JR, int no, int base, int lane,
+                                     double2 (&t)[JA / 2 + kJB / 2]) {
   const double2* A2 = reinterpret_cast<const double2*>(JR);
-  const double2* B2 = reinterpret_cast<const double2*>(JR + (size_t)kJA * no);
-  const int lastA = (kJA / 2) * no - 1, lastB = (kJB / 2) * no - 1;
+  const double2* B2 = reinterpret_cast<const double2*>(JR + (size_t)JA * no);
+  const int lastA = (JA / 2) * no - 1, lastB = (kJB / 2) * no - 1;
 #pragma unroll
-  for (int it = 0; it < kJA / 2; ++it) {
-    const ntd2 x = __builtin_nontemporal_load(reinterpret_cast<const ntd2*>(&A2[min((kJA / 2) * base + it * 64 + lane, lastA)]));
+  for (int it = 0; it < JA / 2; ++it) {
+    const ntd2 x = __builtin_nontemporal_load(reinterpret_cast<const ntd2*>(&A2[min((JA / 2) * base + it * 64 + lane, lastA)]));
     t[it] = make_double2(x.x, x.y);
   }
 #pragma unroll
   for (int it = 0; it < kJB / 2; ++it) {
     const ntd2 x = __builtin_nontemporal_load(reinterpret_cast<const ntd2*>(&B2[min((kJB / 2) * base + it * 64 + lane, lastB)]));
-    t[kJA / 2 + it] = make_double2(x.x, x.y);
+    t[JA / 2 + it] = make_double2(x.x, x.y);
   }
 }
-// scatter them into the wave's LDS rows (record fields 0..19, stride kStageLd)
-__device__ inline void jr_chunk_stage(double* st, int lane, const double2 (&t)[10]) {
+// scatter them into the wave's LDS rows (record fields 0..19, stride kStageLd;
+// a JA copy of the residual is dropped, JB's lands in fields 18..19)
+template <int JA>
+__device__ inline void jr_chunk_stage(double* st, int lane, const double2 (&t)[JA / 2 + kJB / 2]) {
 #pragma unroll
-  for (int it = 0; it < kJA / 2; ++it) {
-    const int e = it * 64 + lane, r = e / (kJA / 2), f = 2 * (e - r * (kJA / 2));
-    st[r * kStageLd + f] = t[it].x;
-    st[r * kStageLd + f + 1] = t[it].y;
+  for (int it = 0; it < JA / 2; ++it) {
+    const int e = it * 64 + lane, r = e / (JA / 2), f = 2 * (e - r * (JA / 2));
+    if (JA == 12 || f < 12) {
+      st[r * kStageLd + f] = t[it].x;
+      st[r * kStageLd + f + 1] = t[it].y;
+    }
   }
 #pragma unroll
   for (int it = 0; it < kJB / 2; ++it) {
-    const int e = it * 64 + lane, r = e / (kJB / 2), f = kJA + 2 * (e - r * (kJB / 2));
-    st[r * kStageLd + f] = t[kJA / 2 + it].x;
-    st[r * kStageLd + f + 1] = t[kJA / 2 + it].y;
+    const int e = it * 64 + lane, r = e / (kJB / 2), f = kFJB + 2 * (e - r * (kJB / 2));
+    st[r * kStageLd + f] = t[JA / 2 + it].x;
+    st[r * kStageLd + f + 1] = t[JA / 2 + it].y;
   }
 }
 
@@ -614,7 +631,7 @@ struct NoInit {
 };
 // init(): block-wide setup (e.g. building the LDS camera table) run by every
 // thread after the prologue loads are issued, so it overlaps their latency
-template <int WAVES, int ROWS, class CamOf, int MODE = 0, class Init = NoInit>
+template <int JA, int WAVES, int ROWS, class CamOf, int MODE = 0, class Init = NoInit>
 __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__ pts, double* __restrict__ JR,
                                  double* stage_all, const CamOf& cam_of, double (&acc)[2], const Init& init = Init{}) {
   static_assert(ROWS == 64 || ROWS == 32, "stage rows");
@@ -706,8 +723,8 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
       continue;
     }
     const int nrec = min(64, P.no - base);
-    double2* dA = reinterpret_cast<double2*>(JR) + (size_t)(kJA / 2) * base;
-    double2* dB = reinterpret_cast<double2*>(JR + (size_t)kJA * P.no) + (size_t)(kJB / 2) * base;
+    double2* dA = reinterpret_cast<double2*>(JR) + (size_t)(JA / 2) * base;
+    double2* dB = reinterpret_cast<double2*>(JR + (size_t)JA * P.no) + (size_t)(kJB / 2) * base;
 #pragma unroll
     for (int h = 0; h < 64 / ROWS; ++h) {
       // all LDS reads into distinct registers first, then the stores: a
@@ -720,20 +737,21 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
         for (int k = 0; k < kJR; ++k) row[k] = out[k];
       }
       wave_lds_sync();
-      constexpr int NA = ROWS * (kJA / 2) / 64, NB = ROWS * (kJB / 2) / 64;
+      // JA: ROWS * JA/2 double2 (JA = 14 with ROWS = 32: the last wave load is half used)
+      constexpr int EA = ROWS * (JA / 2), NA = (EA + 63) / 64, NB = ROWS * (kJB / 2) / 64;
       double2 va[NA], vb[NB];
 #pragma unroll
       for (int it = 0; it < NA; ++it) {
-        const int e = it * 64 + lane, r = e / (kJA / 2), f = 2 * (e - r * (kJA / 2));
+        const int e = min(it * 64 + lane, EA - 1), r = e / (JA / 2), f = ja_field(2 * (e - r * (JA / 2)));
         va[it] = make_double2(stage[r * kStageLd + f], stage[r * kStageLd + f + 1]);
       }
 #pragma unroll
       for (int it = 0; it < NB; ++it) {
-        const int e = it * 64 + lane, r = e / (kJB / 2), f = kJA + 2 * (e - r * (kJB / 2));
+        const int e = it * 64 + lane, r = e / (kJB / 2), f = kFJB + 2 * (e - r * (kJB / 2));
         vb[it] = make_double2(stage[r * kStageLd + f], stage[r * kStageLd + f + 1]);
       }
       wave_lds_sync();
-      double2* dAh = dA + h * ROWS * (kJA / 2);
+      double2* dAh = dA + h * ROWS * (JA / 2);
       double2* dBh = dB + h * ROWS * (kJB / 2);
       if (MODE == 1) {
 #pragma unroll
@@ -744,14 +762,15 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
           if (vb[it].x == 1234.5678) dBh[it * 64 + lane] = vb[it];
       } else if (h * ROWS + ROWS <= nrec) {   // full: unconditional stores
 #pragma unroll
-        for (int it = 0; it < NA; ++it) nt_store(&dAh[it * 64 + lane], va[it]);
+        for (int it = 0; it < NA; ++it)
+          if (EA % 64 == 0 || it * 64 + lane < EA) nt_store(&dAh[it * 64 + lane], va[it]);
 #pragma unroll
         for (int it = 0; it < NB; ++it) nt_store(&dBh[it * 64 + lane], vb[it]);
       } else {
 #pragma unroll
         for (int it = 0; it < NA; ++it) {
           const int e = it * 64 + lane;
-          if (h * ROWS + e / (kJA / 2) < nrec) dAh[e] = va[it];
+          if (e < EA && h * ROWS + e / (JA / 2) < nrec) dAh[e] = va[it];
         }
 #pragma unroll
         for (int it = 0; it < NB; ++it) {
@@ -775,7 +794,8 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem P, const double* _
   __shared__ double lds[2 * 16];
   __shared__ double stage[4 * 64 * kStageLd];
   double acc[2] = {0.0, 0.0};  // cost, bad
-  lin_waves<4, 64>(P, pts, JR, stage, [&](int c) { return CamGlobal{rec + (size_t)c * kCamRec, P.vc[c] >= 0}; }, acc);
+  lin_waves<jr_ja(true), 4, 64>(P, pts, JR, stage,
+                                [&](int c) { return CamGlobal{rec + (size_t)c * kCamRec, P.vc[c] >= 0}; }, acc);
   double tot[2];
   block_sum<2>(acc, lds, tot);
   if (threadIdx.x == 0) {
@@ -790,7 +810,7 @@ __global__ __launch_bounds__(256) void k_linearize_rc(DevProblem P, const double
   __shared__ double lds[2 * 16];
   __shared__ double stage[4 * 64 * kStageLd];
   double acc[2] = {0.0, 0.0};  // cost, bad
-  lin_waves<4, 64>(P, pts, JR, stage, CamRcOf{crec, P.extr}, acc);
+  lin_waves<jr_ja(true), 4, 64>(P, pts, JR, stage, CamRcOf{crec, P.extr}, acc);
   double tot[2];
   block_sum<2>(acc, lds, tot);
   if (threadIdx.x == 0) {
@@ -862,7 +882,7 @@ __global__ __launch_bounds__(NT) void k_linearize_lds_t(DevProblem P, const doub
     else return CamLds{tbl + c * kTblRec, ktb + c * 9};
   };
   auto init = [&] { if (HOOK) fill_lin_table<NT>(P, rec, tbl, ktb); };
-  if (MODE != 3) lin_waves<NT / 64, ROWS, decltype(cam_of), MODE>(P, pts, JR, stage, cam_of, acc, init);
+  if (MODE != 3) lin_waves<jr_ja(false), NT / 64, ROWS, decltype(cam_of), MODE>(P, pts, JR, stage, cam_of, acc, init);
   double tot[2];
   block_sum<2>(acc, lds, tot);
   if (threadIdx.x == 0) {
@@ -875,18 +895,10 @@ __global__ __launch_bounds__(NT) void k_linearize_lds_t(DevProblem P, const doub
 #endif
 constexpr int kLinNT = 512, kLinRows = BA_LIN_ROWS;    // product configuration (tools/lin_probe.hip)
 
-__device__ inline void load_jr(const double* __restrict__ JR, int no, int o, double (&v)[kJR]) {
-  const double2* a = reinterpret_cast<const double2*>(jr_a(JR, o));
-  const double2* b = reinterpret_cast<const double2*>(jr_b(JR, no, o));
-#pragma unroll
-  for (int k = 0; k < kJA / 2; ++k) { const double2 t = a[k]; v[2 * k] = t.x; v[2 * k + 1] = t.y; }
-#pragma unroll
-  for (int k = 0; k < kJB / 2; ++k) { const double2 t = b[k]; v[kJA + 2 * k] = t.x; v[kJA + 2 * k + 1] = t.y; }
-}
-
 // ---------------------------------------------------------------------------
 // point blocks: Hpp (xx,xy,xz,yy,yz,zz), gp, jacobi scale, LM diagonal, norms
 // ---------------------------------------------------------------------------
+template <int JA>
 __global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const double* __restrict__ JR,
                                                         const double* __restrict__ pts, double* __restrict__ Hpp,
                                                         double* __restrict__ gp, double* __restrict__ scale_p,
@@ -901,7 +913,7 @@ __global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const doub
     double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
     const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
     for (int o = o0; o < o1; ++o) {
-      const double2* s = reinterpret_cast<const double2*>(jr_b(JR, P.no, o));
+      const double2* s = reinterpret_cast<const double2*>(jr_b<JA>(JR, P.no, o));
       const double2 t0 = s[0], t1 = s[1], t2 = s[2], t3 = s[3];
       const double jp[2][3] = {{t0.x, t0.y, t1.x}, {t1.y, t2.x, t2.y}};
       const double rr[2] = {t3.x, t3.y};
@@ -952,12 +964,14 @@ __global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const doub
 // Hcc (lower 21) and gc per camera, slice blockIdx.y of its observations;
 // two observations in flight per thread (the camera-order index is one load
 // ahead of the record gathers)
+template <int JA>
 __device__ inline void cam_acc_jr(const double* __restrict__ JR, int no, int o, double (&acc)[27]) {
-  const double2* s = reinterpret_cast<const double2*>(jr_a(JR, o));
+  const double2* s = reinterpret_cast<const double2*>(jr_a<JA>(JR, o));
   double jc[12];
 #pragma unroll
   for (int k = 0; k < 6; ++k) { const double2 t = s[k]; jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
-  const double2 rt = reinterpret_cast<const double2*>(jr_b(JR, no, o))[3];
+  // JA = 14: the residual copy in the same record, else JB's
+  const double2 rt = JA == 14 ? s[6] : reinterpret_cast<const double2*>(jr_b<JA>(JR, no, o))[3];
   const double rr[2] = {rt.x, rt.y};
 #pragma unroll
   for (int row = 0; row < 2; ++row) {
@@ -971,7 +985,7 @@ __device__ inline void cam_acc_jr(const double* __restrict__ JR, int no, int o, 
     for (int a = 0; a < 6; ++a) acc[21 + a] += j[a] * rr[row];
   }
 }
-template <int NT>
+template <int NT, int JA>
 __global__ __launch_bounds__(NT) void k_cam_assemble(DevProblem P, const double* __restrict__ JR,
                                                      double* __restrict__ cpart, double* __restrict__ Hcc,
                                                      double* __restrict__ gc) {
@@ -986,8 +1000,8 @@ __global__ __launch_bounds__(NT) void k_cam_assemble(DevProblem P, const double*
   for (int i = i0 + threadIdx.x; i < i1; i += 2 * bd) {
     const bool two = i + bd < i1;
     const int oa = P.cam_op[i].x, ob = P.cam_op[two ? i + bd : i].x;
-    cam_acc_jr(JR, P.no, oa, acc);
-    if (two) cam_acc_jr(JR, P.no, ob, acc);
+    cam_acc_jr<JA>(JR, P.no, oa, acc);
+    if (two) cam_acc_jr<JA>(JR, P.no, ob, acc);
   }
   double out[27];
   block_sum<27>(acc, lds, out);
@@ -1120,6 +1134,7 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
                                                const double* __restrict__ Linv, WT* __restrict__ W) {
   using V2 = typename std::conditional<sizeof(WT) == 8, double2, float2>::type;
   constexpr int WAVES = 8;
+  constexpr int JA = jr_ja(!TBL);
   __shared__ double stage[WAVES * 64 * kStageLd];
   __shared__ double sct[TBL ? kLinLdsCams * 6 : 1];
   if (TBL) {
@@ -1161,16 +1176,16 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
   int ci0, pi0, ci1, pi1;
   load_idx(base, ci0, pi0);
   load_idx(base + step, ci1, pi1);
-  double2 t[kJR / 2];
-  jr_chunk_load(JR, P.no, min(base, P.no - 1), lane, t);
+  double2 t[JA / 2 + kJB / 2];
+  jr_chunk_load<JA>(JR, P.no, min(base, P.no - 1), lane, t);
   Fac fc;
   load_fac(base, ci0, pi0, fc);
   for (; base < P.no; base += step) {
     const int nb = base + step;
     int ci2, pi2;
     load_idx(nb + step, ci2, pi2);
-    double2 tn[kJR / 2];
-    jr_chunk_load(JR, P.no, min(nb, P.no - 1), lane, tn);
+    double2 tn[JA / 2 + kJB / 2];
+    jr_chunk_load<JA>(JR, P.no, min(nb, P.no - 1), lane, tn);
     Fac fn;
     load_fac(nb, ci1, pi1, fn);
     const bool live = fc.live;
@@ -1180,7 +1195,7 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
     const double s0 = fc.sp[0], s1 = fc.sp[1], s2 = fc.sp[2];
     const double i00 = fc.li[0], i10 = fc.li[1], i11 = fc.li[2];
     const double i20 = fc.li[3], i21 = fc.li[4], i22 = fc.li[5];
-    jr_chunk_stage(st, lane, t);
+    jr_chunk_stage<JA>(st, lane, t);
     wave_lds_sync();
     double j[18];
 #pragma unroll
@@ -1225,7 +1240,7 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
       }
     }
 #pragma unroll
-    for (int k = 0; k < kJR / 2; ++k) t[k] = tn[k];
+    for (int k = 0; k < JA / 2 + kJB / 2; ++k) t[k] = tn[k];
     fc = fn;
     ci1 = ci2; pi1 = pi2;
   }
@@ -1322,6 +1337,7 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
                                                       const double* __restrict__ rec_c,
                                                       const double* __restrict__ pts_c, const double* __restrict__ gtbl,
                                                       double* __restrict__ part) {
+  constexpr int JA = jr_ja(GTBL);
   __shared__ double lds[3 * 16];
   __shared__ double stage[NT * kStageLd];
   __shared__ double tbl_s[GTBL ? 1 : kLinLdsCams * kCandRec];
@@ -1366,7 +1382,7 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
   const int step = gridDim.x * WAVES * 64;
   int base = (blockIdx.x * WAVES + w) * 64;
   if (P.no == 0) base = P.no;
-  double2 t[kJR / 2];
+  double2 t[JA / 2 + kJB / 2];
   int c = 0, p = 0;
   float2 uv = make_float2(0.f, 0.f);
   // GTBL: the lane's camera record (176 B, 16-B aligned) and K are gathered
@@ -1387,7 +1403,7 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
   };
   CandCam cq;
   if (base < P.no) {
-    jr_chunk_load(JR, P.no, base, lane, t);
+    jr_chunk_load<JA>(JR, P.no, base, lane, t);
     const int oc = min(base + lane, P.no - 1);
     c = P.obs_cam[oc]; p = P.obs_pt[oc]; uv = P.uv[oc];
     cam_load(c, cq);
@@ -1395,7 +1411,7 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
   for (; base < P.no; base += step) {
     const int o = base + lane;
     // stage this chunk's records
-    jr_chunk_stage(st, lane, t);
+    jr_chunk_stage<JA>(st, lane, t);
     const double dp0 = delta_p[3 * p], dp1 = delta_p[3 * p + 1], dp2 = delta_p[3 * p + 2];
     const double X0 = pts_c[3 * p], X1 = pts_c[3 * p + 1], X2 = pts_c[3 * p + 2];
     const bool cfix = P.cam_fixed && P.cam_fixed[c];
@@ -1405,7 +1421,7 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
     float2 uvn = uv;
     CandCam cqn;
     if (nb < P.no) {
-      jr_chunk_load(JR, P.no, nb, lane, t);
+      jr_chunk_load<JA>(JR, P.no, nb, lane, t);
       const int oc = min(nb + lane, P.no - 1);
       cn = P.obs_cam[oc]; pn = P.obs_pt[oc]; uvn = P.uv[oc];
       cam_load(cn, cqn);
@@ -1792,11 +1808,14 @@ void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s, hipE
 }
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
                            double max_diag, hipStream_t s) {
-  hipLaunchKernelGGL(k_point_assemble, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.JR, W.pts, W.Hpp, W.gp,
+  const bool many = P.nc > kLinLdsCams;
+  hipLaunchKernelGGL((many ? k_point_assemble<jr_ja(true)> : k_point_assemble<jr_ja(false)>), dim3(grid_for(P.np)),
+                     dim3(kThreads), 0, s, P, W.JR, W.pts, W.Hpp, W.gp,
                      W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
 }
 void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
+  const bool many = P.nc > kLinLdsCams;   // JR layout (jr_ja)
   // one workgroup per camera: measured faster than slicing at C3 (57 vs
   // 66 us at 8 slices) and at C5 (where 2048 / nvc < 1 anyway);
   // BA_ASM_SPLIT (diagnostics) overrides
@@ -1807,11 +1826,14 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (nt < 0) { const char* e = getenv("BA_ASM_THREADS"); nt = e ? atoi(e) : 0; }
   const int th = nt == 256 || nt == 512 || nt == 1024 ? nt : 512;   // C3: 54 us at 512, 57 at 256 / 1024
   if (th == 1024)
-    hipLaunchKernelGGL(k_cam_assemble<1024>, dim3(P.nvc, sl), dim3(1024), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
+    hipLaunchKernelGGL((many ? k_cam_assemble<1024, jr_ja(true)> : k_cam_assemble<1024, jr_ja(false)>), dim3(P.nvc, sl),
+                       dim3(1024), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
   else if (th == 512)
-    hipLaunchKernelGGL(k_cam_assemble<512>, dim3(P.nvc, sl), dim3(512), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
+    hipLaunchKernelGGL((many ? k_cam_assemble<512, jr_ja(true)> : k_cam_assemble<512, jr_ja(false)>), dim3(P.nvc, sl),
+                       dim3(512), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
   else
-    hipLaunchKernelGGL(k_cam_assemble<256>, dim3(P.nvc, sl), dim3(256), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
+    hipLaunchKernelGGL((many ? k_cam_assemble<256, jr_ja(true)> : k_cam_assemble<256, jr_ja(false)>), dim3(P.nvc, sl),
+                       dim3(256), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
   if (sl > 1)
     hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
                        nullptr);
@@ -1943,6 +1965,7 @@ __global__ __launch_bounds__(256) void k_stream_copy(const double2* __restrict__
     __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const ntd2*>(a + i)),
                                 reinterpret_cast<ntd2*>(b + i));
 }
+int jr_ja_host(int nc) { return jr_ja(nc > kLinLdsCams); }
 void launch_stream_copy(const double* a, double* b, size_t n2, hipStream_t s) {
   if (n2 == 0) return;
   const size_t g = std::min<size_t>((n2 + 255) / 256, 262144);

@@ -308,7 +308,7 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.rec_c = ctx->dalloc<double>((size_t)kCamRec * nc);
   W.crec = ctx->dalloc<double>((size_t)16 * nc);
   W.ctbl = ctx->dalloc<double>((size_t)22 * nc);
-  W.JR = ctx->dalloc<double>(20 * (size_t)no);
+  W.JR = ctx->dalloc<double>(22 * (size_t)no);   // JA [no][12 or 14] + JB [no][8] (ba_kernels.hip jr_ja)
   W.delta_p = ctx->dalloc<double>(3 * (size_t)np);
   W.Hpp = ctx->dalloc<double>(6 * (size_t)np);
   W.gp = ctx->dalloc<double>(3 * (size_t)np);
@@ -1034,13 +1034,17 @@ int ba_linearize(ba_ctx* ctx, double* r, double* J, double* cost) {
     ba_default_options(&o);
     LinResult L = linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
     const int no = ctx->no;
-    // record layout of ba_kernels.hip: JA [no][12] (Jc rows) then JB [no][8] (Jp rows, r)
-    std::vector<double> rec(20 * (size_t)no);
+    // record layout of ba_kernels.hip: JA [no][ja] (Jc rows; ja = 14: then r
+    // again) then JB [no][8] (Jp rows, r)
+    const int ja = bahip::jr_ja_host(ctx->P.nc);
+    std::vector<double> rec((size_t)(ja + 8) * no);
     HIP_OK(hipMemcpy(rec.data(), ctx->W.JR, sizeof(double) * rec.size(), hipMemcpyDeviceToHost));
     for (int s = 0; s < no; ++s) {
       const int o2 = ctx->perm[s];
-      const double* qa = &rec[(size_t)s * 12];
-      const double* qb = &rec[(size_t)12 * no + (size_t)s * 8];
+      const double* qa = &rec[(size_t)s * ja];
+      const double* qb = &rec[(size_t)ja * no + (size_t)s * 8];
+      if (ja == 14 && (qa[12] != qb[6] || qa[13] != qb[7]))
+        throw BaError{BA_ERR_DEVICE, "JR: the two residual copies differ"};
       if (r) { r[2 * o2] = qb[6]; r[2 * o2 + 1] = qb[7]; }
       if (J)
         for (int row = 0; row < 2; ++row) {
