@@ -25,7 +25,7 @@ def main():
     def allreduce(v, op):
         dist.all_reduce(torch.from_numpy(v), op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
 
-    p = scene()
+    p = scene(sys.argv[7] if len(sys.argv) > 7 else "c2")
     with Solver(0) as s:
         s.comm_init_host(allreduce, world, rank)
         s.set_problem(shard_points(p, world, rank))

@@ -20,14 +20,19 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from bundleadjustment_amd import Options, make_config
+from bundleadjustment_amd import Options, make_config, make_synthetic
 from bundleadjustment_amd.problem import fix_camera, shard_bounds
 
 ROOT = Path(__file__).resolve().parents[1]
 
 
-def scene():
-    # gauge-fixed (two anchors): one isolated minimum, trajectories comparable
+def scene(name="c2"):
+    # gauge-fixed (two anchors): one isolated minimum, trajectories comparable.
+    # "many": more cameras than the LDS camera table holds (> kLinLdsCams),
+    # so the compact-record linearisation, the global camera tables and the
+    # JR records with the residual copy run through the exchange path
+    if name == "many":
+        return fix_camera(make_synthetic(300, 12_000, 6, seed=0xBA5E0011), 1)
     return fix_camera(make_config("c2", scale=0.5), 1)
 
 
@@ -47,8 +52,19 @@ def free_port() -> int:
 @pytest.mark.parametrize("lin,prec", [("DENSE_SCHUR", "FP64"), ("ITERATIVE_SCHUR", "FP64"),
                                       ("ITERATIVE_SCHUR", "MIXED_FP32")])
 def test_sharded_solve_matches_single_rank(tmp_path, world, lin, prec):
+    run_sharded(tmp_path, world, lin, prec, "c2")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("lin", ["DENSE_SCHUR", "ITERATIVE_SCHUR"])
+def test_sharded_many_cameras_matches_single_rank(tmp_path, lin):
+    run_sharded(tmp_path, 2, lin, "FP64", "many")
+
+
+def run_sharded(tmp_path, world, lin, prec, name):
     from bundleadjustment_amd import Solver
-    p = scene()
+    p = scene(name)
     with Solver(0) as s:
         s.set_problem(p)
         ref = s.solve(solve_options(lin, prec))
@@ -57,7 +73,8 @@ def test_sharded_solve_matches_single_rank(tmp_path, world, lin, prec):
     port = str(free_port())
     env = dict(os.environ, PYTHONPATH=os.pathsep.join([str(ROOT / "tests"), str(ROOT)]))
     procs = [subprocess.Popen([sys.executable, str(ROOT / "tests" / "mr_worker.py"), str(r), str(world), port,
-                               str(tmp_path), lin, prec], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                               str(tmp_path), lin, prec, name], env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT,
                               text=True) for r in range(world)]
     outs = []
     for pr in procs:
