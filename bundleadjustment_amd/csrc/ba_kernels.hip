@@ -898,6 +898,11 @@ constexpr int kLinNT = 512, kLinRows = BA_LIN_ROWS;    // product configuration 
 // ---------------------------------------------------------------------------
 // point blocks: Hpp (xx,xy,xz,yy,yz,zz), gp, jacobi scale, LM diagonal, norms
 // ---------------------------------------------------------------------------
+// kPaLanes lanes per point: lane l of the group sums observations o0 + l,
+// o0 + l + kPaLanes, ... (adjacent lanes read adjacent 64-B JB records, one
+// 256-B segment per load instruction and group), then a fixed-order xor
+// reduction inside the group; lane 0 of the group finishes the point.
+constexpr int kPaLanes = 4;
 template <int JA>
 __global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const double* __restrict__ JR,
                                                         const double* __restrict__ pts, double* __restrict__ Hpp,
@@ -908,11 +913,13 @@ __global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const doub
   double acc[2] = {0.0, 0.0};  // gn2, xn2
   double gmax = 0.0;
   const size_t np = (size_t)P.np;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
+  const int sl = threadIdx.x & (kPaLanes - 1);
+  const int g0 = (blockIdx.x * blockDim.x + threadIdx.x) / kPaLanes, gs = gridDim.x * blockDim.x / kPaLanes;
+  for (int p = g0; p < P.np; p += gs) {      // uniform inside a lane group
     if (!P.pt_var[p]) continue;
     double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
     const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
-    for (int o = o0; o < o1; ++o) {
+    for (int o = o0 + sl; o < o1; o += kPaLanes) {
       const double2* s = reinterpret_cast<const double2*>(jr_b<JA>(JR, P.no, o));
       const double2 t0 = s[0], t1 = s[1], t2 = s[2], t3 = s[3];
       const double jp[2][3] = {{t0.x, t0.y, t1.x}, {t1.y, t2.x, t2.y}};
@@ -924,6 +931,17 @@ __global__ __launch_bounds__(256) void k_point_assemble(DevProblem P, const doub
         g[0] += a * rr[row]; g[1] += b * rr[row]; g[2] += c * rr[row];
       }
     }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+#pragma unroll
+      for (int x = kPaLanes / 2; x >= 1; x >>= 1) H[k] += __shfl_xor(H[k], x, kPaLanes);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int x = kPaLanes / 2; x >= 1; x >>= 1) g[k] += __shfl_xor(g[k], x, kPaLanes);
+    }
+    if (sl != 0) continue;
 #pragma unroll
     for (int k = 0; k < 6; ++k) Hpp[k * np + p] = H[k];
     const double hd[3] = {H[0], H[3], H[5]};
@@ -1809,7 +1827,8 @@ void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s, hipE
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
                            double max_diag, hipStream_t s) {
   const bool many = P.nc > kLinLdsCams;
-  hipLaunchKernelGGL((many ? k_point_assemble<jr_ja(true)> : k_point_assemble<jr_ja(false)>), dim3(grid_for(P.np)),
+  hipLaunchKernelGGL((many ? k_point_assemble<jr_ja(true)> : k_point_assemble<jr_ja(false)>),
+                     dim3(grid_for((int)std::min<long long>((long long)P.np * kPaLanes, 1LL << 30))),
                      dim3(kThreads), 0, s, P, W.JR, W.pts, W.Hpp, W.gp,
                      W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
 }
