@@ -204,11 +204,17 @@ constexpr int kStageLd = kJR + 1;   // LDS row stride of staged records
 // camera-order gathers then read one 112-B record (~1.75 lines) instead of
 // 96 B plus a JB line (~2.5 lines) — C5 shard +1.6 %; at C3 the 16 B/obs of
 // extra writes cost more than the gathers save (profiles/r02_v7_ab_jr_*).
+// JA = 16 (BA_JA_SMALL=16: 128-B records, one line per k_cam_assemble
+// gather) measured slower still at C3: k_linearize +5..7 us against the
+// gathers it saves (profiles/r02_s3_ab_ja16.txt).
 constexpr int kJB = 8;
 constexpr int kFJB = 12;   // record field of the first JB slot
-constexpr int jr_ja(bool many_cams) { return many_cams ? 14 : 12; }
-// JA slot k -> record field
-__device__ __forceinline__ int ja_field(int k) { return k < 12 ? k : k + 6; }
+#ifndef BA_JA_SMALL
+#define BA_JA_SMALL 12
+#endif
+constexpr int jr_ja(bool many_cams) { return many_cams ? 14 : BA_JA_SMALL; }
+// JA slot k -> record field (slots 12.. repeat the residual: 12/14 -> r0, 13/15 -> r1)
+__device__ __forceinline__ int ja_field(int k) { return k < 12 ? k : 18 + ((k - 12) & 1); }
 template <int JA>
 __device__ inline const double* jr_a(const double* JR, int o) { return JR + (size_t)o * JA; }
 template <int JA>
@@ -989,7 +995,7 @@ __device__ inline void cam_acc_jr(const double* __restrict__ JR, int no, int o, 
 #pragma unroll
   for (int k = 0; k < 6; ++k) { const double2 t = s[k]; jc[2 * k] = t.x; jc[2 * k + 1] = t.y; }
   // JA = 14: the residual copy in the same record, else JB's
-  const double2 rt = JA == 14 ? s[6] : reinterpret_cast<const double2*>(jr_b<JA>(JR, no, o))[3];
+  const double2 rt = JA >= 14 ? s[6] : reinterpret_cast<const double2*>(jr_b<JA>(JR, no, o))[3];
   const double rr[2] = {rt.x, rt.y};
 #pragma unroll
   for (int row = 0; row < 2; ++row) {

@@ -308,7 +308,7 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.rec_c = ctx->dalloc<double>((size_t)kCamRec * nc);
   W.crec = ctx->dalloc<double>((size_t)16 * nc);
   W.ctbl = ctx->dalloc<double>((size_t)22 * nc);
-  W.JR = ctx->dalloc<double>(22 * (size_t)no);   // JA [no][12 or 14] + JB [no][8] (ba_kernels.hip jr_ja)
+  W.JR = ctx->dalloc<double>((size_t)(std::max(bahip::jr_ja_host(nc), 14) + 8) * no);   // JA [no][jr_ja] + JB [no][8] (ba_kernels.hip)
   W.delta_p = ctx->dalloc<double>(3 * (size_t)np);
   W.Hpp = ctx->dalloc<double>(6 * (size_t)np);
   W.gp = ctx->dalloc<double>(3 * (size_t)np);
@@ -1043,7 +1043,7 @@ int ba_linearize(ba_ctx* ctx, double* r, double* J, double* cost) {
       const int o2 = ctx->perm[s];
       const double* qa = &rec[(size_t)s * ja];
       const double* qb = &rec[(size_t)ja * no + (size_t)s * 8];
-      if (ja == 14 && (qa[12] != qb[6] || qa[13] != qb[7]))
+      if (ja >= 14 && (qa[12] != qb[6] || qa[13] != qb[7]))
         throw BaError{BA_ERR_DEVICE, "JR: the two residual copies differ"};
       if (r) { r[2 * o2] = qb[6]; r[2 * o2 + 1] = qb[7]; }
       if (J)
