@@ -1558,13 +1558,19 @@ __device__ inline void acc_pair(double (&acc)[36], const double (&a)[18], const 
       acc[i * 6 + j] += a[i * 3] * b[j * 3] + a[i * 3 + 1] * b[j * 3 + 1] + a[i * 3 + 2] * b[j * 3 + 2];
 }
 
-// 16 lanes per block (4 blocks per wave): each lane accumulates every 16th
-// pair (two pairs' gathers in flight), then a 4-stage xor reduction inside
-// the 16-lane group; all 16 lanes then hold the sums and store 36/16 each.
+// PL lanes per block (64 / PL blocks per wave; PL = 16 by default,
+// BA_PAIR_LANES selects 8 or 32): each lane accumulates every PL-th pair
+// (two pairs' gathers in flight), then a log2(PL)-stage xor reduction inside
+// the lane group; all PL lanes then hold the sums and store 36/PL each.
+#ifndef BA_PAIR_LANES
+#define BA_PAIR_LANES 16
+#endif
+constexpr int kPairLanes = BA_PAIR_LANES;
 __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* __restrict__ blocks, int nblocks,
                                                      const int2* __restrict__ pairs, const double* __restrict__ W,
                                                      double* __restrict__ S) {
-  const int lane = threadIdx.x & 63, sl = lane & 15, sub = lane >> 4;
+  constexpr int PL = kPairLanes, BPW = 64 / PL;
+  const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
   // XCD-aware order: workgroups b and b + 8 share an XCD (round-robin
   // dispatch).  XCD x owns the contiguous block range [x R, (x+1) R) (a few
   // rows I of S) and its workgroups sweep it in rounds, so the W rows of the
@@ -1575,7 +1581,7 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
   const int r0 = xcd * R, r1 = min(nblocks, r0 + R);
   const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   const size_t ld = (size_t)P.ld;
-  for (int base = r0 + (wx * nwv + wv) * 4; base < r1; base += nwx * nwv * 4) {
+  for (int base = r0 + (wx * nwv + wv) * BPW; base < r1; base += nwx * nwv * BPW) {
     const int bi = base + sub;
     const bool live = bi < r1;
     const int4 blk = live ? blocks[bi] : make_int4(0, 0, 0, 0);
@@ -1583,8 +1589,8 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
 #pragma unroll
     for (int k = 0; k < 36; ++k) acc[k] = 0.0;
     int e = blk.z + sl;
-    for (; e + 16 < blk.w; e += 32) {
-      const int2 p0 = pairs[e], p1 = pairs[e + 16];
+    for (; e + PL < blk.w; e += 2 * PL) {
+      const int2 p0 = pairs[e], p1 = pairs[e + PL];
       double a0[18], b0[18], a1[18], b1[18];
       load_w(W, p0.x, a0); load_w(W, p0.y, b0);
       load_w(W, p1.x, a1); load_w(W, p1.y, b1);
@@ -1600,17 +1606,15 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
 #pragma unroll
     for (int k = 0; k < 36; ++k) {
       double v = acc[k];
-      v += __shfl_xor(v, 8, 16);
-      v += __shfl_xor(v, 4, 16);
-      v += __shfl_xor(v, 2, 16);
-      v += __shfl_xor(v, 1, 16);
+#pragma unroll
+      for (int x = PL / 2; x >= 1; x >>= 1) v += __shfl_xor(v, x, PL);
       acc[k] = v;
     }
     if (live) {
       const int I = blk.x, Jb = blk.y;
 #pragma unroll
       for (int k = 0; k < 36; ++k) {
-        if ((k & 15) != sl) continue;
+        if ((k % PL) != sl) continue;
         const int i = k / 6, j = k % 6;
         if (I != Jb) S[(size_t)(6 * I + i) * ld + 6 * Jb + j] = -acc[k];
         else if (j <= i) S[(size_t)(6 * I + i) * ld + 6 * I + j] -= acc[k];  // duplicate obs of one point by one camera
