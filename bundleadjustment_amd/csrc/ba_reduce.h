@@ -103,7 +103,10 @@ __device__ inline void w_pair(const float* __restrict__ base, int c, double& x, 
 // 256-B (fp64) segments instead of 64 records 1.4 KB apart -- every cache
 // line is requested once.  Fixed-order xor reduction inside the group: all
 // lanes of the group get the same (deterministic) sum.
-constexpr int kPtLanes = 16;
+#ifndef BA_PT_LANES
+#define BA_PT_LANES 16
+#endif
+constexpr int kPtLanes = BA_PT_LANES;
 // UNROLL: four pairs per round with every load issued first (the PCG point
 // passes: C5 shard +2.6 %); the back substitution keeps the one-pair loop
 // (the unrolled form measured 37.8 -> 41.9 us there at C3)
