@@ -24,8 +24,18 @@ Workloads (--workload):
        (8 blocks of 1.25M points), ITERATIVE_SCHUR with the W blocks stored in
        fp32 (BA_MIXED_FP32).
 
+Default workload: c3 at N = 1 (the single-GPU roofline config), c4 at N > 1
+(BASELINE configs[3], the multi-GPU config).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c4|c5]
-       (N>1 via python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+  N > 1 either under a launcher (python -m torch.distributed.run
+  --nproc-per-node N bench.py --gpus N ...: RANK / LOCAL_RANK / WORLD_SIZE set,
+  WORLD_SIZE must equal N) or standalone: without WORLD_SIZE the process
+  starts N rank processes itself (before touching the GPU), rank r on device
+  r, and relays rank 0's JSON line.
+  --transport host: the exchange goes through torch.distributed gloo on the
+  host instead of RCCL (several ranks on one GPU, tests; --device pins every
+  rank to one device).
 """
 from __future__ import annotations
 
@@ -96,7 +106,7 @@ STRONG = {   # global problems of the strong-scaling workloads: 8 fixed point bl
 }
 
 
-def strong_shard(cfg: str, rank: int, world: int):
+def strong_shard(cfg: str, rank: int, world: int, scale: float = 1.0):
     """Rank `rank`'s part of the fixed global problem of `cfg`: point blocks
     b = rank, rank + world, ... of 8 (block b drawn with point_seed
     seed + 7919 b over the shared cameras), concatenated.  The union over the
@@ -106,7 +116,7 @@ def strong_shard(cfg: str, rank: int, world: int):
     from bundleadjustment_amd.problem import CONFIG_INDEX
     nb = STRONG[cfg]["blocks"]
     seed = 0xBA5E0000 + CONFIG_INDEX[cfg]
-    parts = [make_config(cfg, scale=1.0 / nb, point_seed=seed + 7919 * b) for b in range(rank, nb, world)]
+    parts = [make_config(cfg, scale=scale / nb, point_seed=seed + 7919 * b) for b in range(rank, nb, world)]
     p = parts[0].copy()
     off = np.cumsum([0] + [q.n_pts for q in parts])
     p.pts = np.concatenate([q.pts for q in parts])
@@ -144,15 +154,87 @@ def cpu_baseline_leg(problem, cfg: str, target_s: float):
                                   "note": "num_threads = 4 as configureSolver sets it (Optimizer.cpp:88)"}}
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str], timeout_s: float | None = None) -> int:
+    """Standalone N > 1: start N copies of this script as ranks 0..N-1 (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT set), rank 0's
+    stdout relayed as ours, every rank's stderr passed through.  Runs before
+    anything in this process touches the GPU (the ranks own the devices).
+    Returns the first non-zero exit status (the other ranks are then
+    terminated), else 0."""
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + argv, env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    deadline = None if timeout_s is None else time.time() + timeout_s
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for pr in list(pending):
+            code = pr.poll()
+            if code is None:
+                continue
+            pending.remove(pr)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:   # a failed rank would leave the others waiting in a collective
+                    q.terminate()
+        if deadline is not None and time.time() > deadline:
+            for q in pending:
+                q.kill()
+            rc = rc or 124
+            break
+        time.sleep(0.05)
+    for pr in procs:
+        pr.wait()
+    return rc
+
+
+def host_transport(rank: int, world: int):
+    """gloo process group for --transport host (the ba_comm_init_host hook)."""
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allreduce(v, op):
+        dist.all_reduce(torch.from_numpy(v), op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    return allreduce
+
+
+def dry_run_line(args, rank, world, local_rank, device):
+    """BA_BENCH_DRYRUN=1 (CPU tests of the launch logic): what this rank would
+    run, without any GPU call."""
+    return json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local_rank, "device": device,
+                       "workload": args.workload, "transport": args.transport, "steps": args.steps,
+                       "warmup": args.warmup})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c4", "c5"],
-                    help="c3: weak scaling of configs[2] (default); c4 / c5: strong scaling of configs[3] / [4]")
+    ap.add_argument("--workload", default=None, choices=["c3", "c4", "c5"],
+                    help="c3: weak scaling of configs[2] (default at N = 1); c4 / c5: strong scaling of "
+                         "configs[3] / [4] (c4 is the default at N > 1)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
+                    help="multi-rank exchange: RCCL over xGMI (default) or host-staged through gloo (tests)")
+    ap.add_argument("--device", type=int, default=None, help="HIP device of every rank (default: LOCAL_RANK)")
     ap.add_argument("--config", default=None, help="weak mode: per-GPU config (default c3)")
-    ap.add_argument("--scale", type=float, default=1.0, help="weak mode: point-count scale of the per-GPU shard")
+    ap.add_argument("--scale", type=float, default=1.0,
+                    help="point-count scale of the problem (weak: of the per-GPU shard; strong: of the global "
+                         "problem); 1 = the BASELINE size")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target length of each CPU-baseline sample")
     ap.add_argument("--comm", action="store_true", help="use an RCCL communicator even at one rank (tests)")
@@ -162,32 +244,53 @@ def main():
     ap.add_argument("--precision", default=None, choices=["FP64", "MIXED_FP32"],
                     help="MIXED_FP32: fp32 storage of the per-observation Schur blocks (iterative only)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {args.gpus})")
+    if args.workload is None:
+        args.workload = "c3" if args.gpus == 1 else "c4"
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if args.workload in STRONG and 8 % args.gpus != 0:
+        raise SystemExit(f"--workload {args.workload}: the 8 point blocks need a rank count dividing 8 "
+                         f"(got {args.gpus})")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:   # standalone N > 1: this process only launches and relays
+            sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+        world, rank, local_rank = 1, 0, 0
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+        if world != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a {world}-rank run "
+                             f"as {args.gpus} GPU(s)")
+    device = local_rank if args.device is None else args.device
+    if os.environ.get("BA_BENCH_DRYRUN") == "1":
+        if os.environ.get("BA_BENCH_DRYRUN_FAIL_RANK") == str(rank):
+            raise SystemExit(3)
+        print(dry_run_line(args, rank, world, local_rank, device), flush=True)
+        if rank != 0:   # a surviving rank of a failed launch is terminated by the parent
+            time.sleep(float(os.environ.get("BA_BENCH_DRYRUN_SLEEP", "0")))
+        return
 
     from bundleadjustment_amd import Options, Solver, make_config
     from bundleadjustment_amd.problem import CONFIG_INDEX, CONFIGS
 
     strong = args.workload in STRONG
     cfg = args.workload if strong else (args.config or "c3")
-    if strong and 8 % world != 0:
-        raise SystemExit(f"--workload {cfg}: the 8 point blocks need a rank count dividing 8 (got {world})")
     seed = 0xBA5E0000 + CONFIG_INDEX[cfg]
     t = time.time()
     if strong:
-        problem = strong_shard(cfg, rank, world)
+        problem = strong_shard(cfg, rank, world, args.scale)
     else:
         problem = make_config(cfg, scale=args.scale, point_seed=None if rank == 0 else seed + 7919 * rank)
     log(f"[rank {rank}] problem {cfg}: {problem.n_cams} cams x {problem.n_pts} pts x {problem.n_obs} obs "
         f"(generated in {time.time() - t:.1f}s)")
 
-    solver = Solver(local_rank)
+    solver = Solver(device)
     use_comm = world > 1 or args.comm
-    if use_comm:
+    if use_comm and args.transport == "host":
+        solver.comm_init_host(host_transport(rank, world), world, rank)
+    elif use_comm:
         # RCCL communicator; the 128-byte id travels through a file keyed by the
         # launcher (no second GPU runtime in this process for the rendezvous)
         uid = rendezvous_uid(rank, world)
@@ -294,8 +397,11 @@ def main():
             "data": "synthetic (BAL-style, SURVEY.md §8d generator, seeded)",
             "config": {"workload": workload,
                        "global_obs": n_obs_total,
+                       "scale": args.scale,
                        "solver": solver_s,
-                       "parallelism": f"points sharded x{world}, RCCL all-reduce of {exchange}"},
+                       "parallelism": f"points sharded x{world}, "
+                                      f"{'RCCL' if args.transport == 'rccl' else 'host-staged (gloo)'} "
+                                      f"all-reduce of {exchange}"},
             "device_ms_per_step": round(ms_dev, 4),
             "roofline": roofline,
             "iteration_roofline": iteration_roofline,

@@ -58,7 +58,7 @@ struct DevWork {
   double* rec;   double* rec_c;      // camera records at x / x'
   double* crec;                      // [nc][16] compact camera records (w, t, K, flag, theta terms) for > kLinLdsCams cameras
   double* ctbl;                      // [nc][22] candidate camera table for > kLinLdsCams cameras
-  double* JR;                        // [no][20] AoS: Jc row0 (6), Jc row1 (6), Jp rows (3+3), r (2)
+  double* JR;                        // JA [no][JA] (Jc rows 0..1; JA = 14 beyond kLinLdsCams cameras: + r again), then JB [no][8] (Jp rows 3+3, r 2)
   double* delta_p;                   // [np][3] point step (scaled back)
   double* Hpp;   double* gp;         // [6][np], [3][np]
   double* scale_p; double* diag_p;   // [3][np]

@@ -1169,6 +1169,9 @@ __global__ __launch_bounds__(512) void k_obs_w(DevProblem P, const double* __res
     }
     __syncthreads();
   }
+  // Required before the prologue below: it issues loads at indices clamped to
+  // P.no - 1 (obs_cam, the JR chunk, the factors), which are out of bounds
+  // (index -1) for a rank shard without observations.
   if (P.no == 0) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double* st = stage + w * (64 * kStageLd);

@@ -154,20 +154,28 @@ struct ba_ctx {
       if (host_fn(host_user, host_buf.data(), (int64_t)count, op == ncclMax ? 1 : 0) != 0)
         throw BaError{BA_ERR_COMM, "host all-reduce callback failed"};
       HIP_OK(hipMemcpyAsync(d, host_buf.data(), sizeof(double) * count, hipMemcpyHostToDevice, stream));
+      // host_buf is pageable and reused by the next call: wait for the copy
+      // (test transport, latency irrelevant)
+      HIP_OK(hipStreamSynchronize(stream));
       return;
     }
     NCCL_OK(ncclAllReduce(d, d, count, ncclDouble, op, comm, stream));
   }
-  // host values (set_problem structure, bench timing)
+  // host values (set_problem structure, bench timing); one device scratch
+  // buffer, grown on demand and kept for the context's lifetime
+  double* hv_scratch = nullptr;
+  size_t hv_cap = 0;
   void allreduce_host_values(double* v, size_t count, int op) {
     if (!has_comm() || count == 0) return;
-    double* d = nullptr;
-    HIP_OK(hipMalloc(&d, sizeof(double) * count));
-    HIP_OK(hipMemcpyAsync(d, v, sizeof(double) * count, hipMemcpyHostToDevice, stream));
-    allreduce(d, count, op == 1 ? ncclMax : ncclSum);
-    HIP_OK(hipMemcpyAsync(v, d, sizeof(double) * count, hipMemcpyDeviceToHost, stream));
+    if (count > hv_cap) {
+      if (hv_scratch) { (void)hipStreamSynchronize(stream); (void)hipFree(hv_scratch); hv_scratch = nullptr; hv_cap = 0; }
+      HIP_OK(hipMalloc(&hv_scratch, sizeof(double) * count));
+      hv_cap = count;
+    }
+    HIP_OK(hipMemcpyAsync(hv_scratch, v, sizeof(double) * count, hipMemcpyHostToDevice, stream));
+    allreduce(hv_scratch, count, op == 1 ? ncclMax : ncclSum);
+    HIP_OK(hipMemcpyAsync(v, hv_scratch, sizeof(double) * count, hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
-    (void)hipFree(d);
   }
   void read_scalars() {
     HIP_OK(hipMemcpyAsync(h_scal, W.scal, sizeof(double) * (kNumSlots + kPcgState), hipMemcpyDeviceToHost, stream));
@@ -308,7 +316,7 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.rec_c = ctx->dalloc<double>((size_t)kCamRec * nc);
   W.crec = ctx->dalloc<double>((size_t)16 * nc);
   W.ctbl = ctx->dalloc<double>((size_t)22 * nc);
-  W.JR = ctx->dalloc<double>((size_t)(std::max(bahip::jr_ja_host(nc), 14) + 8) * no);   // JA [no][jr_ja] + JB [no][8] (ba_kernels.hip)
+  W.JR = ctx->dalloc<double>((size_t)(bahip::jr_ja_host(nc) + 8) * no);   // JA [no][jr_ja] + JB [no][8] (ba_kernels.hip)
   W.delta_p = ctx->dalloc<double>(3 * (size_t)np);
   W.Hpp = ctx->dalloc<double>(6 * (size_t)np);
   W.gp = ctx->dalloc<double>(3 * (size_t)np);
@@ -858,27 +866,7 @@ extern "C" {
 
 int ba_abi_version(void) { return BA_ABI_VERSION; }
 
-void ba_default_options(ba_options* o) {
-  if (!o) return;
-  o->max_num_iterations = 50;
-  o->max_num_consecutive_invalid_steps = 5;
-  o->jacobi_scaling = 1;
-  o->linear_solver = BA_DENSE_SCHUR;
-  o->function_tolerance = 1e-6;
-  o->gradient_tolerance = 1e-10;
-  o->parameter_tolerance = 1e-8;
-  o->initial_trust_region_radius = 1e4;
-  o->max_trust_region_radius = 1e16;
-  o->min_trust_region_radius = 1e-32;
-  o->min_relative_decrease = 1e-3;
-  o->min_lm_diagonal = 1e-6;
-  o->max_lm_diagonal = 1e32;
-  o->preconditioner_type = BA_JACOBI;
-  o->max_linear_solver_iterations = 500;
-  o->min_linear_solver_iterations = 0;
-  o->precision = BA_FP64;
-  o->eta = 1e-1;
-}
+// ba_default_options: host/ba_options.cpp (plain C++, shared with the sanitizer build)
 
 int ba_create(ba_ctx** out, int device) {
   if (!out) return BA_ERR_INVALID_ARGUMENT;
@@ -910,6 +898,7 @@ int ba_destroy(ba_ctx* ctx) {
   for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
   if (ctx->h_scal) (void)hipHostFree(ctx->h_scal);
   if (ctx->pose_buf) (void)hipFree(ctx->pose_buf);
+  if (ctx->hv_scratch) (void)hipFree(ctx->hv_scratch);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return BA_OK;
@@ -1043,7 +1032,9 @@ int ba_linearize(ba_ctx* ctx, double* r, double* J, double* cost) {
       const int o2 = ctx->perm[s];
       const double* qa = &rec[(size_t)s * ja];
       const double* qb = &rec[(size_t)ja * no + (size_t)s * 8];
-      if (ja >= 14 && (qa[12] != qb[6] || qa[13] != qb[7]))
+      // bit patterns, not values: a NaN residual (zero depth) is still a
+      // faithful copy of itself
+      if (ja >= 14 && (std::memcmp(&qa[12], &qb[6], 2 * sizeof(double)) != 0))
         throw BaError{BA_ERR_DEVICE, "JR: the two residual copies differ"};
       if (r) { r[2 * o2] = qb[6]; r[2 * o2 + 1] = qb[7]; }
       if (J)

@@ -335,11 +335,12 @@ def make_config(name: str, scale: float = 1.0, **overrides) -> Problem:
     return make_synthetic(seed=seed, name=name, **cfg)
 
 
-def shard_points(problem: Problem, nranks: int, rank: int) -> Problem:
+def shard_points(problem: Problem, nranks: int, rank: int, bounds: list[int] | None = None) -> Problem:
     """Point-sharded slice for multi-GPU: contiguous point
-    ranges balanced by observation count; cameras replicated; the shard keeps
+    ranges balanced by observation count (or the given `bounds`, nranks + 1
+    point offsets; a rank may get none); cameras replicated; the shard keeps
     only its points' observations (re-indexed)."""
-    bounds = shard_bounds(problem, nranks)
+    bounds = shard_bounds(problem, nranks) if bounds is None else bounds
     p0, p1 = bounds[rank], bounds[rank + 1]
     sel = (problem.obs_pt >= p0) & (problem.obs_pt < p1)
     sub = problem.copy()

@@ -37,6 +37,7 @@
 #ifndef BA_HIP_H_
 #define BA_HIP_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus

@@ -44,6 +44,16 @@ struct Scene {
   std::vector<std::shared_ptr<Frame>> frames;
   std::vector<std::shared_ptr<MapPoint>> points;
   int erase_calls = 0;
+  Scene() = default;
+  Scene(Scene&&) = default;
+  Scene& operator=(Scene&&) = default;
+  // frames and points own each other (Frame::mps <-> MapPoint::obs, as the
+  // reference's model does): break the cycles so the scene is freed (the
+  // ASan build's leak check, tests/cpp `make sanitize`)
+  ~Scene() {
+    for (auto& f : frames) if (f) f->mps.clear();
+    for (auto& p : points) if (p) p->obs.clear();
+  }
 };
 
 struct Model {

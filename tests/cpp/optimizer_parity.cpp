@@ -108,6 +108,7 @@ int main(int argc, char** argv) {
     OracleBackend be;
     return run(be, seed);
   }
+#ifndef BA_NO_HIP_BACKEND   // the sanitizer build links the oracle only (make sanitize)
   if (which == "hip") {
     try {
       ba_amd::HipBackend be(0);
@@ -117,6 +118,7 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
+#endif
   std::fprintf(stderr, "usage: %s hip|oracle [seed]\n", argv[0]);
   return 1;
 }

@@ -19,16 +19,17 @@ def main():
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from bundleadjustment_amd import Options, Solver
-    from test_gpu_multirank import scene, solve_options
+    from test_gpu_multirank import scene, scene_bounds, solve_options
     from bundleadjustment_amd.problem import shard_points
 
     def allreduce(v, op):
         dist.all_reduce(torch.from_numpy(v), op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
 
-    p = scene(sys.argv[7] if len(sys.argv) > 7 else "c2")
+    name = sys.argv[7] if len(sys.argv) > 7 else "c2"
+    p = scene(name)
     with Solver(0) as s:
         s.comm_init_host(allreduce, world, rank)
-        s.set_problem(shard_points(p, world, rank))
+        s.set_problem(shard_points(p, world, rank, scene_bounds(p, world, name)))
         summ = s.solve(solve_options(lin, prec))
         cams, pts = s.params()
         log = s.iteration_log()

@@ -38,6 +38,8 @@ from bundleadjustment_amd import Options, Solver, make_config, make_synthetic
 from bundleadjustment_amd import problem as bp
 from conftest import assert_close, compare_logs
 
+from writeback import assert_float_output_within_1ulp  # noqa: E402
+
 pytestmark = pytest.mark.gpu
 
 
@@ -85,6 +87,7 @@ def test_c4_shard_first_iterations_match_oracle(solver, oracle_lib, c4_shard, li
     assert summ.final_cost < summ.initial_cost
     assert_close(cams, oc, 1e-8, 1e-10, "cameras")
     assert_close(pts, op, 1e-8, 1e-10, "points")
+    assert_float_output_within_1ulp(cams, pts, oc, op, f"C4 shard {lin}")   # SURVEY.md §8c float-cast bar
 
 
 # ---------------------------------------------------------------------------

@@ -33,7 +33,18 @@ def scene(name="c2"):
     # JR records with the residual copy run through the exchange path
     if name == "many":
         return fix_camera(make_synthetic(300, 12_000, 6, seed=0xBA5E0011), 1)
+    if name == "empty":
+        return fix_camera(make_config("c2", scale=0.25), 1)
     return fix_camera(make_config("c2", scale=0.5), 1)
+
+
+def scene_bounds(p, world, name):
+    """Point offsets of the ranks' shards: balanced, or for "empty" every
+    point on rank 0 and none on the others (a rank with no observations: the
+    clamped-index prologues of k_obs_w & co. and the max_no choice)."""
+    if name == "empty":
+        return [0] + [p.n_pts] * world
+    return shard_bounds(p, world)
 
 
 def solve_options(lin, prec):
@@ -62,6 +73,14 @@ def test_sharded_many_cameras_matches_single_rank(tmp_path, lin):
     run_sharded(tmp_path, 2, lin, "FP64", "many")
 
 
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("lin,prec", [("DENSE_SCHUR", "FP64"), ("ITERATIVE_SCHUR", "FP64"),
+                                      ("ITERATIVE_SCHUR", "MIXED_FP32")])
+def test_sharded_solve_with_an_empty_rank(tmp_path, lin, prec):
+    run_sharded(tmp_path, 2, lin, prec, "empty")
+
+
 def run_sharded(tmp_path, world, lin, prec, name):
     from bundleadjustment_amd import Solver
     p = scene(name)
@@ -86,7 +105,7 @@ def run_sharded(tmp_path, world, lin, prec, name):
             raise
     assert all(pr.returncode == 0 for pr in procs), "\n".join(outs)
     res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
-    bounds = shard_bounds(p, world)
+    bounds = scene_bounds(p, world, name)
     for r, d in enumerate(res):
         assert np.array_equal(d["cams"], res[0]["cams"])          # replicated, identical decisions
         assert d["ok"].tolist() == [x["step_is_successful"] for x in rlog]
@@ -95,3 +114,27 @@ def run_sharded(tmp_path, world, lin, prec, name):
         np.testing.assert_allclose(d["pts"], rp[bounds[r]:bounds[r + 1]], rtol=1e-8, atol=1e-10)
     np.testing.assert_allclose(res[0]["cams"], rc, rtol=1e-8, atol=1e-10)
     assert float(res[0]["final"]) == pytest.approx(ref.final_cost, rel=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_gpus_2_launches_its_ranks(tmp_path):
+    """`bench.py --gpus 2` without a launcher starts both ranks itself and
+    reports the 2-rank C4 strong-scaling line (host-staged transport: both
+    ranks share the box's one GPU)."""
+    import json
+    sys.path.insert(0, str(ROOT))
+    import bench
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--workload", "c4", "--scale",
+                          "0.02", "--steps", "3", "--warmup", "1", "--transport", "host", "--device", "0",
+                          "--no-cpu-baseline"], capture_output=True, text=True, timeout=500, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    whole = bench.strong_shard("c4", 0, 1, 0.02)
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["steps"] == 3
+    assert d["config"]["global_obs"] == whole.n_obs
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    assert abs(d["value"] - whole.n_obs * 3 / (d["ms_per_step"] * 3e-3) / 1e6) <= 0.01 * d["value"]

@@ -15,6 +15,7 @@ from bundleadjustment_amd import problem as bp
 from bundleadjustment_amd._native import BAError
 from conftest import assert_close, compare_logs
 from golden_problems import golden_expected, golden_problem
+from writeback import assert_float_output_within_1ulp
 
 pytestmark = pytest.mark.gpu
 
@@ -63,10 +64,12 @@ def test_linearize_matches_oracle(solver, oracle_lib, cfg):
 # ---------------------------------------------------------------------------
 # full LM solves: iteration log + final parameters
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("cfg,iters,anchors", [("f2f", 20, 0), ("c2", 50, 2), ("c1", 8, 1)])
+@pytest.mark.parametrize("cfg,iters,anchors", [("f2f", 20, 0), ("c2", 50, 2), ("c1", 50, 2), ("c1", 8, 1)])
 def test_solve_matches_oracle(solver, oracle_lib, cfg, iters, anchors):
     """Well-posed problems (motion-only, or two anchored keyframes: no free
-    gauge): the whole LM trajectory and the final parameters match."""
+    gauge): the whole LM trajectory and the final parameters match, and the
+    observable float write-back (Optimizer.cpp:252-267) is identical or
+    within 1 float ulp per entry."""
     p = make_config(cfg)
     if anchors == 2:
         bp.fix_camera(p, 1)
@@ -79,6 +82,7 @@ def test_solve_matches_oracle(solver, oracle_lib, cfg, iters, anchors):
     assert summ.final_cost == pytest.approx(osum["final_cost"], rel=1e-10)
     assert_close(cams, oc, 1e-8, 1e-10, "cameras")
     assert_close(pts, op, 1e-8, 1e-10, "points")
+    assert_float_output_within_1ulp(cams, pts, oc, op, f"{cfg}/{anchors} anchors")
 
 
 def test_solve_gauge_free_matches_oracle(solver, oracle_lib):

@@ -143,27 +143,11 @@ def test_bal_write_principal_point_shift(tmp_path):
         bio.write_bal(tmp_path / "x.txt", bp.make_config("c1"))
 
 
-CPP = r"""
-#include "ba_io.hpp"
-#include <cstdio>
-int main(int argc, char** argv) {
-  try {
-    ba_amd::ProblemData p = ba_amd::load_problem(argv[1]);
-    ba_amd::save_problem(argv[2], p);
-    ba_amd::ProblemData b = ba_amd::read_bal(argv[3], 2.0, false);
-    ba_amd::save_problem(argv[4], b);
-    ba_problem v = p.view();
-    std::printf("%d %d %d\n", v.n_cams, v.n_pts, v.n_obs);
-  } catch (const std::exception& e) { std::printf("error: %s\n", e.what()); return 1; }
-  return 0;
-}
-"""
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
 def test_cpp_header_is_byte_compatible(tmp_path):
-    src = tmp_path / "io_rt.cpp"
-    src.write_text(CPP)
+    src = ROOT / "tests" / "cpp" / "io_rt.cpp"      # also built with ASan + UBSan (tests/test_sanitize.py)
     exe = tmp_path / "io_rt"
     subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", f"-I{ROOT / 'include'}",
                     f"-I{ROOT / 'bundleadjustment_amd' / 'host'}", str(src), "-o", str(exe)], check=True)

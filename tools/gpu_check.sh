@@ -15,7 +15,7 @@ stop_on_fault() {  # $1 = exit status of a GPU step
 }
 echo "== rocm-smi"; (rocm-smi --showproductname 2>&1 | head -20) || true
 echo "== pytest -m gpu"
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -rA > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 1500 python3 -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -30 $OUT/pytest_gpu.log; stop_on_fault $rc
 echo "== smoke"
 timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
