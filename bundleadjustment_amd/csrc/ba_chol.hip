@@ -160,17 +160,30 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
 constexpr long kSpinMax = 1L << 24;
 typedef int gi4 __attribute__((ext_vector_type(4)));
 
+//
+// The trailing s_nop 1 is part of the protocol.  hipcc treats an asm
+// statement as opaque and pads none of its hazards: without the nop the
+// compiler's next VALU may overwrite the store's data registers before the
+// 16-B store has read them (the VMEM-store-data hazard of stores wider than
+// 8 B; cdna_hip_programming.md §5.7 item 1).  Round 2's "V_K in registers"
+// variant hit exactly this: its register allocation put the y address into
+// the {epoch, 0} half of the granule's registers on the very next
+// instruction (v_lshl_add_u64 v[2:3] right after global_store_dwordx4 ...
+// v[0:3]), the granule went out with a wrong tag, and the consumers spun to
+// kSpinMax.  The shipping allocation happened to reuse no data register.
 __device__ inline void gran_store(double* g, double v, int epoch) {
   const long long b = __double_as_longlong(v);
   const gi4 d = {(int)b, (int)(b >> 32), epoch, 0};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(g), "v"(d) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(g), "v"(d) : "memory");
 }
-// waits for the granule of `epoch`; false if the spin bound was hit
+// waits for the granule of `epoch`; false if the spin bound was hit.  The
+// load and its wait are one statement with an early-clobber output, so the
+// compiler never sees the destination before the data has landed.
 __device__ inline bool gran_wait(const double* g, int epoch, double& v) {
   gi4 d;
   long it = 0;
   while (true) {
-    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(d) : "v"(g) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(d) : "v"(g) : "memory");
     if (d.z == epoch || it >= kSpinMax) break;
     __builtin_amdgcn_s_sleep(1);
     ++it;
@@ -216,6 +229,15 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
   } else if (tid < CB) {
     zs[tid] = tid < bsz ? Lm[(size_t)n * lds + s0 + tid] : 0.0;
   }
+  // V_K (the column block this thread needs for y_K) is loaded before the
+  // hand-off loop, so the final product after the last hand-off reads only
+  // registers and LDS
+  double vk[16];
+  {
+    const double* V = Vall + (size_t)K * CB * CB;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) vk[q] = V[(size_t)(h + 4 * q) * CB + j];
+  }
   double acc = 0.0;
   for (int J = T - 1; J > K; --J) {
     const int sJ = J * CB, bJ = min(CB, n - sJ);
@@ -241,13 +263,9 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
   __syncthreads();
   // y_K[j] = sum_{i >= j} V[i][j] z[i]
   {
-    const double* V = Vall + (size_t)K * CB * CB;
     double t = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int i = h + 4 * q;
-      t += V[(size_t)i * CB + j] * zs[i];
-    }
+    for (int q = 0; q < 16; ++q) t += vk[q] * zs[h + 4 * q];
     part[h][j] = t;
   }
   __syncthreads();
@@ -257,6 +275,20 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
     y[s0 + tid] = val;
   }
   if (tid == 0 && bad) scal[SL_CHOL_BAD] += 1.0;
+}
+
+// Workgroups of k_back_flow the device holds at once (occupancy API x CUs).
+// The dataflow needs no co-residency for progress (workgroup K waits only
+// on J > K, i.e. on lower block ids, which are dispatched first), but a grid
+// that fits keeps every hop a pure hand-off; ensure_dense refuses a system
+// whose T block columns exceed this (ba_solver.hip).
+int back_flow_capacity(int device) {
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_back_flow), 256, 0) !=
+          hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return -1;
+  return per_cu * cus;
 }
 
 // split-form block step (ba_chol_split.hip)

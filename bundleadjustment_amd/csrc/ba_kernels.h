@@ -148,6 +148,7 @@ void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, 
 // Fold the partials of `slots` (bitmask) into d_scal; kernels producing
 // partials always use grid = nblocks_of(...)
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s);
+int back_flow_capacity(int device);   // resident k_back_flow workgroups (-1: query failed)
 int jr_ja_host(int nc);   // JA stride of the JR records for nc cameras (12 or 14)
 void launch_stream_copy(const double* a, double* b, size_t n2, hipStream_t s);
 void launch_residuals(const DevProblem& P, const double* rec, const double* pts, double* r_raw, hipStream_t s);

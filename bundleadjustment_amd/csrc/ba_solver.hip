@@ -400,6 +400,14 @@ void ensure_dense(ba_ctx* ctx) {
     if (!blocks.empty()) blocks.back().w = (int)pe.size();
   }
 
+  {
+    const int T = (ctx->n + 63) / 64, cap = bahip::back_flow_capacity(ctx->device);
+    if (cap < 0) throw BaError{BA_ERR_DEVICE, "occupancy query for the back substitution failed"};
+    if (T > cap)
+      throw BaError{BA_ERR_INVALID_ARGUMENT, "DENSE_SCHUR: " + std::to_string(T) + " block columns exceed the " +
+                                                 std::to_string(cap) + " resident back-substitution workgroups; "
+                                                 "use ITERATIVE_SCHUR"};
+  }
   DevWork& W = ctx->W;
   W.S = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
   W.Lf = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));

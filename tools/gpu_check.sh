@@ -14,6 +14,13 @@ stop_on_fault() {  # $1 = exit status of a GPU step
   esac
 }
 echo "== rocm-smi"; (rocm-smi --showproductname 2>&1 | head -20) || true
+if [ "${CHOL:-0}" = "1" ]; then
+  echo "== chol_bench (stamped build: factor + dataflow back substitution, residual check)"
+  for n in 1194 3000; do
+    timeout -k 10 120 tools/chol_bench $n > $OUT/chol_bench_$n.txt 2>&1
+    rc=$?; tail -4 $OUT/chol_bench_$n.txt; stop_on_fault $rc
+  done
+fi
 echo "== pytest -m gpu"
 timeout -k 10 1500 python3 -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -30 $OUT/pytest_gpu.log; stop_on_fault $rc
