@@ -286,10 +286,13 @@ def main():
     log(f"[rank {rank}] problem {cfg}: {problem.n_cams} cams x {problem.n_pts} pts x {problem.n_obs} obs "
         f"(generated in {time.time() - t:.1f}s)")
 
-    solver = Solver(device)
     use_comm = world > 1 or args.comm
-    if use_comm and args.transport == "host":
-        solver.comm_init_host(host_transport(rank, world), world, rank)
+    # host transport: the gloo group comes up before this process's first HIP
+    # call and is torn down after the solver (as tests/mr_worker.py does)
+    host_ar = host_transport(rank, world) if use_comm and args.transport == "host" else None
+    solver = Solver(device)
+    if host_ar is not None:
+        solver.comm_init_host(host_ar, world, rank)
     elif use_comm:
         # RCCL communicator; the 128-byte id travels through a file keyed by the
         # launcher (no second GPU runtime in this process for the rendezvous)
@@ -409,6 +412,9 @@ def main():
         }
         print(json.dumps(out), flush=True)
     solver.close()
+    if host_ar is not None:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

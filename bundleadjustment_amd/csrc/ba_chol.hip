@@ -300,6 +300,11 @@ void launch_chol_split_step(double* A, double* L, int ld, int n, int k, int tc, 
 // launch per step is cheaper (C3: 19 block columns); above it the trailing
 // GEMMs dominate (C4: 94).
 constexpr int kCholSplitBlocks = 24;
+int chol_split_blocks() { return kCholSplitBlocks; }
+
+// the persistent form (ba_chol_persist.hip)
+void launch_chol_persist(double* A, double* L, int ld, int n, double* Vbuf, double* scal, unsigned* flags,
+                         unsigned epoch, hipStream_t s);
 
 void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hipStream_t s) {
   const int n = P.n;
@@ -307,6 +312,11 @@ void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hi
   const int nrows = n + 1;
   const int T = (n + CB - 1) / CB;
   const bool split = T >= kCholSplitBlocks;
+  if (W.chol_persist && !split) {
+    launch_chol_persist(W.S, W.Lf, P.ld, n, W.Vbuf, W.scal, W.cflags, (unsigned)epoch, s);
+    hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.yg, epoch, W.scal);
+    return;
+  }
   hipLaunchKernelGGL(k_chol_step, dim3(1, 1), dim3(256), 0, s, W.S, W.Lf, P.ld, n, -1, W.Vbuf, W.scal);
   for (int k = 0; k + 1 < T; ++k) {
     const int st = (k + 1) * CB;

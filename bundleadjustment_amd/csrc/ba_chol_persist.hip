@@ -1,0 +1,308 @@
+// ba_chol_persist.hip — the dense Cholesky of the reduced camera system
+// (DENSE_SCHUR, Optimizer.cpp:85) as ONE persistent launch with look-ahead,
+// for systems whose lower tiles fit the chip (C3: 19 block columns, 171
+// workgroups).  Same arithmetic as the per-step launches of ba_chol.hip
+// (k_chol_step), in the same order per tile, so L and the block inverses V
+// come out bitwise identical; only the orchestration differs:
+//
+//   workgroup 0 (critical)  for c = 0 .. T-1: stage A_{c,c-1} and the
+//       diagonal tile A_{c,c} once their workers have published them,
+//       P = A_{c,c-1} V_{c-1}^T (V_{c-1} never leaves its LDS), C = A_cc -
+//       P P^T, factor + invert C -> V_c, publish V_c.
+//   workgroup w > 0 (worker) owns ONE lower tile (I, J), J >= 1, in
+//       registers for the whole factorisation and applies the panel
+//       updates k = 0 .. J-1 (J-2 on the diagonal: the last one is the
+//       critical workgroup's C = A - P P^T) as soon as V_k and the tiles
+//       (I, k), (J, k) are final, then publishes its tile.
+//
+// The per-step form paid, on every one of its T launches, the critical
+// workgroup's re-staging of V_k and the serialisation of the launch
+// boundary; here the chain per block column is: two tile fetches, the panel
+// GEMM, C, the factor.  The trailing updates of step k run beside the
+// factor of block k+1 (look-ahead), on the other CUs.
+//
+// Hand-offs (MI355X_MICROARCH.md, visibility, valid-forms table row 1; the
+// publish/consume recipe of cdna_hip_programming.md Guideline 16, R1):
+// every handed-off byte (published tiles of A, V_c) is stored write-through
+// (16-B buffer stores with sc1), every storing wave drains (s_waitcnt
+// vmcnt(0)) before the workgroup barrier, ONE lane then stores the flag
+// (relaxed agent-scope atomic); the consumer's wave 0 polls the flag
+// (relaxed agent-scope loads + s_sleep), the workgroup barrier releases the
+// other waves, and EVERY load of handed-off bytes is a 16-B sc1 buffer load.
+// Flags carry the factorisation's epoch (never 0, never reset).  Spins are
+// bounded: a missing producer sets SL_CHOL_BAD (the step is then rejected as
+// a failed linear solve) instead of hanging the GPU.  Every workgroup of the
+// grid must be resident at once: the host checks the occupancy first
+// (chol_persist_fits) and otherwise runs the per-step launches.
+#include "ba_chol.h"
+
+namespace bahip {
+
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+constexpr unsigned kPersistSpin = 1u << 20;   // ~1 s of 1 us polls: far beyond any real wait
+constexpr int kAuxSc1 = 16;                    // buffer-instruction cache policy: sc1
+
+__device__ __forceinline__ Rsrc make_rsrc(const void* base, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double2 ld_sc1(Rsrc r, size_t byte_off) {
+  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, kAuxSc1);
+  return __builtin_bit_cast(double2, v);
+}
+__device__ __forceinline__ void st_sc1(Rsrc r, size_t byte_off, double2 x) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, x), r, (int)byte_off, 0, kAuxSc1);
+}
+
+// tile_fetch (ba_chol.h) with sc1 loads: the same clamped, branch-free
+// addresses and the same zeroing, so the staged tile is identical
+template <bool LOWER = false>
+__device__ inline TileRegs tile_fetch_sc1(Rsrc r, size_t ld, int r0, int c0, int rmax, int cmax) {
+  TileRegs t;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int e = tid + 256 * it;
+    const int i = e >> 5, j = (e & 31) * 2;
+    const bool up = LOWER && j > i;
+    const int ri = r0 + i, cj = c0 + (up ? (i & ~1) : j);
+    const int ric = min(ri, rmax - 1), cjc = min(cj, cmax - 2) & ~1;
+    const double2 v = ld_sc1(r, ((size_t)ric * ld + cjc) * sizeof(double));
+    const bool rok = ri < rmax && !up;
+    t.v[it].x = (rok && cj < cmax) ? v.x : 0.0;
+    t.v[it].y = (rok && cj + 1 < cmax) ? v.y : 0.0;
+  }
+  return t;
+}
+
+// drain this wave's stores, join the workgroup, one lane raises the flag
+__device__ __forceinline__ void publish(unsigned* flag, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane 0 polls (relaxed, bounded), the barrier releases the workgroup.
+// Returns false in thread 0 if the bound was hit (the failure is reported by
+// thread 0 alone; other threads return true)
+__device__ __forceinline__ bool wait_flag(const unsigned* flag, unsigned epoch) {
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    unsigned it = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+      if (++it >= kPersistSpin) { ok = false; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  return ok;
+}
+
+struct PersistArgs {
+  double* A;         // working matrix ((n+1) x ld)
+  double* L;         // output factor
+  double* Vbuf;      // [T][64][64] diagonal-block inverses
+  double* scal;
+  unsigned* flags;   // [T] V_c published | [TR][T] tile (I, J) published
+  int ld, n, T, TR;
+  unsigned epoch;
+};
+
+// worker w (>= 1) -> its tile (I, J): tiles with J >= 1 and I >= J, in
+// column order, without the diagonal tile (1, 1) (no update reaches it
+// before the critical workgroup's)
+__device__ inline bool worker_tile(int w, int T, int TR, int& I, int& J) {
+  int idx = w - 1;
+  for (int j = 1; j < T; ++j) {
+    const int first = j == 1 ? 2 : j;   // (1, 1) has no worker
+    const int cnt = TR - first;
+    if (idx < cnt) { I = first + idx; J = j; return true; }
+    idx -= cnt;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
+  __shared__ double S0[CB][LDP];
+  __shared__ double S1[CB][LDP];
+  __shared__ double S2[CB][LDP];
+  __shared__ CholLds cw;
+  const int n = a.n, nrows = n + 1, T = a.T;
+  const size_t ld = (size_t)a.ld;
+  const Rsrc rA = make_rsrc(a.A, (size_t)nrows * ld * sizeof(double));
+  const Rsrc rV = make_rsrc(a.Vbuf, (size_t)(T + 1) * CB * CB * sizeof(double));
+  unsigned* vflag = a.flags;
+  unsigned* tflag = a.flags + T;
+  bool bad = false;
+
+  if (blockIdx.x == 0) {
+    // ---------------- critical workgroup: the diagonal chain
+    for (int c = 0; c < T; ++c) {
+      const int s = c * CB;
+      const int b = min(CB, n - s);
+      const int m = min(CB, nrows - s);
+      if (c == 0) {
+        stage64(S0, a.A, ld, 0, 0, nrows, b);     // written before the launch
+      } else {
+        const int k = c - 1, kc = k * CB, kb = min(CB, n - kc);
+        // A_{c,k} final (its worker; column 0 is never updated) and the
+        // diagonal tile after the updates k' <= c - 2 (no worker for c = 1)
+        if (k >= 1) bad |= !wait_flag(&tflag[c * T + k], a.epoch);
+        if (c >= 2) bad |= !wait_flag(&tflag[c * T + c], a.epoch);
+        const TileRegs tA = tile_fetch_sc1<true>(rA, ld, s, s, nrows, s + b);   // A_{c,c} (+ rhs row)
+        const TileRegs tP = tile_fetch_sc1(rA, ld, s, kc, nrows, kc + kb);      // A_{c,k}
+        tile_put(S0, tA);
+        tile_put(S1, tP);
+        __syncthreads();
+        d4 acc[4];
+        mfma_xVT_strip(S1, S2, acc);            // P = A_{c,k} V_k^T (V_k: S2, from the last iteration)
+        __syncthreads();
+        {
+          const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+          for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int rr = 16 * w + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
+              S1[rr][cc] = acc[bc][g];
+              if (rr < m && cc < kb) a.L[(size_t)(s + rr) * ld + kc + cc] = acc[bc][g];
+            }
+        }
+        __syncthreads();
+        mfma_xxT_col0(S1, S0);                  // C = A - P P^T: column 0 now, the rest beside the first sweep
+      }
+      if (threadIdx.x == 0) cw.bad = 0;
+      factor_invert_blk(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr);
+      __syncthreads();
+      // V_c: cleaned in place (zero above the diagonal, identity rows past b:
+      // exactly the Vbuf image the per-step form re-stages) for the next
+      // iteration's panel GEMM, and published to the workers
+      {
+        for (int e2 = threadIdx.x; e2 < CB * CB / 2; e2 += 256) {
+          const int i = (2 * e2) / CB, j = (2 * e2) % CB;
+          double v[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            v[h] = (j + h <= i && i < b && j + h < b) ? S2[i][j + h] : (i == j + h ? 1.0 : 0.0);
+          S2[i][j] = v[0];
+          S2[i][j + 1] = v[1];
+          st_sc1(rV, ((size_t)c * CB * CB + 2 * (size_t)e2) * sizeof(double), make_double2(v[0], v[1]));
+        }
+        if (m > b)
+          for (int j = threadIdx.x; j < b; j += 256) a.L[(size_t)(s + b) * ld + s + j] = S0[b][j];
+      }
+      bad |= cw.bad != 0;
+      publish(&vflag[c], a.epoch);
+    }
+    if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
+    return;
+  }
+
+  // ---------------- worker: one lower tile (I, J), J >= 1
+  int I, J;
+  if (!worker_tile(blockIdx.x, T, a.TR, I, J)) return;
+  const bool diag = I == J;
+  const int r0 = I * CB, c0 = J * CB;
+  const int mI = min(CB, nrows - r0);
+  // the tile in the MFMA accumulator layout (acc_pos), initial values from
+  // before the launch (plain loads, clamped)
+  double own[2][2][4];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int rr, cc;
+        acc_pos(x, y, g, &rr, &cc);
+        own[x][y][g] = a.A[(size_t)min(r0 + rr, nrows - 1) * ld + min(c0 + cc, n - 1)];
+      }
+  const int kmax = diag ? J - 2 : J - 1;
+  for (int k = 0; k <= kmax; ++k) {
+    const int kc = k * CB, kb = min(CB, n - kc);
+    bad |= !wait_flag(&vflag[k], a.epoch);
+    if (k >= 1) {
+      bad |= !wait_flag(&tflag[I * T + k], a.epoch);
+      if (!diag) bad |= !wait_flag(&tflag[J * T + k], a.epoch);
+    }
+    // the staging of k_chol_step's trailing tile, through sc1 loads
+    {
+      const TileRegs tV = tile_fetch_sc1(rV, CB, k * CB, 0, (k + 1) * CB, CB);   // V_k (stored cleaned)
+      const TileRegs tI = tile_fetch_sc1(rA, ld, r0, kc, nrows, kc + kb);        // A_{I,k}
+      TileRegs tJ;
+      if (!diag) tJ = tile_fetch_sc1(rA, ld, c0, kc, n, kc + kb);              // A_{J,k}
+      tile_put(S2, tV);
+      tile_put(S0, tI);
+      if (!diag) tile_put(S1, tJ);
+    }
+    __syncthreads();
+    d4 acc[2][2];
+    mfma_xyT_64(S0, S2, acc);                  // P_I
+    d4 accJ[2][2];
+    if (!diag) mfma_xyT_64(S1, S2, accJ);      // P_J
+    __syncthreads();
+    acc_to_lds(S0, acc, 0);
+    if (!diag) acc_to_lds(S1, accJ, 0);
+    __syncthreads();
+    if (J == k + 1) lds_to_global(S0, a.L, ld, r0, kc, mI, kb);   // L_{I,k} final
+    mfma_xyT_64(S0, diag ? S0 : S1, acc);      // P_I P_J^T
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) own[x][y][g] -= acc[x][y][g];
+    __syncthreads();                           // S0..S2 are restaged next
+  }
+  // publish the tile (lower part; pairs that start on or left of the
+  // diagonal on a diagonal tile): through S0, as row-contiguous 16-B sc1 stores
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int rr, cc;
+        acc_pos(x, y, g, &rr, &cc);
+        S0[rr][cc] = own[x][y][g];
+      }
+  __syncthreads();
+  for (int e2 = threadIdx.x; e2 < CB * CB / 2; e2 += 256) {
+    const int i = (2 * e2) / CB, j = (2 * e2) % CB;
+    const int ri = r0 + i, cj = c0 + j;
+    if (ri < nrows && cj < n && (!diag || j <= i))   // n = 6 cameras: even, whole pairs
+      st_sc1(rA, ((size_t)ri * ld + cj) * sizeof(double), make_double2(S0[i][j], S0[i][j + 1]));
+  }
+  publish(&tflag[I * T + J], a.epoch);
+  if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
+}
+
+// grid of the persistent factorisation: 1 critical + one worker per tile
+int chol_persist_grid(int n) {
+  const int T = (n + CB - 1) / CB, TR = (n + 1 + CB - 1) / CB;
+  int w = 0;
+  for (int j = 1; j < T; ++j) w += TR - (j == 1 ? 2 : j);
+  return 1 + w;
+}
+
+// every workgroup of the grid resident at once (the dataflow spins)?
+bool chol_persist_fits(int device, int n) {
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_chol_persist), 256, 0) !=
+          hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return false;
+  return chol_persist_grid(n) <= per_cu * cus;
+}
+
+void launch_chol_persist(double* A, double* L, int ld, int n, double* Vbuf, double* scal, unsigned* flags,
+                         unsigned epoch, hipStream_t s) {
+  PersistArgs a;
+  a.A = A; a.L = L; a.Vbuf = Vbuf; a.scal = scal; a.flags = flags;
+  a.ld = ld; a.n = n;
+  a.T = (n + CB - 1) / CB;
+  a.TR = (n + 1 + CB - 1) / CB;
+  a.epoch = epoch;
+  hipLaunchKernelGGL(k_chol_persist, dim3(chol_persist_grid(n)), dim3(256), 0, s, a);
+}
+
+}  // namespace bahip

@@ -75,6 +75,8 @@ struct DevWork {
   double* y;                         // [n] reduced solution
   double* Vbuf;                      // [ceil(n/64)][64][64] inverses of the diagonal Cholesky blocks
   double* yg;                        // [n][2] back-substitution hand-off granules {y, epoch} (zeroed once)
+  unsigned* cflags;                  // [T + TR*T] persistent-Cholesky hand-off flags (epoch-tagged, zeroed once)
+  bool chol_persist;                 // the factorisation runs as one persistent launch (ba_chol_persist.hip)
   const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}
   const int2* eblocks; int neblocks; // lower off-diagonal blocks {I, J} with no observation pair
   bool s_memset;                     // many empty blocks: memset S instead
@@ -148,7 +150,9 @@ void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, 
 // Fold the partials of `slots` (bitmask) into d_scal; kernels producing
 // partials always use grid = nblocks_of(...)
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s);
-int back_flow_capacity(int device);   // resident k_back_flow workgroups (-1: query failed)
+int back_flow_capacity(int device);
+bool chol_persist_fits(int device, int n);   // every workgroup of k_chol_persist resident at once
+int chol_split_blocks();                     // block columns from which the split step form is used   // resident k_back_flow workgroups (-1: query failed)
 int jr_ja_host(int nc);   // JA stride of the JR records for nc cameras (12 or 14)
 void launch_stream_copy(const double* a, double* b, size_t n2, hipStream_t s);
 void launch_residuals(const DevProblem& P, const double* rec, const double* pts, double* r_raw, hipStream_t s);

@@ -21,6 +21,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <numeric>
@@ -413,6 +414,18 @@ void ensure_dense(ba_ctx* ctx) {
   W.Lf = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
   W.Vbuf = ctx->dalloc<double>((size_t)((ctx->n + 63) / 64 + 1) * 64 * 64);
   W.yg = ctx->dalloc<double>(2 * (size_t)std::max(ctx->n, 1));
+  {
+    // persistent factorisation (one launch) when the per-step form would not
+    // split and the whole grid is resident; BA_CHOL_PERSIST=0 forces the
+    // per-step launches (A/B)
+    const int T = (ctx->n + 63) / 64, TR = (ctx->n + 1 + 63) / 64;
+    const char* env = std::getenv("BA_CHOL_PERSIST");
+    W.chol_persist = ctx->n > 0 && T < bahip::chol_split_blocks() && !(env && env[0] == '0') &&
+                     bahip::chol_persist_fits(ctx->device, ctx->n);
+    const size_t nf = (size_t)T + (size_t)TR * T;
+    W.cflags = ctx->dalloc<unsigned>(nf);
+    HIP_OK(hipMemsetAsync(W.cflags, 0, sizeof(unsigned) * std::max<size_t>(nf, 1), ctx->stream));
+  }
   W.Spk = nullptr;
   W.blocks = ctx->upload(blocks);
   W.nblocks = (int)blocks.size();

@@ -8,12 +8,14 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstring>
 #include <cstdio>
 #include <random>
 #include <vector>
 
 #include "ba_chol.hip"
 #include "ba_chol_split.hip"
+#include "ba_chol_persist.hip"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 
@@ -107,6 +109,44 @@ int main(int argc, char** argv) {
   }
   std::vector<double> y(n), Sh(64);
   CK(hipMemcpy(y.data(), dy, sizeof(double) * n, hipMemcpyDeviceToHost));
+  // the persistent form (one launch, look-ahead): time it and check that it
+  // reproduces the per-step factorisation bit for bit
+  if (chol_persist_fits(0, n)) {
+    unsigned* dflags;
+    const int TR = (n + 1 + CB - 1) / CB;
+    CK(hipMalloc(&dflags, sizeof(unsigned) * (T + TR * T)));
+    CK(hipMemset(dflags, 0, sizeof(unsigned) * (T + TR * T)));
+    std::vector<double> Lp(A.size()), Ls(A.size()), yp(n);
+    CK(hipMemcpy(Ls.data(), dL, sizeof(double) * A.size(), hipMemcpyDeviceToHost));
+    for (int rep = 0; rep < 5; ++rep) {
+      CK(hipMemcpy(dA, A.data(), sizeof(double) * A.size(), hipMemcpyHostToDevice));
+      CK(hipMemset(dS, 0, sizeof(double) * 64));
+      CK(hipEventRecord(e0));
+      launch_chol_persist(dA, dL, ld, n, dV, dS, dflags, 100 + rep, 0);
+      CK(hipEventRecord(e1));
+      hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dA, dL, ld, n, dV, dy, dF, 100 + rep, dS);
+      CK(hipEventSynchronize(e1));
+      float mp;
+      CK(hipEventElapsedTime(&mp, e0, e1));
+      CK(hipDeviceSynchronize());
+      printf("persistent factor %.1f us (grid %d)\n", mp * 1e3, chol_persist_grid(n));
+    }
+    CK(hipMemcpy(Lp.data(), dL, sizeof(double) * A.size(), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(yp.data(), dy, sizeof(double) * n, hipMemcpyDeviceToHost));
+    std::vector<double> Sp(64);
+    CK(hipMemcpy(Sp.data(), dS, sizeof(double) * 64, hipMemcpyDeviceToHost));
+    size_t ldiff = 0;
+    for (int i = 0; i <= n; ++i)
+      for (int j = 0; j < n && j <= i; ++j)
+        if (i < n ? true : true) ldiff += std::memcmp(&Lp[(size_t)i * ld + j], &Ls[(size_t)i * ld + j], 8) != 0;
+    size_t ydiff = 0;
+    for (int i = 0; i < n; ++i) ydiff += std::memcmp(&yp[i], &y[i], 8) != 0;
+    printf("persistent vs per-step: L entries differing %zu, y entries differing %zu, chol_bad=%g\n", ldiff, ydiff,
+           Sp[SL_CHOL_BAD]);
+    if (ydiff != 0 || Sp[SL_CHOL_BAD] != 0.0) return 4;
+  } else {
+    printf("persistent form: grid %d does not fit\n", chol_persist_grid(n));
+  }
   CK(hipMemcpy(Sh.data(), dS, sizeof(double) * 64, hipMemcpyDeviceToHost));
   // residual |S y - b| / |b|
   double rn = 0, bn = 0;
