@@ -40,7 +40,7 @@ namespace bahip {
 
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t Rsrc;
-constexpr unsigned kPersistSpin = 1u << 20;   // ~1 s of 1 us polls: far beyond any real wait
+constexpr unsigned kPersistSpin = 1u << 17;   // ~0.2 s of polls: far beyond any real wait (~20 us)
 constexpr int kAuxSc1 = 16;                    // buffer-instruction cache policy: sc1
 
 __device__ __forceinline__ Rsrc make_rsrc(const void* base, size_t bytes) {
