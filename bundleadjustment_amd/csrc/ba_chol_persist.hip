@@ -38,6 +38,22 @@
 
 namespace bahip {
 
+// diagnostic build (tools/chol_bench.hip, BA_CHOL_STAMPS): s_memtime of the
+// critical workgroup's phases per block column
+#ifdef BA_CHOL_STAMPS
+__device__ unsigned long long g_pstamps[64][8];
+#define PSTAMP(c, i)                                                                          \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    unsigned long long t_;                                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (threadIdx.x == 0 && (c) < 64) g_pstamps[c][i] = t_;                                   \
+  } while (0)
+#else
+#define PSTAMP(c, i) do {} while (0)
+#endif
+
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 constexpr unsigned kPersistSpin = 1u << 17;   // ~0.2 s of polls: far beyond any real wait (~20 us)
@@ -140,6 +156,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       const int s = c * CB;
       const int b = min(CB, n - s);
       const int m = min(CB, nrows - s);
+      PSTAMP(c, 0);
       if (c == 0) {
         stage64(S0, a.A, ld, 0, 0, nrows, b);     // written before the launch
       } else {
@@ -148,11 +165,17 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         // diagonal tile after the updates k' <= c - 2 (no worker for c = 1)
         if (k >= 1) bad |= !wait_flag(&tflag[c * T + k], a.epoch);
         if (c >= 2) bad |= !wait_flag(&tflag[c * T + c], a.epoch);
+        PSTAMP(c, 1);
         const TileRegs tA = tile_fetch_sc1<true>(rA, ld, s, s, nrows, s + b);   // A_{c,c} (+ rhs row)
         const TileRegs tP = tile_fetch_sc1(rA, ld, s, kc, nrows, kc + kb);      // A_{c,k}
+        // V_{c-1}'s write-through stores were issued at the end of the last
+        // iteration: drain them together with these loads, then raise its
+        // flag (the workers need V_{c-1} one step later: off the chain)
+        publish(&vflag[k], a.epoch);
         tile_put(S0, tA);
         tile_put(S1, tP);
         __syncthreads();
+        PSTAMP(c, 2);
         d4 acc[4];
         mfma_xVT_strip(S1, S2, acc);            // P = A_{c,k} V_k^T (V_k: S2, from the last iteration)
         __syncthreads();
@@ -168,11 +191,14 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
             }
         }
         __syncthreads();
+        PSTAMP(c, 3);
         mfma_xxT_col0(S1, S0);                  // C = A - P P^T: column 0 now, the rest beside the first sweep
       }
       if (threadIdx.x == 0) cw.bad = 0;
+      PSTAMP(c, 4);
       factor_invert_blk(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr);
       __syncthreads();
+      PSTAMP(c, 5);
       // V_c: cleaned in place (zero above the diagonal, identity rows past b:
       // exactly the Vbuf image the per-step form re-stages) for the next
       // iteration's panel GEMM, and published to the workers
@@ -191,7 +217,8 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
           for (int j = threadIdx.x; j < b; j += 256) a.L[(size_t)(s + b) * ld + s + j] = S0[b][j];
       }
       bad |= cw.bad != 0;
-      publish(&vflag[c], a.epoch);
+      PSTAMP(c, 6);
+      if (c + 1 == T) publish(&vflag[c], a.epoch);   // else at the next iteration's tile fetch
     }
     if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
     return;

@@ -131,6 +131,18 @@ int main(int argc, char** argv) {
       CK(hipDeviceSynchronize());
       printf("persistent factor %.1f us (grid %d)\n", mp * 1e3, chol_persist_grid(n));
     }
+    {
+      unsigned long long ps[64][8];
+      CK(hipMemcpyFromSymbol(ps, HIP_SYMBOL(g_pstamps), sizeof(ps)));
+      double avg[7] = {0, 0, 0, 0, 0, 0, 0};
+      int cnt = 0;
+      for (int c = 1; c < T && c < 64; ++c, ++cnt)
+        for (int i = 0; i < 6; ++i) avg[i] += (double)(ps[c][i + 1] - ps[c][i]);
+      const double tot = cnt ? (double)(ps[T - 1][6] - ps[1][0]) / cnt : 0.0;
+      printf("persistent critical cycles per step (avg of %d): wait %.0f  fetch+V publish %.0f  P gemm+store %.0f"
+             "  C col0 %.0f  factor %.0f  V clean+store %.0f  | step %.0f\n",
+             cnt, avg[0] / cnt, avg[1] / cnt, avg[2] / cnt, avg[3] / cnt, avg[4] / cnt, avg[5] / cnt, tot);
+    }
     CK(hipMemcpy(Lp.data(), dL, sizeof(double) * A.size(), hipMemcpyDeviceToHost));
     CK(hipMemcpy(yp.data(), dy, sizeof(double) * n, hipMemcpyDeviceToHost));
     std::vector<double> Sp(64);
