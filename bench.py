@@ -58,7 +58,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(config: str):
+def pmc_traffic(config: str, kernel: str = "k_linearize"):
     """Per-launch HBM bytes of the residual+Jacobian kernel from the committed
     rocprofv3 PMC summary (profiles/), corrected per MI355X_MICROARCH.md
     (FETCH_SIZE x2 on gfx950), or None."""
@@ -67,7 +67,7 @@ def pmc_traffic(config: str):
         return None
     try:
         d = json.loads(f.read_text())
-        return float(d["k_linearize"]["hbm_bytes_per_launch"])
+        return float(d[kernel]["hbm_bytes_per_launch"])
     except Exception:
         return None
 
@@ -332,12 +332,20 @@ def main():
     #   176 B/obs (uv 8 + two int32 idx 8 + r 16 + J 144) + 24 B/point + 48 B/camera
     B_rj = 176.0 * problem.n_obs + 24.0 * problem.n_pts + 48.0 * problem.n_cams
     achieved = B_rj / (ms_rj * 1e-3) / 1e9
-    traffic = pmc_traffic(cfg) if not strong and args.scale == 1.0 else None
+    # J-free iteration (libba_hip's rule: <= 200 cameras, BA_JR unset): the
+    # timed kernel is k_lin_point, which forms r and J in registers and
+    # reduces them into the point blocks without storing J; SURVEY.md §8d
+    # prices such a fused kernel against the unfused B_rj, labelled "effective"
+    jrfree = problem.n_cams <= 200 and os.environ.get("BA_JR") != "1"
+    traffic = pmc_traffic(cfg, "k_lin_point" if jrfree else "k_linearize") if not strong and args.scale == 1.0 else None
     # measured copy bandwidth of this GPU (reported beside the
     # vendor peak, which stays the denominator of `frac`): 1 GiB non-temporal
     # 16-B copy, 10 launches, after the timed region
     copy_gbs = solver.stream_copy(1 << 30, 10)
-    roofline = {"kernel": "k_linearize (residual+Jacobian)", "bound": "hbm", "achieved": round(achieved, 1),
+    roofline = {"kernel": ("k_lin_point (residual + Jacobian + Huber + point blocks; J not materialised)" if jrfree
+                           else "k_linearize (residual+Jacobian)"),
+                "effective": jrfree,
+                "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "algorithmic_bytes": B_rj, "avg_launch_ms": round(ms_rj, 5),
                 "measured_copy": round(copy_gbs, 1), "frac_of_copy": round(achieved / copy_gbs, 4)}

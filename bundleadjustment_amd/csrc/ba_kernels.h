@@ -58,6 +58,7 @@ struct DevWork {
   double* rec;   double* rec_c;      // camera records at x / x'
   double* crec;                      // [nc][16] compact camera records (w, t, K, flag, theta terms) for > kLinLdsCams cameras
   double* ctbl;                      // [nc][22] candidate camera table for > kLinLdsCams cameras
+  bool jrfree;                       // J-free iteration (nc <= kLinLdsCams): consumers recompute J, JR unused
   double* JR;                        // JA [no][JA] (Jc rows 0..1; JA = 14 beyond kLinLdsCams cameras: + r again), then JB [no][8] (Jp rows 3+3, r 2)
   double* delta_p;                   // [np][3] point step (scaled back)
   double* Hpp;   double* gp;         // [6][np], [3][np]
@@ -115,7 +116,10 @@ void launch_lin_prep(const DevProblem& P, const DevWork& W, hipStream_t s);   //
 void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s, hipEvent_t t0 = nullptr,
                       hipEvent_t t1 = nullptr);
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
-                           double max_diag, hipStream_t s);
+                           double max_diag, hipStream_t s, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+// the JR-writing linearisation (launch_linearize in JR mode; ba_linearize's read-back in J-free mode)
+void launch_linearize_jr(const DevProblem& P, const DevWork& W, hipStream_t s, hipEvent_t t0 = nullptr,
+                         hipEvent_t t1 = nullptr);
 void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
                       hipStream_t s);
@@ -153,6 +157,7 @@ void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipSt
 int back_flow_capacity(int device);
 bool chol_persist_fits(int device, int n);   // every workgroup of k_chol_persist resident at once
 int chol_split_blocks();                     // block columns from which the split step form is used   // resident k_back_flow workgroups (-1: query failed)
+constexpr int kLinLdsCamsHost = 200;   // = kLinLdsCams (ba_kernels.hip): cameras the LDS camera table holds
 int jr_ja_host(int nc);   // JA stride of the JR records for nc cameras (12 or 14)
 void launch_stream_copy(const double* a, double* b, size_t n2, hipStream_t s);
 void launch_residuals(const DevProblem& P, const double* rec, const double* pts, double* r_raw, hipStream_t s);

@@ -830,7 +830,7 @@ __global__ __launch_bounds__(256) void k_linearize_rc(DevProblem P, const double
 // path (the gathers, 24 x 16 B per lane from random cameras, saturate the
 // TA: measured 46 % issue stalls).  One 512-thread block per CU.
 constexpr int kLinLdsThreads = 512;
-constexpr int kLinLdsCams = 200;
+constexpr int kLinLdsCams = kLinLdsCamsHost;
 // Camera table -> LDS, every global load of the fill issued before the
 // first LDS store (one round trip; an element-wise loop serialises ~16 L2
 // round trips in the block prologue).
@@ -1796,6 +1796,338 @@ static bool lin_legacy() {
   if (v < 0) { const char* e = getenv("BA_LIN_LEGACY"); v = e && atoi(e) ? 1 : 0; }
   return v != 0;
 }
+// ---------------------------------------------------------------------------
+// J-free iteration (nc <= kLinLdsCams, the camera table fits the LDS).
+//
+// The per-observation Jacobian costs ~18 us of arithmetic at C3 but 176 B of
+// HBM writes plus 4 x 160 B of re-reads per observation when it is
+// materialised (k_linearize -> JR -> k_point_assemble, k_cam_assemble,
+// k_obs_w, k_candidate_lds: ~0.8 GB per LM iteration).  Here every consumer
+// recomputes r and J from the camera table (LDS), the point and the pixel with
+// the same lin_obs() (same operations on the same operands: bitwise the JR
+// values), so J never leaves the registers:
+//   k_lin_point       r, J, Huber, cost + the point blocks Hpp / gp, scaling,
+//                     LM diagonal, gradient norms (k_linearize + k_point_assemble)
+//   k_cam_assemble_rc Hcc / gc per camera, the camera's table row in registers
+//   k_obs_w_rc        W_o = s_c Jc^T Jp s_p L_p^-T
+//   k_candidate_rc    model cost change J d . (r + J d / 2) and candidate cost
+// Per point / camera the sums run in the order of the JR kernels they replace.
+// ---------------------------------------------------------------------------
+// a variable camera's table row held in registers (the camera of a whole
+// workgroup in k_cam_assemble_rc)
+struct CamRegs {
+  double t[kLin];
+  double k[9];
+  __device__ bool var() const { return true; }
+  __device__ void load(double (&o)[kLin]) const {
+#pragma unroll
+    for (int i = 0; i < kLin; ++i) o[i] = t[i];
+  }
+  __device__ double K(int i) const { return k[i]; }
+};
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __restrict__ rec,
+                                                  const double* __restrict__ pts, double* __restrict__ Hpp,
+                                                  double* __restrict__ gp, double* __restrict__ scale_p,
+                                                  double* __restrict__ diag_p, int compute_scale, double min_diag,
+                                                  double max_diag, double* __restrict__ part) {
+  __shared__ double lds[5 * 16];
+  __shared__ __attribute__((aligned(16))) double tbl[kLinLdsCams * kTblRec];
+  __shared__ float ktb[kLinLdsCams * 9];
+  fill_lin_table<NT>(P, rec, tbl, ktb);
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};   // cost, bad, gn2, xn2
+  double gmax = 0.0;
+  const size_t np = (size_t)P.np;
+  const int sl = threadIdx.x & (kPaLanes - 1);
+  const int g0 = (blockIdx.x * NT + threadIdx.x) / kPaLanes, gs = gridDim.x * NT / kPaLanes;
+  for (int p = g0; p < P.np; p += gs) {     // uniform inside a lane group
+    const bool pv = P.pt_var[p];
+    const double X0 = pts[3 * p], X1 = pts[3 * p + 1], X2 = pts[3 * p + 2];
+    double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+    const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
+    for (int o = o0 + sl; o < o1; o += kPaLanes) {
+      const int c = P.obs_cam[o];
+      const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
+      double out[kJR];
+      bool fin;
+      const double rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, P.uv[o], out, fin);
+      acc[0] += 0.5 * rho;
+      acc[1] += fin ? 0.0 : 1.0;
+      // k_point_assemble's accumulation of the JB record (Jp rows, r)
+      const double jp[2][3] = {{out[12], out[13], out[14]}, {out[15], out[16], out[17]}};
+      const double rr[2] = {out[18], out[19]};
+#pragma unroll
+      for (int row = 0; row < 2; ++row) {
+        const double a = jp[row][0], b = jp[row][1], cc = jp[row][2];
+        H[0] += a * a; H[1] += a * b; H[2] += a * cc; H[3] += b * b; H[4] += b * cc; H[5] += cc * cc;
+        g[0] += a * rr[row]; g[1] += b * rr[row]; g[2] += cc * rr[row];
+      }
+    }
+    if (!pv) continue;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+#pragma unroll
+      for (int x = kPaLanes / 2; x >= 1; x >>= 1) H[k] += __shfl_xor(H[k], x, kPaLanes);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+#pragma unroll
+      for (int x = kPaLanes / 2; x >= 1; x >>= 1) g[k] += __shfl_xor(g[k], x, kPaLanes);
+    }
+    if (sl != 0) continue;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Hpp[k * np + p] = H[k];
+    const double hd[3] = {H[0], H[3], H[5]};
+    const double Xk[3] = {X0, X1, X2};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      gp[k * np + p] = g[k];
+      double s;
+      if (compute_scale) {
+        s = 1.0 / (1.0 + sqrt(hd[k]));
+        scale_p[k * np + p] = s;
+      } else {
+        s = scale_p[k * np + p];
+      }
+      diag_p[k * np + p] = fmin(fmax(hd[k] * s * s, min_diag), max_diag);
+      const double x = Xk[k];
+      const double d = x - (x + (-g[k]));
+      gmax = fmax(gmax, fabs(d));
+      acc[2] += d * d;
+      acc[3] += x * x;
+    }
+  }
+  double tot[4];
+  block_sum<4>(acc, lds, tot);
+  const double m = block_max1(gmax, lds + 64);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_COST)[blockIdx.x] = tot[0];
+    part_of(part, SL_LIN_BAD)[blockIdx.x] = tot[1];
+    part_of(part, SL_GN2_P)[blockIdx.x] = tot[2];
+    part_of(part, SL_XN2_P)[blockIdx.x] = tot[3];
+    part_of(part, SL_GMAX_P)[blockIdx.x] = m;
+  }
+}
+
+// Hcc (lower 21) and gc per variable camera, its observations in camera order
+// (k_cam_assemble's order: thread i takes i0 + tid, i0 + tid + NT, ...)
+template <int NT>
+__global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const double* __restrict__ rec,
+                                                        const double* __restrict__ pts, double* __restrict__ cpart,
+                                                        double* __restrict__ Hcc, double* __restrict__ gc) {
+  __shared__ double lds[27 * 16];
+  const int v = blockIdx.x;
+  const int c = P.cam_of_vc[v];
+  CamRegs cam;
+  {
+    const double2* s2 = reinterpret_cast<const double2*>(rec + (size_t)c * kCamRec + kRecL);
+#pragma unroll
+    for (int k = 0; k < kLin / 2; ++k) { const double2 u = s2[k]; cam.t[2 * k] = u.x; cam.t[2 * k + 1] = u.y; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) cam.k[k] = (double)P.K[9 * c + k];   // float-valued (Matrix3f)
+  }
+  double acc[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+  int i0, i1;
+  cam_slice(P, v, i0, i1);
+  for (int i = i0 + threadIdx.x; i < i1; i += NT) {
+    const int2 op = P.cam_op[i];
+    const int p = op.y;
+    double out[kJR];
+    bool fin;
+    (void)lin_obs(P, cam, true, P.pt_var[p] != 0, pts[3 * p], pts[3 * p + 1], pts[3 * p + 2], P.uv[op.x], out, fin);
+    // cam_acc_jr on the record: Jc rows (0..11) and the residual (18, 19)
+    const double rr[2] = {out[18], out[19]};
+#pragma unroll
+    for (int row = 0; row < 2; ++row) {
+      const double* j = out + 6 * row;
+      int t = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int b = 0; b <= a; ++b) acc[t++] += j[a] * j[b];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) acc[21 + a] += j[a] * rr[row];
+    }
+  }
+  double out27[27];
+  block_sum<27>(acc, lds, out27);
+  if (gridDim.y == 1) {
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int k = 0; k < 21; ++k) Hcc[(size_t)v * 21 + k] = out27[k];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) gc[(size_t)v * 6 + k] = out27[21 + k];
+    }
+    return;
+  }
+  cam_slice_store(out27, cpart, v, P.nvc);
+}
+
+// W_o from recomputed J (k_obs_w<true, WT> with the JR chunk replaced by
+// lin_obs; the records leave through the same wave-private LDS staging)
+constexpr int kObsWRcWaves = 6;   // table + K + scales + 6 staging slots fit the 160 KB LDS
+template <typename WT>
+__global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, const double* __restrict__ rec,
+                                                                const double* __restrict__ pts,
+                                                                const double* __restrict__ scale_c,
+                                                                const double* __restrict__ scale_p,
+                                                                const double* __restrict__ Linv, WT* __restrict__ W) {
+  using V2 = typename std::conditional<sizeof(WT) == 8, double2, float2>::type;
+  constexpr int WAVES = kObsWRcWaves, NT = 64 * WAVES;
+  __shared__ double stage[WAVES * 64 * kStageLd];
+  __shared__ __attribute__((aligned(16))) double tbl[kLinLdsCams * kTblRec];
+  __shared__ float ktb[kLinLdsCams * 9];
+  __shared__ double sct[kLinLdsCams * 6];
+  fill_lin_table<NT>(P, rec, tbl, ktb);   // (ends with a barrier)
+  for (int e = threadIdx.x; e < P.nc * 6; e += NT) {
+    const int c = e / 6, a = e - 6 * c;
+    const int v = P.vc[c];
+    sct[e] = v >= 0 ? scale_c[(size_t)v * 6 + a] : 0.0;
+  }
+  __syncthreads();
+  if (P.no == 0) return;   // (the clamped prefetch indices below need no >= 1)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* st = stage + w * (64 * kStageLd);
+  const int step = gridDim.x * WAVES * 64;
+  const size_t np = (size_t)P.np;
+  int base = (blockIdx.x * WAVES + w) * 64;
+  // indices one chunk ahead (clamped, unconditional)
+  int oc = min(base + lane, P.no - 1);
+  int c = P.obs_cam[oc], p = P.obs_pt[oc];
+  float2 uv = P.uv[oc];
+  for (; base < P.no; base += step) {
+    const int nb = base + step;
+    const int ocn = min(nb + lane, P.no - 1);
+    const int cn = P.obs_cam[ocn], pn = P.obs_pt[ocn];
+    const float2 uvn = P.uv[ocn];
+    const int v = P.vc[c];
+    const bool pv = P.pt_var[p] != 0;
+    const bool live = base + lane < P.no && v >= 0 && pv;
+    const double X0 = pts[3 * p], X1 = pts[3 * p + 1], X2 = pts[3 * p + 2];
+    const double s0 = scale_p[p], s1 = scale_p[np + p], s2 = scale_p[2 * np + p];
+    const double i00 = Linv[p], i10 = Linv[np + p], i11 = Linv[2 * np + p];
+    const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
+    const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
+    double j[kJR];
+    bool fin;
+    (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
+    double sc[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) sc[a] = sct[c * 6 + a];
+    const double jp0[3] = {j[12] * s0, j[13] * s1, j[14] * s2};
+    const double jp1[3] = {j[15] * s0, j[16] * s1, j[17] * s2};
+    double wv[18];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const double c0 = j[a] * sc[a], c1 = j[6 + a] * sc[a];
+      const double e0 = c0 * jp0[0] + c1 * jp1[0];
+      const double e1 = c0 * jp0[1] + c1 * jp1[1];
+      const double e2 = c0 * jp0[2] + c1 * jp1[2];
+      wv[a * 3 + 0] = live ? e0 * i00 : 0.0;
+      wv[a * 3 + 1] = live ? e0 * i10 + e1 * i11 : 0.0;
+      wv[a * 3 + 2] = live ? e0 * i20 + e1 * i21 + e2 * i22 : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kWRec; ++k) st[lane * kStageLd + k] = wv[k];
+    wave_lds_sync();
+    constexpr int NIT = kWRec / 2;
+    V2 ov[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int e = it * 64 + lane;
+      const int r = e / (kWRec / 2), f = 2 * (e - r * (kWRec / 2));
+      ov[it].x = (WT)st[r * kStageLd + f];
+      ov[it].y = (WT)st[r * kStageLd + f + 1];
+    }
+    wave_lds_sync();
+    V2* dst = reinterpret_cast<V2*>(W + (size_t)base * kWRec);
+    const int nrec = min(64, P.no - base);
+    if (nrec == 64) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) nt_store(&dst[it * 64 + lane], ov[it]);
+    } else {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int e = it * 64 + lane;
+        if (e / (kWRec / 2) < nrec) dst[e] = ov[it];
+      }
+    }
+    c = cn; p = pn; uv = uvn;
+  }
+}
+
+// model cost change + candidate cost with J recomputed at x (the lin table of
+// the linearisation point) beside the value-only candidate table
+template <int NT>
+__global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double* __restrict__ rec,
+                                                     const double* __restrict__ pts,
+                                                     const double* __restrict__ delta_c,
+                                                     const double* __restrict__ delta_p,
+                                                     const double* __restrict__ rec_c,
+                                                     const double* __restrict__ pts_c, double* __restrict__ part) {
+  __shared__ double lds[3 * 16];
+  __shared__ __attribute__((aligned(16))) double tbl[kLinLdsCams * kTblRec];
+  __shared__ float ktb[kLinLdsCams * 9];
+  __shared__ double ctb[kLinLdsCams * kCandRec];
+  fill_lin_table<NT>(P, rec, tbl, ktb);
+  {
+    const int n = P.nc * kCandRec;
+    for (int e = threadIdx.x; e < n; e += NT) ctb[e] = cand_entry(P, rec_c, delta_c, e);
+  }
+  __syncthreads();
+  double acc[3] = {0.0, 0.0, 0.0};  // mneg, ccost, cand_bad
+  for (int o = blockIdx.x * NT + threadIdx.x; o < P.no; o += gridDim.x * NT) {
+    const int c = P.obs_cam[o], p = P.obs_pt[o];
+    const float2 uv = P.uv[o];
+    const bool pv = P.pt_var[p] != 0;
+    const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
+    double j[kJR];
+    bool fin;
+    (void)lin_obs(P, cam, cam.var(), pv, pts[3 * p], pts[3 * p + 1], pts[3 * p + 2], uv, j, fin);
+    const double dp0 = delta_p[3 * p], dp1 = delta_p[3 * p + 1], dp2 = delta_p[3 * p + 2];
+    const double X0 = pts_c[3 * p], X1 = pts_c[3 * p + 1], X2 = pts_c[3 * p + 2];
+    const bool cfix = P.cam_fixed && P.cam_fixed[c];
+    const double* cr = ctb + c * kCandRec;
+    // k_candidate_lds' arithmetic on the same values
+    double jd0 = 0.0, jd1 = 0.0;
+#pragma unroll
+    for (int a2 = 0; a2 < 6; ++a2) { jd0 += j[a2] * cr[16 + a2]; jd1 += j[6 + a2] * cr[16 + a2]; }
+    jd0 += j[12] * dp0 + j[13] * dp1 + j[14] * dp2;
+    jd1 += j[15] * dp0 + j[16] * dp1 + j[17] * dp2;
+    const double mneg = jd0 * (j[18] + jd0 / 2.0) + jd1 * (j[19] + jd1 / 2.0);
+    double pc[3];
+    if (!cfix) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) pc[i] = cr[i] * X0 + cr[3 + i] * X1 + cr[6 + i] * X2 + cr[9 + i];
+    } else {
+      double ph[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ph[i] = X0 * cr[i] + X1 * cr[4 + i] + X2 * cr[8 + i] + cr[12 + i];
+      pc[0] = ph[0] / ph[3]; pc[1] = ph[1] / ph[3]; pc[2] = ph[2] / ph[3];
+    }
+    const float* Kc = ktb + c * 9;
+    double q[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) q[i] = pc[0] * (double)Kc[i] + pc[1] * (double)Kc[3 + i] + pc[2] * (double)Kc[6 + i];
+    const double rc0 = q[0] / q[2] - (double)uv.x, rc1 = q[1] / q[2] - (double)uv.y;
+    double sc;
+    const double rho = huber(rc0 * rc0 + rc1 * rc1, P.huber_a, P.huber_b, &sc);
+    acc[0] += mneg;
+    acc[1] += 0.5 * rho;
+    if (!isfinite(rc0) || !isfinite(rc1)) acc[2] += 1.0;
+  }
+  double out[3];
+  block_sum<3>(acc, lds, out);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_MCC_NEG)[blockIdx.x] = out[0];
+    part_of(part, SL_CCOST)[blockIdx.x] = out[1];
+    part_of(part, SL_CAND_BAD)[blockIdx.x] = out[2];
+  }
+}
+
 void launch_cam_prep(const DevProblem& P, const double* cams, double* rec, bool deriv, hipStream_t s) {
   if (P.nc == 0) return;
   hipLaunchKernelGGL(k_cam_prep, dim3(P.nc), dim3(64), 0, s, P.nc, cams, P.K, P.cam_fixed, P.extr, rec,
@@ -1823,6 +2155,11 @@ void launch_lin_prep(const DevProblem& P, const DevWork& W, hipStream_t s) {
 void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   // t0 / t1 (optional): start / stop of the kernel's execution, stamped by
   // hipExtLaunchKernel itself (no separate event records around the launch)
+  if (W.jrfree) return;   // J-free: r and J are formed inside k_lin_point (launch_point_assemble)
+  launch_linearize_jr(P, W, s, t0, t1);
+}
+// the JR-writing linearisation (also ba_linearize's read-back in J-free mode)
+void launch_linearize_jr(const DevProblem& P, const DevWork& W, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   if (P.nc > 0 && P.nc <= kLinLdsCams) {
     hipExtLaunchKernelGGL((k_linearize_lds_t<kLinNT, kLinRows>), dim3(lds_grid(P.no)), dim3(kLinNT), 0, s, t0, t1, 0,
                           P, (const double*)W.rec, (const double*)W.pts, W.JR, W.part);
@@ -1838,7 +2175,16 @@ void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s, hipE
   if (t1) (void)hipEventRecord(t1, s);
 }
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
-                           double max_diag, hipStream_t s) {
+                           double max_diag, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
+  if (W.jrfree) {   // r, J, cost and the point blocks in one pass (J never materialised)
+    constexpr int NT = 512;
+    const int want = (int)std::min<long long>(((long long)P.np * kPaLanes + NT - 1) / NT, 1LL << 30);
+    const int g = std::max(1, std::min(want, 2 * lds_grid(1 << 30)));   // two 74-KB-LDS workgroups per CU
+    hipExtLaunchKernelGGL(k_lin_point<NT>, dim3(g), dim3(NT), 0, s, t0, t1, 0, P, (const double*)W.rec,
+                          (const double*)W.pts, W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag,
+                          max_diag, W.part);
+    return;
+  }
   const bool many = P.nc > kLinLdsCams;
   hipLaunchKernelGGL((many ? k_point_assemble<jr_ja(true)> : k_point_assemble<jr_ja(false)>),
                      dim3(grid_for((int)std::min<long long>((long long)P.np * kPaLanes, 1LL << 30))),
@@ -1847,6 +2193,11 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
 }
 void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
+  if (W.jrfree) {
+    hipLaunchKernelGGL(k_cam_assemble_rc<512>, dim3(P.nvc, 1), dim3(512), 0, s, P, (const double*)W.rec,
+                       (const double*)W.pts, W.cpart, W.Hcc, W.gc);
+    return;
+  }
   const bool many = P.nc > kLinLdsCams;   // JR layout (jr_ja)
   // one workgroup per camera: measured faster than slicing at C3 (57 vs
   // 66 us at 8 slices) and at C5 (where 2048 / nvc < 1 anyway);
@@ -1879,6 +2230,16 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
   hipLaunchKernelGGL(k_point_elim, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.Hpp, W.gp, W.scale_p, W.diag_p,
                      radius, W.Linv, W.u, W.part);
   if (P.no == 0) return;
+  if (W.jrfree) {   // one 148-KB-LDS workgroup per CU
+    const int g = lds_grid(P.no);
+    if (W.w32)
+      hipLaunchKernelGGL(k_obs_w_rc<float>, dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, (const double*)W.rec,
+                         (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.Wf);
+    else
+      hipLaunchKernelGGL(k_obs_w_rc<double>, dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, (const double*)W.rec,
+                         (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.W);
+    return;
+  }
   const int g = lds_grid(P.no);
   if (W.w32) {
     if (P.nc <= kLinLdsCams)
@@ -1976,6 +2337,11 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
   else
     hipLaunchKernelGGL(k_backsub<double>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p,
                        W.W, W.u, W.Linv, W.y, W.scale_p, W.part);
+  if (W.jrfree) {
+    hipLaunchKernelGGL(k_candidate_rc<512>, dim3(lds_grid(P.no)), dim3(512), 0, s, P, (const double*)W.rec,
+                       (const double*)W.pts, W.delta_c, W.delta_p, W.rec_c, W.pts_c, W.part);
+    return;
+  }
   if (P.nc <= kLinLdsCams) {
     const int g = lds_grid(P.no);
     hipLaunchKernelGGL((k_candidate_lds<kLinLdsThreads, false>), dim3(g), dim3(kLinLdsThreads), 0, s, P, W.JR,

@@ -317,7 +317,15 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.rec_c = ctx->dalloc<double>((size_t)kCamRec * nc);
   W.crec = ctx->dalloc<double>((size_t)16 * nc);
   W.ctbl = ctx->dalloc<double>((size_t)22 * nc);
-  W.JR = ctx->dalloc<double>((size_t)(bahip::jr_ja_host(nc) + 8) * no);   // JA [no][jr_ja] + JB [no][8] (ba_kernels.hip)
+  // J-free iteration where the camera table fits the LDS (nc <= 200): r and J
+  // are recomputed by every consumer and never stored; BA_JR=1 forces the
+  // JR-materialising kernels (A/B, diagnostics).  JR is then allocated only
+  // for ba_linearize's read-back.
+  {
+    const char* e = std::getenv("BA_JR");
+    W.jrfree = nc > 0 && nc <= bahip::kLinLdsCamsHost && !(e && e[0] == '1');
+  }
+  W.JR = W.jrfree ? nullptr : ctx->dalloc<double>((size_t)(bahip::jr_ja_host(nc) + 8) * no);   // JA [no][jr_ja] + JB [no][8] (ba_kernels.hip)
   W.delta_p = ctx->dalloc<double>(3 * (size_t)np);
   W.Hpp = ctx->dalloc<double>(6 * (size_t)np);
   W.gp = ctx->dalloc<double>(3 * (size_t)np);
@@ -528,7 +536,9 @@ void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double 
   launch_lin_prep(P, W, s);
   // time_rj: kernel execution stamps from the launch itself (bench roofline)
   launch_linearize(P, W, s, time_rj ? ctx->ev[2] : nullptr, time_rj ? ctx->ev[3] : nullptr);
-  launch_point_assemble(P, W, compute_scale, min_diag, max_diag, s);
+  // (J-free: the timed residual + Jacobian kernel is k_lin_point, launched here)
+  launch_point_assemble(P, W, compute_scale, min_diag, max_diag, s, time_rj && W.jrfree ? ctx->ev[2] : nullptr,
+                        time_rj && W.jrfree ? ctx->ev[3] : nullptr);
   launch_cam_assemble(P, W, s);
   // point-side scalars: folded here when they must be all-reduced before
   // cam_norms, else together with the camera-side ones (one launch less)
@@ -1044,6 +1054,14 @@ int ba_linearize(ba_ctx* ctx, double* r, double* J, double* cost) {
     ba_default_options(&o);
     LinResult L = linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
     const int no = ctx->no;
+    if (ctx->W.jrfree) {   // the iteration never stores J: write the records once for the read-back
+      if (!ctx->W.JR) ctx->W.JR = ctx->dalloc<double>((size_t)(bahip::jr_ja_host(ctx->P.nc) + 8) * no);
+      bahip::launch_linearize_jr(ctx->P, ctx->W, ctx->stream);
+      // its cost partials are not this call's result (k_lin_point's were): fold
+      // and clear them so no later reduction counts them
+      launch_reduce(ctx->W, bit(SL_COST) | bit(SL_LIN_BAD), 0, ctx->stream);
+      HIP_OK(hipStreamSynchronize(ctx->stream));
+    }
     // record layout of ba_kernels.hip: JA [no][ja] (Jc rows; ja = 14: then r
     // again) then JB [no][8] (Jp rows, r)
     const int ja = bahip::jr_ja_host(ctx->P.nc);
