@@ -1826,7 +1826,11 @@ struct CamRegs {
   __device__ double K(int i) const { return k[i]; }
 };
 
-template <int NT>
+// LANES lanes per point (lane l of a group takes the point's observations l,
+// l + LANES, ...; fixed-order xor fold inside the group); the next
+// observation's indices and pixel, and the group's next point, are loaded one
+// step ahead (clamped, unconditional loads)
+template <int NT, int LANES>
 __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __restrict__ rec,
                                                   const double* __restrict__ pts, double* __restrict__ Hpp,
                                                   double* __restrict__ gp, double* __restrict__ scale_p,
@@ -1839,19 +1843,36 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
   double acc[4] = {0.0, 0.0, 0.0, 0.0};   // cost, bad, gn2, xn2
   double gmax = 0.0;
   const size_t np = (size_t)P.np;
-  const int sl = threadIdx.x & (kPaLanes - 1);
-  const int g0 = (blockIdx.x * NT + threadIdx.x) / kPaLanes, gs = gridDim.x * NT / kPaLanes;
-  for (int p = g0; p < P.np; p += gs) {     // uniform inside a lane group
-    const bool pv = P.pt_var[p];
-    const double X0 = pts[3 * p], X1 = pts[3 * p + 1], X2 = pts[3 * p + 2];
+  const int sl = threadIdx.x & (LANES - 1);
+  const int g0 = (blockIdx.x * NT + threadIdx.x) / LANES, gs = gridDim.x * NT / LANES;
+  const int lastp = max(P.np - 1, 0), lasto = max(P.no - 1, 0);
+  // the group's point p and its data, one point ahead (np = 0: no prologue,
+  // pt_off has a single entry)
+  int p = P.np > 0 ? g0 : P.np;
+  if (P.np > 0) {
+  // (prologue and loop)
+  int pc = min(p, lastp);
+  int o0 = P.pt_off[pc], o1 = P.pt_off[pc + 1];
+  double X0 = pts[3 * pc], X1 = pts[3 * pc + 1], X2 = pts[3 * pc + 2];
+  bool pv = P.pt_var[pc] != 0;
+  for (; p < P.np; p += gs) {     // uniform inside a lane group
+    const int pn = min(p + gs, lastp);
+    const int o0n = P.pt_off[pn], o1n = P.pt_off[pn + 1];
+    const double Y0 = pts[3 * pn], Y1 = pts[3 * pn + 1], Y2 = pts[3 * pn + 2];
+    const bool pvn = P.pt_var[pn] != 0;
     double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-    const int o0 = P.pt_off[p], o1 = P.pt_off[p + 1];
-    for (int o = o0 + sl; o < o1; o += kPaLanes) {
-      const int c = P.obs_cam[o];
+    int o = o0 + sl;
+    int oc = min(o, lasto);
+    int c = P.obs_cam[oc];
+    float2 uv = P.uv[oc];
+    for (; o < o1; o += LANES) {
+      const int on = min(o + LANES, lasto);
+      const int cn = P.obs_cam[on];
+      const float2 uvn = P.uv[on];
       const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
       double out[kJR];
       bool fin;
-      const double rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, P.uv[o], out, fin);
+      const double rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
       acc[0] += 0.5 * rho;
       acc[1] += fin ? 0.0 : 1.0;
       // k_point_assemble's accumulation of the JB record (Jp rows, r)
@@ -1863,40 +1884,48 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
         H[0] += a * a; H[1] += a * b; H[2] += a * cc; H[3] += b * b; H[4] += b * cc; H[5] += cc * cc;
         g[0] += a * rr[row]; g[1] += b * rr[row]; g[2] += cc * rr[row];
       }
+      c = cn;
+      uv = uvn;
     }
-    if (!pv) continue;
+    if (pv) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
+      for (int k = 0; k < 6; ++k) {
 #pragma unroll
-      for (int x = kPaLanes / 2; x >= 1; x >>= 1) H[k] += __shfl_xor(H[k], x, kPaLanes);
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-#pragma unroll
-      for (int x = kPaLanes / 2; x >= 1; x >>= 1) g[k] += __shfl_xor(g[k], x, kPaLanes);
-    }
-    if (sl != 0) continue;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Hpp[k * np + p] = H[k];
-    const double hd[3] = {H[0], H[3], H[5]};
-    const double Xk[3] = {X0, X1, X2};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      gp[k * np + p] = g[k];
-      double s;
-      if (compute_scale) {
-        s = 1.0 / (1.0 + sqrt(hd[k]));
-        scale_p[k * np + p] = s;
-      } else {
-        s = scale_p[k * np + p];
+        for (int x = LANES / 2; x >= 1; x >>= 1) H[k] += __shfl_xor(H[k], x, LANES);
       }
-      diag_p[k * np + p] = fmin(fmax(hd[k] * s * s, min_diag), max_diag);
-      const double x = Xk[k];
-      const double d = x - (x + (-g[k]));
-      gmax = fmax(gmax, fabs(d));
-      acc[2] += d * d;
-      acc[3] += x * x;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+#pragma unroll
+        for (int x = LANES / 2; x >= 1; x >>= 1) g[k] += __shfl_xor(g[k], x, LANES);
+      }
+      if (sl == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) Hpp[k * np + p] = H[k];
+        const double hd[3] = {H[0], H[3], H[5]};
+        const double Xk[3] = {X0, X1, X2};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          gp[k * np + p] = g[k];
+          double s;
+          if (compute_scale) {
+            s = 1.0 / (1.0 + sqrt(hd[k]));
+            scale_p[k * np + p] = s;
+          } else {
+            s = scale_p[k * np + p];
+          }
+          diag_p[k * np + p] = fmin(fmax(hd[k] * s * s, min_diag), max_diag);
+          const double x = Xk[k];
+          const double d = x - (x + (-g[k]));
+          gmax = fmax(gmax, fabs(d));
+          acc[2] += d * d;
+          acc[3] += x * x;
+        }
+      }
     }
+    o0 = o0n; o1 = o1n;
+    X0 = Y0; X1 = Y1; X2 = Y2;
+    pv = pvn;
+  }
   }
   double tot[4];
   block_sum<4>(acc, lds, tot);
@@ -2079,16 +2108,43 @@ __global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double*
   }
   __syncthreads();
   double acc[3] = {0.0, 0.0, 0.0};  // mneg, ccost, cand_bad
-  for (int o = blockIdx.x * NT + threadIdx.x; o < P.no; o += gridDim.x * NT) {
-    const int c = P.obs_cam[o], p = P.obs_pt[o];
-    const float2 uv = P.uv[o];
-    const bool pv = P.pt_var[p] != 0;
+  // the next observation's indices, pixel and point data are loaded one step
+  // ahead (clamped, unconditional)
+  struct ObsIn {
+    int c, p;
+    float2 uv;
+    bool pv;
+    double X[3], Xc[3], dp[3];
+  };
+  const int lasto = max(P.no - 1, 0);
+  auto load_in = [&](int o, ObsIn& q) {
+    const int oc = min(o, lasto);
+    q.c = P.obs_cam[oc];
+    q.p = P.obs_pt[oc];
+    q.uv = P.uv[oc];
+    q.pv = P.pt_var[q.p] != 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      q.X[k] = pts[3 * q.p + k];
+      q.Xc[k] = pts_c[3 * q.p + k];
+      q.dp[k] = delta_p[3 * q.p + k];
+    }
+  };
+  const int ostep = gridDim.x * NT;
+  int o = P.no > 0 ? blockIdx.x * NT + threadIdx.x : P.no;
+  ObsIn cur;
+  if (P.no > 0) load_in(o, cur);
+  for (; o < P.no; o += ostep) {
+    ObsIn nxt;
+    load_in(o + ostep, nxt);
+    const int c = cur.c;
+    const float2 uv = cur.uv;
     const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
     double j[kJR];
     bool fin;
-    (void)lin_obs(P, cam, cam.var(), pv, pts[3 * p], pts[3 * p + 1], pts[3 * p + 2], uv, j, fin);
-    const double dp0 = delta_p[3 * p], dp1 = delta_p[3 * p + 1], dp2 = delta_p[3 * p + 2];
-    const double X0 = pts_c[3 * p], X1 = pts_c[3 * p + 1], X2 = pts_c[3 * p + 2];
+    (void)lin_obs(P, cam, cam.var(), cur.pv, cur.X[0], cur.X[1], cur.X[2], uv, j, fin);
+    const double dp0 = cur.dp[0], dp1 = cur.dp[1], dp2 = cur.dp[2];
+    const double X0 = cur.Xc[0], X1 = cur.Xc[1], X2 = cur.Xc[2];
     const bool cfix = P.cam_fixed && P.cam_fixed[c];
     const double* cr = ctb + c * kCandRec;
     // k_candidate_lds' arithmetic on the same values
@@ -2118,6 +2174,7 @@ __global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double*
     acc[0] += mneg;
     acc[1] += 0.5 * rho;
     if (!isfinite(rc0) || !isfinite(rc1)) acc[2] += 1.0;
+    cur = nxt;
   }
   double out[3];
   block_sum<3>(acc, lds, out);
@@ -2178,11 +2235,14 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
                            double max_diag, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   if (W.jrfree) {   // r, J, cost and the point blocks in one pass (J never materialised)
     constexpr int NT = 512;
-    const int want = (int)std::min<long long>(((long long)P.np * kPaLanes + NT - 1) / NT, 1LL << 30);
+    static int lanes = -1;   // diagnostics: BA_LP_LANES (2 / 4 / 8 lanes per point)
+    if (lanes < 0) { const char* e = getenv("BA_LP_LANES"); lanes = e ? atoi(e) : 4; }
+    const int L = lanes == 2 || lanes == 8 ? lanes : 4;
+    const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
     const int g = std::max(1, std::min(want, 2 * lds_grid(1 << 30)));   // two 74-KB-LDS workgroups per CU
-    hipExtLaunchKernelGGL(k_lin_point<NT>, dim3(g), dim3(NT), 0, s, t0, t1, 0, P, (const double*)W.rec,
-                          (const double*)W.pts, W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag,
-                          max_diag, W.part);
+    auto kern = L == 2 ? k_lin_point<NT, 2> : (L == 8 ? k_lin_point<NT, 8> : k_lin_point<NT, 4>);
+    hipExtLaunchKernelGGL(kern, dim3(g), dim3(NT), 0, s, t0, t1, 0, P, (const double*)W.rec, (const double*)W.pts,
+                          W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
     return;
   }
   const bool many = P.nc > kLinLdsCams;
