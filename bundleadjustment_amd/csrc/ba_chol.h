@@ -490,9 +490,15 @@ __device__ __forceinline__ void inverse_rowblock(const double (*T)[LDP], const d
 // from sub-panel 1 on).
 // Z: inverse scratch, rows 16..63 used (row stride ZLD >= 16).  X may alias
 // Pc (written from the second sub-panel on).
-template <int ZLD = LDP>
+// Hook: work for waves 2 and 3 while wave 0 sweeps the last sub-panel and
+// wave 1 inverts row block 2 (the persistent factorisation prefetches its next
+// panel tile there); the per-step kernels pass none.
+struct NoFactorHook {
+  __device__ void operator()() const {}
+};
+template <int ZLD = LDP, class Hook = NoFactorHook>
 __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z)[ZLD], CholLds& W, int b, int m,
-                                  const double (*Pc)[LDP] = nullptr) {
+                                  const double (*Pc)[LDP] = nullptr, const Hook& hook = Hook{}) {
   const int w = threadIdx.x >> 6;
   __syncthreads();
   CHOL_STAMP(2);
@@ -504,6 +510,7 @@ __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z
     if (w == 0) panel_sweep(T, W, c0, b, m);
     else if (w == 1 && p > 0) inverse_rowblock(T, W.rsv, X, Z, p - 1, b, 1);
     else if (p == 0 && Pc != nullptr) mfma_xxT_rest(Pc, T);
+    else if (p == 3) hook();
     CHOL_STAMP(10 + 2 * p);
     __syncthreads();
     // trailing update of the remaining sub-panels: tiles (i, s), p < s <= i

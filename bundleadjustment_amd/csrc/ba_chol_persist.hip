@@ -137,10 +137,76 @@ __device__ inline bool worker_tile(int w, int T, int TR, int& I, int& J) {
   return false;
 }
 
+// The next panel tile A_{c+1,c} into S3 by waves 2 and 3 (each wave one half,
+// 32 rows), if its worker has already published it: one relaxed poll per
+// wave, no spin (a wave that finds it unpublished leaves its half to the
+// next step's fetch).  ok[w - 2] tells the critical loop which halves landed.
+struct PanelPrefetch {
+  Rsrc rA;
+  size_t ld;
+  const unsigned* flag;   // nullptr: column 0, never updated (always ready)
+  unsigned epoch;
+  double (*S3)[LDP];
+  int* ok;
+  int r0, kc, nrows, cmax;
+  __device__ void operator()() const {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;   // w = 2 or 3
+    bool ready = true;
+    if (flag) {
+      const unsigned f = lane == 0 ? __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      ready = __builtin_amdgcn_readfirstlane(f) == epoch;
+    }
+    if (!ready) {
+      if (lane == 0) ok[w - 2] = 0;
+      return;
+    }
+    const int hr = 32 * (w - 2);                                                       // this wave's rows
+    double2 v[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {   // 32 rows x 32 pairs = 1024 pairs, 16 per lane in two rounds of 8
+      const int e = lane + 64 * it;    // 0..511: rows hr + (e >> 5) for it < 8 covers 16 rows
+      const int i = hr + (e >> 5), j = (e & 31) * 2;
+      const int ri = r0 + i, cj = kc + j;
+      const int ric = min(ri, nrows - 1), cjc = min(cj, cmax - 2) & ~1;
+      v[it] = ld_sc1(rA, ((size_t)ric * ld + cjc) * sizeof(double));
+      const bool rok = ri < nrows;
+      v[it].x = (rok && cj < cmax) ? v[it].x : 0.0;
+      v[it].y = (rok && cj + 1 < cmax) ? v[it].y : 0.0;
+    }
+    double2 u[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int e = lane + 64 * (it + 8);
+      const int i = hr + (e >> 5), j = (e & 31) * 2;
+      const int ri = r0 + i, cj = kc + j;
+      const int ric = min(ri, nrows - 1), cjc = min(cj, cmax - 2) & ~1;
+      u[it] = ld_sc1(rA, ((size_t)ric * ld + cjc) * sizeof(double));
+      const bool rok = ri < nrows;
+      u[it].x = (rok && cj < cmax) ? u[it].x : 0.0;
+      u[it].y = (rok && cj + 1 < cmax) ? u[it].y : 0.0;
+    }
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int e = lane + 64 * it, i = hr + (e >> 5), j = (e & 31) * 2;
+      S3[i][j] = v[it].x;
+      S3[i][j + 1] = v[it].y;
+    }
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int e = lane + 64 * (it + 8), i = hr + (e >> 5), j = (e & 31) * 2;
+      S3[i][j] = u[it].x;
+      S3[i][j + 1] = u[it].y;
+    }
+    if (lane == 0) ok[w - 2] = 1;
+  }
+};
+
 __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   __shared__ double S0[CB][LDP];
   __shared__ double S1[CB][LDP];
   __shared__ double S2[CB][LDP];
+  __shared__ double S3[CB][LDP];   // the next panel tile A_{c+1,c}, prefetched during the factor
+  __shared__ int pref_ok[2];
   __shared__ CholLds cw;
   const int n = a.n, nrows = n + 1, T = a.T;
   const size_t ld = (size_t)a.ld;
@@ -152,6 +218,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
 
   if (blockIdx.x == 0) {
     // ---------------- critical workgroup: the diagonal chain
+    if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; }
     for (int c = 0; c < T; ++c) {
       const int s = c * CB;
       const int b = min(CB, n - s);
@@ -161,24 +228,29 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         stage64(S0, a.A, ld, 0, 0, nrows, b);     // written before the launch
       } else {
         const int k = c - 1, kc = k * CB, kb = min(CB, n - kc);
-        // A_{c,k} final (its worker; column 0 is never updated) and the
-        // diagonal tile after the updates k' <= c - 2 (no worker for c = 1)
-        if (k >= 1) bad |= !wait_flag(&tflag[c * T + k], a.epoch);
-        if (c >= 2) bad |= !wait_flag(&tflag[c * T + c], a.epoch);
+        // A_{c,k} final (its worker; column 0 is never updated): prefetched
+        // into S3 during the last factor when published by then, else fetched
+        // here; the diagonal tile after the updates k' <= c - 2 (no worker for
+        // c = 1) is fetched into registers and lands behind the panel GEMM
+        const bool have_pref = pref_ok[0] != 0 && pref_ok[1] != 0;   // (read after the factor's last barrier)
+        if (!have_pref) {
+          if (k >= 1) bad |= !wait_flag(&tflag[c * T + k], a.epoch);
+          const TileRegs tP = tile_fetch_sc1(rA, ld, s, kc, nrows, kc + kb);   // A_{c,k}
+          tile_put(S3, tP);
+        }
+        if (c >= 2) bad |= !wait_flag(&tflag[c * T + c], a.epoch);   // (its barrier also covers S3)
+        else __syncthreads();
+        if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; }
         PSTAMP(c, 1);
-        const TileRegs tA = tile_fetch_sc1<true>(rA, ld, s, s, nrows, s + b);   // A_{c,c} (+ rhs row)
-        const TileRegs tP = tile_fetch_sc1(rA, ld, s, kc, nrows, kc + kb);      // A_{c,k}
-        // V_{c-1}'s write-through stores were issued at the end of the last
-        // iteration: drain them together with these loads, then raise its
-        // flag (the workers need V_{c-1} one step later: off the chain)
-        publish(&vflag[k], a.epoch);
-        tile_put(S0, tA);
-        tile_put(S1, tP);
-        __syncthreads();
+        const TileRegs tA = tile_fetch_sc1<true>(rA, ld, s, s, nrows, s + b);   // A_{c,c} (+ rhs row), in flight
         PSTAMP(c, 2);
         d4 acc[4];
-        mfma_xVT_strip(S1, S2, acc);            // P = A_{c,k} V_k^T (V_k: S2, from the last iteration)
-        __syncthreads();
+        mfma_xVT_strip(S3, S2, acc);            // P = A_{c,k} V_k^T (V_k: S2, from the last iteration)
+        // V_{c-1}'s write-through stores (issued at the end of the last
+        // iteration) drain with the diagonal tile's loads, then its flag goes
+        // up (the workers need V_{c-1} one step later: off the chain)
+        publish(&vflag[k], a.epoch);
+        tile_put(S0, tA);
         {
           const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -196,7 +268,15 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       }
       if (threadIdx.x == 0) cw.bad = 0;
       PSTAMP(c, 4);
-      factor_invert_blk(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr);
+      if (c + 1 < T) {
+        // next step's panel tile A_{c+1,c}: final once its worker published
+        // it (column 0: from before the launch)
+        const PanelPrefetch pf{rA, ld, c >= 1 ? &tflag[(c + 1) * T + c] : nullptr, a.epoch, S3, pref_ok,
+                               (c + 1) * CB, c * CB, nrows, c * CB + min(CB, n - c * CB)};
+        factor_invert_blk(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr, pf);
+      } else {
+        factor_invert_blk(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr);
+      }
       __syncthreads();
       PSTAMP(c, 5);
       // V_c: cleaned in place (zero above the diagonal, identity rows past b:
