@@ -1553,6 +1553,13 @@ __device__ inline void load_w(const double* __restrict__ W, int o, double (&w)[1
 #pragma unroll
   for (int k = 0; k < 9; ++k) { const double2 t = s[k]; w[2 * k] = t.x; w[2 * k + 1] = t.y; }
 }
+// the same as a streaming (non-temporal) load: the partner side of a camera
+// pair, read once, should not evict the row side's records from L2
+__device__ inline void load_w_nt(const double* __restrict__ W, int o, double (&w)[18]) {
+  const ntd2* s = reinterpret_cast<const ntd2*>(W + (size_t)o * 18);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) { const ntd2 t = __builtin_nontemporal_load(s + k); w[2 * k] = t.x; w[2 * k + 1] = t.y; }
+}
 __device__ inline void acc_pair(double (&acc)[36], const double (&a)[18], const double (&b)[18]) {
 #pragma unroll
   for (int i = 0; i < 6; ++i)
@@ -1569,9 +1576,14 @@ __device__ inline void acc_pair(double (&acc)[36], const double (&a)[18], const 
 #define BA_PAIR_LANES 16
 #endif
 constexpr int kPairLanes = BA_PAIR_LANES;
+template <bool NTB>
 __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* __restrict__ blocks, int nblocks,
                                                      const int2* __restrict__ pairs, const double* __restrict__ W,
                                                      double* __restrict__ S) {
+  auto load_b = [&](int o, double (&w)[18]) {
+    if constexpr (NTB) load_w_nt(W, o, w);
+    else load_w(W, o, w);
+  };
   constexpr int PL = kPairLanes, BPW = 64 / PL;
   const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
   // XCD-aware order: workgroups b and b + 8 share an XCD (round-robin
@@ -1595,15 +1607,15 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
     for (; e + PL < blk.w; e += 2 * PL) {
       const int2 p0 = pairs[e], p1 = pairs[e + PL];
       double a0[18], b0[18], a1[18], b1[18];
-      load_w(W, p0.x, a0); load_w(W, p0.y, b0);
-      load_w(W, p1.x, a1); load_w(W, p1.y, b1);
+      load_w(W, p0.x, a0); load_b(p0.y, b0);
+      load_w(W, p1.x, a1); load_b(p1.y, b1);
       acc_pair(acc, a0, b0);
       acc_pair(acc, a1, b1);
     }
     if (e < blk.w) {
       const int2 p0 = pairs[e];
       double a0[18], b0[18];
-      load_w(W, p0.x, a0); load_w(W, p0.y, b0);
+      load_w(W, p0.x, a0); load_b(p0.y, b0);
       acc_pair(acc, a0, b0);
     }
 #pragma unroll
@@ -1830,7 +1842,7 @@ struct CamRegs {
 // l + LANES, ...; fixed-order xor fold inside the group); the next
 // observation's indices and pixel, and the group's next point, are loaded one
 // step ahead (clamped, unconditional loads)
-template <int NT, int LANES>
+template <int NT, int LANES, bool LAZY = false>
 __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __restrict__ rec,
                                                   const double* __restrict__ pts, double* __restrict__ Hpp,
                                                   double* __restrict__ gp, double* __restrict__ scale_p,
@@ -1869,10 +1881,16 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
       const int on = min(o + LANES, lasto);
       const int cn = P.obs_cam[on];
       const float2 uvn = P.uv[on];
-      const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
       double out[kJR];
       bool fin;
-      const double rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
+      double rho;
+      if constexpr (LAZY) {   // table entries read from LDS at use (fewer registers)
+        const CamLdsLazy cam{tbl + c * kTblRec, ktb + c * 9};
+        rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
+      } else {
+        const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
+        rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
+      }
       acc[0] += 0.5 * rho;
       acc[1] += fin ? 0.0 : 1.0;
       // k_point_assemble's accumulation of the JB record (Jp rows, r)
@@ -2234,13 +2252,28 @@ void launch_linearize_jr(const DevProblem& P, const DevWork& W, hipStream_t s, h
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
                            double max_diag, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   if (W.jrfree) {   // r, J, cost and the point blocks in one pass (J never materialised)
-    constexpr int NT = 512;
-    static int lanes = -1;   // diagnostics: BA_LP_LANES (2 / 4 / 8 lanes per point)
+    // diagnostics: BA_LP_LANES (2 / 4 / 8 lanes per point), BA_LP_LAZY=1
+    // (camera-table entries read from LDS at use), BA_LP_NT (256 / 512)
+    static int lanes = -1, lazy = -1, nt = -1;
     if (lanes < 0) { const char* e = getenv("BA_LP_LANES"); lanes = e ? atoi(e) : 4; }
+    if (lazy < 0) { const char* e = getenv("BA_LP_LAZY"); lazy = e ? atoi(e) : 0; }
+    if (nt < 0) { const char* e = getenv("BA_LP_NT"); nt = e ? atoi(e) : 256; }
     const int L = lanes == 2 || lanes == 8 ? lanes : 4;
+    const int NT = nt == 512 ? 512 : 256;
+    // two 74-KB-LDS workgroups per CU at most: a grid of that size, grid-stride
+    // over the points (no second round of table fills)
     const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
-    const int g = std::max(1, std::min(want, 2 * lds_grid(1 << 30)));   // two 74-KB-LDS workgroups per CU
-    auto kern = L == 2 ? k_lin_point<NT, 2> : (L == 8 ? k_lin_point<NT, 8> : k_lin_point<NT, 4>);
+    const int g = std::max(1, std::min(want, 2 * lds_grid(1 << 30)));
+    using KF = void (*)(DevProblem, const double*, const double*, double*, double*, double*, double*, int, double,
+                        double, double*);
+    KF kern;
+    if (NT == 256) {
+      if (lazy) kern = L == 2 ? k_lin_point<256, 2, true> : (L == 8 ? k_lin_point<256, 8, true> : k_lin_point<256, 4, true>);
+      else kern = L == 2 ? k_lin_point<256, 2> : (L == 8 ? k_lin_point<256, 8> : k_lin_point<256, 4>);
+    } else {
+      if (lazy) kern = L == 2 ? k_lin_point<512, 2, true> : (L == 8 ? k_lin_point<512, 8, true> : k_lin_point<512, 4, true>);
+      else kern = L == 2 ? k_lin_point<512, 2> : (L == 8 ? k_lin_point<512, 8> : k_lin_point<512, 4>);
+    }
     hipExtLaunchKernelGGL(kern, dim3(g), dim3(NT), 0, s, t0, t1, 0, P, (const double*)W.rec, (const double*)W.pts,
                           W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
     return;
@@ -2343,7 +2376,12 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   int grid = (waves + 3) / 4;
   if (grid > grid_cap) grid = grid_cap;
   grid = (grid + 7) / 8 * 8;   // k_schur_pairs' XCD ranges need a multiple of 8
-  hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
+  static int ntb = -1;   // diagnostics: BA_PAIRS_NTB=1 streams the partner records (non-temporal)
+  if (ntb < 0) { const char* e = getenv("BA_PAIRS_NTB"); ntb = e ? atoi(e) : 0; }
+  if (ntb)
+    hipLaunchKernelGGL(k_schur_pairs<true>, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
+  else
+    hipLaunchKernelGGL(k_schur_pairs<false>, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
 }
 // one workgroup per row of S: row i < n holds its lower part (j <= i), row n
 // the rhs (all n entries)

@@ -15,7 +15,7 @@ fi
 timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; cat $OUT/bench.json; stop_on_fault $rc
 for v in ${AB:-}; do
-  timeout -k 10 300 env $v python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_$v.json 2>> $OUT/bench.err
+  timeout -k 10 300 env ${v//,/ } python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_$v.json 2>> $OUT/bench.err
   rc=$?; echo "== $v"; python3 -c "import json,sys; d=json.load(open('$OUT/bench_$v.json')); print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'])"; stop_on_fault $rc
 done
 timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench2.json 2>> $OUT/bench.err
