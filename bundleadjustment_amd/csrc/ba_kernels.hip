@@ -2203,6 +2203,178 @@ __global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double*
   }
 }
 
+// Back substitution of the points fused with the model cost change and the
+// candidate cost (J-free; replaces k_backsub + k_candidate_rc).  Per point,
+// LANES lanes (k_lin_point's layout):
+//   pass 1  v = sum_o Jp_o^T (Jc_o dc_o) over the point's observations (J
+//           recomputed at x), folded in the group; then
+//           w = u_p + L_p^-1 (s_p o v) = u_p - sum_o W_o^T y_c  (W_o = s_c Jc^T
+//           Jp s_p L_p^-T and s_c o y_c = -dc: the same step without reading
+//           the 144-B W records), y_p = L_p^-T w, d_p = -s_p o y_p, x'_p.
+//   pass 2  J again: J d . (r + J d / 2) and the candidate residual at
+//           (camera', x'_p) per observation.
+template <int NT, int LANES, bool LAZY>
+__global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double* __restrict__ rec,
+                                                      const double* __restrict__ pts,
+                                                      const double* __restrict__ delta_c,
+                                                      const double* __restrict__ rec_c, const double* __restrict__ u,
+                                                      const double* __restrict__ Linv,
+                                                      const double* __restrict__ scale_p, double* __restrict__ pts_c,
+                                                      double* __restrict__ delta_p, double* __restrict__ part) {
+  __shared__ double lds[5 * 16];
+  __shared__ __attribute__((aligned(16))) double tbl[kLinLdsCams * kTblRec];
+  __shared__ float ktb[kLinLdsCams * 9];
+  __shared__ double ctb[kLinLdsCams * kCandRec];
+  fill_lin_table<NT>(P, rec, tbl, ktb);
+  {
+    const int n = P.nc * kCandRec;
+    for (int e = threadIdx.x; e < n; e += NT) ctb[e] = cand_entry(P, rec_c, delta_c, e);
+  }
+  __syncthreads();
+  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // step2, step_bad, mneg, ccost, cand_bad
+  const size_t np = (size_t)P.np;
+  const int sl = threadIdx.x & (LANES - 1);
+  const int g0 = (blockIdx.x * NT + threadIdx.x) / LANES, gs = gridDim.x * NT / LANES;
+  const int lastp = max(P.np - 1, 0), lasto = max(P.no - 1, 0);
+  auto lin = [&](int c, bool pv, double X0, double X1, double X2, float2 uv, double (&j)[kJR]) {
+    bool fin;
+    if constexpr (LAZY) {
+      const CamLdsLazy cam{tbl + c * kTblRec, ktb + c * 9};
+      (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
+    } else {
+      const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
+      (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
+    }
+  };
+  int p = P.np > 0 ? g0 : P.np;
+  if (P.np > 0) {
+    int pc = min(p, lastp);
+    int o0 = P.pt_off[pc], o1 = P.pt_off[pc + 1];
+    double X0 = pts[3 * pc], X1 = pts[3 * pc + 1], X2 = pts[3 * pc + 2];
+    bool pv = P.pt_var[pc] != 0;
+    for (; p < P.np; p += gs) {   // uniform inside a lane group
+      const int pn = min(p + gs, lastp);
+      const int o0n = P.pt_off[pn], o1n = P.pt_off[pn + 1];
+      const double Y0 = pts[3 * pn], Y1 = pts[3 * pn + 1], Y2 = pts[3 * pn + 2];
+      const bool pvn = P.pt_var[pn] != 0;
+      double dX[3] = {0.0, 0.0, 0.0};
+      if (pv) {
+        // pass 1: v = sum Jp^T (Jc dc)
+        double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+        int o = o0 + sl;
+        int oc = min(o, lasto);
+        int c = P.obs_cam[oc];
+        float2 uv = P.uv[oc];
+        for (; o < o1; o += LANES) {
+          const int on = min(o + LANES, lasto);
+          const int cn = P.obs_cam[on];
+          const float2 uvn = P.uv[on];
+          double j[kJR];
+          lin(c, true, X0, X1, X2, uv, j);
+          const double* dc = ctb + c * kCandRec + 16;   // the camera step (0 for a fixed camera)
+          double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+          for (int a = 0; a < 6; ++a) { t0 += j[a] * dc[a]; t1 += j[6 + a] * dc[a]; }
+          v0 += j[12] * t0 + j[15] * t1;
+          v1 += j[13] * t0 + j[16] * t1;
+          v2 += j[14] * t0 + j[17] * t1;
+          c = cn;
+          uv = uvn;
+        }
+#pragma unroll
+        for (int x = LANES / 2; x >= 1; x >>= 1) {
+          v0 += __shfl_xor(v0, x, LANES);
+          v1 += __shfl_xor(v1, x, LANES);
+          v2 += __shfl_xor(v2, x, LANES);
+        }
+        const double s0 = scale_p[p], s1 = scale_p[np + p], s2 = scale_p[2 * np + p];
+        const double i00 = Linv[p], i10 = Linv[np + p], i11 = Linv[2 * np + p];
+        const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
+        const double z0 = s0 * v0, z1 = s1 * v1, z2 = s2 * v2;
+        const double w0 = u[4 * p] + i00 * z0;
+        const double w1 = u[4 * p + 1] + (i10 * z0 + i11 * z1);
+        const double w2 = u[4 * p + 2] + (i20 * z0 + i21 * z1 + i22 * z2);
+        const double yp[3] = {i00 * w0 + i10 * w1 + i20 * w2, i11 * w1 + i21 * w2, i22 * w2};
+        const double sp[3] = {s0, s1, s2};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dX[k] = (-yp[k]) * sp[k];
+      }
+      const double Xc[3] = {X0 + dX[0], X1 + dX[1], X2 + dX[2]};
+      if (sl == 0) {
+        const double Xk[3] = {X0, X1, X2};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          pts_c[3 * p + k] = pv ? Xc[k] : Xk[k];
+          delta_p[3 * p + k] = dX[k];
+          if (pv) {
+            const double e = Xk[k] - Xc[k];
+            acc[0] += e * e;
+            if (!isfinite(dX[k])) acc[1] += 1.0;
+          }
+        }
+      }
+      // pass 2: model cost change and candidate cost per observation
+      {
+        int o = o0 + sl;
+        int oc = min(o, lasto);
+        int c = P.obs_cam[oc];
+        float2 uv = P.uv[oc];
+        for (; o < o1; o += LANES) {
+          const int on = min(o + LANES, lasto);
+          const int cn = P.obs_cam[on];
+          const float2 uvn = P.uv[on];
+          double j[kJR];
+          lin(c, pv, X0, X1, X2, uv, j);
+          const bool cfix = P.cam_fixed && P.cam_fixed[c];
+          const double* cr = ctb + c * kCandRec;
+          // k_candidate_lds' arithmetic
+          double jd0 = 0.0, jd1 = 0.0;
+#pragma unroll
+          for (int a2 = 0; a2 < 6; ++a2) { jd0 += j[a2] * cr[16 + a2]; jd1 += j[6 + a2] * cr[16 + a2]; }
+          jd0 += j[12] * dX[0] + j[13] * dX[1] + j[14] * dX[2];
+          jd1 += j[15] * dX[0] + j[16] * dX[1] + j[17] * dX[2];
+          const double mneg = jd0 * (j[18] + jd0 / 2.0) + jd1 * (j[19] + jd1 / 2.0);
+          double pcand[3];
+          if (!cfix) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) pcand[i] = cr[i] * Xc[0] + cr[3 + i] * Xc[1] + cr[6 + i] * Xc[2] + cr[9 + i];
+          } else {
+            double ph[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ph[i] = Xc[0] * cr[i] + Xc[1] * cr[4 + i] + Xc[2] * cr[8 + i] + cr[12 + i];
+            pcand[0] = ph[0] / ph[3]; pcand[1] = ph[1] / ph[3]; pcand[2] = ph[2] / ph[3];
+          }
+          const float* Kc = ktb + c * 9;
+          double q[3];
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+            q[i] = pcand[0] * (double)Kc[i] + pcand[1] * (double)Kc[3 + i] + pcand[2] * (double)Kc[6 + i];
+          const double rc0 = q[0] / q[2] - (double)uv.x, rc1 = q[1] / q[2] - (double)uv.y;
+          double sc;
+          const double rho = huber(rc0 * rc0 + rc1 * rc1, P.huber_a, P.huber_b, &sc);
+          acc[2] += mneg;
+          acc[3] += 0.5 * rho;
+          if (!isfinite(rc0) || !isfinite(rc1)) acc[4] += 1.0;
+          c = cn;
+          uv = uvn;
+        }
+      }
+      o0 = o0n; o1 = o1n;
+      X0 = Y0; X1 = Y1; X2 = Y2;
+      pv = pvn;
+    }
+  }
+  double tot[5];
+  block_sum<5>(acc, lds, tot);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_STEP2_P)[blockIdx.x] = tot[0];
+    part_of(part, SL_STEP_BAD)[blockIdx.x] += tot[1];
+    part_of(part, SL_MCC_NEG)[blockIdx.x] = tot[2];
+    part_of(part, SL_CCOST)[blockIdx.x] = tot[3];
+    part_of(part, SL_CAND_BAD)[blockIdx.x] = tot[4];
+  }
+}
+
 void launch_cam_prep(const DevProblem& P, const double* cams, double* rec, bool deriv, hipStream_t s) {
   if (P.nc == 0) return;
   hipLaunchKernelGGL(k_cam_prep, dim3(P.nc), dim3(64), 0, s, P.nc, cams, P.K, P.cam_fixed, P.extr, rec,
@@ -2429,17 +2601,39 @@ void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) 
                      W.scale_c, W.cams_c, W.delta_c, W.rec_c, W.part);
 }
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  if (W.jrfree) {
+    // back substitution + candidate in one point-major pass (diagnostics:
+    // BA_PSTEP=0 runs k_backsub + k_candidate_rc instead; BA_PSTEP_LAZY=1)
+    static int fused = -1, lazy = -1;
+    if (fused < 0) { const char* e = getenv("BA_PSTEP"); fused = e ? atoi(e) : 1; }
+    if (lazy < 0) { const char* e = getenv("BA_PSTEP_LAZY"); lazy = e ? atoi(e) : 0; }
+    // (fp32 W storage keeps the W-based back substitution: the step then
+    // solves with the stored fp32 blocks, as the oracle's fp32-W mode does)
+    if (fused && !W.w32) {
+      constexpr int NT = 512, L = 4;
+      const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
+      const int g = std::max(1, std::min(want, lds_grid(1 << 30)));   // one 110-KB-LDS workgroup per CU
+      hipLaunchKernelGGL((lazy ? k_point_step_rc<NT, L, true> : k_point_step_rc<NT, L, false>), dim3(g), dim3(NT), 0,
+                         s, P, (const double*)W.rec, (const double*)W.pts, W.delta_c, W.rec_c, W.u, W.Linv,
+                         W.scale_p, W.pts_c, W.delta_p, W.part);
+      return;
+    }
+    if (W.w32)
+      hipLaunchKernelGGL(k_backsub<float>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c,
+                         W.delta_p, W.Wf, W.u, W.Linv, W.y, W.scale_p, W.part);
+    else
+      hipLaunchKernelGGL(k_backsub<double>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c,
+                         W.delta_p, W.W, W.u, W.Linv, W.y, W.scale_p, W.part);
+    hipLaunchKernelGGL(k_candidate_rc<512>, dim3(lds_grid(P.no)), dim3(512), 0, s, P, (const double*)W.rec,
+                       (const double*)W.pts, W.delta_c, W.delta_p, W.rec_c, W.pts_c, W.part);
+    return;
+  }
   if (W.w32)
     hipLaunchKernelGGL(k_backsub<float>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p,
                        W.Wf, W.u, W.Linv, W.y, W.scale_p, W.part);
   else
     hipLaunchKernelGGL(k_backsub<double>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c, W.delta_p,
                        W.W, W.u, W.Linv, W.y, W.scale_p, W.part);
-  if (W.jrfree) {
-    hipLaunchKernelGGL(k_candidate_rc<512>, dim3(lds_grid(P.no)), dim3(512), 0, s, P, (const double*)W.rec,
-                       (const double*)W.pts, W.delta_c, W.delta_p, W.rec_c, W.pts_c, W.part);
-    return;
-  }
   if (P.nc <= kLinLdsCams) {
     const int g = lds_grid(P.no);
     hipLaunchKernelGGL((k_candidate_lds<kLinLdsThreads, false>), dim3(g), dim3(kLinLdsThreads), 0, s, P, W.JR,
