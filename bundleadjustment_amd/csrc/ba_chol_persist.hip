@@ -246,10 +246,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         PSTAMP(c, 2);
         d4 acc[4];
         mfma_xVT_strip(S3, S2, acc);            // P = A_{c,k} V_k^T (V_k: S2, from the last iteration)
-        // V_{c-1}'s write-through stores (issued at the end of the last
-        // iteration) drain with the diagonal tile's loads, then its flag goes
-        // up (the workers need V_{c-1} one step later: off the chain)
-        publish(&vflag[k], a.epoch);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the diagonal tile has landed
         tile_put(S0, tA);
         {
           const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -298,7 +295,9 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       }
       bad |= cw.bad != 0;
       PSTAMP(c, 6);
-      if (c + 1 == T) publish(&vflag[c], a.epoch);   // else at the next iteration's tile fetch
+      // V_c to the workers at once: the trailing updates of step c, and with
+      // them the next panel and diagonal tiles, wait for it
+      publish(&vflag[c], a.epoch);
     }
     if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
     return;
@@ -342,14 +341,27 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       if (!diag) tile_put(S1, tJ);
     }
     __syncthreads();
+    // P_I = A_{I,k} V_k^T, P_J likewise: V_k is lower triangular, so the
+    // strip products skip its zero blocks (40 instead of 64 MFMAs per wave;
+    // the skipped terms are exact zeros, so the sums are those of the full
+    // product)
+    d4 sI[4], sJ[4];
+    mfma_xVT_strip(S0, S2, sI);
+    if (!diag) mfma_xVT_strip(S1, S2, sJ);
+    __syncthreads();
+    {
+      const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+      for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int rr = 16 * wv + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
+          S0[rr][cc] = sI[bc][g];
+          if (!diag) S1[rr][cc] = sJ[bc][g];
+        }
+    }
+    __syncthreads();
     d4 acc[2][2];
-    mfma_xyT_64(S0, S2, acc);                  // P_I
-    d4 accJ[2][2];
-    if (!diag) mfma_xyT_64(S1, S2, accJ);      // P_J
-    __syncthreads();
-    acc_to_lds(S0, acc, 0);
-    if (!diag) acc_to_lds(S1, accJ, 0);
-    __syncthreads();
     if (J == k + 1) lds_to_global(S0, a.L, ld, r0, kc, mI, kb);   // L_{I,k} final
     mfma_xyT_64(S0, diag ? S0 : S1, acc);      // P_I P_J^T
 #pragma unroll

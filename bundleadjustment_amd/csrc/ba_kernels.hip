@@ -1553,13 +1553,6 @@ __device__ inline void load_w(const double* __restrict__ W, int o, double (&w)[1
 #pragma unroll
   for (int k = 0; k < 9; ++k) { const double2 t = s[k]; w[2 * k] = t.x; w[2 * k + 1] = t.y; }
 }
-// the same as a streaming (non-temporal) load: the partner side of a camera
-// pair, read once, should not evict the row side's records from L2
-__device__ inline void load_w_nt(const double* __restrict__ W, int o, double (&w)[18]) {
-  const ntd2* s = reinterpret_cast<const ntd2*>(W + (size_t)o * 18);
-#pragma unroll
-  for (int k = 0; k < 9; ++k) { const ntd2 t = __builtin_nontemporal_load(s + k); w[2 * k] = t.x; w[2 * k + 1] = t.y; }
-}
 __device__ inline void acc_pair(double (&acc)[36], const double (&a)[18], const double (&b)[18]) {
 #pragma unroll
   for (int i = 0; i < 6; ++i)
@@ -1576,14 +1569,9 @@ __device__ inline void acc_pair(double (&acc)[36], const double (&a)[18], const 
 #define BA_PAIR_LANES 16
 #endif
 constexpr int kPairLanes = BA_PAIR_LANES;
-template <bool NTB>
 __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* __restrict__ blocks, int nblocks,
                                                      const int2* __restrict__ pairs, const double* __restrict__ W,
                                                      double* __restrict__ S) {
-  auto load_b = [&](int o, double (&w)[18]) {
-    if constexpr (NTB) load_w_nt(W, o, w);
-    else load_w(W, o, w);
-  };
   constexpr int PL = kPairLanes, BPW = 64 / PL;
   const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
   // XCD-aware order: workgroups b and b + 8 share an XCD (round-robin
@@ -1607,15 +1595,15 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
     for (; e + PL < blk.w; e += 2 * PL) {
       const int2 p0 = pairs[e], p1 = pairs[e + PL];
       double a0[18], b0[18], a1[18], b1[18];
-      load_w(W, p0.x, a0); load_b(p0.y, b0);
-      load_w(W, p1.x, a1); load_b(p1.y, b1);
+      load_w(W, p0.x, a0); load_w(W, p0.y, b0);
+      load_w(W, p1.x, a1); load_w(W, p1.y, b1);
       acc_pair(acc, a0, b0);
       acc_pair(acc, a1, b1);
     }
     if (e < blk.w) {
       const int2 p0 = pairs[e];
       double a0[18], b0[18];
-      load_w(W, p0.x, a0); load_b(p0.y, b0);
+      load_w(W, p0.x, a0); load_w(W, p0.y, b0);
       acc_pair(acc, a0, b0);
     }
 #pragma unroll
@@ -2427,7 +2415,9 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
     // diagnostics: BA_LP_LANES (2 / 4 / 8 lanes per point), BA_LP_LAZY=1
     // (camera-table entries read from LDS at use), BA_LP_NT (256 / 512)
     static int lanes = -1, lazy = -1, nt = -1;
-    if (lanes < 0) { const char* e = getenv("BA_LP_LANES"); lanes = e ? atoi(e) : 4; }
+    // 2 lanes per point: 30.7 us at C3 vs 32.4 at 4 and 38 at 512 threads;
+    // lazy table reads 42.5 (profiles/r03_v4_ab_lin_point.txt)
+    if (lanes < 0) { const char* e = getenv("BA_LP_LANES"); lanes = e ? atoi(e) : 2; }
     if (lazy < 0) { const char* e = getenv("BA_LP_LAZY"); lazy = e ? atoi(e) : 0; }
     if (nt < 0) { const char* e = getenv("BA_LP_NT"); nt = e ? atoi(e) : 256; }
     const int L = lanes == 2 || lanes == 8 ? lanes : 4;
@@ -2548,12 +2538,7 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   int grid = (waves + 3) / 4;
   if (grid > grid_cap) grid = grid_cap;
   grid = (grid + 7) / 8 * 8;   // k_schur_pairs' XCD ranges need a multiple of 8
-  static int ntb = -1;   // diagnostics: BA_PAIRS_NTB=1 streams the partner records (non-temporal)
-  if (ntb < 0) { const char* e = getenv("BA_PAIRS_NTB"); ntb = e ? atoi(e) : 0; }
-  if (ntb)
-    hipLaunchKernelGGL(k_schur_pairs<true>, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
-  else
-    hipLaunchKernelGGL(k_schur_pairs<false>, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
+  hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
 }
 // one workgroup per row of S: row i < n holds its lower part (j <= i), row n
 // the rhs (all n entries)
