@@ -29,13 +29,14 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 // critical workgroup records s_memtime at phase boundaries into g_stamps.
 #ifdef BA_CHOL_STAMPS
 __device__ unsigned long long g_stamps[64];
+__device__ int g_stamp_on = 1;   // the persistent kernel records one chosen step only
 #define CHOL_STAMP(i)                                                                         \
   do {                                                                                        \
     __builtin_amdgcn_sched_barrier(0);                                                        \
     unsigned long long t_;                                                                    \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
     __builtin_amdgcn_sched_barrier(0);                                                        \
-    if (threadIdx.x == 0) g_stamps[i] = t_;                                                   \
+    if (threadIdx.x == 0 && g_stamp_on) g_stamps[i] = t_;                                     \
   } while (0)
 #else
 #define CHOL_STAMP(i) do {} while (0)
@@ -326,11 +327,17 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // form (a_r,j+1 -= a_rj e / d_j) off the chain, so the final scaling and
 // the pivots on the diagonal are those of the column-by-column sweep.
 // Per pair the chain is: LDS read of B -> det, reciprocal -> f -> update of
-// the NEXT pair's two columns -> LDS publish (sched_barriers keep the publish
-// and the next reads ahead of the remaining updates).  Measured per 16
-// columns (tools/chol_bench.hip): 1 x 1 pivots ~5.7k cycles.
+// the NEXT pair's two columns -> LDS publish -> the next reads (the compiler
+// interleaves the remaining updates; wave_barrier only keeps the publish
+// ahead of the reads).  Measured per 16 columns (tools/sweep_probe.hip):
+// ~3.4k cycles with compile-time c0 / b / m, 4% below sched_barrier fencing.
 __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0, int b, int m) {
-  const int r = threadIdx.x & 63;
+  // the row index is made opaque here, so that the sweep's row masks are
+  // formed per sweep instead of being hoisted out of the caller's loops
+  // (in the persistent kernel they would stay live, as spilled SGPRs, across
+  // its whole block-column loop)
+  int r = threadIdx.x & 63;
+  asm volatile("" : "+v"(r));
   double a[16];
   {  // row r, columns c0..c0+15: 8 unconditional 16-B reads, then selects
     const double2* src = reinterpret_cast<const double2*>(&T[r][c0]);
@@ -346,7 +353,7 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
   }
   CHOL_STAMP(30 + c0 / 16 * 4);
   W.colp[0][r] = make_double2(a[0], a[1]);
-  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_wave_barrier();
   double2 q0 = W.colp[0][c0], q1 = W.colp[0][c0 + 1];
   double2 ct[16];
 #pragma unroll
@@ -358,6 +365,7 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
     const int buf = (jj >> 1) & 1;
     const double d0 = q0.x, e = q1.x, d1 = q1.y;
     const double rdet = recip(d0 * d1 - e * e);
+    const double rd0 = recip(d0);
     const bool row = r > j + 1 && r < m;
     const double u0 = a[jj], u1 = a[jj + 1];
     const double f0 = row ? fma(u0, d1, -u1 * e) * rdet : 0.0;
@@ -366,12 +374,11 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
       a[jj + 2] = fma(-f1, ct[jj + 2].y, fma(-f0, ct[jj + 2].x, a[jj + 2]));
       a[jj + 3] = fma(-f1, ct[jj + 3].y, fma(-f0, ct[jj + 3].x, a[jj + 3]));
       W.colp[buf ^ 1][r] = make_double2(a[jj + 2], a[jj + 3]);
-      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_wave_barrier();
       const double2 q0n = W.colp[buf ^ 1][c0 + jj + 2], q1n = W.colp[buf ^ 1][c0 + jj + 3];
       double2 ctn[16];
 #pragma unroll
       for (int t = jj + 4; t < 16; ++t) ctn[t] = W.colp[buf ^ 1][c0 + t];
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = jj + 4; t < 16; ++t) a[t] = fma(-f1, ct[t].y, fma(-f0, ct[t].x, a[t]));
       q0 = q0n;
@@ -380,7 +387,7 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
       for (int t = jj + 4; t < 16; ++t) ct[t] = ctn[t];
     }
     // column j+1 to its 1 x 1 form (rows r > j; lane j+1 gets the pivot d1 - e^2/d0)
-    if (r > j && r < m) a[jj + 1] -= u0 * (e * recip(d0));
+    if (r > j && r < m) a[jj + 1] -= u0 * (e * rd0);
   }
   CHOL_STAMP(31 + c0 / 16 * 4);
   // own pivot (lanes c0..c0+15): d_r = a_rr
@@ -416,38 +423,44 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
   }
 }
 
-// X_pp = L_pp^-1 for one 16x16 diagonal block p by the calling wave (lane
-// c < 16 solves L_pp x = e_c by forward substitution; L values are uniform
-// LDS broadcasts; 1/L_ii is the sweep's 1/sqrt(d_i), no divisions).  (A
-// recursive-doubling form, lane per entry and 8 LDS round trips, measured
-// slower in the pipeline.)
+// X_pp = L_pp^-1 for one 16x16 diagonal block p by the calling wave: lane
+// c < 16 solves L_pp x = e_c by column-oriented forward substitution (x_k
+// final -> every later row's sum takes its term at once), so the chain per
+// row is one multiply and one FMA; L values are uniform LDS broadcasts, the
+// next column read one step ahead; 1/L_ii is the sweep's 1/sqrt(d_i), no
+// divisions.  The sums run over k in the same order as a row-oriented
+// substitution (fma(-L_ik, x_k, s), k ascending).  (The row-oriented form has
+// a 120-FMA chain: ~5.7k cycles on the critical path of the last row block.)
 __device__ __forceinline__ void diag_inverse16(const double (*T)[LDP], const double* rinv, double (*X)[LDP], int p,
                                                int b) {
   const int c = threadIdx.x & 63;
   const int c0 = 16 * p;
   if (c0 >= b || c >= 16) return;
-  double x[16];
-  // rows are read two ahead of the substitution (the LDS latency would
-  // otherwise sit on the chain of every row)
-  double Lr[3][16];
+  double ri[16];
+  {
+    const double2* src = reinterpret_cast<const double2*>(&rinv[c0]);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+    for (int k = 0; k < 8; ++k) { const double2 v = src[k]; ri[2 * k] = v.x; ri[2 * k + 1] = v.y; }
+  }
+  double acc[16], col[16];
 #pragma unroll
-    for (int k = 0; k < i; ++k) Lr[i][k] = T[c0 + i][c0 + k];
+  for (int i = 0; i < 16; ++i) acc[i] = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+  for (int i = 1; i < 16; ++i) col[i] = T[c0 + i][c0];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    double nxt[16];
+#pragma unroll
+    for (int i = k + 2; i < 16; ++i) nxt[i] = T[c0 + i][c0 + k + 1];
+    const double xk = (c0 + k < b) ? acc[k] * ri[k] : 0.0;
+    acc[k] = xk;
+#pragma unroll
+    for (int i = k + 1; i < 16; ++i) acc[i] = fma(-col[i], xk, acc[i]);
+#pragma unroll
+    for (int i = k + 2; i < 16; ++i) col[i] = nxt[i];
   }
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    if (i + 2 < 16) {
-#pragma unroll
-      for (int k = 0; k < i + 2; ++k) Lr[(i + 2) % 3][k] = T[c0 + i + 2][c0 + k];
-    }
-    double s = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-    for (int k = 0; k < i; ++k) s -= Lr[i % 3][k] * x[k];
-    x[i] = (c0 + i < b) ? s * rinv[c0 + i] : 0.0;   // rinv = 1 / L_ii from the sweep
-  }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) X[c0 + i][c0 + c] = x[i];
+  for (int i = 0; i < 16; ++i) X[c0 + i][c0 + c] = acc[i];
 }
 
 // Z_q (16x16, rows zr.. of Z; Z's row stride ZLD) = sum_{k=q}^{p-1} L_pk X_kq, by the calling wave
@@ -490,27 +503,33 @@ __device__ __forceinline__ void inverse_rowblock(const double (*T)[LDP], const d
 // from sub-panel 1 on).
 // Z: inverse scratch, rows 16..63 used (row stride ZLD >= 16).  X may alias
 // Pc (written from the second sub-panel on).
-// Hook: work for waves 2 and 3 while wave 0 sweeps the last sub-panel and
-// wave 1 inverts row block 2 (the persistent factorisation prefetches its next
-// panel tile there); the per-step kernels pass none.
+// Hook: work for waves 2 and 3 while wave 0 sweeps sub-panel p = 1, 2, 3 and
+// wave 1 inverts row block p - 1 (the persistent factorisation prefetches its
+// next panel tile there); the per-step kernels pass none.
+// hook.finish(): waves 2 and 3 again, at the end of the inverse tail.
 struct NoFactorHook {
-  __device__ void operator()() const {}
+  __device__ void operator()(int) const {}
+  __device__ void finish() const {}
 };
-template <int ZLD = LDP, class Hook = NoFactorHook>
-__device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z)[ZLD], CholLds& W, int b, int m,
-                                  const double (*Pc)[LDP] = nullptr, const Hook& hook = Hook{}) {
+// FULL: b = m = CB (every block but the last): the sub-panel loop is
+// unrolled, so the sweeps' row predicates and LDS offsets are compile-time
+// (tools/sweep_probe.hip: a sweep with run-time c0 / b / m costs ~800 more
+// cycles of its ~3.5k).
+template <bool FULL, int ZLD, class Hook>
+__device__ __forceinline__ void factor_invert_impl(double (*T)[LDP], double (*X)[LDP], double (*Z)[ZLD], CholLds& W,
+                                                   int b, int m, const double (*Pc)[LDP], const Hook& hook) {
+  if constexpr (FULL) { b = CB; m = CB; }
   const int w = threadIdx.x >> 6;
   __syncthreads();
   CHOL_STAMP(2);
   int last = 0;
-  for (int p = 0; p < 4; ++p) {
+  auto subpanel = [&](const int p) {
     const int c0 = 16 * p;
-    if (c0 >= b) break;                      // uniform
     last = p;
     if (w == 0) panel_sweep(T, W, c0, b, m);
     else if (w == 1 && p > 0) inverse_rowblock(T, W.rsv, X, Z, p - 1, b, 1);
     else if (p == 0 && Pc != nullptr) mfma_xxT_rest(Pc, T);
-    else if (p == 3) hook();
+    else if (p >= 1) hook(p);
     CHOL_STAMP(10 + 2 * p);
     __syncthreads();
     // trailing update of the remaining sub-panels: tiles (i, s), p < s <= i
@@ -529,6 +548,13 @@ __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z
     }
     __syncthreads();
     CHOL_STAMP(11 + 2 * p);
+  };
+  if constexpr (FULL) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) subpanel(p);
+  } else {
+#pragma unroll 1
+    for (int p = 0; p < 4 && 16 * p < b; ++p) subpanel(p);
   }
   CHOL_STAMP(3);
   // last row block: diagonal inverse (wave 0) beside the sums Z_q (wave q + 1)
@@ -538,8 +564,19 @@ __device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z
   __syncthreads();
   CHOL_STAMP(41);
   if (w >= 1 && w - 1 < last) inv_offdiag_fin(X, Z, last, w - 1, 16 * w);
+  if (w >= 2) hook.finish();
   __syncthreads();
   CHOL_STAMP(4);
+}
+// KIND: 1 = the caller guarantees b = m = CB, 0 = the general form, -1 =
+// chosen at run time (two copies of the code)
+template <int KIND = -1, int ZLD = LDP, class Hook = NoFactorHook>
+__device__ void factor_invert_blk(double (*T)[LDP], double (*X)[LDP], double (*Z)[ZLD], CholLds& W, int b, int m,
+                                  const double (*Pc)[LDP] = nullptr, const Hook& hook = Hook{}) {
+  if constexpr (KIND == 1) factor_invert_impl<true>(T, X, Z, W, b, m, Pc, hook);
+  else if constexpr (KIND == 0) factor_invert_impl<false>(T, X, Z, W, b, m, Pc, hook);
+  else if (b == CB && m == CB) factor_invert_impl<true>(T, X, Z, W, b, m, Pc, hook);
+  else factor_invert_impl<false>(T, X, Z, W, b, m, Pc, hook);
 }
 
 }  // namespace bahip

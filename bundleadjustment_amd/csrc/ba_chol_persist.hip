@@ -138,9 +138,15 @@ __device__ inline bool worker_tile(int w, int T, int TR, int& I, int& J) {
 }
 
 // The next panel tile A_{c+1,c} into S3 by waves 2 and 3 (each wave one half,
-// 32 rows), if its worker has already published it: one relaxed poll per
-// wave, no spin (a wave that finds it unpublished leaves its half to the
-// next step's fetch).  ok[w - 2] tells the critical loop which halves landed.
+// 32 rows), spread over the factor so that no global round trip lands on a
+// sub-panel barrier: p = 1 polls the worker's flag (one relaxed load, no
+// spin); p = 2 fetches the half if the flag was seen, else polls again and
+// fetches at once when it is up; p = 3 polls if needed and only ISSUES the
+// loads, which land in LDS at the end of the inverse tail (finish()).  A half
+// still missing then is fetched at the next step's start.  (The worker of
+// A_{c+1,c} publishes it ~30k cycles after V_{c-1}: in sub-panel 3 mostly,
+// tools/chol_bench.hip.)  ok[w - 2]: 0 not yet, 2 flag seen, 1 landed in S3
+// (only lane 0 of the owning wave writes it; LDS is in order within the wave).
 struct PanelPrefetch {
   Rsrc rA;
   size_t ld;
@@ -149,55 +155,59 @@ struct PanelPrefetch {
   double (*S3)[LDP];
   int* ok;
   int r0, kc, nrows, cmax;
-  __device__ void operator()() const {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;   // w = 2 or 3
-    bool ready = true;
-    if (flag) {
-      const unsigned f = lane == 0 ? __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-      ready = __builtin_amdgcn_readfirstlane(f) == epoch;
-    }
-    if (!ready) {
-      if (lane == 0) ok[w - 2] = 0;
-      return;
-    }
-    const int hr = 32 * (w - 2);                                                       // this wave's rows
-    double2 v[8];
+  int c;                  // diagnostics (BA_CHOL_STAMPS): the step, for the fetch-phase record
+  mutable double2 v[16];  // loads in flight between p = 3 and finish()
+  mutable bool pending = false;
+  __device__ bool poll() const {
+    if (!flag) return true;
+    const unsigned f = (threadIdx.x & 63) == 0 ? __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                               : 0u;
+    return __builtin_amdgcn_readfirstlane(f) == epoch;
+  }
+  // this wave's 32 rows x 32 pairs = 1024 pairs, 16 per lane
+  __device__ void issue() const {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, hr = 32 * (w - 2);
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {   // 32 rows x 32 pairs = 1024 pairs, 16 per lane in two rounds of 8
-      const int e = lane + 64 * it;    // 0..511: rows hr + (e >> 5) for it < 8 covers 16 rows
+    for (int it = 0; it < 16; ++it) {
+      const int e = lane + 64 * it;
       const int i = hr + (e >> 5), j = (e & 31) * 2;
       const int ri = r0 + i, cj = kc + j;
       const int ric = min(ri, nrows - 1), cjc = min(cj, cmax - 2) & ~1;
       v[it] = ld_sc1(rA, ((size_t)ric * ld + cjc) * sizeof(double));
-      const bool rok = ri < nrows;
-      v[it].x = (rok && cj < cmax) ? v[it].x : 0.0;
-      v[it].y = (rok && cj + 1 < cmax) ? v[it].y : 0.0;
     }
-    double2 u[8];
+  }
+  __device__ void land(int p) const {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, hr = 32 * (w - 2);
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int e = lane + 64 * (it + 8);
-      const int i = hr + (e >> 5), j = (e & 31) * 2;
-      const int ri = r0 + i, cj = kc + j;
-      const int ric = min(ri, nrows - 1), cjc = min(cj, cmax - 2) & ~1;
-      u[it] = ld_sc1(rA, ((size_t)ric * ld + cjc) * sizeof(double));
-      const bool rok = ri < nrows;
-      u[it].x = (rok && cj < cmax) ? u[it].x : 0.0;
-      u[it].y = (rok && cj + 1 < cmax) ? u[it].y : 0.0;
-    }
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
+    for (int it = 0; it < 16; ++it) {
       const int e = lane + 64 * it, i = hr + (e >> 5), j = (e & 31) * 2;
-      S3[i][j] = v[it].x;
-      S3[i][j + 1] = v[it].y;
-    }
-#pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int e = lane + 64 * (it + 8), i = hr + (e >> 5), j = (e & 31) * 2;
-      S3[i][j] = u[it].x;
-      S3[i][j + 1] = u[it].y;
+      const int ri = r0 + i, cj = kc + j;
+      const bool rok = ri < nrows;
+      S3[i][j] = (rok && cj < cmax) ? v[it].x : 0.0;
+      S3[i][j + 1] = (rok && cj + 1 < cmax) ? v[it].y : 0.0;
     }
     if (lane == 0) ok[w - 2] = 1;
+#ifdef BA_CHOL_STAMPS
+    if (lane == 0 && w == 2 && c < 64) g_pstamps[c][7] = (unsigned long long)p;   // sub-panel of the fetch
+#endif
+  }
+  __device__ void operator()(int p) const {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;   // w = 2 or 3
+    const int st = __builtin_amdgcn_readfirstlane(ok[w - 2]);   // 0 at p = 1 (reset at the step start)
+    if (st == 1) return;
+    if (st == 0) {
+      if (!poll()) return;
+      if (p == 1) {
+        if (lane == 0) ok[w - 2] = 2;
+        return;
+      }
+    }
+    issue();
+    if (p == 2) land(p);
+    else pending = true;
+  }
+  __device__ void finish() const {
+    if (pending) land(3);
   }
 };
 
@@ -224,6 +234,10 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       const int b = min(CB, n - s);
       const int m = min(CB, nrows - s);
       PSTAMP(c, 0);
+#ifdef BA_CHOL_STAMPS
+      if (threadIdx.x == 0) g_stamp_on = c == T / 2;   // the factor's inner stamps: one mid step
+      if (threadIdx.x == 0 && c < 64) g_pstamps[c][7] = 0;
+#endif
       if (c == 0) {
         stage64(S0, a.A, ld, 0, 0, nrows, b);     // written before the launch
       } else {
@@ -232,7 +246,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         // into S3 during the last factor when published by then, else fetched
         // here; the diagonal tile after the updates k' <= c - 2 (no worker for
         // c = 1) is fetched into registers and lands behind the panel GEMM
-        const bool have_pref = pref_ok[0] != 0 && pref_ok[1] != 0;   // (read after the factor's last barrier)
+        const bool have_pref = pref_ok[0] == 1 && pref_ok[1] == 1;   // (read after the factor's last barrier)
         if (!have_pref) {
           if (k >= 1) bad |= !wait_flag(&tflag[c * T + k], a.epoch);
           const TileRegs tP = tile_fetch_sc1(rA, ld, s, kc, nrows, kc + kb);   // A_{c,k}
@@ -269,10 +283,10 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         // next step's panel tile A_{c+1,c}: final once its worker published
         // it (column 0: from before the launch)
         const PanelPrefetch pf{rA, ld, c >= 1 ? &tflag[(c + 1) * T + c] : nullptr, a.epoch, S3, pref_ok,
-                               (c + 1) * CB, c * CB, nrows, c * CB + min(CB, n - c * CB)};
-        factor_invert_blk(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr, pf);
+                               (c + 1) * CB, c * CB, nrows, c * CB + min(CB, n - c * CB), c};
+        factor_invert_blk<1>(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr, pf);   // b = m = CB before the last block
       } else {
-        factor_invert_blk(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr);
+        factor_invert_blk<0>(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr);
       }
       __syncthreads();
       PSTAMP(c, 5);
@@ -300,6 +314,9 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       publish(&vflag[c], a.epoch);
     }
     if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
+#ifdef BA_CHOL_STAMPS
+    if (threadIdx.x == 0) g_stamp_on = 1;
+#endif
     return;
   }
 

@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void k_chol_step_split(double* __restrict__ A,
     }
     if (threadIdx.x == 0) cw.bad = 0;
     CHOL_STAMP(1);
-    factor_invert_blk<18>(S0, S1, Zs, cw, b, m, k >= 0 ? S1 : nullptr);   // rows b..m-1 (rhs) come out as L rows too
+    factor_invert_blk<-1, 18>(S0, S1, Zs, cw, b, m, k >= 0 ? S1 : nullptr);   // rows b..m-1 (rhs) come out as L rows too
     CHOL_STAMP(5);
     __syncthreads();
     // only V_{k+1} and the rhs row of L leave the workgroup: the diagonal L

@@ -1,10 +1,12 @@
 // chol_bench.hip — diagnostic harness for the reduced-camera Cholesky
 // (bundleadjustment_amd/csrc/ba_chol.hip), built with in-kernel s_memtime
-// stamps.  Factors a random SPD (n+1) x n trapezoid, times every block step
+// stamps (-DBA_CHOL_STAMPS; they cost ~1.3k cycles per sub-panel sweep, so
+// time with a build without them: tools/chol_bench_ns).  Factors a random SPD (n+1) x n trapezoid, times every block step
 // with HIP events, prints the critical workgroup's phase cycles, solves and
 // checks the solution against a CPU Cholesky.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DBA_CHOL_STAMPS -I bundleadjustment_amd/csrc \
 //         tools/chol_bench.hip -o tools/chol_bench && tools/chol_bench 1194
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I bundleadjustment_amd/csrc tools/chol_bench.hip -o tools/chol_bench_ns
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -76,6 +78,7 @@ int main(int argc, char** argv) {
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
       tot += ms;
+#ifdef BA_CHOL_STAMPS
       unsigned long long st_h[64];
       CK(hipMemcpyFromSymbol(st_h, HIP_SYMBOL(g_stamps), sizeof(st_h)));
       if (verbose && (k < 2 || k == T / 2 || k + 2 == T))
@@ -97,6 +100,7 @@ int main(int argc, char** argv) {
                st_h[11] - st_h[10], st_h[12] - st_h[11], st_h[13] - st_h[12], st_h[14] - st_h[13], st_h[15] - st_h[14],
                st_h[16] - st_h[15], st_h[17] - st_h[16]);
 
+#endif
     }
     CK(hipMemset(dF, 0, sizeof(double) * 2 * n));
     CK(hipEventRecord(e0));
@@ -131,6 +135,7 @@ int main(int argc, char** argv) {
       CK(hipDeviceSynchronize());
       printf("persistent factor %.1f us (grid %d)\n", mp * 1e3, chol_persist_grid(n));
     }
+#ifdef BA_CHOL_STAMPS
     {
       unsigned long long ps[64][8];
       CK(hipMemcpyFromSymbol(ps, HIP_SYMBOL(g_pstamps), sizeof(ps)));
@@ -142,7 +147,18 @@ int main(int argc, char** argv) {
       printf("persistent critical cycles per step (avg of %d): wait %.0f  fetch+V publish %.0f  P gemm+store %.0f"
              "  C col0 %.0f  factor %.0f  V clean+store %.0f  | step %.0f\n",
              cnt, avg[0] / cnt, avg[1] / cnt, avg[2] / cnt, avg[3] / cnt, avg[4] / cnt, avg[5] / cnt, tot);
+      int ph[4] = {0, 0, 0, 0};
+      for (int c = 0; c + 1 < T && c < 64; ++c) ph[ps[c][7] & 3]++;
+      printf("    next panel tile prefetched in sub-panel 1/2/3: %d/%d/%d, at the next step's start: %d\n", ph[1], ph[2],
+             ph[3], ph[0]);
+      unsigned long long st_h[64];
+      CK(hipMemcpyFromSymbol(st_h, HIP_SYMBOL(g_stamps), sizeof(st_h)));
+      printf("    persistent step %d: sub-panels (sweep / update) %llu/%llu %llu/%llu %llu/%llu %llu/%llu"
+             "  inverse tail %llu/%llu/%llu\n", T / 2, st_h[10] - st_h[2], st_h[11] - st_h[10], st_h[12] - st_h[11],
+             st_h[13] - st_h[12], st_h[14] - st_h[13], st_h[15] - st_h[14], st_h[16] - st_h[15], st_h[17] - st_h[16],
+             st_h[40] - st_h[3], st_h[41] - st_h[40], st_h[4] - st_h[41]);
     }
+#endif
     CK(hipMemcpy(Lp.data(), dL, sizeof(double) * A.size(), hipMemcpyDeviceToHost));
     CK(hipMemcpy(yp.data(), dy, sizeof(double) * n, hipMemcpyDeviceToHost));
     std::vector<double> Sp(64);

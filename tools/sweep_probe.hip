@@ -5,7 +5,8 @@
 // (contention as in the product's first sub-panel).  Variants of the sweep's
 // schedule are compared against the product code; every variant must leave
 // the same L columns.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I bundleadjustment_amd/csrc tools/sweep_probe.hip -o tools/sweep_probe
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DBA_CHOL_STAMPS -I bundleadjustment_amd/csrc tools/sweep_probe.hip \
+//         -o tools/sweep_probe   (BA_CHOL_STAMPS: the sweep's own column-loop stamps)
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -100,9 +101,12 @@ __device__ __forceinline__ void panel_sweep_free(double (*T)[LDP], CholLds& W, i
   }
 }
 
+// V2: the product sweep with c0 / b / m as run-time values (as in
+// factor_invert_blk's sub-panel loop) instead of compile-time constants
 template <int V, bool BUSY>
 __global__ __launch_bounds__(256) void k_sweep(const double* __restrict__ A, double* __restrict__ out,
-                                               unsigned long long* __restrict__ cyc, int reps) {
+                                               unsigned long long* __restrict__ cyc, int reps, int rc0, int rb,
+                                               int rm) {
   __shared__ double T[CB][LDP];
   __shared__ double T0[CB][LDP];
   __shared__ double M[CB][LDP];
@@ -119,7 +123,8 @@ __global__ __launch_bounds__(256) void k_sweep(const double* __restrict__ A, dou
       unsigned long long t0, t1;
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
       if (V == 0) panel_sweep(T, W, 0, CB, CB);
-      else panel_sweep_free(T, W, 0, CB, CB);
+      else if (V == 1) panel_sweep_free(T, W, 0, CB, CB);
+      else panel_sweep(T, W, rc0, rb, rm);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
       tot += t1 - t0;
       mn = t1 - t0 < mn ? t1 - t0 : mn;
@@ -148,8 +153,8 @@ int main() {
   hipMalloc(&dA, 8 * 4096); hipMalloc(&dO, 8 * 4096); hipMalloc(&dC, 16);
   hipMemcpy(dA, A.data(), 8 * 4096, hipMemcpyHostToDevice);
   std::vector<double> ref(4096), o(4096);
-  auto run = [&](auto kern, const char* name, bool check) {
-    hipLaunchKernelGGL(kern, dim3(1), dim3(256), 0, 0, dA, dO, dC, 64);
+  auto run = [&](auto kern, const char* name, bool check, int rc0 = 0) {
+    hipLaunchKernelGGL(kern, dim3(1), dim3(256), 0, 0, dA, dO, dC, 64, rc0, 64, 64);
     hipDeviceSynchronize();
     unsigned long long c[2];
     hipMemcpy(c, dC, 16, hipMemcpyDeviceToHost);
@@ -157,13 +162,18 @@ int main() {
     if (!check) ref = o;
     size_t diff = 0;
     for (int i = 0; i < 64; ++i)
-      for (int j = 0; j < 16; ++j) diff += std::memcmp(&o[i * 64 + j], &ref[i * 64 + j], 8) != 0;
-    printf("%-34s avg %6llu  min %6llu cycles per 16-column sweep   L entries differing from V0: %zu\n", name, c[0],
-           c[1], diff);
+      for (int j = 0; j < 16; ++j) diff += check && std::memcmp(&o[i * 64 + j], &ref[i * 64 + j], 8) != 0;
+    unsigned long long st[64];
+    hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st));
+    printf("%-34s avg %6llu  min %6llu cycles per 16-column sweep (columns %llu)  L entries differing from V0: %zu\n",
+           name, c[0], c[1], st[31] - st[30], diff);
   };
   run(k_sweep<0, false>, "V0 product, other waves idle", false);
   run(k_sweep<0, true>, "V0 product, MFMA LDS stream", true);
   run(k_sweep<1, false>, "V1 no sched barriers, idle", true);
   run(k_sweep<1, true>, "V1 no sched barriers, MFMA stream", true);
+  run(k_sweep<2, false>, "V2 run-time c0/b/m, idle", true);
+  run(k_sweep<2, true>, "V2 run-time c0/b/m, MFMA stream", true);
+  run(k_sweep<2, false>, "V2 run-time c0=32, idle", false, 32);
   return 0;
 }
