@@ -70,6 +70,7 @@ struct DevWork {
   double* W;                         // [no][18]  (E L^-T per observation), fp64
   float* Wf;                         // [no][18]  the same in fp32 (BA_MIXED_FP32)
   bool w32;                          // W blocks stored in Wf
+  bool wcompact;                     // W as 128-B compact records (J-free fp64 DENSE_SCHUR; ba_kernels.hip)
   double* S;                         // [(n+1) x ld] reduced system, row n = rhs (working matrix)
   double* Lf;                        // [(n+1) x ld] Cholesky factor, row n = L^-1 rhs
   double* Spk;                       // [n(n+1)/2 + n] packed lower triangle + rhs of S (multi-rank exchange)
@@ -155,6 +156,7 @@ void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, 
 // partials always use grid = nblocks_of(...)
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s);
 int back_flow_capacity(int device);
+bool point_step_fused();                      // J-free back substitution fused with the candidate (BA_PSTEP)
 bool chol_persist_fits(int device, int n);   // every workgroup of k_chol_persist resident at once
 int chol_split_blocks();                     // block columns from which the split step form is used   // resident k_back_flow workgroups (-1: query failed)
 constexpr int kLinLdsCamsHost = 200;   // = kLinLdsCams (ba_kernels.hip): cameras the LDS camera table holds

@@ -463,7 +463,7 @@ __global__ __launch_bounds__(256) void k_cam_compact(DevProblem P, const double*
 //   r = q01 / q2 - uv,  dr/d* = (dq01 - r' dq2) / q2,  Huber corrector sqrt(rho')
 template <class Cam>
 __device__ inline double lin_obs(const DevProblem& P, const Cam& cr, bool cvar, bool pvar, double X0, double X1,
-                                 double X2, float2 uv, double (&out)[kJR], bool& fin) {
+                                 double X2, float2 uv, double (&out)[kJR], bool& fin, double* prf = nullptr) {
   const auto T = cam_row(cr);
   double q[3], iw = 1.0;
   if (cvar) {
@@ -484,6 +484,7 @@ __device__ inline double lin_obs(const DevProblem& P, const Cam& cr, bool cvar, 
   const double rho = huber(r0 * r0 + r1 * r1, P.huber_a, P.huber_b, &scale);
   const double f = iq * scale;
   fin = isfinite(r0) && isfinite(r1) && isfinite(f);
+  if (prf) { prf[0] = pr0; prf[1] = pr1; prf[2] = f; }   // (k_obs_w_rc's compact records)
   if (cvar) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -1504,6 +1505,44 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
   }
 }
 
+// compact W records (k_obs_w_rc<double, true>, described there): 16 doubles
+constexpr int kWcRec = 16;
+// the camera constants of the compact records: Jc's scaled translation
+// columns are f (A_row,k - pr_row B_k), A_row,k = s_{3+k} K_{3k+row},
+// B_k = s_{3+k} K_{3k+2}
+struct WcCam {
+  double a0[3], a1[3], b[3];
+  __device__ void load(const DevProblem& P, const double* __restrict__ scale_c, int v) {
+    const int c = P.cam_of_vc[v];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double st = scale_c[(size_t)v * 6 + 3 + k];
+      a0[k] = st * (double)P.K[9 * c + 3 * k];
+      a1[k] = st * (double)P.K[9 * c + 3 * k + 1];
+      b[k] = st * (double)P.K[9 * c + 3 * k + 2];
+    }
+  }
+};
+struct WcRaw { double r[kWcRec]; };
+__device__ inline WcRaw wc_fetch(const double* __restrict__ Wc, int o) {
+  WcRaw w;
+  const double2* s = reinterpret_cast<const double2*>(Wc + (size_t)o * kWcRec);
+#pragma unroll
+  for (int k = 0; k < kWcRec / 2; ++k) { const double2 t = s[k]; w.r[2 * k] = t.x; w.r[2 * k + 1] = t.y; }
+  return w;
+}
+// c = Jc s_c (rows c0, c1) of a compact record
+__device__ inline void wc_rows(const WcRaw& w, const WcCam& m, double (&c0)[6], double (&c1)[6]) {
+  const double pr0 = w.r[6], pr1 = w.r[7], f = w.r[8];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    c0[k] = w.r[k];
+    c1[k] = w.r[3 + k];
+    c0[3 + k] = f * (m.a0[k] - pr0 * m.b[k]);
+    c1[3 + k] = f * (m.a1[k] - pr1 * m.b[k]);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // diagonal Schur blocks and rhs (local part): one workgroup per camera
 //   S_cc = -sum W W^T (lower 21) ; b_c = -sum W u_p
@@ -1605,6 +1644,90 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
       double a0[18], b0[18];
       load_w(W, p0.x, a0); load_w(W, p0.y, b0);
       acc_pair(acc, a0, b0);
+    }
+#pragma unroll
+    for (int k = 0; k < 36; ++k) {
+      double v = acc[k];
+#pragma unroll
+      for (int x = PL / 2; x >= 1; x >>= 1) v += __shfl_xor(v, x, PL);
+      acc[k] = v;
+    }
+    if (live) {
+      const int I = blk.x, Jb = blk.y;
+#pragma unroll
+      for (int k = 0; k < 36; ++k) {
+        if ((k % PL) != sl) continue;
+        const int i = k / 6, j = k % 6;
+        if (I != Jb) S[(size_t)(6 * I + i) * ld + 6 * Jb + j] = -acc[k];
+        else if (j <= i) S[(size_t)(6 * I + i) * ld + 6 * I + j] -= acc[k];  // duplicate obs of one point by one camera
+      }
+    }
+  }
+}
+
+// k_schur_pairs on compact records (the same blocks, lanes and reduction):
+//   W_a W_b^T = c_a^T M c_b,  M = Z_a Z_b^T (2 x 2)
+// the partner record is one 128-B line (W: two) and is fetched one pair
+// ahead; the row camera's record is an L2 hit.
+__global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4* __restrict__ blocks, int nblocks,
+                                                       const int2* __restrict__ pairs, const double* __restrict__ Wc,
+                                                       const double* __restrict__ scale_c, double* __restrict__ S) {
+  // the camera constants of every variable camera in LDS (nvc <= 200 in the
+  // J-free mode: 14.4 KB), read per pair (registers: 1 -> 2 waves per SIMD)
+  __shared__ WcCam ctab[kLinLdsCams];
+  for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
+  __syncthreads();
+  constexpr int PL = kPairLanes, BPW = 64 / PL;
+  const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
+  const int xcd = blockIdx.x & 7, wx = blockIdx.x >> 3, nwx = gridDim.x >> 3;
+  const int R = (nblocks + 7) / 8;
+  const int r0 = xcd * R, r1 = min(nblocks, r0 + R);
+  const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  const size_t ld = (size_t)P.ld;
+  for (int base = r0 + (wx * nwv + wv) * BPW; base < r1; base += nwx * nwv * BPW) {
+    const int bi = base + sub;
+    const bool live = bi < r1;
+    const int4 blk = live ? blocks[bi] : make_int4(0, 0, 0, 0);
+    const WcCam& mI = ctab[blk.x];
+    const WcCam& mJ = ctab[blk.y];
+    double acc[36];
+#pragma unroll
+    for (int k = 0; k < 36; ++k) acc[k] = 0.0;
+    int e = blk.z + sl;
+    WcRaw nb;                 // the partner (cold) record one pair ahead
+    int2 pr = make_int2(0, 0);
+    if (e < blk.w) {
+      pr = pairs[e];
+      nb = wc_fetch(Wc, pr.y);
+    }
+    for (; e < blk.w; e += PL) {
+      const WcRaw wa = wc_fetch(Wc, pr.x);   // row camera I: re-read from L2 by its blocks
+      const WcRaw wb = nb;
+      if (e + PL < blk.w) {
+        pr = pairs[e + PL];
+        nb = wc_fetch(Wc, pr.y);
+      }
+      double ca0[6], ca1[6], cb0[6], cb1[6];
+      wc_rows(wa, mI, ca0, ca1);
+      wc_rows(wb, mJ, cb0, cb1);
+      const double* za0 = wa.r + 9;
+      const double* za1 = wa.r + 12;
+      const double* zb0 = wb.r + 9;
+      const double* zb1 = wb.r + 12;
+      const double m00 = za0[0] * zb0[0] + za0[1] * zb0[1] + za0[2] * zb0[2];
+      const double m01 = za0[0] * zb1[0] + za0[1] * zb1[1] + za0[2] * zb1[2];
+      const double m10 = za1[0] * zb0[0] + za1[1] * zb0[1] + za1[2] * zb0[2];
+      const double m11 = za1[0] * zb1[0] + za1[1] * zb1[1] + za1[2] * zb1[2];
+      double n0[6], n1[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        n0[j] = m00 * cb0[j] + m01 * cb1[j];
+        n1[j] = m10 * cb0[j] + m11 * cb1[j];
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) acc[i * 6 + j] += ca0[i] * n0[j] + ca1[i] * n1[j];
     }
 #pragma unroll
     for (int k = 0; k < 36; ++k) {
@@ -2002,9 +2125,18 @@ __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const doub
 }
 
 // W_o from recomputed J (k_obs_w<true, WT> with the JR chunk replaced by
-// lin_obs; the records leave through the same wave-private LDS staging)
+// lin_obs; the records leave through the same wave-private LDS staging).
+//
+// COMPACT (J-free fp64 DENSE_SCHUR): W_o = c^T Z is rank 2 (c = Jc s_c, 2 x 6;
+// Z = Jp s_p L_p^-T, 2 x 3) and the translation columns of Jc are
+// (K_k - pr K_k2) f (lin_obs): the record keeps the scaled rotation columns
+// of c, pr0, pr1, f and Z — 15 doubles in one 128-B line instead of W's
+// 144 B, which straddle two.  The camera-side consumers (k_cam_schur_diag_c,
+// k_schur_pairs_c) gather one line per observation and form their products
+// through the 2 x 2 inner matrices Z Z'^T (WcCam: the camera's K and
+// translation scalings).
 constexpr int kObsWRcWaves = 6;   // table + K + scales + 6 staging slots fit the 160 KB LDS
-template <typename WT>
+template <typename WT, bool COMPACT = false>
 __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, const double* __restrict__ rec,
                                                                 const double* __restrict__ pts,
                                                                 const double* __restrict__ scale_c,
@@ -2048,37 +2180,53 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
     const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
     double j[kJR];
     bool fin;
-    (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
+    double prf[3];
+    (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin, prf);
     double sc[6];
 #pragma unroll
     for (int a = 0; a < 6; ++a) sc[a] = sct[c * 6 + a];
     const double jp0[3] = {j[12] * s0, j[13] * s1, j[14] * s2};
     const double jp1[3] = {j[15] * s0, j[16] * s1, j[17] * s2};
-    double wv[18];
+    constexpr int REC = COMPACT ? kWcRec : kWRec;
+    double wv[REC];
+    if constexpr (COMPACT) {
+      const double z[6] = {jp0[0] * i00, jp0[0] * i10 + jp0[1] * i11, jp0[0] * i20 + jp0[1] * i21 + jp0[2] * i22,
+                           jp1[0] * i00, jp1[0] * i10 + jp1[1] * i11, jp1[0] * i20 + jp1[1] * i21 + jp1[2] * i22};
 #pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      const double c0 = j[a] * sc[a], c1 = j[6 + a] * sc[a];
-      const double e0 = c0 * jp0[0] + c1 * jp1[0];
-      const double e1 = c0 * jp0[1] + c1 * jp1[1];
-      const double e2 = c0 * jp0[2] + c1 * jp1[2];
-      wv[a * 3 + 0] = live ? e0 * i00 : 0.0;
-      wv[a * 3 + 1] = live ? e0 * i10 + e1 * i11 : 0.0;
-      wv[a * 3 + 2] = live ? e0 * i20 + e1 * i21 + e2 * i22 : 0.0;
+      for (int a = 0; a < 3; ++a) {
+        wv[a] = live ? j[a] * sc[a] : 0.0;
+        wv[3 + a] = live ? j[6 + a] * sc[a] : 0.0;
+        wv[6 + a] = live ? prf[a] : 0.0;   // pr0, pr1, f
+      }
+#pragma unroll
+      for (int k = 0; k < 6; ++k) wv[9 + k] = live ? z[k] : 0.0;
+      wv[15] = 0.0;
+    } else {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const double c0 = j[a] * sc[a], c1 = j[6 + a] * sc[a];
+        const double e0 = c0 * jp0[0] + c1 * jp1[0];
+        const double e1 = c0 * jp0[1] + c1 * jp1[1];
+        const double e2 = c0 * jp0[2] + c1 * jp1[2];
+        wv[a * 3 + 0] = live ? e0 * i00 : 0.0;
+        wv[a * 3 + 1] = live ? e0 * i10 + e1 * i11 : 0.0;
+        wv[a * 3 + 2] = live ? e0 * i20 + e1 * i21 + e2 * i22 : 0.0;
+      }
     }
 #pragma unroll
-    for (int k = 0; k < kWRec; ++k) st[lane * kStageLd + k] = wv[k];
+    for (int k = 0; k < REC; ++k) st[lane * kStageLd + k] = wv[k];
     wave_lds_sync();
-    constexpr int NIT = kWRec / 2;
+    constexpr int NIT = REC / 2;
     V2 ov[NIT];
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int e = it * 64 + lane;
-      const int r = e / (kWRec / 2), f = 2 * (e - r * (kWRec / 2));
+      const int r = e / (REC / 2), f = 2 * (e - r * (REC / 2));
       ov[it].x = (WT)st[r * kStageLd + f];
       ov[it].y = (WT)st[r * kStageLd + f + 1];
     }
     wave_lds_sync();
-    V2* dst = reinterpret_cast<V2*>(W + (size_t)base * kWRec);
+    V2* dst = reinterpret_cast<V2*>(W + (size_t)base * REC);
     const int nrec = min(64, P.no - base);
     if (nrec == 64) {
 #pragma unroll
@@ -2087,11 +2235,76 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
         const int e = it * 64 + lane;
-        if (e / (kWRec / 2) < nrec) dst[e] = ov[it];
+        if (e / (REC / 2) < nrec) dst[e] = ov[it];
       }
     }
     c = cn; p = pn; uv = uvn;
   }
+}
+
+// k_cam_schur_diag on compact records:
+//   W W^T = c^T (Z Z^T) c,  W u = c^T (Z u)
+__global__ __launch_bounds__(256) void k_cam_schur_diag_c(DevProblem P, const double* __restrict__ Wc,
+                                                          const double* __restrict__ scale_c,
+                                                          const double* __restrict__ u, double* __restrict__ cpart) {
+  __shared__ double lds[27 * 16];
+  const int v = blockIdx.x;
+  WcCam m;
+  m.load(P, scale_c, v);
+  double acc[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+  int i0, i1;
+  cam_slice(P, v, i0, i1);
+  // the next observation's record and u one step ahead (clamped: the slice's
+  // last entry; an empty slice loads nothing)
+  int i = i0 + threadIdx.x;
+  WcRaw nw;
+  double2 nu01 = make_double2(0.0, 0.0);
+  double nu2 = 0.0;
+  if (i < i1) {
+    const int2 op = P.cam_op[i];
+    nw = wc_fetch(Wc, op.x);
+    nu01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
+    nu2 = u[4 * (size_t)op.y + 2];
+  }
+  for (; i < i1; i += blockDim.x) {
+    const WcRaw w = nw;
+    const double2 u01 = nu01;
+    const double u2 = nu2;
+    if (i + (int)blockDim.x < i1) {
+      const int2 op = P.cam_op[i + blockDim.x];
+      nw = wc_fetch(Wc, op.x);
+      nu01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
+      nu2 = u[4 * (size_t)op.y + 2];
+    }
+    double c0[6], c1[6];
+    wc_rows(w, m, c0, c1);
+    const double* z0 = w.r + 9;
+    const double* z1 = w.r + 12;
+    const double m00 = z0[0] * z0[0] + z0[1] * z0[1] + z0[2] * z0[2];
+    const double m01 = z0[0] * z1[0] + z0[1] * z1[1] + z0[2] * z1[2];
+    const double m11 = z1[0] * z1[0] + z1[1] * z1[1] + z1[2] * z1[2];
+    const double zu0 = z0[0] * u01.x + z0[1] * u01.y + z0[2] * u2;
+    const double zu1 = z1[0] * u01.x + z1[1] * u01.y + z1[2] * u2;
+    double n0[6], n1[6];
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      n0[b] = m00 * c0[b] + m01 * c1[b];
+      n1[b] = m01 * c0[b] + m11 * c1[b];
+    }
+    int t = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+#pragma unroll
+      for (int b = 0; b <= a; ++b) acc[t++] += c0[a] * n0[b] + c1[a] * n1[b];
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] += c0[a] * zu0 + c1[a] * zu1;
+  }
+  double tot[27];
+  block_sum<27>(acc, lds, tot);
+  cam_slice_store(tot, cpart, v, P.nvc);
 }
 
 // model cost change + candidate cost with J recomputed at x (the lin table of
@@ -2490,6 +2703,9 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
     if (W.w32)
       hipLaunchKernelGGL(k_obs_w_rc<float>, dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, (const double*)W.rec,
                          (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.Wf);
+    else if (W.wcompact)
+      hipLaunchKernelGGL((k_obs_w_rc<double, true>), dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, (const double*)W.rec,
+                         (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.W);
     else
       hipLaunchKernelGGL(k_obs_w_rc<double>, dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, (const double*)W.rec,
                          (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.W);
@@ -2515,6 +2731,8 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
   const int sl = dsplit > 0 ? std::min(dsplit, kCamSplit) : W.cam_split;
   if (W.w32)
     hipLaunchKernelGGL(k_cam_schur_diag<float>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wf, W.u, W.S, W.cpart);
+  else if (W.wcompact)
+    hipLaunchKernelGGL(k_cam_schur_diag_c, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.W, W.scale_c, W.u, W.cpart);
   else
     hipLaunchKernelGGL(k_cam_schur_diag<double>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.W, W.u, W.S, W.cpart);
   if (!compact && radius > 0.0) {   // single rank: the LM diagonal goes in with the fold
@@ -2538,7 +2756,11 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   int grid = (waves + 3) / 4;
   if (grid > grid_cap) grid = grid_cap;
   grid = (grid + 7) / 8 * 8;   // k_schur_pairs' XCD ranges need a multiple of 8
-  hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
+  if (W.wcompact)
+    hipLaunchKernelGGL(k_schur_pairs_c, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.scale_c,
+                       W.S);
+  else
+    hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
 }
 // one workgroup per row of S: row i < n holds its lower part (j <= i), row n
 // the rhs (all n entries)
@@ -2585,12 +2807,18 @@ void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) 
   hipLaunchKernelGGL(k_cam_candidate, dim3(P.nc < kMaxBlocks ? P.nc : kMaxBlocks), dim3(64), 0, s, P, W.cams, W.y,
                      W.scale_c, W.cams_c, W.delta_c, W.rec_c, W.part);
 }
+// back substitution + candidate in one point-major pass (diagnostics:
+// BA_PSTEP=0 runs k_backsub + k_candidate_rc instead), read once per process
+bool point_step_fused() {
+  static int fused = -1;
+  if (fused < 0) { const char* e = getenv("BA_PSTEP"); fused = e ? atoi(e) : 1; }
+  return fused != 0;
+}
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (W.jrfree) {
-    // back substitution + candidate in one point-major pass (diagnostics:
-    // BA_PSTEP=0 runs k_backsub + k_candidate_rc instead; BA_PSTEP_LAZY=1)
-    static int fused = -1, lazy = -1;
-    if (fused < 0) { const char* e = getenv("BA_PSTEP"); fused = e ? atoi(e) : 1; }
+    // (BA_PSTEP_LAZY=1: lazy camera-table reads, diagnostics)
+    static int lazy = -1;
+    const bool fused = point_step_fused();
     if (lazy < 0) { const char* e = getenv("BA_PSTEP_LAZY"); lazy = e ? atoi(e) : 0; }
     // (fp32 W storage keeps the W-based back substitution: the step then
     // solves with the stored fp32 blocks, as the oracle's fp32-W mode does)

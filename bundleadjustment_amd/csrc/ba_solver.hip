@@ -685,6 +685,15 @@ int step_enqueue(ba_ctx* ctx, double radius, const ba_options& o) {
   W.w32 = o.precision == BA_MIXED_FP32;
   if (W.w32 && !W.Wf) W.Wf = ctx->dalloc<float>(18 * (size_t)ctx->no);
   if (!W.w32 && !W.W) W.W = ctx->dalloc<double>(18 * (size_t)ctx->no);
+  {
+    // compact W records (ba_kernels.hip k_obs_w_rc<double, true>): the
+    // J-free fp64 DENSE_SCHUR iteration with the fused point step (the only
+    // W readers are then k_cam_schur_diag_c and k_schur_pairs_c);
+    // BA_WCOMPACT=0 (diagnostics, read per solve) keeps the 18-double blocks
+    const char* e = getenv("BA_WCOMPACT");
+    W.wcompact = W.jrfree && !W.w32 && o.linear_solver == BA_DENSE_SCHUR && !(e && e[0] == '0') &&
+                 point_step_fused();
+  }
   // (SL_CHOL_BAD is cleared by k_cam_add_diag / k_pcg_setup_fin, the first
   // kernels that may set it, so no separate memset per step)
   int ls_iters = 1;

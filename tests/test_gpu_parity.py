@@ -300,3 +300,30 @@ def test_persistent_cholesky_is_bitwise_the_per_step_form(monkeypatch, cfg, scal
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
     assert [r["cost"] for r in a[3]] == [r["cost"] for r in b[3]]
     assert [r["step_is_successful"] for r in a[3]] == [r["step_is_successful"] for r in b[3]]
+
+
+# ---------------------------------------------------------------------------
+# compact W records (k_obs_w_rc<double, true>: one 128-B line per
+# observation; S through the 2 x 2 inner products Z_a Z_b^T) against the
+# 18-double blocks: the same system up to rounding (the products associate
+# differently), so the same LM trajectory to ~1e-9
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("cfg,scale,fix", [("c3", 0.05, 1), ("c2", 1.0, 0)])
+def test_compact_w_records_match_full_blocks(monkeypatch, cfg, scale, fix):
+    p = make_config(cfg, scale=scale)
+    if fix:
+        bp.fix_camera(p, 1)
+    runs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("BA_WCOMPACT", mode)
+        with Solver(0) as s:
+            runs[mode] = run_gpu(s, p, Options(max_num_iterations=6))
+    a, b = runs["0"], runs["1"]
+    assert [r["step_is_successful"] for r in a[3]] == [r["step_is_successful"] for r in b[3]]
+    np.testing.assert_allclose([r["cost"] for r in b[3]], [r["cost"] for r in a[3]], rtol=1e-10)
+    np.testing.assert_allclose(b[0], a[0], rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(b[1], a[1], rtol=1e-8, atol=1e-10)
+    # and the compact path is reproducible bit for bit
+    with Solver(0) as s:
+        c = run_gpu(s, p, Options(max_num_iterations=6))
+    assert np.array_equal(b[0], c[0]) and np.array_equal(b[1], c[1])
