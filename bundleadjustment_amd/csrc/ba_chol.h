@@ -326,11 +326,11 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // reciprocal per pair on the chain.  Column j+1 is then brought to its 1 x 1
 // form (a_r,j+1 -= a_rj e / d_j) off the chain, so the final scaling and
 // the pivots on the diagonal are those of the column-by-column sweep.
-// Per pair the chain is: LDS read of B -> det, reciprocal -> f -> update of
-// the NEXT pair's two columns -> LDS publish -> the next reads (the compiler
-// interleaves the remaining updates; wave_barrier only keeps the publish
-// ahead of the reads).  Measured per 16 columns (tools/sweep_probe.hip):
-// ~3.4k cycles with compile-time c0 / b / m, 4% below sched_barrier fencing.
+// Per pair the chain is: B by readlane from its two lanes -> det, reciprocal
+// -> f -> update of the NEXT pair's two columns; the other columns' entries
+// of the pivot columns travel through LDS one pair ahead (wave_barrier keeps
+// the publish ahead of the reads), off the chain.  Measured per 16 columns
+// (tools/sweep_probe.hip): ~3.4k cycles with B through LDS too.
 __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0, int b, int m) {
   // the row index is made opaque here, so that the sweep's row masks are
   // formed per sweep instead of being hoisted out of the caller's loops
@@ -354,40 +354,55 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
   CHOL_STAMP(30 + c0 / 16 * 4);
   W.colp[0][r] = make_double2(a[0], a[1]);
   __builtin_amdgcn_wave_barrier();
-  double2 q0 = W.colp[0][c0], q1 = W.colp[0][c0 + 1];
   double2 ct[16];
 #pragma unroll
   for (int t = 2; t < 16; ++t) ct[t] = W.colp[0][c0 + t];
+  // the pivot block of the first pair from its two rows' lanes (readlane: no
+  // LDS round trip on the chain; the same bits an LDS broadcast carries)
+  double d0 = readlane_f64(a[0], c0), e = readlane_f64(a[0], c0 + 1), d1 = readlane_f64(a[1], c0 + 1);
+  double rdet = recip(d0 * d1 - e * e), rd0 = recip(d0);
 #pragma unroll
   for (int jj = 0; jj < 16; jj += 2) {
     const int j = c0 + jj;
     if (j + 1 >= b) break;                   // uniform: a last single column needs no update
     const int buf = (jj >> 1) & 1;
-    const double d0 = q0.x, e = q1.x, d1 = q1.y;
-    const double rdet = recip(d0 * d1 - e * e);
-    const double rd0 = recip(d0);
-    const bool row = r > j + 1 && r < m;
+    // (no row mask: rows r <= j + 1 and r >= m update only entries that are
+    // never read again — strictly-upper ones, or rows outside the tile — and
+    // the final store masks them; every row > j + 1 of the tile computes
+    // exactly what the masked form computed)
     const double u0 = a[jj], u1 = a[jj + 1];
-    const double f0 = row ? fma(u0, d1, -u1 * e) * rdet : 0.0;
-    const double f1 = row ? fma(u1, d0, -u0 * e) * rdet : 0.0;
+    const double f0 = fma(u0, d1, -u1 * e) * rdet;
+    const double f1 = fma(u1, d0, -u0 * e) * rdet;
+    const double ej = e, rd0j = rd0;
     if (jj + 2 < 16) {
+      // the chain: the next pair's two columns, then its pivot block
       a[jj + 2] = fma(-f1, ct[jj + 2].y, fma(-f0, ct[jj + 2].x, a[jj + 2]));
       a[jj + 3] = fma(-f1, ct[jj + 3].y, fma(-f0, ct[jj + 3].x, a[jj + 3]));
-      W.colp[buf ^ 1][r] = make_double2(a[jj + 2], a[jj + 3]);
-      __builtin_amdgcn_wave_barrier();
-      const double2 q0n = W.colp[buf ^ 1][c0 + jj + 2], q1n = W.colp[buf ^ 1][c0 + jj + 3];
+      if (j + 3 < b) {
+        d0 = readlane_f64(a[jj + 2], j + 2);
+        e = readlane_f64(a[jj + 2], j + 3);
+        d1 = readlane_f64(a[jj + 3], j + 3);
+        rdet = recip(d0 * d1 - e * e);
+        rd0 = recip(d0);
+      }
+      // off the chain (their latency hides under it): the later columns'
+      // pivot-column entries through LDS one pair ahead (wave_barrier keeps
+      // the publish ahead of the reads) and their updates
       double2 ctn[16];
+      if (jj + 4 < 16) {
+        W.colp[buf ^ 1][r] = make_double2(a[jj + 2], a[jj + 3]);
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int t = jj + 4; t < 16; ++t) ctn[t] = W.colp[buf ^ 1][c0 + t];
+        for (int t = jj + 4; t < 16; ++t) ctn[t] = W.colp[buf ^ 1][c0 + t];
+      }
 #pragma unroll
       for (int t = jj + 4; t < 16; ++t) a[t] = fma(-f1, ct[t].y, fma(-f0, ct[t].x, a[t]));
-      q0 = q0n;
-      q1 = q1n;
 #pragma unroll
       for (int t = jj + 4; t < 16; ++t) ct[t] = ctn[t];
     }
-    // column j+1 to its 1 x 1 form (rows r > j; lane j+1 gets the pivot d1 - e^2/d0)
-    if (r > j && r < m) a[jj + 1] -= u0 * (e * rd0);
+    // column j+1 to its 1 x 1 form (rows r > j; lane j+1 gets the pivot
+    // d1 - e^2/d0; unmasked like the updates above)
+    a[jj + 1] -= u0 * (ej * rd0j);
   }
   CHOL_STAMP(31 + c0 / 16 * 4);
   // own pivot (lanes c0..c0+15): d_r = a_rr
