@@ -2397,9 +2397,10 @@ __global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double*
 //           w = u_p + L_p^-1 (s_p o v) = u_p - sum_o W_o^T y_c  (W_o = s_c Jc^T
 //           Jp s_p L_p^-T and s_c o y_c = -dc: the same step without reading
 //           the 144-B W records), y_p = L_p^-T w, d_p = -s_p o y_p, x'_p.
-//   pass 2  J again: J d . (r + J d / 2) and the candidate residual at
-//           (camera', x'_p) per observation.
-template <int NT, int LANES, bool LAZY>
+//   pass 2  J d . (r + J d / 2) (Jc dc, Jp and r kept from pass 1 for the
+//           lane's first KC observations, J again past them) and the
+//           candidate residual at (camera', x'_p) per observation.
+template <int NT, int LANES, bool LAZY, int KC = 3>
 __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double* __restrict__ rec,
                                                       const double* __restrict__ pts,
                                                       const double* __restrict__ delta_c,
@@ -2444,6 +2445,11 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
       const double Y0 = pts[3 * pn], Y1 = pts[3 * pn + 1], Y2 = pts[3 * pn + 2];
       const bool pvn = P.pt_var[pn] != 0;
       double dX[3] = {0.0, 0.0, 0.0};
+      // the first KC observations of the lane keep what pass 2 needs from
+      // pass 1's J (Jc dc, Jp, r: 10 doubles), so pass 2 recomputes J only
+      // past them (points with more than LANES * KC observations) and for
+      // fixed points (no pass 1)
+      double kc[KC][10];
       if (pv) {
         // pass 1: v = sum Jp^T (Jc dc)
         double v0 = 0.0, v1 = 0.0, v2 = 0.0;
@@ -2451,7 +2457,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
         int oc = min(o, lasto);
         int c = P.obs_cam[oc];
         float2 uv = P.uv[oc];
-        for (; o < o1; o += LANES) {
+        auto obs1 = [&](double (&keep)[10], bool store) {
           const int on = min(o + LANES, lasto);
           const int cn = P.obs_cam[on];
           const float2 uvn = P.uv[on];
@@ -2464,9 +2470,19 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
           v0 += j[12] * t0 + j[15] * t1;
           v1 += j[13] * t0 + j[16] * t1;
           v2 += j[14] * t0 + j[17] * t1;
+          if (store) {
+            keep[0] = t0; keep[1] = t1;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) keep[2 + k] = j[12 + k];
+          }
           c = cn;
           uv = uvn;
-        }
+          o += LANES;
+        };
+#pragma unroll
+        for (int k = 0; k < KC; ++k)
+          if (o < o1) obs1(kc[k], true);
+        while (o < o1) obs1(kc[0], false);
 #pragma unroll
         for (int x = LANES / 2; x >= 1; x >>= 1) {
           v0 += __shfl_xor(v0, x, LANES);
@@ -2505,21 +2521,33 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
         int oc = min(o, lasto);
         int c = P.obs_cam[oc];
         float2 uv = P.uv[oc];
-        for (; o < o1; o += LANES) {
+        // keep: pass 1's values of this observation (nullptr: J again)
+        auto obs2 = [&](const double* keep) {
           const int on = min(o + LANES, lasto);
           const int cn = P.obs_cam[on];
           const float2 uvn = P.uv[on];
-          double j[kJR];
-          lin(c, pv, X0, X1, X2, uv, j);
           const bool cfix = P.cam_fixed && P.cam_fixed[c];
           const double* cr = ctb + c * kCandRec;
           // k_candidate_lds' arithmetic
-          double jd0 = 0.0, jd1 = 0.0;
+          double jd0, jd1, jp[6], r0, r1;
+          if (keep) {
+            jd0 = keep[0]; jd1 = keep[1];
 #pragma unroll
-          for (int a2 = 0; a2 < 6; ++a2) { jd0 += j[a2] * cr[16 + a2]; jd1 += j[6 + a2] * cr[16 + a2]; }
-          jd0 += j[12] * dX[0] + j[13] * dX[1] + j[14] * dX[2];
-          jd1 += j[15] * dX[0] + j[16] * dX[1] + j[17] * dX[2];
-          const double mneg = jd0 * (j[18] + jd0 / 2.0) + jd1 * (j[19] + jd1 / 2.0);
+            for (int k = 0; k < 6; ++k) jp[k] = keep[2 + k];
+            r0 = keep[8]; r1 = keep[9];
+          } else {
+            double j[kJR];
+            lin(c, pv, X0, X1, X2, uv, j);
+            jd0 = 0.0; jd1 = 0.0;
+#pragma unroll
+            for (int a2 = 0; a2 < 6; ++a2) { jd0 += j[a2] * cr[16 + a2]; jd1 += j[6 + a2] * cr[16 + a2]; }
+#pragma unroll
+            for (int k = 0; k < 6; ++k) jp[k] = j[12 + k];
+            r0 = j[18]; r1 = j[19];
+          }
+          jd0 += jp[0] * dX[0] + jp[1] * dX[1] + jp[2] * dX[2];
+          jd1 += jp[3] * dX[0] + jp[4] * dX[1] + jp[5] * dX[2];
+          const double mneg = jd0 * (r0 + jd0 / 2.0) + jd1 * (r1 + jd1 / 2.0);
           double pcand[3];
           if (!cfix) {
 #pragma unroll
@@ -2543,7 +2571,14 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
           if (!isfinite(rc0) || !isfinite(rc1)) acc[4] += 1.0;
           c = cn;
           uv = uvn;
+          o += LANES;
+        };
+        if (pv) {
+#pragma unroll
+          for (int k = 0; k < KC; ++k)
+            if (o < o1) obs2(kc[k]);
         }
+        while (o < o1) obs2(nullptr);
       }
       o0 = o0n; o1 = o1n;
       X0 = Y0; X1 = Y1; X2 = Y2;
