@@ -25,6 +25,17 @@ constexpr int LDP = CB + 2;      // padded LDS row (doubles): conflict-free MFMA
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// threadIdx.x through an opaque copy: the index arithmetic derived from it is
+// formed where it is used instead of being hoisted, as loop invariants, out
+// of the persistent kernel's block-column loop (where ~120 such values stayed
+// live, in AGPRs, for the whole kernel); the wave index stays uniform
+__device__ __forceinline__ int ctid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+__device__ __forceinline__ int cwave() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 // Diagnostic build only (tools/chol_bench.hip defines BA_CHOL_STAMPS): the
 // critical workgroup records s_memtime at phase boundaries into g_stamps.
 #ifdef BA_CHOL_STAMPS
@@ -55,7 +66,7 @@ struct TileRegs { double2 v[8]; };
 template <bool LOWER = false>
 __device__ inline TileRegs tile_fetch(const double* __restrict__ M, size_t ld, int r0, int c0, int rmax, int cmax) {
   TileRegs t;
-  const int tid = threadIdx.x;
+  const int tid = ctid();
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
     const int e = tid + 256 * it;          // 2048 double2
@@ -71,7 +82,7 @@ __device__ inline TileRegs tile_fetch(const double* __restrict__ M, size_t ld, i
   return t;
 }
 __device__ inline void tile_put(double (*D)[LDP], const TileRegs& t) {
-  const int tid = threadIdx.x;
+  const int tid = ctid();
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
     const int e = tid + 256 * it;
@@ -87,7 +98,7 @@ __device__ inline void stage64(double (*D)[LDP], const double* __restrict__ M, s
 
 // C (64x64, distributed as 4 waves x 2x2 MFMA tiles of 16x16) = sum_k Xs[i][k] Ys[j][k]
 __device__ inline void mfma_xyT_64(const double (*Xs)[LDP], const double (*Ys)[LDP], d4 acc[2][2]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = ctid() & 63, w = cwave();
   const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
   const int li = lane & 15, lk = lane >> 4;
 #pragma unroll
@@ -115,7 +126,7 @@ __device__ inline int lower_tiles_of(int w, int (*tl)[2]) {
   return cnt;
 }
 __device__ inline void mfma_xxT_lower_sub(const double (*Xs)[LDP], double (*D)[LDP]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = ctid() & 63, w = cwave();
   const int li = lane & 15, lk = lane >> 4;
   int tl[3][2];
   const int cnt = lower_tiles_of(w, tl);
@@ -146,7 +157,7 @@ __device__ inline void mfma_xxT_lower_sub(const double (*Xs)[LDP], double (*D)[L
 // Each tile accumulates over k in the order of mfma_xxT_lower_sub (bitwise
 // the same C).
 __device__ inline void mfma_xxT_tile(const double (*Xs)[LDP], double (*D)[LDP], int ti, int tj) {
-  const int lane = threadIdx.x & 63;
+  const int lane = ctid() & 63;
   const int li = lane & 15, lk = lane >> 4;
   d4 acc = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
@@ -159,11 +170,11 @@ __device__ inline void mfma_xxT_tile(const double (*Xs)[LDP], double (*D)[LDP], 
   for (int g = 0; g < 4; ++g) D[16 * ti + lk + 4 * g][16 * tj + li] -= acc[g];
 }
 __device__ inline void mfma_xxT_col0(const double (*Xs)[LDP], double (*D)[LDP]) {
-  mfma_xxT_tile(Xs, D, threadIdx.x >> 6, 0);
+  mfma_xxT_tile(Xs, D, cwave(), 0);
 }
 __device__ inline void mfma_xxT_rest(const double (*Xs)[LDP], double (*D)[LDP]) {
   constexpr int T[6][2] = {{1, 1}, {2, 1}, {2, 2}, {3, 1}, {3, 2}, {3, 3}};
-  const int w = threadIdx.x >> 6;
+  const int w = cwave();
   if (w == 0) return;
 #pragma unroll
   for (int h = 0; h < 2; ++h) mfma_xxT_tile(Xs, D, T[2 * (w - 1) + h][0], T[2 * (w - 1) + h][1]);
@@ -174,7 +185,7 @@ __device__ inline void mfma_xxT_rest(const double (*Xs)[LDP], double (*D)[LDP]) 
 // 16 (bc + 1) -> 40 MFMAs per wave (the square product: 64).
 // acc[bc] element g: row 16w + (lane >> 4) + 4g, col 16bc + (lane & 15).
 __device__ inline void mfma_xVT_strip(const double (*Xs)[LDP], const double (*Vs)[LDP], d4 acc[4]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = ctid() & 63, w = cwave();
   const int li = lane & 15, lk = lane >> 4;
 #pragma unroll
   for (int bc = 0; bc < 4; ++bc) acc[bc] = d4{0.0, 0.0, 0.0, 0.0};
@@ -190,7 +201,7 @@ __device__ inline void mfma_xVT_strip(const double (*Xs)[LDP], const double (*Vs
 // accumulator element (a, b, reg) -> tile-local (row, col); v_mfma_f64_16x16x4
 // D layout: col = lane & 15, row = (lane >> 4) + 4 * reg
 __device__ inline void acc_pos(int a, int b, int reg, int* row, int* col) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = ctid() & 63, w = cwave();
   *row = (w >> 1) * 32 + 16 * a + (lane >> 4) + 4 * reg;
   *col = (w & 1) * 32 + 16 * b + (lane & 15);
 }
@@ -213,7 +224,7 @@ __device__ inline void acc_to_lds(double (*D)[LDP], const d4 acc[2][2], int op) 
 // Store rows [0, m) x cols [0, w) of an LDS tile to global (coalesced).
 __device__ inline void lds_to_global(const double (*Sx)[LDP], double* __restrict__ G, size_t ld, int r0, int c0,
                                      int m, int w) {
-  for (int e = threadIdx.x; e < CB * CB; e += 256) {
+  for (int e = ctid(); e < CB * CB; e += 256) {
     const int i = e / CB, j = e % CB;
     if (i < m && j < w) G[(size_t)(r0 + i) * ld + c0 + j] = Sx[i][j];
   }
@@ -267,7 +278,7 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 template <int K>
 __device__ __forceinline__ d4 mfma_tile(d4 acc, const double (*Xs)[LDP], int xr, int xc, const double (*Ys)[LDP],
                                         int yr, int yc, double sgn) {
-  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const int lane = ctid() & 63, li = lane & 15, lk = lane >> 4;
 #pragma unroll
   for (int k0 = 0; k0 < K; k0 += 4) {
     const double x = sgn * Xs[xr + li][xc + k0 + lk];
@@ -281,7 +292,7 @@ __device__ __forceinline__ d4 mfma_tile(d4 acc, const double (*Xs)[LDP], int xr,
 template <int K, int YLD = LDP>
 __device__ __forceinline__ d4 mfma_tile_n(d4 acc, const double (*Xs)[LDP], int xr, int xc, const double (*Ys)[YLD],
                                           int yr, int yc, double sgn) {
-  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+  const int lane = ctid() & 63, li = lane & 15, lk = lane >> 4;
 #pragma unroll
   for (int k0 = 0; k0 < K; k0 += 4) {
     const double x = sgn * Xs[xr + li][xc + k0 + lk];
@@ -292,7 +303,7 @@ __device__ __forceinline__ d4 mfma_tile_n(d4 acc, const double (*Xs)[LDP], int x
 }
 
 __device__ __forceinline__ d4 tile_load(const double (*S)[LDP], int r0, int c0) {
-  const int lane = threadIdx.x & 63;
+  const int lane = ctid() & 63;
   d4 v;
 #pragma unroll
   for (int g = 0; g < 4; ++g) v[g] = S[r0 + (lane >> 4) + 4 * g][c0 + (lane & 15)];
@@ -301,7 +312,7 @@ __device__ __forceinline__ d4 tile_load(const double (*S)[LDP], int r0, int c0) 
 
 template <int SLD = LDP>
 __device__ __forceinline__ void tile_store(double (*S)[SLD], int r0, int c0, d4 v) {
-  const int lane = threadIdx.x & 63;
+  const int lane = ctid() & 63;
 #pragma unroll
   for (int g = 0; g < 4; ++g) S[r0 + (lane >> 4) + 4 * g][c0 + (lane & 15)] = v[g];
 }
@@ -336,8 +347,13 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
   // formed per sweep instead of being hoisted out of the caller's loops
   // (in the persistent kernel they would stay live, as spilled SGPRs, across
   // its whole block-column loop)
-  int r = threadIdx.x & 63;
-  asm volatile("" : "+v"(r));
+  const int r = ctid() & 63;
+  // likewise the broadcast reads' base (an opaque zero in the column index):
+  // with compile-time c0 their LDS addresses are constants, and hoisted out
+  // of the loops they held one VGPR each for the whole kernel
+  int zo = 0;
+  asm volatile("" : "+v"(zo));
+  double2 (*colp)[CB] = reinterpret_cast<double2 (*)[CB]>(&W.colp[0][zo]);
   double a[16];
   {  // row r, columns c0..c0+15: 8 unconditional 16-B reads, then selects
     const double2* src = reinterpret_cast<const double2*>(&T[r][c0]);
@@ -356,7 +372,7 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
   __builtin_amdgcn_wave_barrier();
   double2 ct[16];
 #pragma unroll
-  for (int t = 2; t < 16; ++t) ct[t] = W.colp[0][c0 + t];
+  for (int t = 2; t < 16; ++t) ct[t] = colp[0][c0 + t];
   // the pivot block of the first pair from its two rows' lanes (readlane: no
   // LDS round trip on the chain; the same bits an LDS broadcast carries)
   double d0 = readlane_f64(a[0], c0), e = readlane_f64(a[0], c0 + 1), d1 = readlane_f64(a[1], c0 + 1);
@@ -393,7 +409,7 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
         W.colp[buf ^ 1][r] = make_double2(a[jj + 2], a[jj + 3]);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int t = jj + 4; t < 16; ++t) ctn[t] = W.colp[buf ^ 1][c0 + t];
+        for (int t = jj + 4; t < 16; ++t) ctn[t] = colp[buf ^ 1][c0 + t];
       }
 #pragma unroll
       for (int t = jj + 4; t < 16; ++t) a[t] = fma(-f1, ct[t].y, fma(-f0, ct[t].x, a[t]));
@@ -448,9 +464,13 @@ __device__ __forceinline__ void panel_sweep(double (*T)[LDP], CholLds& W, int c0
 // a 120-FMA chain: ~5.7k cycles on the critical path of the last row block.)
 __device__ __forceinline__ void diag_inverse16(const double (*T)[LDP], const double* rinv, double (*X)[LDP], int p,
                                                int b) {
-  const int c = threadIdx.x & 63;
+  const int c = ctid() & 63;
   const int c0 = 16 * p;
   if (c0 >= b || c >= 16) return;
+  // (uniform reads from an opaque base: see panel_sweep)
+  int zo = 0;
+  asm volatile("" : "+v"(zo));
+  T = reinterpret_cast<const double (*)[LDP]>(&T[0][zo]);
   double ri[16];
   {
     const double2* src = reinterpret_cast<const double2*>(&rinv[c0]);
@@ -534,7 +554,7 @@ template <bool FULL, int ZLD, class Hook>
 __device__ __forceinline__ void factor_invert_impl(double (*T)[LDP], double (*X)[LDP], double (*Z)[ZLD], CholLds& W,
                                                    int b, int m, const double (*Pc)[LDP], const Hook& hook) {
   if constexpr (FULL) { b = CB; m = CB; }
-  const int w = threadIdx.x >> 6;
+  const int w = cwave();
   __syncthreads();
   CHOL_STAMP(2);
   int last = 0;

@@ -42,6 +42,15 @@ namespace bahip {
 // critical workgroup's phases per block column
 #ifdef BA_CHOL_STAMPS
 __device__ unsigned long long g_pstamps[64][8];
+__device__ unsigned long long g_wstamps[64][6];   // worker (J+1, J), its last update: see WSTAMP
+#define WSTAMP(j, i)                                                                          \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    unsigned long long t_;                                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (threadIdx.x == 0 && (j) < 64) g_wstamps[j][i] = t_;                                   \
+  } while (0)
 #define PSTAMP(c, i)                                                                          \
   do {                                                                                        \
     __builtin_amdgcn_sched_barrier(0);                                                        \
@@ -52,6 +61,7 @@ __device__ unsigned long long g_pstamps[64][8];
   } while (0)
 #else
 #define PSTAMP(c, i) do {} while (0)
+#define WSTAMP(j, i) do {} while (0)
 #endif
 
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
@@ -75,7 +85,7 @@ __device__ __forceinline__ void st_sc1(Rsrc r, size_t byte_off, double2 x) {
 template <bool LOWER = false>
 __device__ inline TileRegs tile_fetch_sc1(Rsrc r, size_t ld, int r0, int c0, int rmax, int cmax) {
   TileRegs t;
-  const int tid = threadIdx.x;
+  const int tid = ctid();
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
     const int e = tid + 256 * it;
@@ -94,6 +104,14 @@ __device__ inline TileRegs tile_fetch_sc1(Rsrc r, size_t ld, int r0, int c0, int
 // drain this wave's stores, join the workgroup, one lane raises the flag
 __device__ __forceinline__ void publish(unsigned* flag, unsigned epoch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the same with the 8 tile loads of tile_fetch_sc1 issued after the stores
+// still in flight: vector memory operations complete in issue order, so
+// vmcnt(8) drains exactly the stores
+__device__ __forceinline__ void publish_before_loads(unsigned* flag, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -156,17 +174,19 @@ struct PanelPrefetch {
   int* ok;
   int r0, kc, nrows, cmax;
   int c;                  // diagnostics (BA_CHOL_STAMPS): the step, for the fetch-phase record
+  const unsigned* dflag;  // the next diagonal tile's flag (nullptr: no worker, ready)
+  int* dready;            // finish(): that flag seen up (polled once by wave 2)
   mutable double2 v[16];  // loads in flight between p = 3 and finish()
   mutable bool pending = false;
   __device__ bool poll() const {
     if (!flag) return true;
-    const unsigned f = (threadIdx.x & 63) == 0 ? __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+    const unsigned f = (ctid() & 63) == 0 ? __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                                : 0u;
     return __builtin_amdgcn_readfirstlane(f) == epoch;
   }
   // this wave's 32 rows x 32 pairs = 1024 pairs, 16 per lane
   __device__ void issue() const {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, hr = 32 * (w - 2);
+    const int w = cwave(), lane = ctid() & 63, hr = 32 * (w - 2);
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int e = lane + 64 * it;
@@ -177,7 +197,7 @@ struct PanelPrefetch {
     }
   }
   __device__ void land(int p) const {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, hr = 32 * (w - 2);
+    const int w = cwave(), lane = ctid() & 63, hr = 32 * (w - 2);
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int e = lane + 64 * it, i = hr + (e >> 5), j = (e & 31) * 2;
@@ -192,7 +212,7 @@ struct PanelPrefetch {
 #endif
   }
   __device__ void operator()(int p) const {
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;   // w = 2 or 3
+    const int w = cwave(), lane = ctid() & 63;   // w = 2 or 3
     const int st = __builtin_amdgcn_readfirstlane(ok[w - 2]);   // 0 at p = 1 (reset at the step start)
     if (st == 1) return;
     if (st == 0) {
@@ -208,6 +228,16 @@ struct PanelPrefetch {
   }
   __device__ void finish() const {
     if (pending) land(3);
+    if (cwave() == 2) {
+      bool up = true;
+      if (dflag) {
+        const unsigned f = (ctid() & 63) == 0
+                               ? __hip_atomic_load(dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : 0u;
+        up = __builtin_amdgcn_readfirstlane(f) == epoch;
+      }
+      if ((ctid() & 63) == 0) *dready = up ? 1 : 0;
+    }
   }
 };
 
@@ -217,6 +247,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   __shared__ double S2[CB][LDP];
   __shared__ double S3[CB][LDP];   // the next panel tile A_{c+1,c}, prefetched during the factor
   __shared__ int pref_ok[2];
+  __shared__ int dready[1];        // the next diagonal tile's flag was up at the factor's end
   __shared__ CholLds cw;
   const int n = a.n, nrows = n + 1, T = a.T;
   const size_t ld = (size_t)a.ld;
@@ -228,11 +259,52 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
 
   if (blockIdx.x == 0) {
     // ---------------- critical workgroup: the diagonal chain
-    if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; }
+    if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
+    // the end of step cp: V_cp cleaned in place (zero above the diagonal,
+    // identity rows past b: exactly the Vbuf image the per-step form
+    // re-stages) for the next panel GEMM, stored write-through and published
+    // to the workers (their trailing updates of step cp, and with them the
+    // next panel and diagonal tiles, wait for it).  The loop is rotated: this
+    // runs at the start of iteration cp + 1, so that the next diagonal tile's
+    // loads (issued here behind the V stores when its flag was up at the end
+    // of the factor, hook.finish) are consumed in the same iteration — tD is
+    // never live across the loop's back edge.
+    auto end_step = [&](int cp) {
+      const int sp = cp * CB, bp = min(CB, n - sp), mp = min(CB, nrows - sp);
+      for (int e2 = ctid(); e2 < CB * CB / 2; e2 += 256) {
+        const int i = (2 * e2) / CB, j = (2 * e2) % CB;
+        double v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          v[h] = (j + h <= i && i < bp && j + h < bp) ? S2[i][j + h] : (i == j + h ? 1.0 : 0.0);
+        S2[i][j] = v[0];
+        S2[i][j + 1] = v[1];
+        st_sc1(rV, ((size_t)cp * CB * CB + 2 * (size_t)e2) * sizeof(double), make_double2(v[0], v[1]));
+      }
+      if (mp > bp)
+        for (int j = ctid(); j < bp; j += 256) a.L[(size_t)(sp + bp) * ld + sp + j] = S0[bp][j];
+      bad |= cw.bad != 0;
+    };
     for (int c = 0; c < T; ++c) {
       const int s = c * CB;
       const int b = min(CB, n - s);
       const int m = min(CB, nrows - s);
+      bool have_diag = false;
+      TileRegs tD;
+      if (c > 0) {
+        end_step(c - 1);
+        // A_{c,c}: in flight from here when its worker had published it by
+        // the end of the factor (S0 is rewritten only at the panel GEMM,
+        // after L's last read above); the V drain waits for the stores only
+        have_diag = dready[0] != 0;
+        if (have_diag) {
+          asm volatile("" ::: "memory");   // (the loads after the V stores)
+          tD = tile_fetch_sc1<true>(rA, ld, s, s, nrows, s + b);
+        }
+        PSTAMP(c - 1, 6);
+        if (have_diag) publish_before_loads(&vflag[c - 1], a.epoch);
+        else publish(&vflag[c - 1], a.epoch);
+      }
       PSTAMP(c, 0);
 #ifdef BA_CHOL_STAMPS
       if (threadIdx.x == 0) g_stamp_on = c == T / 2;   // the factor's inner stamps: one mid step
@@ -245,25 +317,26 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         // A_{c,k} final (its worker; column 0 is never updated): prefetched
         // into S3 during the last factor when published by then, else fetched
         // here; the diagonal tile after the updates k' <= c - 2 (no worker for
-        // c = 1) is fetched into registers and lands behind the panel GEMM
+        // c = 1), unless already in flight, is fetched into registers here;
+        // it lands behind the panel GEMM
         const bool have_pref = pref_ok[0] == 1 && pref_ok[1] == 1;   // (read after the factor's last barrier)
         if (!have_pref) {
           if (k >= 1) bad |= !wait_flag(&tflag[c * T + k], a.epoch);
           const TileRegs tP = tile_fetch_sc1(rA, ld, s, kc, nrows, kc + kb);   // A_{c,k}
           tile_put(S3, tP);
         }
-        if (c >= 2) bad |= !wait_flag(&tflag[c * T + c], a.epoch);   // (its barrier also covers S3)
+        if (c >= 2 && !have_diag) bad |= !wait_flag(&tflag[c * T + c], a.epoch);   // (its barrier also covers S3)
         else __syncthreads();
-        if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; }
+        if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
         PSTAMP(c, 1);
-        const TileRegs tA = tile_fetch_sc1<true>(rA, ld, s, s, nrows, s + b);   // A_{c,c} (+ rhs row), in flight
+        if (!have_diag) tD = tile_fetch_sc1<true>(rA, ld, s, s, nrows, s + b);   // A_{c,c} (+ rhs row), in flight
         PSTAMP(c, 2);
         d4 acc[4];
         mfma_xVT_strip(S3, S2, acc);            // P = A_{c,k} V_k^T (V_k: S2, from the last iteration)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the diagonal tile has landed
-        tile_put(S0, tA);
+        tile_put(S0, tD);
         {
-          const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+          const int lane = ctid() & 63, w = cwave();
 #pragma unroll
           for (int bc = 0; bc < 4; ++bc)
 #pragma unroll
@@ -283,36 +356,18 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         // next step's panel tile A_{c+1,c}: final once its worker published
         // it (column 0: from before the launch)
         const PanelPrefetch pf{rA, ld, c >= 1 ? &tflag[(c + 1) * T + c] : nullptr, a.epoch, S3, pref_ok,
-                               (c + 1) * CB, c * CB, nrows, c * CB + min(CB, n - c * CB), c};
+                               (c + 1) * CB, c * CB, nrows, c * CB + min(CB, n - c * CB), c,
+                               c + 1 >= 2 ? &tflag[(c + 1) * T + c + 1] : nullptr, dready};
         factor_invert_blk<1>(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr, pf);   // b = m = CB before the last block
       } else {
         factor_invert_blk<0>(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr);
       }
       __syncthreads();
       PSTAMP(c, 5);
-      // V_c: cleaned in place (zero above the diagonal, identity rows past b:
-      // exactly the Vbuf image the per-step form re-stages) for the next
-      // iteration's panel GEMM, and published to the workers
-      {
-        for (int e2 = threadIdx.x; e2 < CB * CB / 2; e2 += 256) {
-          const int i = (2 * e2) / CB, j = (2 * e2) % CB;
-          double v[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-            v[h] = (j + h <= i && i < b && j + h < b) ? S2[i][j + h] : (i == j + h ? 1.0 : 0.0);
-          S2[i][j] = v[0];
-          S2[i][j + 1] = v[1];
-          st_sc1(rV, ((size_t)c * CB * CB + 2 * (size_t)e2) * sizeof(double), make_double2(v[0], v[1]));
-        }
-        if (m > b)
-          for (int j = threadIdx.x; j < b; j += 256) a.L[(size_t)(s + b) * ld + s + j] = S0[b][j];
-      }
-      bad |= cw.bad != 0;
-      PSTAMP(c, 6);
-      // V_c to the workers at once: the trailing updates of step c, and with
-      // them the next panel and diagonal tiles, wait for it
-      publish(&vflag[c], a.epoch);
     }
+    end_step(T - 1);
+    PSTAMP(T - 1, 6);
+    publish(&vflag[T - 1], a.epoch);
     if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
 #ifdef BA_CHOL_STAMPS
     if (threadIdx.x == 0) g_stamp_on = 1;
@@ -340,9 +395,11 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         own[x][y][g] = a.A[(size_t)min(r0 + rr, nrows - 1) * ld + min(c0 + cc, n - 1)];
       }
   const int kmax = diag ? J - 2 : J - 1;
+  const bool stamp = I == J + 1;   // (diagnostics: the next-panel tiles' last update)
   for (int k = 0; k <= kmax; ++k) {
     const int kc = k * CB, kb = min(CB, n - kc);
     bad |= !wait_flag(&vflag[k], a.epoch);
+    if (stamp && k == kmax) WSTAMP(J, 0);
     if (k >= 1) {
       bad |= !wait_flag(&tflag[I * T + k], a.epoch);
       if (!diag) bad |= !wait_flag(&tflag[J * T + k], a.epoch);
@@ -358,6 +415,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       if (!diag) tile_put(S1, tJ);
     }
     __syncthreads();
+    if (stamp && k == kmax) WSTAMP(J, 1);
     // P_I = A_{I,k} V_k^T, P_J likewise: V_k is lower triangular, so the
     // strip products skip its zero blocks (40 instead of 64 MFMAs per wave;
     // the skipped terms are exact zeros, so the sums are those of the full
@@ -366,8 +424,9 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
     mfma_xVT_strip(S0, S2, sI);
     if (!diag) mfma_xVT_strip(S1, S2, sJ);
     __syncthreads();
+    if (stamp && k == kmax) WSTAMP(J, 2);
     {
-      const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+      const int lane = ctid() & 63, wv = cwave();
 #pragma unroll
       for (int bc = 0; bc < 4; ++bc)
 #pragma unroll
@@ -388,6 +447,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) own[x][y][g] -= acc[x][y][g];
     __syncthreads();                           // S0..S2 are restaged next
+    if (stamp && k == kmax) WSTAMP(J, 3);
   }
   // publish the tile (lower part; pairs that start on or left of the
   // diagonal on a diagonal tile): through S0, as row-contiguous 16-B sc1 stores
@@ -402,13 +462,14 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         S0[rr][cc] = own[x][y][g];
       }
   __syncthreads();
-  for (int e2 = threadIdx.x; e2 < CB * CB / 2; e2 += 256) {
+  for (int e2 = ctid(); e2 < CB * CB / 2; e2 += 256) {
     const int i = (2 * e2) / CB, j = (2 * e2) % CB;
     const int ri = r0 + i, cj = c0 + j;
     if (ri < nrows && cj < n && (!diag || j <= i))   // n = 6 cameras: even, whole pairs
       st_sc1(rA, ((size_t)ri * ld + cj) * sizeof(double), make_double2(S0[i][j], S0[i][j + 1]));
   }
   publish(&tflag[I * T + J], a.epoch);
+  if (stamp) WSTAMP(J, 4);
   if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
 }
 

@@ -147,6 +147,24 @@ int main(int argc, char** argv) {
       printf("persistent critical cycles per step (avg of %d): wait %.0f  fetch+V publish %.0f  P gemm+store %.0f"
              "  C col0 %.0f  factor %.0f  V clean+store %.0f  | step %.0f\n",
              cnt, avg[0] / cnt, avg[1] / cnt, avg[2] / cnt, avg[3] / cnt, avg[4] / cnt, avg[5] / cnt, tot);
+      {
+        // the next-panel tile's worker (J+1, J), its last update (k = J-1),
+        // against the critical workgroup: cycles after V_{J-1}'s publish
+        // stamp (ps[J-1][6]) and the hook's sub-panel 1 start of step J
+        unsigned long long ws[64][6];
+        CK(hipMemcpyFromSymbol(ws, HIP_SYMBOL(g_wstamps), sizeof(ws)));
+        double av[5] = {0, 0, 0, 0, 0}, sp1 = 0, st = 0;
+        int nn = 0;
+        for (int J = 2; J + 1 < T && J < 64; ++J, ++nn) {
+          for (int i = 0; i < 5; ++i) av[i] += (double)(long long)(ws[J][i] - ps[J - 1][6]);
+          sp1 += (double)(long long)(ps[J][4] - ps[J - 1][6]);
+          st += (double)(long long)(ps[J][5] - ps[J - 1][6]);
+        }
+        if (nn)
+          printf("    panel-tile worker, last update, cycles after V_{J-1} publish (avg of %d): V seen %.0f  tiles in LDS %.0f"
+                 "  strips %.0f  GEMM %.0f  published %.0f | critical: factor starts %.0f, ends %.0f\n",
+                 nn, av[0] / nn, av[1] / nn, av[2] / nn, av[3] / nn, av[4] / nn, sp1 / nn, st / nn);
+      }
       int ph[4] = {0, 0, 0, 0};
       for (int c = 0; c + 1 < T && c < 64; ++c) ph[ps[c][7] & 3]++;
       printf("    next panel tile prefetched in sub-panel 1/2/3: %d/%d/%d, at the next step's start: %d\n", ph[1], ph[2],
