@@ -42,12 +42,13 @@ namespace bahip {
 // critical workgroup's phases per block column
 #ifdef BA_CHOL_STAMPS
 __device__ unsigned long long g_pstamps[64][8];
-__device__ unsigned long long g_wstamps[64][6];   // worker (J+1, J), its last update: see WSTAMP
+__device__ unsigned long long g_prt[64][8];       // the same stamps in s_memrealtime (100 MHz, chip-wide)
+__device__ unsigned long long g_wstamps[64][6];   // worker (J+1, J), its last update (s_memrealtime)
 #define WSTAMP(j, i)                                                                          \
   do {                                                                                        \
     __builtin_amdgcn_sched_barrier(0);                                                        \
     unsigned long long t_;                                                                    \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
     __builtin_amdgcn_sched_barrier(0);                                                        \
     if (threadIdx.x == 0 && (j) < 64) g_wstamps[j][i] = t_;                                   \
   } while (0)
@@ -58,6 +59,8 @@ __device__ unsigned long long g_wstamps[64][6];   // worker (J+1, J), its last u
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
     __builtin_amdgcn_sched_barrier(0);                                                        \
     if (threadIdx.x == 0 && (c) < 64) g_pstamps[c][i] = t_;                                   \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+    if (threadIdx.x == 0 && (c) < 64) g_prt[c][i] = t_;                                       \
   } while (0)
 #else
 #define PSTAMP(c, i) do {} while (0)
@@ -112,8 +115,16 @@ __device__ __forceinline__ void publish(unsigned* flag, unsigned epoch) {
 // vmcnt(8) drains exactly the stores
 __device__ __forceinline__ void publish_before_loads(unsigned* flag, unsigned epoch) {
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  __syncthreads();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
   if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a workgroup barrier for LDS only: __syncthreads' release fence would also
+// drain every outstanding global store and load of the waves
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 // lane 0 polls (relaxed, bounded), the barrier releases the workgroup.
 // Returns false in thread 0 if the bound was hit (the failure is reported by
@@ -325,8 +336,10 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
           const TileRegs tP = tile_fetch_sc1(rA, ld, s, kc, nrows, kc + kb);   // A_{c,k}
           tile_put(S3, tP);
         }
-        if (c >= 2 && !have_diag) bad |= !wait_flag(&tflag[c * T + c], a.epoch);   // (its barrier also covers S3)
-        else __syncthreads();
+        // (its barrier also covers S3; the plain form is an LDS-only
+        // barrier, so the diagonal tile's loads stay in flight across it)
+        if (c >= 2 && !have_diag) bad |= !wait_flag(&tflag[c * T + c], a.epoch);
+        else lds_barrier();
         if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
         PSTAMP(c, 1);
         if (!have_diag) tD = tile_fetch_sc1<true>(rA, ld, s, s, nrows, s + b);   // A_{c,c} (+ rhs row), in flight
@@ -335,6 +348,9 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         mfma_xVT_strip(S3, S2, acc);            // P = A_{c,k} V_k^T (V_k: S2, from the last iteration)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the diagonal tile has landed
         tile_put(S0, tD);
+        // P = L_{c,k} to the factor: here only without a worker (c+1, c),
+        // which otherwise stores the same product (its P_J) off this chain
+        const bool store_l = c + 1 >= a.TR;
         {
           const int lane = ctid() & 63, w = cwave();
 #pragma unroll
@@ -343,7 +359,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
             for (int g = 0; g < 4; ++g) {
               const int rr = 16 * w + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
               S1[rr][cc] = acc[bc][g];
-              if (rr < m && cc < kb) a.L[(size_t)(s + rr) * ld + kc + cc] = acc[bc][g];
+              if (store_l && rr < m && cc < kb) a.L[(size_t)(s + rr) * ld + kc + cc] = acc[bc][g];
             }
         }
         __syncthreads();
@@ -396,24 +412,27 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       }
   const int kmax = diag ? J - 2 : J - 1;
   const bool stamp = I == J + 1;   // (diagnostics: the next-panel tiles' last update)
-  for (int k = 0; k <= kmax; ++k) {
+  // the panel tiles A_{I,k}, A_{J,k} of update k are final long before V_k
+  // (their workers finished update k - 1 one step earlier): they are staged
+  // while V_k is awaited, so only V_k's fetch follows its flag
+  auto stage_panels = [&](int k) {
     const int kc = k * CB, kb = min(CB, n - kc);
-    bad |= !wait_flag(&vflag[k], a.epoch);
-    if (stamp && k == kmax) WSTAMP(J, 0);
     if (k >= 1) {
       bad |= !wait_flag(&tflag[I * T + k], a.epoch);
       if (!diag) bad |= !wait_flag(&tflag[J * T + k], a.epoch);
     }
-    // the staging of k_chol_step's trailing tile, through sc1 loads
-    {
-      const TileRegs tV = tile_fetch_sc1(rV, CB, k * CB, 0, (k + 1) * CB, CB);   // V_k (stored cleaned)
-      const TileRegs tI = tile_fetch_sc1(rA, ld, r0, kc, nrows, kc + kb);        // A_{I,k}
-      TileRegs tJ;
-      if (!diag) tJ = tile_fetch_sc1(rA, ld, c0, kc, n, kc + kb);              // A_{J,k}
-      tile_put(S2, tV);
-      tile_put(S0, tI);
-      if (!diag) tile_put(S1, tJ);
-    }
+    const TileRegs tI = tile_fetch_sc1(rA, ld, r0, kc, nrows, kc + kb);        // A_{I,k}
+    TileRegs tJ;
+    if (!diag) tJ = tile_fetch_sc1(rA, ld, c0, kc, n, kc + kb);              // A_{J,k}
+    tile_put(S0, tI);
+    if (!diag) tile_put(S1, tJ);
+  };
+  if (kmax >= 0) stage_panels(0);
+  for (int k = 0; k <= kmax; ++k) {
+    const int kc = k * CB, kb = min(CB, n - kc);
+    bad |= !wait_flag(&vflag[k], a.epoch);
+    if (stamp && k == kmax) WSTAMP(J, 0);
+    tile_put(S2, tile_fetch_sc1(rV, CB, k * CB, 0, (k + 1) * CB, CB));          // V_k (stored cleaned)
     __syncthreads();
     if (stamp && k == kmax) WSTAMP(J, 1);
     // P_I = A_{I,k} V_k^T, P_J likewise: V_k is lower triangular, so the
@@ -434,11 +453,11 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
           const int rr = 16 * wv + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
           S0[rr][cc] = sI[bc][g];
           if (!diag) S1[rr][cc] = sJ[bc][g];
+          if (J == k + 1) S3[rr][cc] = sI[bc][g];   // L_{I,k} final: stored after the publish
         }
     }
     __syncthreads();
     d4 acc[2][2];
-    if (J == k + 1) lds_to_global(S0, a.L, ld, r0, kc, mI, kb);   // L_{I,k} final
     mfma_xyT_64(S0, diag ? S0 : S1, acc);      // P_I P_J^T
 #pragma unroll
     for (int x = 0; x < 2; ++x)
@@ -448,6 +467,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         for (int g = 0; g < 4; ++g) own[x][y][g] -= acc[x][y][g];
     __syncthreads();                           // S0..S2 are restaged next
     if (stamp && k == kmax) WSTAMP(J, 3);
+    if (k < kmax) stage_panels(k + 1);
   }
   // publish the tile (lower part; pairs that start on or left of the
   // diagonal on a diagonal tile): through S0, as row-contiguous 16-B sc1 stores
@@ -470,6 +490,14 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   }
   publish(&tflag[I * T + J], a.epoch);
   if (stamp) WSTAMP(J, 4);
+  // L_{I,J-1} (the last update of an off-diagonal tile: J == k + 1) to the
+  // factor, after the publish: no in-kernel reader, and its drain would
+  // otherwise sit in the barriers before the tile's hand-off
+  if (!diag && kmax == J - 1) lds_to_global(S3, a.L, ld, r0, kmax * CB, mI, min(CB, n - kmax * CB));
+  // the worker (J+1, J) also stores P_J = L_{J,J-1}, the critical
+  // workgroup's panel product of step J (bitwise the same: the same tiles
+  // through the same strip product; block row J has no rhs row here)
+  if (I == J + 1) lds_to_global(S1, a.L, ld, c0, kmax * CB, CB, min(CB, n - kmax * CB));
   if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
 }
 

@@ -151,18 +151,19 @@ int main(int argc, char** argv) {
         // the next-panel tile's worker (J+1, J), its last update (k = J-1),
         // against the critical workgroup: cycles after V_{J-1}'s publish
         // stamp (ps[J-1][6]) and the hook's sub-panel 1 start of step J
-        unsigned long long ws[64][6];
+        unsigned long long ws[64][6], pr[64][8];
         CK(hipMemcpyFromSymbol(ws, HIP_SYMBOL(g_wstamps), sizeof(ws)));
+        CK(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_prt), sizeof(pr)));
         double av[5] = {0, 0, 0, 0, 0}, sp1 = 0, st = 0;
         int nn = 0;
         for (int J = 2; J + 1 < T && J < 64; ++J, ++nn) {
-          for (int i = 0; i < 5; ++i) av[i] += (double)(long long)(ws[J][i] - ps[J - 1][6]);
-          sp1 += (double)(long long)(ps[J][4] - ps[J - 1][6]);
-          st += (double)(long long)(ps[J][5] - ps[J - 1][6]);
+          for (int i = 0; i < 5; ++i) av[i] += 10.0 * (double)(long long)(ws[J][i] - pr[J - 1][6]);
+          sp1 += 10.0 * (double)(long long)(pr[J][4] - pr[J - 1][6]);
+          st += 10.0 * (double)(long long)(pr[J][5] - pr[J - 1][6]);
         }
         if (nn)
-          printf("    panel-tile worker, last update, cycles after V_{J-1} publish (avg of %d): V seen %.0f  tiles in LDS %.0f"
-                 "  strips %.0f  GEMM %.0f  published %.0f | critical: factor starts %.0f, ends %.0f\n",
+          printf("    panel-tile worker, last update, ns after V_{J-1}'s publish stamp (avg of %d): V seen %.0f  tiles in"
+                 " LDS %.0f  strips %.0f  GEMM %.0f  published %.0f | critical: factor starts %.0f, ends %.0f\n",
                  nn, av[0] / nn, av[1] / nn, av[2] / nn, av[3] / nn, av[4] / nn, sp1 / nn, st / nn);
       }
       int ph[4] = {0, 0, 0, 0};
