@@ -1669,6 +1669,9 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
 //   W_a W_b^T = c_a^T M c_b,  M = Z_a Z_b^T (2 x 2)
 // the partner record is one 128-B line (W: two) and is fetched one pair
 // ahead; the row camera's record is an L2 hit.
+// (Measured and not kept: the row camera's record one pair ahead as well,
+// with the camera constants re-read from LDS per pair to keep 2 waves per
+// SIMD: 168 vs 165 us, profiles/r03_v13_ab_pairs_ca.txt.)
 __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4* __restrict__ blocks, int nblocks,
                                                        const int2* __restrict__ pairs, const double* __restrict__ Wc,
                                                        const double* __restrict__ scale_c, double* __restrict__ S) {
@@ -2244,9 +2247,15 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
 
 // k_cam_schur_diag on compact records:
 //   W W^T = c^T (Z Z^T) c,  W u = c^T (Z u)
-__global__ __launch_bounds__(256) void k_cam_schur_diag_c(DevProblem P, const double* __restrict__ Wc,
-                                                          const double* __restrict__ scale_c,
-                                                          const double* __restrict__ u, double* __restrict__ cpart) {
+// NT threads per workgroup (W.cam_split workgroups per camera).  PREF: the
+// next observation's record and u one step ahead.  At 256 threads a thread
+// has ~2.5 observations at C3 and the 27-value workgroup reduction (DS
+// permutes) is a third of the kernel's instructions (SQ counters,
+// profiles/r03_v12_pmc_sq.txt); one wave per workgroup has ~10.
+template <int NT, bool PREF>
+__global__ __launch_bounds__(NT) void k_cam_schur_diag_c(DevProblem P, const double* __restrict__ Wc,
+                                                         const double* __restrict__ scale_c,
+                                                         const double* __restrict__ u, double* __restrict__ cpart) {
   __shared__ double lds[27 * 16];
   const int v = blockIdx.x;
   WcCam m;
@@ -2256,13 +2265,7 @@ __global__ __launch_bounds__(256) void k_cam_schur_diag_c(DevProblem P, const do
   for (int k = 0; k < 27; ++k) acc[k] = 0.0;
   int i0, i1;
   cam_slice(P, v, i0, i1);
-  // (~2.5 observations per thread at C3: a one-step-ahead prefetch measured
-  // 84 vs 66 us, profiles/r03_v8_ab_pairs_diag.txt)
-  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int2 op = P.cam_op[i];
-    const WcRaw w = wc_fetch(Wc, op.x);
-    const double2 u01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
-    const double u2 = u[4 * (size_t)op.y + 2];
+  auto add = [&](const WcRaw& w, double2 u01, double u2) {
     double c0[6], c1[6];
     wc_rows(w, m, c0, c1);
     const double* z0 = w.r + 9;
@@ -2286,6 +2289,37 @@ __global__ __launch_bounds__(256) void k_cam_schur_diag_c(DevProblem P, const do
     }
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[21 + a] += c0[a] * zu0 + c1[a] * zu1;
+  };
+  if constexpr (PREF) {
+    int i = i0 + threadIdx.x;
+    WcRaw nw;
+    double2 nu01 = make_double2(0.0, 0.0);
+    double nu2 = 0.0;
+    if (i < i1) {
+      const int2 op = P.cam_op[i];
+      nw = wc_fetch(Wc, op.x);
+      nu01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
+      nu2 = u[4 * (size_t)op.y + 2];
+    }
+    for (; i < i1; i += NT) {
+      const WcRaw w = nw;
+      const double2 u01 = nu01;
+      const double u2 = nu2;
+      if (i + NT < i1) {
+        const int2 op = P.cam_op[i + NT];
+        nw = wc_fetch(Wc, op.x);
+        nu01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
+        nu2 = u[4 * (size_t)op.y + 2];
+      }
+      add(w, u01, u2);
+    }
+  } else {
+    for (int i = i0 + threadIdx.x; i < i1; i += NT) {
+      const int2 op = P.cam_op[i];
+      const WcRaw w = wc_fetch(Wc, op.x);
+      const double2 u01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
+      add(w, u01, u[4 * (size_t)op.y + 2]);
+    }
   }
   double tot[27];
   block_sum<27>(acc, lds, tot);
@@ -2682,8 +2716,27 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
 void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
   if (W.jrfree) {
-    hipLaunchKernelGGL(k_cam_assemble_rc<512>, dim3(P.nvc, 1), dim3(512), 0, s, P, (const double*)W.rec,
-                       (const double*)W.pts, W.cpart, W.Hcc, W.gc);
+    // diagnostics: BA_CA_NT (128 / 256 / 512 threads), BA_CA_SPLIT (workgroups
+    // per camera, <= W.cam_split; > 1 adds the ordered slice fold).  One
+    // 512-thread workgroup per camera measured best: 30.6 us vs 37 / 49 us at
+    // 2 / 4 slices, 32.5 us at 256 threads x 2 (profiles/r03_v13_ab_pairs_ca.txt)
+    static int nt = -1, sp = -1;
+    if (nt < 0) { const char* e = getenv("BA_CA_NT"); nt = e ? atoi(e) : 512; }
+    if (sp < 0) { const char* e = getenv("BA_CA_SPLIT"); sp = e ? atoi(e) : 1; }
+    const int sl = std::max(1, std::min(sp, W.cam_split));
+    const dim3 g(P.nvc, sl);
+    if (nt == 128)
+      hipLaunchKernelGGL(k_cam_assemble_rc<128>, g, dim3(128), 0, s, P, (const double*)W.rec, (const double*)W.pts,
+                         W.cpart, W.Hcc, W.gc);
+    else if (nt == 256)
+      hipLaunchKernelGGL(k_cam_assemble_rc<256>, g, dim3(256), 0, s, P, (const double*)W.rec, (const double*)W.pts,
+                         W.cpart, W.Hcc, W.gc);
+    else
+      hipLaunchKernelGGL(k_cam_assemble_rc<512>, g, dim3(512), 0, s, P, (const double*)W.rec, (const double*)W.pts,
+                         W.cpart, W.Hcc, W.gc);
+    if (sl > 1)
+      hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
+                         nullptr);
     return;
   }
   const bool many = P.nc > kLinLdsCams;   // JR layout (jr_ja)
@@ -2751,8 +2804,24 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
   const int sl = dsplit > 0 ? std::min(dsplit, kCamSplit) : W.cam_split;
   if (W.w32)
     hipLaunchKernelGGL(k_cam_schur_diag<float>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wf, W.u, W.S, W.cpart);
-  else if (W.wcompact)
-    hipLaunchKernelGGL(k_cam_schur_diag_c, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.W, W.scale_c, W.u, W.cpart);
+  else if (W.wcompact) {
+    // diagnostics: BA_DIAG_NT (64 / 128 / 256 threads), BA_DIAG_PREF (0 / 1)
+    static int nt = -1, pref = -1;
+    // 64: 49 vs 65.5 us at C3, 1355-1369 vs 1331-1338 M-obs/s
+    // (profiles/r03_v13_ab_diag_nt.txt); the one-ahead prefetch measured 52 us
+    if (nt < 0) { const char* e = getenv("BA_DIAG_NT"); nt = e ? atoi(e) : 64; }
+    if (pref < 0) { const char* e = getenv("BA_DIAG_PREF"); pref = e ? atoi(e) : 0; }
+    const dim3 g(P.nvc, sl);
+    if (nt == 64)
+      hipLaunchKernelGGL((pref ? k_cam_schur_diag_c<64, true> : k_cam_schur_diag_c<64, false>), g, dim3(64), 0, s, P,
+                         W.W, W.scale_c, W.u, W.cpart);
+    else if (nt == 128)
+      hipLaunchKernelGGL((pref ? k_cam_schur_diag_c<128, true> : k_cam_schur_diag_c<128, false>), g, dim3(128), 0, s, P,
+                         W.W, W.scale_c, W.u, W.cpart);
+    else
+      hipLaunchKernelGGL((pref ? k_cam_schur_diag_c<256, true> : k_cam_schur_diag_c<256, false>), g, dim3(256), 0, s, P,
+                         W.W, W.scale_c, W.u, W.cpart);
+  }
   else
     hipLaunchKernelGGL(k_cam_schur_diag<double>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.W, W.u, W.S, W.cpart);
   if (!compact && radius > 0.0) {   // single rank: the LM diagonal goes in with the fold
