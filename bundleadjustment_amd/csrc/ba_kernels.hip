@@ -1604,23 +1604,26 @@ __device__ inline void acc_pair(double (&acc)[36], const double (&a)[18], const 
 // BA_PAIR_LANES selects 8 or 32): each lane accumulates every PL-th pair
 // (two pairs' gathers in flight), then a log2(PL)-stage xor reduction inside
 // the lane group; all PL lanes then hold the sums and store 36/PL each.
+#ifndef BA_PAIRS_IDX2
+#define BA_PAIRS_IDX2 1
+#endif
 #ifndef BA_PAIR_LANES
 #define BA_PAIR_LANES 16
 #endif
 constexpr int kPairLanes = BA_PAIR_LANES;
-__global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* __restrict__ blocks, int nblocks,
-                                                     const int2* __restrict__ pairs, const double* __restrict__ W,
-                                                     double* __restrict__ S) {
+__global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* __restrict__ blocks,
+                                                     const int* __restrict__ xoff, const int2* __restrict__ pairs,
+                                                     const double* __restrict__ W, double* __restrict__ S) {
   constexpr int PL = kPairLanes, BPW = 64 / PL;
   const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
   // XCD-aware order: workgroups b and b + 8 share an XCD (round-robin
-  // dispatch).  XCD x owns the contiguous block range [x R, (x+1) R) (a few
-  // rows I of S) and its workgroups sweep it in rounds, so the W rows of the
-  // few cameras I active on an XCD are re-read from its L2 by the ~9 blocks
-  // (I, J) each observation contributes to.  gridDim.x is a multiple of 8.
+  // dispatch).  XCD x owns the block range [xoff[x], xoff[x+1]) (the rows I
+  // of S with I mod 8 = x, ascending) and its workgroups sweep it in rounds,
+  // so the W rows of the few cameras I active on an XCD are re-read from its
+  // L2 by the ~9 blocks (I, J) each observation contributes to.  gridDim.x is
+  // a multiple of 8.
   const int xcd = blockIdx.x & 7, wx = blockIdx.x >> 3, nwx = gridDim.x >> 3;
-  const int R = (nblocks + 7) / 8;
-  const int r0 = xcd * R, r1 = min(nblocks, r0 + R);
+  const int r0 = xoff[xcd], r1 = xoff[xcd + 1];
   const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   const size_t ld = (size_t)P.ld;
   for (int base = r0 + (wx * nwv + wv) * BPW; base < r1; base += nwx * nwv * BPW) {
@@ -1672,19 +1675,32 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
 // (Measured and not kept: the row camera's record one pair ahead as well,
 // with the camera constants re-read from LDS per pair to keep 2 waves per
 // SIMD: 168 vs 165 us, profiles/r03_v13_ab_pairs_ca.txt.)
-__global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4* __restrict__ blocks, int nblocks,
-                                                       const int2* __restrict__ pairs, const double* __restrict__ Wc,
-                                                       const double* __restrict__ scale_c, double* __restrict__ S) {
+//
+// SIGNAL (the overlapped step: the persistent factorisation runs beside this
+// pass and reads a camera row of S once it is complete, ba_chol_persist.hip
+// wait_rows): every S entry is stored write-through (sc1), each wave drains
+// its stores (vmcnt(0)) and one lane per block then adds 1 to the row
+// camera's counter (relaxed agent atomic; MI355X_MICROARCH.md "Valid forms":
+// the consumer acquires).  The XCD ranges xoff interleave the camera rows
+// (row a on XCD a mod 8, ascending), so rows complete in order over time.
+template <bool SIGNAL>
+__global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4* __restrict__ blocks,
+                                                       const int* __restrict__ xoff, const int2* __restrict__ pairs,
+                                                       const double* __restrict__ Wc,
+                                                       const double* __restrict__ scale_c, double* __restrict__ S,
+                                                       unsigned* __restrict__ rowcnt,
+                                                       unsigned long long* __restrict__ trace) {
   // the camera constants of every variable camera in LDS (nvc <= 200 in the
   // J-free mode: 14.4 KB), read per pair (registers: 1 -> 2 waves per SIMD)
   __shared__ WcCam ctab[kLinLdsCams];
+  if (SIGNAL && trace && blockIdx.x == 0 && threadIdx.x == 0)   // (the first launch of the step)
+    atomicCAS(trace + 255, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
   __syncthreads();
   constexpr int PL = kPairLanes, BPW = 64 / PL;
   const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
   const int xcd = blockIdx.x & 7, wx = blockIdx.x >> 3, nwx = gridDim.x >> 3;
-  const int R = (nblocks + 7) / 8;
-  const int r0 = xcd * R, r1 = min(nblocks, r0 + R);
+  const int r0 = xoff[xcd], r1 = xoff[xcd + 1];
   const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   const size_t ld = (size_t)P.ld;
   for (int base = r0 + (wx * nwv + wv) * BPW; base < r1; base += nwx * nwv * BPW) {
@@ -1703,12 +1719,24 @@ __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4*
       pr = pairs[e];
       nb = wc_fetch(Wc, pr.y);
     }
+#if BA_PAIRS_IDX2
+    // the pair indices two pairs ahead: the next partner's fetch then waits
+    // for no index load of its own iteration (one latency per pair, not two)
+    int2 pn = make_int2(0, 0);
+    if (e + PL < blk.w) pn = pairs[e + PL];
+#endif
     for (; e < blk.w; e += PL) {
       const WcRaw wa = wc_fetch(Wc, pr.x);   // row camera I: re-read from L2 by its blocks
       const WcRaw wb = nb;
       if (e + PL < blk.w) {
+#if BA_PAIRS_IDX2
+        pr = pn;
+        nb = wc_fetch(Wc, pr.y);
+        if (e + 2 * PL < blk.w) pn = pairs[e + 2 * PL];
+#else
         pr = pairs[e + PL];
         nb = wc_fetch(Wc, pr.y);
+#endif
       }
       double ca0[6], ca1[6], cb0[6], cb1[6];
       wc_rows(wa, mI, ca0, ca1);
@@ -1745,8 +1773,27 @@ __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4*
       for (int k = 0; k < 36; ++k) {
         if ((k % PL) != sl) continue;
         const int i = k / 6, j = k % 6;
-        if (I != Jb) S[(size_t)(6 * I + i) * ld + 6 * Jb + j] = -acc[k];
-        else if (j <= i) S[(size_t)(6 * I + i) * ld + 6 * I + j] -= acc[k];  // duplicate obs of one point by one camera
+        if (I != Jb) {
+          double* d = S + (size_t)(6 * I + i) * ld + 6 * Jb + j;
+          if (SIGNAL)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(d), __builtin_bit_cast(unsigned long long, -acc[k]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            *d = -acc[k];
+        } else if (j <= i) {
+          S[(size_t)(6 * I + i) * ld + 6 * I + j] -= acc[k];  // duplicate obs of one point by one camera (never SIGNAL)
+        }
+      }
+    }
+    if (SIGNAL) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores (every lane) have left
+      if (live && sl == 0) {
+        const unsigned c = __hip_atomic_fetch_add(rowcnt + (size_t)blk.x * kRowCntStride, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        // diagnostics (BA_OVERLAP_TRACE): the time of each row's last block
+        if (trace && blk.x < 256) __hip_atomic_fetch_max(trace + blk.x, __builtin_amdgcn_s_memrealtime() | 0ull,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (void)c;
       }
     }
   }
@@ -2833,7 +2880,7 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
                      compact ? 2 : 1, W.Hcc,
                      W.gc, compact ? compact : W.S);
 }
-void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, bool signal, int part) {
   if (W.nblocks == 0) return;
   static int grid_cap = 0;
   if (grid_cap == 0) {
@@ -2841,15 +2888,20 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
     grid_cap = e ? atoi(e) : 2048;
     if (grid_cap < 8) grid_cap = 8;
   }
-  int waves = (W.nblocks + 3) / 4;
-  int grid = (waves + 3) / 4;
+  // 16 blocks per workgroup (4 waves of 4) over the largest XCD range
+  const int* xoff = W.xoff + (part == 1 ? 9 : 0);
+  int grid = 8 * ((W.xmax[part == 1 ? 1 : 0] + 15) / 16);
+  if (grid == 0) return;
   if (grid > grid_cap) grid = grid_cap;
   grid = (grid + 7) / 8 * 8;   // k_schur_pairs' XCD ranges need a multiple of 8
-  if (W.wcompact)
-    hipLaunchKernelGGL(k_schur_pairs_c, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.scale_c,
-                       W.S);
+  if (W.wcompact && signal)
+    hipLaunchKernelGGL(k_schur_pairs_c<true>, dim3(grid), dim3(256), 0, s, P, W.blocks, xoff, W.pairs, W.W,
+                       W.scale_c, W.S, W.rowcnt, W.trace);
+  else if (W.wcompact)
+    hipLaunchKernelGGL(k_schur_pairs_c<false>, dim3(grid), dim3(256), 0, s, P, W.blocks, xoff, W.pairs, W.W,
+                       W.scale_c, W.S, nullptr, nullptr);
   else
-    hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, W.nblocks, W.pairs, W.W, W.S);
+    hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, xoff, W.pairs, W.W, W.S);
 }
 // one workgroup per row of S: row i < n holds its lower part (j <= i), row n
 // the rhs (all n entries)

@@ -303,6 +303,29 @@ def test_persistent_cholesky_is_bitwise_the_per_step_form(monkeypatch, cfg, scal
 
 
 # ---------------------------------------------------------------------------
+# overlapped DENSE_SCHUR step (BA_OVERLAP=1: the split persistent
+# factorisation waits row by row for the pair pass running beside it; 2: the
+# same kernels in the serial order): the same operations on the same values,
+# so bitwise the serial step
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("cfg,scale,fix", [("c3", 0.05, 1), ("c2", 1.0, 0), ("c3", 1.0, 0)])
+def test_overlapped_step_is_bitwise_the_serial_step(monkeypatch, cfg, scale, fix):
+    p = make_config(cfg, scale=scale)
+    if fix:
+        bp.fix_camera(p, 1)
+    runs = {}
+    for mode in ("0", "1", "2"):
+        monkeypatch.setenv("BA_OVERLAP", mode)
+        with Solver(0) as s:
+            runs[mode] = run_gpu(s, p, Options(max_num_iterations=4))
+    for mode in ("1", "2"):
+        a, b = runs["0"], runs[mode]
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), mode
+        assert [r["cost"] for r in a[3]] == [r["cost"] for r in b[3]], mode
+        assert [r["step_is_successful"] for r in a[3]] == [r["step_is_successful"] for r in b[3]], mode
+
+
+# ---------------------------------------------------------------------------
 # compact W records (k_obs_w_rc<double, true>: one 128-B line per
 # observation; S through the 2 x 2 inner products Z_a Z_b^T) against the
 # 18-double blocks: the same system up to rounding (the products associate
