@@ -189,6 +189,9 @@ int chol_split_blocks();                     // block columns from which the spl
 constexpr int kLinLdsCamsHost = 200;   // = kLinLdsCams (ba_kernels.hip): cameras the LDS camera table holds
 int jr_ja_host(int nc);   // JA stride of the JR records for nc cameras (12 or 14)
 void launch_stream_copy(const double* a, double* b, size_t n2, hipStream_t s);
+// the scalar record into pinned host memory, then its sequence number
+// (system-scope release): ba_solver.hip read_scalars
+void launch_publish_scalars(const double* scal, double* host, int n, unsigned* host_seq, unsigned seq, hipStream_t s);
 void launch_residuals(const DevProblem& P, const double* rec, const double* pts, double* r_raw, hipStream_t s);
 
 // pruneCorrespondences per (keyframe, keypoint) pair (ba_prune.hip)

@@ -2853,6 +2853,8 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
     hipLaunchKernelGGL(k_cam_schur_diag<float>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wf, W.u, W.S, W.cpart);
   else if (W.wcompact) {
     // diagnostics: BA_DIAG_NT (64 / 128 / 256 threads), BA_DIAG_PREF (0 / 1)
+    // (the observation index alone one step ahead measured 50.7 vs 49 us,
+    // profiles/r03_v15_ab_scal_spin.txt)
     static int nt = -1, pref = -1;
     // 64: 49 vs 65.5 us at C3, 1355-1369 vs 1331-1338 M-obs/s
     // (profiles/r03_v13_ab_diag_nt.txt); the one-ahead prefetch measured 52 us
@@ -3318,6 +3320,18 @@ void launch_pose_batch(int nprob, const int* off, const double* cams_in, const f
   if (nprob <= 0) return;
   hipLaunchKernelGGL(k_pose_batch, dim3(nprob), dim3(64), 0, s, nprob, off, cams_in, K, X, uv, huber_a, o, cams_out,
                      summ);
+}
+
+__global__ __launch_bounds__(64) void k_publish_scalars(const double* __restrict__ scal, double* __restrict__ host,
+                                                        int n, unsigned* __restrict__ host_seq, unsigned seq) {
+  for (int i = threadIdx.x; i < n; i += 64) host[i] = scal[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the record reaches host memory first
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(host_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+void launch_publish_scalars(const double* scal, double* host, int n, unsigned* host_seq, unsigned seq, hipStream_t s) {
+  hipLaunchKernelGGL(k_publish_scalars, dim3(1), dim3(64), 0, s, scal, host, n, host_seq, seq);
 }
 
 }  // namespace bahip

@@ -91,7 +91,11 @@ struct ba_ctx {
   DevProblem P{};
   DevWork W{};
   std::vector<void*> allocs;     // device buffers of the current problem
-  double* h_scal = nullptr;      // pinned scalar record
+  double* h_scal = nullptr;      // pinned scalar record (device-mapped, coherent)
+  double* d_hscal = nullptr;     // its device address
+  unsigned* h_seq = nullptr;     // the record's sequence number (after the record), host / device address
+  unsigned* d_hseq = nullptr;
+  unsigned scal_seq = 0;
   char* pose_buf = nullptr;      // ba_solve_pose_batch device staging (grown on demand)
   size_t pose_cap = 0;
   std::vector<char> pose_host;
@@ -185,9 +189,32 @@ struct ba_ctx {
     HIP_OK(hipMemcpyAsync(v, hv_scratch, sizeof(double) * count, hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
   }
+  // The scalar record to the host: a one-workgroup kernel stores it into the
+  // pinned, device-mapped record and then a sequence number (system-scope
+  // release), and the host spins on that number, instead of a D2H blit and
+  // a stream synchronisation (whose wake-up left ~20 us of idle device
+  // between an LM step and the next linearisation).  A device error or a
+  // missing number (bounded wait) falls back to the synchronisation, which
+  // reports it.  BA_SCAL_SPIN=0: the blit + synchronisation (A/B).
   void read_scalars() {
-    HIP_OK(hipMemcpyAsync(h_scal, W.scal, sizeof(double) * (kNumSlots + kPcgState), hipMemcpyDeviceToHost, stream));
-    HIP_OK(hipStreamSynchronize(stream));
+    static const bool spin = [] { const char* e = std::getenv("BA_SCAL_SPIN"); return !(e && e[0] == '0'); }();
+    const size_t cnt = kNumSlots + kPcgState;
+    if (!spin || !d_hscal) {
+      HIP_OK(hipMemcpyAsync(h_scal, W.scal, sizeof(double) * cnt, hipMemcpyDeviceToHost, stream));
+      HIP_OK(hipStreamSynchronize(stream));
+      return;
+    }
+    const unsigned seq = ++scal_seq;
+    bahip::launch_publish_scalars(W.scal, d_hscal, (int)cnt, d_hseq, seq, stream);
+    HIP_OK(hipGetLastError());
+    const double t0 = now_s();
+    for (unsigned it = 1;; ++it) {
+      if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) == seq) return;
+      if ((it & 1023u) == 0 && now_s() - t0 > 2.0) break;
+    }
+    HIP_OK(hipStreamSynchronize(stream));   // (raises a device error)
+    if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) != seq)
+      throw BaError{BA_ERR_DEVICE, "scalar record: sequence number not received"};
   }
 };
 
@@ -1038,7 +1065,16 @@ int ba_create(ba_ctx** out, int device) {
     HIP_OK(hipSetDevice(device));
     HIP_OK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     for (auto& e : ctx->ev) HIP_OK(hipEventCreate(&e));
-    HIP_OK(hipHostMalloc(&ctx->h_scal, sizeof(double) * (kNumSlots + kPcgState), hipHostMallocDefault));
+    {
+      const size_t rec = sizeof(double) * (kNumSlots + kPcgState);
+      HIP_OK(hipHostMalloc(&ctx->h_scal, rec + 64, hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(ctx->h_scal, 0, rec + 64);
+      ctx->h_seq = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ctx->h_scal) + rec);
+      void* d = nullptr;
+      HIP_OK(hipHostGetDevicePointer(&d, ctx->h_scal, 0));
+      ctx->d_hscal = static_cast<double*>(d);
+      ctx->d_hseq = reinterpret_cast<unsigned*>(static_cast<char*>(d) + rec);
+    }
   } catch (const BaError& e) {
     std::fprintf(stderr, "ba_create: %s\n", e.msg.c_str());
     delete ctx;
