@@ -65,7 +65,11 @@ struct ba_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::string err;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};   // [2..5]: two r+J stamp pairs, [6]: scalar blit
+  int rj_slot = 0;   // the stamp pair of the next timed linearisation (bench)
+  // the device linearisation state is at the candidate of the last step (a
+  // speculative linearisation, enqueued behind the step's scalar record)
+  bool lin_at_cand = false;
   // overlapped DENSE_SCHUR step: the factorisation's stream, the fork / join events
   hipStream_t stream2 = nullptr, stream3 = nullptr;   // critical workgroup / workers
   hipEvent_t evf = nullptr, evj = nullptr, evj3 = nullptr;
@@ -196,17 +200,32 @@ struct ba_ctx {
   // between an LM step and the next linearisation).  A device error or a
   // missing number (bounded wait) falls back to the synchronisation, which
   // reports it.  BA_SCAL_SPIN=0: the blit + synchronisation (A/B).
+  // publish_scalars() enqueues the record's transfer, wait_scalars() waits
+  // for it (work enqueued in between keeps the device busy meanwhile)
   void read_scalars() {
+    publish_scalars();
+    wait_scalars();
+  }
+  bool scal_spin() const {
     static const bool spin = [] { const char* e = std::getenv("BA_SCAL_SPIN"); return !(e && e[0] == '0'); }();
+    return spin && d_hscal;
+  }
+  void publish_scalars() {
     const size_t cnt = kNumSlots + kPcgState;
-    if (!spin || !d_hscal) {
+    if (!scal_spin()) {
       HIP_OK(hipMemcpyAsync(h_scal, W.scal, sizeof(double) * cnt, hipMemcpyDeviceToHost, stream));
-      HIP_OK(hipStreamSynchronize(stream));
+      HIP_OK(hipEventRecord(ev[6], stream));
       return;
     }
-    const unsigned seq = ++scal_seq;
-    bahip::launch_publish_scalars(W.scal, d_hscal, (int)cnt, d_hseq, seq, stream);
+    bahip::launch_publish_scalars(W.scal, d_hscal, (int)cnt, d_hseq, ++scal_seq, stream);
     HIP_OK(hipGetLastError());
+  }
+  void wait_scalars() {
+    if (!scal_spin()) {
+      HIP_OK(hipEventSynchronize(ev[6]));
+      return;
+    }
+    const unsigned seq = scal_seq;
     const double t0 = now_s();
     for (unsigned it = 1;; ++it) {
       if (__atomic_load_n(h_seq, __ATOMIC_ACQUIRE) == seq) return;
@@ -628,12 +647,14 @@ void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double 
   const hipStream_t s = ctx->stream;
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
+  ctx->lin_at_cand = false;
   launch_lin_prep(P, W, s);
-  // time_rj: kernel execution stamps from the launch itself (bench roofline)
-  launch_linearize(P, W, s, time_rj ? ctx->ev[2] : nullptr, time_rj ? ctx->ev[3] : nullptr);
+  // time_rj: kernel execution stamps from the launch itself (bench roofline),
+  // into the stamp pair ctx->rj_slot
+  hipEvent_t e0 = time_rj ? ctx->ev[2 + 2 * ctx->rj_slot] : nullptr, e1 = time_rj ? ctx->ev[3 + 2 * ctx->rj_slot] : nullptr;
+  launch_linearize(P, W, s, e0, e1);
   // (J-free: the timed residual + Jacobian kernel is k_lin_point, launched here)
-  launch_point_assemble(P, W, compute_scale, min_diag, max_diag, s, time_rj && W.jrfree ? ctx->ev[2] : nullptr,
-                        time_rj && W.jrfree ? ctx->ev[3] : nullptr);
+  launch_point_assemble(P, W, compute_scale, min_diag, max_diag, s, W.jrfree ? e0 : nullptr, W.jrfree ? e1 : nullptr);
   launch_cam_assemble(P, W, s);
   // point-side scalars: folded here when they must be all-reduced before
   // cam_norms, else together with the camera-side ones (one launch less)
@@ -872,6 +893,21 @@ void accept_candidate(ba_ctx* ctx) {
   std::swap(ctx->W.pts, ctx->W.pts_c);
 }
 
+// Speculative linearisation at the last step's candidate, enqueued behind
+// the step's scalar record: it runs while the host reads the record and
+// decides, and it is the next iteration's linearisation when the step is
+// accepted (the common case).  A rejected step re-linearises at x
+// (ctx->lin_at_cand); the values are the same either way.  Single rank only
+// (the exchange path's collectives keep their order).  BA_SPEC_LIN=0: off.
+void spec_lin_enqueue(ba_ctx* ctx, const ba_options& o) {
+  static const bool on = [] { const char* e = std::getenv("BA_SPEC_LIN"); return !(e && e[0] == '0'); }();
+  if (!on || ctx->coll()) return;
+  accept_candidate(ctx);   // (the kernels read W.cams / W.pts: point them at the candidate)
+  linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, false, true);
+  accept_candidate(ctx);
+  ctx->lin_at_cand = true;
+}
+
 void check_options(const ba_options& o) {
   if (o.linear_solver != BA_DENSE_SCHUR && o.linear_solver != BA_ITERATIVE_SCHUR)
     throw BaError{BA_ERR_INVALID_ARGUMENT, "unknown linear_solver " + std::to_string(o.linear_solver)};
@@ -950,8 +986,13 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
     double ts = now_s();
     int ls = spec_ls;
     if (!have_step) {
+      // (after a rejected or invalid step the speculative linearisation at
+      // its candidate replaced the one at x)
+      if (ctx->lin_at_cand) linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, false, true);
       ls = step_enqueue(ctx, radius, o);
-      ctx->read_scalars();
+      ctx->publish_scalars();
+      spec_lin_enqueue(ctx, o);
+      ctx->wait_scalars();
     }
     have_step = false;
     StepResult st = step_result(ctx, ls);
@@ -988,9 +1029,19 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
       // speculate: the next step at the new radius, unless the loop ends on
       // grounds already known (iteration cap, radius floor)
       const bool spec = iteration < o.max_num_iterations && radius > o.min_trust_region_radius;
-      linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, false, spec);
-      if (spec) spec_ls = step_enqueue(ctx, radius, o);
-      ctx->read_scalars();
+      // the linearisation at the new x: already enqueued behind the step
+      // (spec_lin_enqueue; its scalars are pending), else now
+      if (!ctx->lin_at_cand) linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, false, spec);
+      ctx->lin_at_cand = false;
+      if (spec) {
+        spec_ls = step_enqueue(ctx, radius, o);
+      } else if (ctx->pend_sum | ctx->pend_max) {
+        launch_reduce(ctx->W, ctx->pend_sum, ctx->pend_max, ctx->stream);
+        ctx->pend_sum = ctx->pend_max = 0;
+      }
+      ctx->publish_scalars();
+      if (spec) spec_lin_enqueue(ctx, o);
+      ctx->wait_scalars();
       L = lin_result(ctx);
       have_step = spec;
       ctx->t_lin += now_s() - tl;
@@ -1420,17 +1471,33 @@ int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double ra
     if (!ctx->scale_valid) linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
     double rj_total = 0.0;
     long ls_total = 0;
+    static const bool spec_on = [] { const char* e = std::getenv("BA_SPEC_LIN"); return !(e && e[0] == '0'); }();
+    const bool spec = spec_on && !ctx->coll();
+    const bool trj = ms_rj_kernel != nullptr;   // event pair around the r+J kernel
     HIP_OK(hipEventRecord(ctx->ev[0], ctx->stream));
+    ctx->rj_slot = 0;
+    if (spec) linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, trj, true);
     for (int i = 0; i < iters; ++i) {
-      // the solver's steady state after an accepted step: linearisation and
-      // the (speculative) next step enqueued back to back, one host read
-      linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, true, true);
+      // the solver's steady state after an accepted step: the step, its
+      // scalar record, and the next linearisation (spec_lin_enqueue) behind
+      // it while the host reads the record; K linearisations and K steps
+      // (BA_SPEC_LIN=0: linearisation + step, then the read)
+      const int slot = ctx->rj_slot;
+      if (!spec) linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, trj, true);
       const int ls = step_enqueue(ctx, radius, o);
-      ctx->read_scalars();
+      ctx->publish_scalars();
+      if (spec && i + 1 < iters) {
+        ctx->rj_slot ^= 1;
+        linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, trj, true);
+      }
+      ctx->wait_scalars();
       const StepResult st = step_result(ctx, ls);
-      float rj = 0.0f;
-      HIP_OK(hipEventElapsedTime(&rj, ctx->ev[2], ctx->ev[3]));
-      rj_total += rj;
+      if (trj) {
+        float rj = 0.0f;
+        HIP_OK(hipEventSynchronize(ctx->ev[3 + 2 * slot]));
+        HIP_OK(hipEventElapsedTime(&rj, ctx->ev[2 + 2 * slot], ctx->ev[3 + 2 * slot]));
+        rj_total += rj;
+      }
       ls_total += st.ls_iters;
     }
     HIP_OK(hipEventRecord(ctx->ev[1], ctx->stream));

@@ -245,19 +245,22 @@ class Solver:
         self._check(self.lib.ba_synchronize(self.h), "ba_synchronize")
 
     def bench_iterations(self, iters: int, radius: float = 1e4, options: Options | None = None,
-                         with_linear_iters: bool = False):
+                         with_linear_iters: bool = False, time_rj: bool = True):
         """Device time of `iters` LM iterations at a fixed radius: returns
         (ms per iteration, ms of the residual+Jacobian kernel[, mean linear
-        solver iterations per LM iteration])."""
+        solver iterations per LM iteration]).  time_rj=False: no event pair
+        around the residual+Jacobian kernel (its ms is then None)."""
         ms = C.c_double()
         rj = C.c_double()
         li = C.c_double()
         o = (options or Options()).to_c()
         self._check(self.lib.ba_bench_iterations(self.h, C.byref(o), int(iters), float(radius), C.byref(ms),
-                                                 C.byref(rj), C.byref(li)), "ba_bench_iterations")
+                                                 C.byref(rj) if time_rj else None, C.byref(li)),
+                    "ba_bench_iterations")
+        r = rj.value if time_rj else None
         if with_linear_iters:
-            return ms.value, rj.value, li.value
-        return ms.value, rj.value
+            return ms.value, r, li.value
+        return ms.value, r
 
     def stream_copy(self, nbytes: int = 1 << 30, reps: int = 10) -> float:
         """Measured device copy bandwidth in GB/s (read + write bytes), the

@@ -282,7 +282,9 @@ int ba_synchronize(ba_ctx* ctx);
  * bookkeeping).  Runs `iters` iterations on the context's stream and returns
  * the device-measured (HIP events) average milliseconds of the whole
  * iteration and of the residual+Jacobian kernel alone, and the mean number
- * of linear-solver iterations per LM iteration (may be NULL). */
+ * of linear-solver iterations per LM iteration (may be NULL).  ms_rj_kernel
+ * NULL: no event pair around the kernel (each pair's packets idle the device
+ * ~5 us per iteration; bench.py times the kernel in a second pass). */
 int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double radius, double* ms_per_iter,
                         double* ms_rj_kernel, double* linear_iters);
 
