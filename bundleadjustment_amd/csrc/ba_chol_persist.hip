@@ -166,14 +166,16 @@ struct PersistArgs {
 
 constexpr unsigned kRowSpin = 1u << 18;   // polls (s_sleep 32): ~0.4 s, far beyond the pair pass (~0.2 ms)
 
-// Rows [r0, r1] of A complete: lanes of wave 0 poll the cameras' counters
-// (relaxed agent loads), plus the cameras either side (a 128-B line may
-// straddle two rows), then wave 0 acquires and the barrier releases the
-// workgroup (MI355X_MICROARCH.md, "Consumer, always": poll -> agent acquire
-// -> vmcnt(0) -> barrier; the producer stores every byte sc1 and adds after
-// its wave's vmcnt(0), k_schur_pairs_c).  The rhs row n is written before the
-// launch.  Returns false in wave 0 if the bound was hit.
-__device__ inline bool wait_rows(const PersistArgs& a, int r0, int r1) {
+// Columns [r0, r1] of A's lower triangle complete (every off-diagonal camera
+// block (I, J) with J a camera of those columns: k_schur_pairs_c counts per
+// column camera): lanes of wave 0 poll the cameras' counters (relaxed agent
+// loads), plus the cameras either side (a 128-B line may straddle two
+// cameras), then wave 0 acquires and the barrier releases the workgroup
+// (MI355X_MICROARCH.md, "Consumer, always": poll -> agent acquire ->
+// vmcnt(0) -> barrier; the producer stores every byte sc1 and adds after its
+// wave's vmcnt(0)).  The diagonal blocks and the rhs row n are written before
+// the launch.  Returns false in wave 0 if the bound was hit.
+__device__ inline bool wait_cols(const PersistArgs& a, int r0, int r1) {
   bool ok = true;
   if (!a.rowcnt) return ok;
   r1 = min(r1, a.n - 1);
@@ -354,9 +356,9 @@ __device__ __forceinline__ void chol_persist_body(const PersistArgs& a) {
         for (int j = ctid(); j < bp; j += 256) a.L[(size_t)(sp + bp) * ld + sp + j] = S0[bp][j];
       bad |= cw.bad != 0;
     };
-    // (overlapped step) tile rows 0 and 1: read from A by this workgroup
+    // (overlapped step) tile columns 0 and 1: read from A by this workgroup
     // (A_00, A_10, A_11: no workers); the other tiles reach it through theirs
-    bad |= !wait_rows(a, 0, 2 * CB - 1);
+    bad |= !wait_cols(a, 0, 2 * CB - 1);
     for (int c = 0; c < T; ++c) {
       const int s = c * CB;
       const int b = min(CB, n - s);
@@ -459,10 +461,12 @@ __device__ __forceinline__ void chol_persist_body(const PersistArgs& a) {
   const bool diag = I == J;
   const int r0 = I * CB, c0 = J * CB;
   const int mI = min(CB, nrows - r0);
-  // (overlapped step) the tile rows this worker reads from A: its own (I)
-  // and the panel tile row J of update 0
-  if (!diag) bad |= !wait_rows(a, c0, c0 + CB - 1);
-  bad |= !wait_rows(a, r0, r0 + CB - 1);
+  // (overlapped step) the tile columns this worker reads from A: its own
+  // tile's (J) and the panel tiles A_{I,0}, A_{J,0} of update 0 (column 0);
+  // the later panels are published tiles.  The columns complete in order, so
+  // a tile whose column arrives late finds its earlier panels already final
+  bad |= !wait_cols(a, 0, CB - 1);
+  bad |= !wait_cols(a, c0, c0 + CB - 1);
   // the tile in the MFMA accumulator layout (acc_pos), initial values from
   // before the launch (plain loads, clamped)
   double own[2][2][4];

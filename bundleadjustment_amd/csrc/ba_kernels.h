@@ -182,6 +182,9 @@ void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, 
 // Fold the partials of `slots` (bitmask) into d_scal; kernels producing
 // partials always use grid = nblocks_of(...)
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s);
+// the same, then (last workgroup) the scalar record to the host as launch_publish_scalars
+void launch_reduce_publish(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, double* host, int n,
+                           unsigned* host_seq, unsigned seq, unsigned* ticket, hipStream_t s);
 int back_flow_capacity(int device);
 bool point_step_fused();                      // J-free back substitution fused with the candidate (BA_PSTEP)
 bool chol_persist_fits(int device, int n);   // every workgroup of k_chol_persist resident at once

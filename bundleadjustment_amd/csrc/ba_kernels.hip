@@ -1678,11 +1678,16 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
 //
 // SIGNAL (the overlapped step: the persistent factorisation runs beside this
 // pass and reads a camera row of S once it is complete, ba_chol_persist.hip
-// wait_rows): every S entry is stored write-through (sc1), each wave drains
-// its stores (vmcnt(0)) and one lane per block then adds 1 to the row
+// wait_cols): every S entry is stored write-through (sc1), each wave drains
+// its stores (vmcnt(0)) and one lane per block then adds 1 to the COLUMN
 // camera's counter (relaxed agent atomic; MI355X_MICROARCH.md "Valid forms":
-// the consumer acquires).  The XCD ranges xoff interleave the camera rows
-// (row a on XCD a mod 8, ascending), so rows complete in order over time.
+// the consumer acquires).  The XCD ranges xoff interleave the camera columns
+// (column b on XCD b mod 8, ascending), so the columns of S complete in
+// order over time: a left-looking factorisation consumes them in that order
+// (a late column's tiles then catch up on panels already published, where
+// late ROWS each had to run their whole chain of updates after arriving).
+// The column camera's records are then the L2-resident ones, so the row
+// camera's record is the one fetched a pair ahead.
 template <bool SIGNAL>
 __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4* __restrict__ blocks,
                                                        const int* __restrict__ xoff, const int2* __restrict__ pairs,
@@ -1715,9 +1720,12 @@ __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4*
     int e = blk.z + sl;
     WcRaw nb;                 // the partner (cold) record one pair ahead
     int2 pr = make_int2(0, 0);
+    // (SIGNAL: column-ordered pass, the row camera's record is the cold one)
+    auto cold = [](int2 q) { return SIGNAL ? q.x : q.y; };
+    auto hot = [](int2 q) { return SIGNAL ? q.y : q.x; };
     if (e < blk.w) {
       pr = pairs[e];
-      nb = wc_fetch(Wc, pr.y);
+      nb = wc_fetch(Wc, cold(pr));
     }
 #if BA_PAIRS_IDX2
     // the pair indices two pairs ahead: the next partner's fetch then waits
@@ -1726,16 +1734,18 @@ __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4*
     if (e + PL < blk.w) pn = pairs[e + PL];
 #endif
     for (; e < blk.w; e += PL) {
-      const WcRaw wa = wc_fetch(Wc, pr.x);   // row camera I: re-read from L2 by its blocks
-      const WcRaw wb = nb;
+      const WcRaw wh = wc_fetch(Wc, hot(pr));   // re-read from L2 by the camera's blocks
+      const WcRaw wc = nb;
+      const WcRaw& wa = SIGNAL ? wc : wh;   // row camera I's record
+      const WcRaw& wb = SIGNAL ? wh : wc;   // column camera J's
       if (e + PL < blk.w) {
 #if BA_PAIRS_IDX2
         pr = pn;
-        nb = wc_fetch(Wc, pr.y);
+        nb = wc_fetch(Wc, cold(pr));
         if (e + 2 * PL < blk.w) pn = pairs[e + 2 * PL];
 #else
         pr = pairs[e + PL];
-        nb = wc_fetch(Wc, pr.y);
+        nb = wc_fetch(Wc, cold(pr));
 #endif
       }
       double ca0[6], ca1[6], cb0[6], cb1[6];
@@ -1788,10 +1798,10 @@ __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4*
     if (SIGNAL) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores (every lane) have left
       if (live && sl == 0) {
-        const unsigned c = __hip_atomic_fetch_add(rowcnt + (size_t)blk.x * kRowCntStride, 1u, __ATOMIC_RELAXED,
+        const unsigned c = __hip_atomic_fetch_add(rowcnt + (size_t)blk.y * kRowCntStride, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
-        // diagnostics (BA_OVERLAP_TRACE): the time of each row's last block
-        if (trace && blk.x < 256) __hip_atomic_fetch_max(trace + blk.x, __builtin_amdgcn_s_memrealtime() | 0ull,
+        // diagnostics (BA_OVERLAP_TRACE): the time of each column's last block
+        if (trace && blk.y < 256) __hip_atomic_fetch_max(trace + blk.y, __builtin_amdgcn_s_memrealtime() | 0ull,
                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         (void)c;
       }
@@ -1935,11 +1945,22 @@ __global__ __launch_bounds__(256) void k_residuals(DevProblem P, const double* _
 // fixed strided subset, then a fixed-order shuffle tree.
 // one 64-lane workgroup per slot (the slots' 16-KB folds run on separate
 // CUs; as waves of one workgroup they all went through one CU)
-__global__ __launch_bounds__(64) void k_reduce(double* __restrict__ part, double* __restrict__ scal,
-                                               uint32_t sum_mask, uint32_t max_mask) {
-  const int slot = blockIdx.x, lane = threadIdx.x & 63;
-  const bool is_sum = (sum_mask >> slot) & 1u, is_max = (max_mask >> slot) & 1u;
-  if (!is_sum && !is_max) return;
+//
+// PUB (the scalar record of ba_ctx::publish_scalars folded into the same
+// launch): every workgroup then takes a ticket after its slot (agent-scope
+// release fence first), and the last one acquires and does what
+// k_publish_scalars does: the record into the pinned host-mapped copy,
+// system-scope release, then the sequence number.  The ticket is reset by
+// that workgroup for the next launch (stream order).
+struct ReducePub {
+  double* host = nullptr;
+  int n = 0;
+  unsigned* host_seq = nullptr;
+  unsigned seq = 0;
+  unsigned* ticket = nullptr;
+};
+__device__ __forceinline__ void reduce_slot(double* __restrict__ part, double* __restrict__ scal, int slot, int lane,
+                                            bool is_max) {
   double* pp = part + (size_t)slot * kMaxBlocks;
   constexpr int PER = kMaxBlocks / 64;
   double v[PER];
@@ -1958,6 +1979,25 @@ __global__ __launch_bounds__(64) void k_reduce(double* __restrict__ part, double
     x = wave_sum(x);
   }
   if (lane == 0) scal[slot] = x;
+}
+template <bool PUB>
+__global__ __launch_bounds__(64) void k_reduce(double* __restrict__ part, double* __restrict__ scal,
+                                               uint32_t sum_mask, uint32_t max_mask, ReducePub pub) {
+  const int slot = blockIdx.x, lane = threadIdx.x & 63;
+  const bool is_sum = (sum_mask >> slot) & 1u, is_max = (max_mask >> slot) & 1u;
+  if (is_sum || is_max) reduce_slot(part, scal, slot, lane, is_max);
+  if (!PUB) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this slot before the ticket
+  unsigned t = 0;
+  if (lane == 0) t = __hip_atomic_fetch_add(pub.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __builtin_amdgcn_readfirstlane(t);
+  if (t != gridDim.x - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every slot after it
+  for (int i = lane; i < pub.n; i += 64) pub.host[i] = scal[i];
+  if (lane == 0) *pub.ticket = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the record reaches host memory first
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_store(pub.host_seq, pub.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
@@ -3019,7 +3059,13 @@ void launch_stream_copy(const double* a, double* b, size_t n2, hipStream_t s) {
                      reinterpret_cast<double2*>(b), n2);
 }
 void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce, dim3(kNumSlots), dim3(64), 0, s, W.part, W.scal, sum_mask, max_mask);
+  hipLaunchKernelGGL(k_reduce<false>, dim3(kNumSlots), dim3(64), 0, s, W.part, W.scal, sum_mask, max_mask,
+                     ReducePub{});
+}
+void launch_reduce_publish(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, double* host, int n,
+                           unsigned* host_seq, unsigned seq, unsigned* ticket, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce<true>, dim3(kNumSlots), dim3(64), 0, s, W.part, W.scal, sum_mask, max_mask,
+                     ReducePub{host, n, host_seq, seq, ticket});
 }
 void launch_residuals(const DevProblem& P, const double* rec, const double* pts, double* r_raw, hipStream_t s) {
   hipLaunchKernelGGL(k_residuals, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, rec, pts, r_raw);

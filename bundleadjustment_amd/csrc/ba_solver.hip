@@ -99,6 +99,7 @@ struct ba_ctx {
   double* d_hscal = nullptr;     // its device address
   unsigned* h_seq = nullptr;     // the record's sequence number (after the record), host / device address
   unsigned* d_hseq = nullptr;
+  unsigned* d_ticket = nullptr;  // k_reduce<true>'s last-workgroup ticket (zero between launches)
   unsigned scal_seq = 0;
   char* pose_buf = nullptr;      // ba_solve_pose_batch device staging (grown on demand)
   size_t pose_cap = 0;
@@ -213,11 +214,24 @@ struct ba_ctx {
   void publish_scalars() {
     const size_t cnt = kNumSlots + kPcgState;
     if (!scal_spin()) {
+      if (pend_sum | pend_max) bahip::launch_reduce(W, pend_sum, pend_max, stream);
+      pend_sum = pend_max = 0;
       HIP_OK(hipMemcpyAsync(h_scal, W.scal, sizeof(double) * cnt, hipMemcpyDeviceToHost, stream));
       HIP_OK(hipEventRecord(ev[6], stream));
       return;
     }
-    bahip::launch_publish_scalars(W.scal, d_hscal, (int)cnt, d_hseq, ++scal_seq, stream);
+    // scalars still to be folded (pend_*: the step's and the deferred
+    // linearisation's, single rank): one launch folds and publishes them
+    // (BA_REDUCE_PUB=0: a separate fold launch before the publish, A/B)
+    static const bool fused = [] { const char* e = std::getenv("BA_REDUCE_PUB"); return !(e && e[0] == '0'); }();
+    if ((pend_sum | pend_max) && d_ticket && fused) {
+      bahip::launch_reduce_publish(W, pend_sum, pend_max, d_hscal, (int)cnt, d_hseq, ++scal_seq, d_ticket, stream);
+      pend_sum = pend_max = 0;
+    } else {
+      if (pend_sum | pend_max) bahip::launch_reduce(W, pend_sum, pend_max, stream);
+      pend_sum = pend_max = 0;
+      bahip::launch_publish_scalars(W.scal, d_hscal, (int)cnt, d_hseq, ++scal_seq, stream);
+    }
     HIP_OK(hipGetLastError());
   }
   void wait_scalars() {
@@ -521,26 +535,28 @@ void ensure_dense(ba_ctx* ctx) {
     if (W.overlap == 1 && !ctx->split_ok) W.overlap = 0;
   }
   // k_schur_pairs*: XCD x sweeps the blocks [xoff[x], xoff[x+1]).  Overlapped
-  // step: camera rows interleaved over the XCDs (row I on XCD I mod 8,
-  // ascending), so the rows of S complete in order over the pass, which the
-  // factorisation waits on row by row (rowexp: blocks per row); else equal
-  // contiguous ranges (bands of rows: C3 165 vs 188 us for the interleave)
+  // step: camera COLUMNS interleaved over the XCDs (column J on XCD J mod 8,
+  // ascending), so the block columns of S complete in order over the pass,
+  // which the factorisation waits on column by column (rowexp: blocks per
+  // column camera); else equal contiguous ranges of the row-major list
+  // (bands of rows: C3 165 vs 188 us for an interleave).
   // The overlapped step launches the pass in two parts: the head (the camera
-  // rows of the first two tile rows, which the critical workgroup needs
-  // first: on the otherwise idle chip they complete in ~15 us instead of
-  // with the pass's first round of waves, ~65 us), then the tail.
+  // columns of the first two tile columns, which the critical workgroup
+  // needs first), then the tail.
   std::vector<int> xoff(18, 0);
   std::vector<unsigned> rowexp((size_t)std::max(nvc, 1), 0u);
-  for (const int4& b : blocks) rowexp[b.x]++;
+  for (const int4& b : blocks) rowexp[W.overlap ? b.y : b.x]++;
   W.xmax[0] = W.xmax[1] = 0;
   if (W.overlap) {
-    const int vh = std::min(nvc - 1, (2 * 64 - 1) / 6 + 1);   // (+1: wait_rows' margin camera)
+    const int vh = std::min(nvc - 1, (2 * 64 - 1) / 6 + 1);   // (+1: wait_cols' margin camera)
+    std::vector<int4> bycol(blocks);
+    std::stable_sort(bycol.begin(), bycol.end(), [](const int4& p, const int4& q) { return p.y < q.y; });
     std::vector<int4> ord;
     ord.reserve(blocks.size());
     for (int h = 0; h < 2; ++h) {
       for (int x = 0; x < 8; ++x) {
         xoff[9 * h + x] = (int)ord.size();
-        for (const int4& b : blocks) if (b.x % 8 == x && (b.x <= vh) == (h == 0)) ord.push_back(b);
+        for (const int4& b : bycol) if (b.y % 8 == x && (b.y <= vh) == (h == 0)) ord.push_back(b);
       }
       xoff[9 * h + 8] = (int)ord.size();
       for (int x = 0; x < 8; ++x) W.xmax[h] = std::max(W.xmax[h], xoff[9 * h + x + 1] - xoff[9 * h + x]);
@@ -690,6 +706,10 @@ LinResult lin_result(ba_ctx* ctx) {
 }
 
 LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max_diag) {
+  // a fresh start (solve / bench entry): folds still pending belong to work
+  // an earlier call abandoned (e.g. the speculative linearisation behind a
+  // solve's last step) and must not be folded into this record
+  ctx->pend_sum = ctx->pend_max = 0;
   linearize_enqueue(ctx, compute_scale, min_diag, max_diag);
   ctx->read_scalars();
   return lin_result(ctx);
@@ -867,8 +887,15 @@ int step_enqueue(ba_ctx* ctx, double radius, const ba_options& o) {
   else reduced_solve_dense(ctx, radius);
   launch_cam_candidate(P, W, s);
   launch_backsub_candidate(P, W, s);
-  launch_reduce(W, bit(SL_MCC_NEG) | bit(SL_CCOST) | bit(SL_STEP2_P) | bit(SL_CAND_BAD) | bit(SL_STEP_BAD) |
-                       bit(SL_STEP2_C) | (ctx->coll() ? 0u : bit(SL_ELIM_BAD)) | ctx->pend_sum, ctx->pend_max, s);
+  const uint32_t step_sum = bit(SL_MCC_NEG) | bit(SL_CCOST) | bit(SL_STEP2_P) | bit(SL_CAND_BAD) | bit(SL_STEP_BAD) |
+                            bit(SL_STEP2_C) | (ctx->coll() ? 0u : bit(SL_ELIM_BAD));
+  if (!ctx->coll()) {
+    // folded by the scalar record's publish that follows every step
+    // (ba_ctx::publish_scalars: one launch for the fold and the record)
+    ctx->pend_sum |= step_sum;
+    return ls_iters;
+  }
+  launch_reduce(W, step_sum | ctx->pend_sum, ctx->pend_max, s);
   ctx->pend_sum = ctx->pend_max = 0;
   if (ctx->coll()) {
     ctx->allreduce(W.scal + SL_MCC_NEG, 5);  // MCC_NEG, CCOST, STEP2_P, CAND_BAD, STEP_BAD
@@ -1125,6 +1152,8 @@ int ba_create(ba_ctx** out, int device) {
       HIP_OK(hipHostGetDevicePointer(&d, ctx->h_scal, 0));
       ctx->d_hscal = static_cast<double*>(d);
       ctx->d_hseq = reinterpret_cast<unsigned*>(static_cast<char*>(d) + rec);
+      HIP_OK(hipMalloc(&ctx->d_ticket, 64));
+      HIP_OK(hipMemset(ctx->d_ticket, 0, 64));
     }
   } catch (const BaError& e) {
     std::fprintf(stderr, "ba_create: %s\n", e.msg.c_str());
@@ -1142,6 +1171,7 @@ int ba_destroy(ba_ctx* ctx) {
   if (ctx->comm) ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
   if (ctx->h_scal) (void)hipHostFree(ctx->h_scal);
+  if (ctx->d_ticket) (void)hipFree(ctx->d_ticket);
   if (ctx->pose_buf) (void)hipFree(ctx->pose_buf);
   if (ctx->hv_scratch) (void)hipFree(ctx->hv_scratch);
   if (ctx->evf) (void)hipEventDestroy(ctx->evf);
