@@ -499,7 +499,6 @@ __device__ __forceinline__ void chol_persist_body(const PersistArgs& a) {
   };
   if (kmax >= 0) stage_panels(0);
   for (int k = 0; k <= kmax; ++k) {
-    const int kc = k * CB, kb = min(CB, n - kc);
     bad |= !wait_flag(&vflag[k], a.epoch);
     if (stamp && k == kmax) WSTAMP(J, 0);
     tile_put(S2, tile_fetch_sc1(rV, CB, k * CB, 0, (k + 1) * CB, CB));          // V_k (stored cleaned)
