@@ -304,15 +304,7 @@ int chol_split_blocks() { return kCholSplitBlocks; }
 
 // the persistent form (ba_chol_persist.hip)
 void launch_chol_persist(double* A, double* L, int ld, int n, double* Vbuf, double* scal, unsigned* flags,
-                         unsigned epoch, hipStream_t s, const unsigned* rowcnt = nullptr,
-                         const unsigned* rowexp = nullptr, unsigned* checkin = nullptr, unsigned sgen = 0,
-                         int nvc = 0, unsigned long long* trace = nullptr);
-void launch_chol_persist2(double* A, double* L, int ld, int n, double* Vbuf, double* scal, unsigned* flags,
-                          unsigned epoch, hipStream_t s_crit, hipStream_t s_work, const unsigned* rowcnt = nullptr,
-                          const unsigned* rowexp = nullptr, unsigned* checkin = nullptr, unsigned sgen = 0,
-                          int nvc = 0, unsigned long long* trace = nullptr);
-void launch_gate(const unsigned* c, unsigned target, hipStream_t s);
-int chol_persist_grid(int n);
+                         unsigned epoch, hipStream_t s);
 
 void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hipStream_t s) {
   const int n = P.n;
@@ -338,25 +330,5 @@ void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hi
   hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.yg, epoch, W.scal);
 }
 
-void launch_chol_overlapped(const DevProblem& P, const DevWork& W, int epoch, unsigned sgen, hipStream_t s_chol,
-                            hipStream_t s_work) {
-  if (P.n == 0) return;
-  if (s_work)
-    launch_chol_persist2(W.S, W.Lf, P.ld, P.n, W.Vbuf, W.scal, W.cflags, (unsigned)epoch, s_chol, s_work, W.rowcnt,
-                         W.rowexp, W.checkin, sgen, P.nvc, W.trace);
-  else
-    launch_chol_persist(W.S, W.Lf, P.ld, P.n, W.Vbuf, W.scal, W.cflags, (unsigned)epoch, s_chol, W.rowcnt, W.rowexp,
-                        W.checkin, sgen, P.nvc, W.trace);
-}
-void launch_chol_gate(const DevProblem& P, const DevWork& W, unsigned sgen, hipStream_t s) {
-  if (P.n == 0) return;
-  launch_gate(W.checkin, sgen * (unsigned)chol_persist_grid(P.n), s);
-}
-void launch_back_flow(const DevProblem& P, const DevWork& W, int epoch, hipStream_t s) {
-  const int n = P.n;
-  if (n == 0) return;
-  const int T = (n + CB - 1) / CB;
-  hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.yg, epoch, W.scal);
-}
 
 }  // namespace bahip

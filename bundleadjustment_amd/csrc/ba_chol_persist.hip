@@ -150,57 +150,7 @@ struct PersistArgs {
   unsigned* flags;   // [T] V_c published | [TR][T] tile (I, J) published
   int ld, n, T, TR;
   unsigned epoch;
-  // overlapped step (ba_solver.hip reduced_solve_dense): A's off-diagonal
-  // camera blocks are still being written by k_schur_pairs_c when the
-  // factorisation starts.  rowcnt[v]: blocks of camera row v written so far
-  // (cumulative over formations), rowexp[v]: blocks per formation, sgen: the
-  // formations so far; checkin: +1 per workgroup at its start (the launch
-  // gate before the pair pass).  nullptr: A is complete at the launch
-  const unsigned* rowcnt = nullptr;
-  const unsigned* rowexp = nullptr;
-  unsigned* checkin = nullptr;
-  unsigned sgen = 0;
-  int nvc = 0;
-  unsigned long long* trace = nullptr;   // diagnostics (BA_OVERLAP_TRACE): [256 + c] step c starts, [300 + I] tile (I, I-1) published
 };
-
-constexpr unsigned kRowSpin = 1u << 18;   // polls (s_sleep 32): ~0.4 s, far beyond the pair pass (~0.2 ms)
-
-// Columns [r0, r1] of A's lower triangle complete (every off-diagonal camera
-// block (I, J) with J a camera of those columns: k_schur_pairs_c counts per
-// column camera): lanes of wave 0 poll the cameras' counters (relaxed agent
-// loads), plus the cameras either side (a 128-B line may straddle two
-// cameras), then wave 0 acquires and the barrier releases the workgroup
-// (MI355X_MICROARCH.md, "Consumer, always": poll -> agent acquire ->
-// vmcnt(0) -> barrier; the producer stores every byte sc1 and adds after its
-// wave's vmcnt(0)).  The diagonal blocks and the rhs row n are written before
-// the launch.  Returns false in wave 0 if the bound was hit.
-__device__ inline bool wait_cols(const PersistArgs& a, int r0, int r1) {
-  bool ok = true;
-  if (!a.rowcnt) return ok;
-  r1 = min(r1, a.n - 1);
-  if (r0 > r1) return ok;
-  const int v0 = max(0, r0 / 6 - 1), v1 = min(a.nvc - 1, r1 / 6 + 1);
-  if (threadIdx.x < 64) {
-    unsigned it = 0;
-    for (int vb = v0; vb <= v1 && ok; vb += 64) {
-      const int v = vb + (int)threadIdx.x;
-      const bool mine = v <= v1;
-      const unsigned target = mine ? a.sgen * a.rowexp[v] : 0u;
-      for (;;) {
-        const unsigned c = mine ? __hip_atomic_load(a.rowcnt + (size_t)v * kRowCntStride, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT) : 0u;
-        if (__all(c == target)) break;
-        if (++it >= kRowSpin) { ok = false; break; }
-        __builtin_amdgcn_s_sleep(32);   // ~0.9 us: 171 workers polling ~15 counters each
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  return ok;
-}
 
 // worker w (>= 1) -> its tile (I, J): tiles with J >= 1 and I >= J, in
 // column order, without the diagonal tile (1, 1) (no update reaches it
@@ -302,13 +252,8 @@ struct PanelPrefetch {
   }
 };
 
-// ROLE 0: the whole factorisation (block 0 critical, block w > 0 worker w);
-// 1: the critical workgroup alone (grid 1); 2: the workers alone (block b is
-// worker b + 1).  The split forms run as two concurrent launches (the
-// overlapped DENSE_SCHUR step, ba_solver.hip): the workers then carry their
-// own register allocation instead of the critical workgroup's
-template <int ROLE>
-__device__ __forceinline__ void chol_persist_body(const PersistArgs& a) {
+// block 0: the critical workgroup, block w > 0: worker w
+__global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   __shared__ double S0[CB][LDP];
   __shared__ double S1[CB][LDP];
   __shared__ double S2[CB][LDP];
@@ -323,12 +268,8 @@ __device__ __forceinline__ void chol_persist_body(const PersistArgs& a) {
   unsigned* vflag = a.flags;
   unsigned* tflag = a.flags + T;
   bool bad = false;
-  if (a.checkin && threadIdx.x == 0) __hip_atomic_fetch_add(a.checkin, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // (overlapped step) the factorisation's waves issue ahead of the pair
-  // pass's on a shared SIMD: its chain is latency-bound, the pass is not
-  if (a.rowcnt) __builtin_amdgcn_s_setprio(3);
 
-  if (ROLE == 1 || (ROLE == 0 && blockIdx.x == 0)) {
+  if (blockIdx.x == 0) {
     // ---------------- critical workgroup: the diagonal chain
     if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
     // the end of step cp: V_cp cleaned in place (zero above the diagonal,
@@ -356,14 +297,10 @@ __device__ __forceinline__ void chol_persist_body(const PersistArgs& a) {
         for (int j = ctid(); j < bp; j += 256) a.L[(size_t)(sp + bp) * ld + sp + j] = S0[bp][j];
       bad |= cw.bad != 0;
     };
-    // (overlapped step) tile columns 0 and 1: read from A by this workgroup
-    // (A_00, A_10, A_11: no workers); the other tiles reach it through theirs
-    bad |= !wait_cols(a, 0, 2 * CB - 1);
     for (int c = 0; c < T; ++c) {
       const int s = c * CB;
       const int b = min(CB, n - s);
       const int m = min(CB, nrows - s);
-      if (a.trace && threadIdx.x == 0 && c < 40) a.trace[256 + c] = __builtin_amdgcn_s_memrealtime();
       bool have_diag = false;
       TileRegs tD;
       if (c > 0) {
@@ -457,16 +394,10 @@ __device__ __forceinline__ void chol_persist_body(const PersistArgs& a) {
 
   // ---------------- worker: one lower tile (I, J), J >= 1
   int I, J;
-  if (!worker_tile(ROLE == 2 ? blockIdx.x + 1 : blockIdx.x, T, a.TR, I, J)) return;
+  if (!worker_tile(blockIdx.x, T, a.TR, I, J)) return;
   const bool diag = I == J;
   const int r0 = I * CB, c0 = J * CB;
   const int mI = min(CB, nrows - r0);
-  // (overlapped step) the tile columns this worker reads from A: its own
-  // tile's (J) and the panel tiles A_{I,0}, A_{J,0} of update 0 (column 0);
-  // the later panels are published tiles.  The columns complete in order, so
-  // a tile whose column arrives late finds its earlier panels already final
-  bad |= !wait_cols(a, 0, CB - 1);
-  bad |= !wait_cols(a, c0, c0 + CB - 1);
   // the tile in the MFMA accumulator layout (acc_pos), initial values from
   // before the launch (plain loads, clamped)
   double own[2][2][4];
@@ -559,7 +490,6 @@ __device__ __forceinline__ void chol_persist_body(const PersistArgs& a) {
   }
   publish(&tflag[I * T + J], a.epoch);
   if (stamp) WSTAMP(J, 4);
-  if (a.trace && threadIdx.x == 0 && I == J + 1 && I < 40) a.trace[300 + I] = __builtin_amdgcn_s_memrealtime();
   // L_{I,J-1} (the last update of an off-diagonal tile: J == k + 1) to the
   // factor, after the publish: no in-kernel reader, and its drain would
   // otherwise sit in the barriers before the tile's hand-off
@@ -570,10 +500,6 @@ __device__ __forceinline__ void chol_persist_body(const PersistArgs& a) {
   if (I == J + 1) lds_to_global(S1, a.L, ld, c0, kmax * CB, CB, min(CB, n - kmax * CB));
   if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
 }
-
-__global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) { chol_persist_body<0>(a); }
-__global__ __launch_bounds__(256) void k_chol_crit(PersistArgs a) { chol_persist_body<1>(a); }
-__global__ __launch_bounds__(256) void k_chol_work(PersistArgs a) { chol_persist_body<2>(a); }
 
 // grid of the persistent factorisation: 1 critical + one worker per tile
 int chol_persist_grid(int n) {
@@ -594,78 +520,14 @@ bool chol_persist_fits(int device, int n) {
 }
 
 void launch_chol_persist(double* A, double* L, int ld, int n, double* Vbuf, double* scal, unsigned* flags,
-                         unsigned epoch, hipStream_t s, const unsigned* rowcnt, const unsigned* rowexp,
-                         unsigned* checkin, unsigned sgen, int nvc, unsigned long long* trace) {
+                         unsigned epoch, hipStream_t s) {
   PersistArgs a;
   a.A = A; a.L = L; a.Vbuf = Vbuf; a.scal = scal; a.flags = flags;
   a.ld = ld; a.n = n;
   a.T = (n + CB - 1) / CB;
   a.TR = (n + 1 + CB - 1) / CB;
   a.epoch = epoch;
-  a.rowcnt = rowcnt; a.rowexp = rowexp; a.checkin = checkin; a.sgen = sgen; a.nvc = nvc; a.trace = trace;
   hipLaunchKernelGGL(k_chol_persist, dim3(chol_persist_grid(n)), dim3(256), 0, s, a);
-}
-
-// the launch gate of the overlapped step: the pair pass (behind this on its
-// stream) starts once every workgroup of the factorisation is resident, so
-// that it fills only the CUs the factorisation leaves.  Bounded (~0.2 ms; the
-// factorisation checks in within a few us of its dispatch): a late
-// factorisation only delays itself, the pair pass never waits for it
-__global__ void k_gate(const unsigned* __restrict__ c, unsigned target) {
-  if (threadIdx.x != 0) return;
-  for (unsigned it = 0; it < 256u; ++it) {
-    if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == target) return;
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-void launch_gate(const unsigned* c, unsigned target, hipStream_t s) {
-  hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, s, c, target);
-}
-
-// the same factorisation as two concurrent launches: the critical workgroup
-// on s_crit, the workers on s_work (the caller orders both streams after the
-// writes of A and joins them afterwards).  Both grids must be resident at
-// once and the two streams must run concurrently (ba_solver.hip probes it)
-void launch_chol_persist2(double* A, double* L, int ld, int n, double* Vbuf, double* scal, unsigned* flags,
-                          unsigned epoch, hipStream_t s_crit, hipStream_t s_work, const unsigned* rowcnt,
-                          const unsigned* rowexp, unsigned* checkin, unsigned sgen, int nvc,
-                          unsigned long long* trace) {
-  PersistArgs a;
-  a.A = A; a.L = L; a.Vbuf = Vbuf; a.scal = scal; a.flags = flags;
-  a.ld = ld; a.n = n;
-  a.T = (n + CB - 1) / CB;
-  a.TR = (n + 1 + CB - 1) / CB;
-  a.epoch = epoch;
-  a.rowcnt = rowcnt; a.rowexp = rowexp; a.checkin = checkin; a.sgen = sgen; a.nvc = nvc; a.trace = trace;
-  const int nw = chol_persist_grid(n) - 1;
-  hipLaunchKernelGGL(k_chol_crit, dim3(1), dim3(256), 0, s_crit, a);
-  if (nw > 0) hipLaunchKernelGGL(k_chol_work, dim3(nw), dim3(256), 0, s_work, a);
-}
-
-// Do two streams run concurrently?  (Streams that share a hardware queue run
-// in submission order; the split factorisation's two launches wait on each
-// other and would spin to their bound.)  A waiter on `a`, submitted first,
-// polls a flag that a kernel on `b` sets; scratch: 2 words, device memory.
-__global__ void k_probe_wait(const unsigned* __restrict__ f, unsigned* __restrict__ res) {
-  if (threadIdx.x != 0) return;
-  unsigned ok = 0;
-  for (unsigned it = 0; it < (1u << 14) && !ok; ++it) {
-    ok = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
-    if (!ok) __builtin_amdgcn_s_sleep(8);
-  }
-  *res = ok;
-}
-__global__ void k_probe_set(unsigned* __restrict__ f) {
-  if (threadIdx.x == 0) __hip_atomic_store(f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-bool streams_concurrent(hipStream_t a, hipStream_t b, unsigned* scratch) {
-  unsigned h = 0;
-  if (hipMemset(scratch, 0, 2 * sizeof(unsigned)) != hipSuccess) return false;
-  hipLaunchKernelGGL(k_probe_wait, dim3(1), dim3(64), 0, a, scratch, scratch + 1);
-  hipLaunchKernelGGL(k_probe_set, dim3(1), dim3(64), 0, b, scratch);
-  if (hipStreamSynchronize(a) != hipSuccess || hipStreamSynchronize(b) != hipSuccess) return false;
-  if (hipMemcpy(&h, scratch + 1, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) return false;
-  return h == 1u;
 }
 
 }  // namespace bahip

@@ -52,10 +52,6 @@ struct DevProblem {
 };
 
 // Device workspace pointers (see ba_solver.hip for sizes).
-// one row counter per 64 B (the factorisation's polls and the pair pass's
-// adds spread over lines instead of hammering a few)
-constexpr int kRowCntStride = 16;
-
 struct DevWork {
   double* cams;  double* pts;        // x
   double* cams_c; double* pts_c;     // candidate x'
@@ -84,14 +80,8 @@ struct DevWork {
   unsigned* cflags;                  // [T + TR*T] persistent-Cholesky hand-off flags (epoch-tagged, zeroed once)
   bool chol_persist;                 // the factorisation runs as one persistent launch (ba_chol_persist.hip)
   const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}, camera rows interleaved over the XCDs
-  const int* xoff;                   // [18] k_schur_pairs* block range of XCD x: [xoff[x], xoff[x+1]); overlapped step: the head's, then [9 + x] the tail's
-  int xmax[2];                       // largest XCD range of the (head, tail) launch
-  // overlapped DENSE_SCHUR step (the factorisation runs beside k_schur_pairs_c)
-  unsigned* rowcnt;                  // [nvc][kRowCntStride] pair blocks of camera row v written (cumulative, zeroed once)
-  const unsigned* rowexp;            // [nvc] pair blocks of camera row v per formation
-  unsigned* checkin;                 // [1] factorisation workgroups started (cumulative, zeroed once)
-  unsigned long long* trace;         // diagnostics (BA_OVERLAP_TRACE): [0..255] row done, [256..] factorisation stamps (s_memrealtime)
-  int overlap;                       // use it (single rank, persistent factorisation, compact records); 2: serialised (diagnostics)
+  const int* xoff;                   // [9] k_schur_pairs* block range of XCD x: [xoff[x], xoff[x+1])
+  int xmax;                          // largest XCD range
   const int2* eblocks; int neblocks; // lower off-diagonal blocks {I, J} with no observation pair
   bool s_memset;                     // many empty blocks: memset S instead
   const int2* pairs;                 // observation pairs per block
@@ -142,26 +132,11 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
 // rank): add s Hcc s + D^2 and s g_c in the same pass (no launch_cam_add_diag)
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact = nullptr,
                            double radius = 0.0);
-// signal: count the written blocks per camera row (W.rowcnt, write-through
-// stores) for a factorisation running beside it
-// part: -1 every block (xoff[0..8]), 0 the head (the same ranges: the
-// overlapped step's first camera rows), 1 the tail (xoff[9..17])
-void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, bool signal = false, int part = -1);
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
 // ba_chol.hip; epoch: per-context launch counter (>= 1) tagging the
 // back substitution's hand-off flags
 void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hipStream_t s);
-// overlapped step: the persistent factorisation on s_chol (its off-diagonal
-// blocks still being written, W.rowcnt), the gate on s (the pair pass goes
-// behind it), then, once s has joined s_chol, the back substitution
-// s_work != nullptr: the split form, critical workgroup on s_chol, workers
-// on s_work (their own register allocation leaves room for the pair pass on
-// their CUs); the two streams must run concurrently (streams_concurrent)
-void launch_chol_overlapped(const DevProblem& P, const DevWork& W, int epoch, unsigned sgen, hipStream_t s_chol,
-                            hipStream_t s_work = nullptr);
-bool streams_concurrent(hipStream_t a, hipStream_t b, unsigned* scratch);
-void launch_chol_gate(const DevProblem& P, const DevWork& W, unsigned sgen, hipStream_t s);
-void launch_back_flow(const DevProblem& P, const DevWork& W, int epoch, hipStream_t s);
 // zero the lower Schur blocks no observation pair writes (the Cholesky
 // leaves its updates there)
 void launch_zero_blocks(const DevProblem& P, const DevWork& W, hipStream_t s);

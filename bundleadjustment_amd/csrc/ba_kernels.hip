@@ -1675,31 +1675,14 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
 // (Measured and not kept: the row camera's record one pair ahead as well,
 // with the camera constants re-read from LDS per pair to keep 2 waves per
 // SIMD: 168 vs 165 us, profiles/r03_v13_ab_pairs_ca.txt.)
-//
-// SIGNAL (the overlapped step: the persistent factorisation runs beside this
-// pass and reads a camera row of S once it is complete, ba_chol_persist.hip
-// wait_cols): every S entry is stored write-through (sc1), each wave drains
-// its stores (vmcnt(0)) and one lane per block then adds 1 to the COLUMN
-// camera's counter (relaxed agent atomic; MI355X_MICROARCH.md "Valid forms":
-// the consumer acquires).  The XCD ranges xoff interleave the camera columns
-// (column b on XCD b mod 8, ascending), so the columns of S complete in
-// order over time: a left-looking factorisation consumes them in that order
-// (a late column's tiles then catch up on panels already published, where
-// late ROWS each had to run their whole chain of updates after arriving).
-// The column camera's records are then the L2-resident ones, so the row
-// camera's record is the one fetched a pair ahead.
-template <bool SIGNAL>
+
 __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4* __restrict__ blocks,
                                                        const int* __restrict__ xoff, const int2* __restrict__ pairs,
                                                        const double* __restrict__ Wc,
-                                                       const double* __restrict__ scale_c, double* __restrict__ S,
-                                                       unsigned* __restrict__ rowcnt,
-                                                       unsigned long long* __restrict__ trace) {
+                                                       const double* __restrict__ scale_c, double* __restrict__ S) {
   // the camera constants of every variable camera in LDS (nvc <= 200 in the
   // J-free mode: 14.4 KB), read per pair (registers: 1 -> 2 waves per SIMD)
   __shared__ WcCam ctab[kLinLdsCams];
-  if (SIGNAL && trace && blockIdx.x == 0 && threadIdx.x == 0)   // (the first launch of the step)
-    atomicCAS(trace + 255, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
   for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
   __syncthreads();
   constexpr int PL = kPairLanes, BPW = 64 / PL;
@@ -1718,14 +1701,11 @@ __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4*
 #pragma unroll
     for (int k = 0; k < 36; ++k) acc[k] = 0.0;
     int e = blk.z + sl;
-    WcRaw nb;                 // the partner (cold) record one pair ahead
+    WcRaw nb;                 // the partner record one pair ahead
     int2 pr = make_int2(0, 0);
-    // (SIGNAL: column-ordered pass, the row camera's record is the cold one)
-    auto cold = [](int2 q) { return SIGNAL ? q.x : q.y; };
-    auto hot = [](int2 q) { return SIGNAL ? q.y : q.x; };
     if (e < blk.w) {
       pr = pairs[e];
-      nb = wc_fetch(Wc, cold(pr));
+      nb = wc_fetch(Wc, pr.y);
     }
 #if BA_PAIRS_IDX2
     // the pair indices two pairs ahead: the next partner's fetch then waits
@@ -1734,18 +1714,16 @@ __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4*
     if (e + PL < blk.w) pn = pairs[e + PL];
 #endif
     for (; e < blk.w; e += PL) {
-      const WcRaw wh = wc_fetch(Wc, hot(pr));   // re-read from L2 by the camera's blocks
-      const WcRaw wc = nb;
-      const WcRaw& wa = SIGNAL ? wc : wh;   // row camera I's record
-      const WcRaw& wb = SIGNAL ? wh : wc;   // column camera J's
+      const WcRaw wa = wc_fetch(Wc, pr.x);   // row camera I's record: re-read from L2 by the camera's blocks
+      const WcRaw wb = nb;                    // column camera J's
       if (e + PL < blk.w) {
 #if BA_PAIRS_IDX2
         pr = pn;
-        nb = wc_fetch(Wc, cold(pr));
+        nb = wc_fetch(Wc, pr.y);
         if (e + 2 * PL < blk.w) pn = pairs[e + 2 * PL];
 #else
         pr = pairs[e + PL];
-        nb = wc_fetch(Wc, cold(pr));
+        nb = wc_fetch(Wc, pr.y);
 #endif
       }
       double ca0[6], ca1[6], cb0[6], cb1[6];
@@ -1783,27 +1761,8 @@ __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4*
       for (int k = 0; k < 36; ++k) {
         if ((k % PL) != sl) continue;
         const int i = k / 6, j = k % 6;
-        if (I != Jb) {
-          double* d = S + (size_t)(6 * I + i) * ld + 6 * Jb + j;
-          if (SIGNAL)
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(d), __builtin_bit_cast(unsigned long long, -acc[k]),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else
-            *d = -acc[k];
-        } else if (j <= i) {
-          S[(size_t)(6 * I + i) * ld + 6 * I + j] -= acc[k];  // duplicate obs of one point by one camera (never SIGNAL)
-        }
-      }
-    }
-    if (SIGNAL) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores (every lane) have left
-      if (live && sl == 0) {
-        const unsigned c = __hip_atomic_fetch_add(rowcnt + (size_t)blk.y * kRowCntStride, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        // diagnostics (BA_OVERLAP_TRACE): the time of each column's last block
-        if (trace && blk.y < 256) __hip_atomic_fetch_max(trace + blk.y, __builtin_amdgcn_s_memrealtime() | 0ull,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        (void)c;
+        if (I != Jb) S[(size_t)(6 * I + i) * ld + 6 * Jb + j] = -acc[k];
+        else if (j <= i) S[(size_t)(6 * I + i) * ld + 6 * I + j] -= acc[k];  // duplicate obs of one point by one camera
       }
     }
   }
@@ -2922,7 +2881,7 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
                      compact ? 2 : 1, W.Hcc,
                      W.gc, compact ? compact : W.S);
 }
-void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, bool signal, int part) {
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (W.nblocks == 0) return;
   static int grid_cap = 0;
   if (grid_cap == 0) {
@@ -2931,17 +2890,13 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, bo
     if (grid_cap < 8) grid_cap = 8;
   }
   // 16 blocks per workgroup (4 waves of 4) over the largest XCD range
-  const int* xoff = W.xoff + (part == 1 ? 9 : 0);
-  int grid = 8 * ((W.xmax[part == 1 ? 1 : 0] + 15) / 16);
+  const int* xoff = W.xoff;
+  int grid = 8 * ((W.xmax + 15) / 16);
   if (grid == 0) return;
   if (grid > grid_cap) grid = grid_cap;
   grid = (grid + 7) / 8 * 8;   // k_schur_pairs' XCD ranges need a multiple of 8
-  if (W.wcompact && signal)
-    hipLaunchKernelGGL(k_schur_pairs_c<true>, dim3(grid), dim3(256), 0, s, P, W.blocks, xoff, W.pairs, W.W,
-                       W.scale_c, W.S, W.rowcnt, W.trace);
-  else if (W.wcompact)
-    hipLaunchKernelGGL(k_schur_pairs_c<false>, dim3(grid), dim3(256), 0, s, P, W.blocks, xoff, W.pairs, W.W,
-                       W.scale_c, W.S, nullptr, nullptr);
+  if (W.wcompact)
+    hipLaunchKernelGGL(k_schur_pairs_c, dim3(grid), dim3(256), 0, s, P, W.blocks, xoff, W.pairs, W.W, W.scale_c, W.S);
   else
     hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, xoff, W.pairs, W.W, W.S);
 }

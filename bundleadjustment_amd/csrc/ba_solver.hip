@@ -70,11 +70,6 @@ struct ba_ctx {
   // the device linearisation state is at the candidate of the last step (a
   // speculative linearisation, enqueued behind the step's scalar record)
   bool lin_at_cand = false;
-  // overlapped DENSE_SCHUR step: the factorisation's stream, the fork / join events
-  hipStream_t stream2 = nullptr, stream3 = nullptr;   // critical workgroup / workers
-  hipEvent_t evf = nullptr, evj = nullptr, evj3 = nullptr;
-  bool split_ok = false;   // stream2 and stream3 run concurrently (probed once)
-  unsigned sgen = 0;   // overlapped formations of S since the counters were zeroed
 
   // multi-GPU
   int nranks = 1, rank = 0;
@@ -145,8 +140,6 @@ struct ba_ctx {
     return d;
   }
   void free_problem() {
-    if (stream2) (void)hipStreamSynchronize(stream2);
-    if (stream3) (void)hipStreamSynchronize(stream3);
     if (stream) (void)hipStreamSynchronize(stream);
     for (void* p : allocs) (void)hipFree(p);
     allocs.clear();
@@ -207,9 +200,16 @@ struct ba_ctx {
     publish_scalars();
     wait_scalars();
   }
-  bool scal_spin() const {
-    static const bool spin = [] { const char* e = std::getenv("BA_SCAL_SPIN"); return !(e && e[0] == '0'); }();
-    return spin && d_hscal;
+  bool scal_spin() const { return spin && d_hscal; }
+  // per-call switches (read at every ba_solve / ba_bench_iterations entry, so
+  // tests can A/B them in one process): BA_SPEC_LIN=0 turns the speculative
+  // linearisation off, BA_SCAL_SPIN=0 the spin-published scalar record
+  bool spec_lin = true, spin = true;
+  void read_env() {
+    const char* e = std::getenv("BA_SPEC_LIN");
+    spec_lin = !(e && e[0] == '0');
+    e = std::getenv("BA_SCAL_SPIN");
+    spin = !(e && e[0] == '0');
   }
   void publish_scalars() {
     const size_t cnt = kNumSlots + kPcgState;
@@ -505,72 +505,18 @@ void ensure_dense(ba_ctx* ctx) {
   // S diagonal after the fold: the LM diagonal is then added after them
   // (separate k_cam_add_diag), in the order the exchange path uses
   ctx->dup_diag = std::any_of(blocks.begin(), blocks.end(), [](const int4& b) { return b.x == b.y; });
-  W.trace = std::getenv("BA_OVERLAP_TRACE") ? ctx->dalloc<unsigned long long>(512) : nullptr;
-  W.rowcnt = ctx->dalloc<unsigned>((size_t)std::max(nvc, 1) * kRowCntStride);
-  W.checkin = ctx->dalloc<unsigned>(2);
-  HIP_OK(hipMemsetAsync(W.rowcnt, 0, sizeof(unsigned) * (size_t)std::max(nvc, 1) * kRowCntStride, ctx->stream));
-  HIP_OK(hipMemsetAsync(W.checkin, 0, 2 * sizeof(unsigned), ctx->stream));
-  ctx->sgen = 0;
+  // k_schur_pairs*: XCD x sweeps the blocks [xoff[x], xoff[x+1]): equal
+  // contiguous ranges of the row-major list (bands of rows: C3 165 vs 188 us
+  // for an interleave)
+  std::vector<int> xoff(9, 0);
   {
-    // Overlapped step (reduced_solve_dense): single rank, persistent
-    // factorisation, no duplicate-observation blocks on the diagonal (they
-    // would update S after the fold).  Measured negative at C3 (DESIGN §12:
-    // the rows of S reach the factorisation too late for its row chains), so
-    // off by default.  BA_OVERLAP=1: the split factorisation (critical
-    // workgroup and workers on two streams, when they are found to run
-    // concurrently) beside the pair pass; 2: the same kernels in the serial
-    // order (diagnostics)
-    const char* e = std::getenv("BA_OVERLAP");
-    W.overlap = W.chol_persist && !ctx->coll() && !ctx->dup_diag && e ? std::min(2, std::max(0, atoi(e))) : 0;
-    if (W.overlap && !ctx->stream2) {
-      HIP_OK(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
-      HIP_OK(hipStreamCreateWithFlags(&ctx->stream3, hipStreamNonBlocking));
-      HIP_OK(hipEventCreateWithFlags(&ctx->evf, hipEventDisableTiming));
-      HIP_OK(hipEventCreateWithFlags(&ctx->evj, hipEventDisableTiming));
-      HIP_OK(hipEventCreateWithFlags(&ctx->evj3, hipEventDisableTiming));
-      HIP_OK(hipStreamSynchronize(ctx->stream));
-      ctx->split_ok = bahip::streams_concurrent(ctx->stream2, ctx->stream3, W.checkin);
-      HIP_OK(hipMemsetAsync(W.checkin, 0, 2 * sizeof(unsigned), ctx->stream));
-    }
-    if (W.overlap == 1 && !ctx->split_ok) W.overlap = 0;
-  }
-  // k_schur_pairs*: XCD x sweeps the blocks [xoff[x], xoff[x+1]).  Overlapped
-  // step: camera COLUMNS interleaved over the XCDs (column J on XCD J mod 8,
-  // ascending), so the block columns of S complete in order over the pass,
-  // which the factorisation waits on column by column (rowexp: blocks per
-  // column camera); else equal contiguous ranges of the row-major list
-  // (bands of rows: C3 165 vs 188 us for an interleave).
-  // The overlapped step launches the pass in two parts: the head (the camera
-  // columns of the first two tile columns, which the critical workgroup
-  // needs first), then the tail.
-  std::vector<int> xoff(18, 0);
-  std::vector<unsigned> rowexp((size_t)std::max(nvc, 1), 0u);
-  for (const int4& b : blocks) rowexp[W.overlap ? b.y : b.x]++;
-  W.xmax[0] = W.xmax[1] = 0;
-  if (W.overlap) {
-    const int vh = std::min(nvc - 1, (2 * 64 - 1) / 6 + 1);   // (+1: wait_cols' margin camera)
-    std::vector<int4> bycol(blocks);
-    std::stable_sort(bycol.begin(), bycol.end(), [](const int4& p, const int4& q) { return p.y < q.y; });
-    std::vector<int4> ord;
-    ord.reserve(blocks.size());
-    for (int h = 0; h < 2; ++h) {
-      for (int x = 0; x < 8; ++x) {
-        xoff[9 * h + x] = (int)ord.size();
-        for (const int4& b : bycol) if (b.y % 8 == x && (b.y <= vh) == (h == 0)) ord.push_back(b);
-      }
-      xoff[9 * h + 8] = (int)ord.size();
-      for (int x = 0; x < 8; ++x) W.xmax[h] = std::max(W.xmax[h], xoff[9 * h + x + 1] - xoff[9 * h + x]);
-    }
-    blocks.swap(ord);
-  } else {
     const int R = ((int)blocks.size() + 7) / 8;
     for (int x = 0; x <= 8; ++x) xoff[x] = std::min((int)blocks.size(), x * R);
-    W.xmax[0] = R;
+    W.xmax = R;
   }
   W.blocks = ctx->upload(blocks);
   W.nblocks = (int)blocks.size();
   W.xoff = ctx->upload(xoff);
-  W.rowexp = ctx->upload(rowexp);
   W.pairs = ctx->upload(pairs);
   HIP_OK(hipMemsetAsync(W.yg, 0, sizeof(double) * 2 * (size_t)std::max(ctx->n, 1), ctx->stream));
   // S is rewritten every step (diagonal blocks, rhs and every co-observed
@@ -732,56 +678,6 @@ void reduced_solve_dense(ba_ctx* ctx, double radius) {
   // fold (same operation order as the exchange path's, bitwise)
   const bool fused_diag = !ctx->coll() && !ctx->dup_diag;
   launch_cam_schur_diag(P, W, s, nullptr, fused_diag ? radius : 0.0);
-  if (W.overlap && W.wcompact && fused_diag && ctx->n > 0) {
-    // Overlapped step: the persistent factorisation starts once the diagonal
-    // blocks and the rhs are in S (the fold) and waits row by row for the
-    // off-diagonal blocks the pair pass writes beside it (rows in order,
-    // counted in W.rowcnt).  The gate holds the pair pass until every
-    // factorisation workgroup is resident, so the pass fills only the CUs
-    // the factorisation leaves; the factorisation never blocks it.  Same
-    // operations on the same values as the serial order: bitwise identical.
-    const unsigned gen = ++ctx->sgen;
-    const int epoch = ++ctx->chol_epoch;
-    if (W.overlap == 2) {   // diagnostics: the same kernels in the serial order
-      launch_schur_pairs(P, W, s, true, 0);
-      launch_schur_pairs(P, W, s, true, 1);
-      launch_chol_overlapped(P, W, epoch, gen, s);
-      launch_back_flow(P, W, epoch, s);
-      return;
-    }
-    // Submission order: the gate and the pair pass BEFORE the factorisation.
-    // Should the two streams share a hardware queue (they are then run in
-    // submission order), the gate times out, the pair pass completes and the
-    // factorisation runs after it: slower, never a factorisation spinning on
-    // rows that a pass queued behind it would write.
-    if (W.trace) HIP_OK(hipMemsetAsync(W.trace, 0, 512 * sizeof(unsigned long long), s));
-    HIP_OK(hipEventRecord(ctx->evf, s));
-    launch_chol_gate(P, W, gen, s);
-    launch_schur_pairs(P, W, s, true, 0);
-    launch_schur_pairs(P, W, s, true, 1);
-    HIP_OK(hipStreamWaitEvent(ctx->stream2, ctx->evf, 0));
-    HIP_OK(hipStreamWaitEvent(ctx->stream3, ctx->evf, 0));
-    launch_chol_overlapped(P, W, epoch, gen, ctx->stream2, ctx->stream3);
-    HIP_OK(hipEventRecord(ctx->evj, ctx->stream2));
-    HIP_OK(hipEventRecord(ctx->evj3, ctx->stream3));
-    HIP_OK(hipStreamWaitEvent(s, ctx->evj, 0));
-    HIP_OK(hipStreamWaitEvent(s, ctx->evj3, 0));
-    launch_back_flow(P, W, epoch, s);
-    if (W.trace && gen == 6) {   // diagnostics: one step's timeline (us after the pair pass started)
-      std::vector<unsigned long long> h(512);
-      HIP_OK(hipMemcpyAsync(h.data(), W.trace, 512 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-      HIP_OK(hipStreamSynchronize(s));
-      const int T = (ctx->n + 63) / 64;
-      auto us = [&](unsigned long long t) { return t ? ((long long)t - (long long)h[255]) / 100.0 : -1.0; };
-      std::fprintf(stderr, "overlap trace (us after the pair pass starts)\n  tile row: done / (I, I-1) published / step I starts\n");
-      for (int I = 0; I < T && I < 40; ++I) {
-        unsigned long long done = 0;
-        for (int v = (64 * I) / 6; v <= std::min(ctx->nvc - 1, (64 * I + 63) / 6); ++v) done = std::max(done, h[v]);
-        std::fprintf(stderr, "  %2d: %7.1f %7.1f %7.1f\n", I, us(done), us(h[300 + I]), us(h[256 + I]));
-      }
-    }
-    return;
-  }
   launch_schur_pairs(P, W, s);
   if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
   if (ctx->coll()) {
@@ -956,6 +852,7 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
   ba_options o;
   if (opt) o = *opt; else ba_default_options(&o);
   check_options(o);
+  ctx->read_env();
   const double t0 = now_s();
   ctx->log.clear();
   ctx->t_lin = ctx->t_solve = 0.0;
@@ -1174,11 +1071,6 @@ int ba_destroy(ba_ctx* ctx) {
   if (ctx->d_ticket) (void)hipFree(ctx->d_ticket);
   if (ctx->pose_buf) (void)hipFree(ctx->pose_buf);
   if (ctx->hv_scratch) (void)hipFree(ctx->hv_scratch);
-  if (ctx->evf) (void)hipEventDestroy(ctx->evf);
-  if (ctx->evj) (void)hipEventDestroy(ctx->evj);
-  if (ctx->evj3) (void)hipEventDestroy(ctx->evj3);
-  if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
-  if (ctx->stream3) (void)hipStreamDestroy(ctx->stream3);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return BA_OK;
@@ -1501,8 +1393,8 @@ int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double ra
     if (!ctx->scale_valid) linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
     double rj_total = 0.0;
     long ls_total = 0;
-    static const bool spec_on = [] { const char* e = std::getenv("BA_SPEC_LIN"); return !(e && e[0] == '0'); }();
-    const bool spec = spec_on && !ctx->coll();
+    ctx->read_env();
+    const bool spec = ctx->spec_lin;
     const bool trj = ms_rj_kernel != nullptr;   // event pair around the r+J kernel
     HIP_OK(hipEventRecord(ctx->ev[0], ctx->stream));
     ctx->rj_slot = 0;

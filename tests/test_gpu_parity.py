@@ -303,26 +303,32 @@ def test_persistent_cholesky_is_bitwise_the_per_step_form(monkeypatch, cfg, scal
 
 
 # ---------------------------------------------------------------------------
-# overlapped DENSE_SCHUR step (BA_OVERLAP=1: the split persistent
-# factorisation waits row by row for the pair pass running beside it; 2: the
-# same kernels in the serial order): the same operations on the same values,
-# so bitwise the serial step
+# speculative linearisation (BA_SPEC_LIN: the linearisation at a step's
+# candidate is enqueued behind the step's scalar record; a rejected or invalid
+# step re-linearises at x) and the spin-published scalar record
+# (BA_SCAL_SPIN): pure orchestration, so every on/off combination must give
+# the bitwise-identical trajectory.  The tolerances are switched off so the
+# solve runs into the late iterations where steps get rejected.
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("cfg,scale,fix", [("c3", 0.05, 1), ("c2", 1.0, 0), ("c3", 1.0, 0)])
-def test_overlapped_step_is_bitwise_the_serial_step(monkeypatch, cfg, scale, fix):
-    p = make_config(cfg, scale=scale)
-    if fix:
-        bp.fix_camera(p, 1)
+@pytest.mark.parametrize("solver_type", ["DENSE_SCHUR", "ITERATIVE_SCHUR"])
+def test_speculative_linearisation_and_spin_are_bitwise_neutral(monkeypatch, solver_type):
+    p = make_config("c1", scale=1.0)
+    opts = Options(max_num_iterations=40, function_tolerance=0.0, gradient_tolerance=0.0,
+                   parameter_tolerance=0.0, linear_solver_type=solver_type)
     runs = {}
-    for mode in ("0", "1", "2"):
-        monkeypatch.setenv("BA_OVERLAP", mode)
-        with Solver(0) as s:
-            runs[mode] = run_gpu(s, p, Options(max_num_iterations=4))
-    for mode in ("1", "2"):
-        a, b = runs["0"], runs[mode]
-        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), mode
-        assert [r["cost"] for r in a[3]] == [r["cost"] for r in b[3]], mode
-        assert [r["step_is_successful"] for r in a[3]] == [r["step_is_successful"] for r in b[3]], mode
+    for spec in ("0", "1"):
+        for spin in ("0", "1"):
+            monkeypatch.setenv("BA_SPEC_LIN", spec)
+            monkeypatch.setenv("BA_SCAL_SPIN", spin)
+            with Solver(0) as s:
+                runs[spec + spin] = run_gpu(s, p, opts)
+    ref = runs["11"]
+    assert any(not r["step_is_successful"] for r in ref[3]), "no rejected step: the test does not exercise the path"
+    for k, r in runs.items():
+        assert np.array_equal(ref[0], r[0]) and np.array_equal(ref[1], r[1]), k
+        assert [x["cost"] for x in ref[3]] == [x["cost"] for x in r[3]], k
+        assert [x["step_is_successful"] for x in ref[3]] == [x["step_is_successful"] for x in r[3]], k
+        assert [x["step_is_valid"] for x in ref[3]] == [x["step_is_valid"] for x in r[3]], k
 
 
 # ---------------------------------------------------------------------------
