@@ -272,6 +272,8 @@ def main():
             time.sleep(float(os.environ.get("BA_BENCH_DRYRUN_SLEEP", "0")))
         return
 
+    import numpy as np
+
     from bundleadjustment_amd import Options, Solver, make_config
     from bundleadjustment_amd.problem import CONFIG_INDEX, CONFIGS
 
@@ -326,6 +328,9 @@ def main():
     solver.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+    # per-iteration host wall times of the timed region (the
+    # median of >= 10 iterations after 2 warm-ups), reported beside the mean
+    it_ms = solver.bench_iteration_times()
     if not rj_in_loop:
         _, ms_rj = solver.bench_iterations(args.steps, options=opts)
         barrier()
@@ -334,6 +339,8 @@ def main():
     n_pts_total = problem.n_pts
     if use_comm:   # max over ranks of the timed region, total observations
         dt = float(solver.allreduce_host([dt], "max")[0])
+        if len(it_ms):   # the slowest rank per iteration
+            it_ms = np.asarray(solver.allreduce_host(list(it_ms), "max"))
         tot = solver.allreduce_host([float(problem.n_obs), float(problem.n_pts)], "sum")
         n_obs_total, n_pts_total = int(tot[0]), int(tot[1])
 
@@ -341,11 +348,12 @@ def main():
     #   176 B/obs (uv 8 + two int32 idx 8 + r 16 + J 144) + 24 B/point + 48 B/camera
     B_rj = 176.0 * problem.n_obs + 24.0 * problem.n_pts + 48.0 * problem.n_cams
     achieved = B_rj / (ms_rj * 1e-3) / 1e9
-    # J-free iteration (libba_hip's rule: <= 200 cameras, BA_JR unset): the
-    # timed kernel is k_lin_point, which forms r and J in registers and
-    # reduces them into the point blocks without storing J; SURVEY.md §8d
-    # prices such a fused kernel against the unfused B_rj, labelled "effective"
-    jrfree = problem.n_cams <= 200 and os.environ.get("BA_JR") != "1"
+    # J-free iteration (libba_hip's default, BA_JR unset): the timed kernel is
+    # k_lin_point, which forms r and J in registers and reduces them into the
+    # point blocks without storing J (camera table in LDS up to 200 cameras,
+    # the L2-resident global table beyond); SURVEY.md §8d prices such a fused
+    # kernel against the unfused B_rj, labelled "effective"
+    jrfree = os.environ.get("BA_JR") != "1"
     traffic = pmc_traffic(cfg, "k_lin_point" if jrfree else "k_linearize") if not strong and args.scale == 1.0 else None
     # measured copy bandwidth of this GPU (reported beside the
     # vendor peak, which stays the denominator of `frac`): 1 GiB non-temporal
@@ -412,6 +420,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
+            "ms_per_step_median": round(float(np.median(it_ms)), 4) if len(it_ms) else None,
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,

@@ -109,6 +109,9 @@ SIGNATURES = [
     ("ba_get_iteration_log", C.c_int, [C.c_void_p, C.POINTER(ba_iteration), C.c_int]),
     ("ba_eval_residuals", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]),
     ("ba_linearize", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(C.c_double)]),
+    ("ba_bench_iteration_times", C.c_int, [C.c_void_p, C.c_void_p, C.c_int]),
+    ("ba_debug_blocks", C.c_int, [C.c_void_p, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.POINTER(C.c_int)]),
     ("ba_prune", C.c_int, [C.c_void_p, C.POINTER(ba_prune_problem), C.c_void_p]),
     ("ba_solve_pose_batch", C.c_int, [C.c_void_p, C.POINTER(ba_pose_batch), C.POINTER(ba_options), C.c_void_p,
                                       C.POINTER(ba_summary)]),

@@ -58,7 +58,9 @@ struct DevWork {
   double* rec;   double* rec_c;      // camera records at x / x'
   double* crec;                      // [nc][16] compact camera records (w, t, K, flag, theta terms) for > kLinLdsCams cameras
   double* ctbl;                      // [nc][22] candidate camera table for > kLinLdsCams cameras
-  bool jrfree;                       // J-free iteration (nc <= kLinLdsCams): consumers recompute J, JR unused
+  double* gtbl;                      // [nc][48] global lin table of the J-free kernels beyond kLinLdsCams cameras (ba_kernels.hip kGRec)
+  bool jrfree;                       // J-free iteration: consumers recompute J, JR unused (camera table in LDS up to kLinLdsCams cameras, gtbl / crec beyond)
+  int jtab;                          // camera source of the J-free kernels beyond kLinLdsCams cameras: 1 gtbl, 2 crec
   double* JR;                        // JA [no][JA] (Jc rows 0..1; JA = 14 beyond kLinLdsCams cameras: + r again), then JB [no][8] (Jp rows 3+3, r 2)
   double* delta_p;                   // [np][3] point step (scaled back)
   double* Hpp;   double* gp;         // [6][np], [3][np]
@@ -68,6 +70,12 @@ struct DevWork {
   double* scale_c; double* diag_c;   // [nvc][6]
   double* delta_c;                   // [nvc][6]
   double* W;                         // [no][18]  (E L^-T per observation), fp64
+  // camera-major copies of W (ITERATIVE_SCHUR, W.wcm): row i = the i-th entry
+  // of cam_op, so the camera-side passes stream instead of gathering
+  bool wcm;
+  double* Wcm;                       // [n_camobs][18] fp64
+  float* Wcmf;                       // [n_camobs][18] fp32 (BA_MIXED_FP32)
+  double* prec;                      // [np][16] point record for the camera-major W: X (3), var flag, s_p (3), L_p^-1 (6)
   float* Wf;                         // [no][18]  the same in fp32 (BA_MIXED_FP32)
   bool w32;                          // W blocks stored in Wf
   bool wcompact;                     // W as 128-B compact records (J-free fp64 DENSE_SCHUR; ba_kernels.hip)
@@ -165,6 +173,7 @@ bool point_step_fused();                      // J-free back substitution fused 
 bool chol_persist_fits(int device, int n);   // every workgroup of k_chol_persist resident at once
 int chol_split_blocks();                     // block columns from which the split step form is used   // resident k_back_flow workgroups (-1: query failed)
 constexpr int kLinLdsCamsHost = 200;   // = kLinLdsCams (ba_kernels.hip): cameras the LDS camera table holds
+constexpr int kWcCamsHost = 1024;      // = kWcCams: variable cameras of the compact-W DENSE_SCHUR pair pass
 int jr_ja_host(int nc);   // JA stride of the JR records for nc cameras (12 or 14)
 void launch_stream_copy(const double* a, double* b, size_t n2, hipStream_t s);
 // the scalar record into pinned host memory, then its sequence number

@@ -307,8 +307,48 @@ struct CamLdsLazy {
   __device__ double K(int i) const { return (double)k[i]; }
 };
 
-// camera row as an indexable value: a register copy (CamGlobal, CamLds) or
-// an LDS view (CamLdsLazy)
+// Many cameras (nc > kLinLdsCams) in the J-free iteration: the same table
+// rows in global memory, one 384-B row (three whole cache lines) per camera:
+//   [0..39] the lin table, [40] the variable flag, [41..45] K as 9 floats
+// C4 (1k cameras): 384 KB, C5 (10k): 3.8 MB — L2-resident, gathered per
+// observation by the point-major kernels (the same values as the LDS rows,
+// so the same arithmetic as the <= 200-camera kernels)
+constexpr int kGRec = 48;
+constexpr int kGRecK = 41;
+struct CamG {
+  const double* r;
+  __device__ bool var() const { return r[kLin] != 0.0; }
+  __device__ void load(double (&t)[kLin]) const {
+    const double2* s = reinterpret_cast<const double2*>(r);
+#pragma unroll
+    for (int k = 0; k < kLin / 2; ++k) { const double2 u = s[k]; t[2 * k] = u.x; t[2 * k + 1] = u.y; }
+  }
+  __device__ double K(int i) const { return (double)reinterpret_cast<const float*>(r + kGRecK)[i]; }
+  __device__ const float* Kf() const { return reinterpret_cast<const float*>(r + kGRecK); }
+};
+// gtbl from the camera records (thread per entry)
+__global__ __launch_bounds__(256) void k_lin_gtbl(DevProblem P, const double* __restrict__ rec,
+                                                  double* __restrict__ gtbl) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= P.nc * kGRec) return;
+  const int c = e / kGRec, k = e - c * kGRec;
+  const double* r = rec + (size_t)c * kCamRec;
+  double v = 0.0;
+  if (k < kLin) {
+    v = r[kRecL + k];
+  } else if (k == kLin) {
+    v = P.vc[c] >= 0 ? 1.0 : 0.0;
+  } else if (k < kGRecK + 5) {
+    const int i = 2 * (k - kGRecK);
+    const float lo = (float)r[kRecK + i], hi = i + 1 < 9 ? (float)r[kRecK + i + 1] : 0.0f;
+    v = __builtin_bit_cast(double, ((unsigned long long)__builtin_bit_cast(unsigned, hi) << 32) |
+                                       __builtin_bit_cast(unsigned, lo));
+  }
+  gtbl[e] = v;
+}
+
+// camera row as an indexable value: a register copy (CamGlobal, CamLds, CamG)
+// or an LDS view (CamLdsLazy)
 struct RowRegs {
   double t[kLin];
   __device__ double operator[](int i) const { return t[i]; }
@@ -531,19 +571,19 @@ __device__ inline double lin_obs(const DevProblem& P, const Cam& cr, bool cvar, 
 // The same record from a compact camera (CamRc): the Jets' evaluation order
 // itself — p = R X + t on duals of w, q = K p, dq/dX = K R — with R and its
 // w-derivatives from the dual Rodrigues of k_cam_prep.  Fixed cameras read
-// their float extrinsic.
-__device__ inline double lin_obs(const DevProblem& P, const CamRc& cr, bool cvar, bool pvar, double X0, double X1,
-                                 double X2, float2 uv, double (&out)[kJR], bool& fin) {
-  const double* Kd = cr.Kd;
+// their float extrinsic.  lin_obs_rc: the part after the dual Rodrigues (R
+// given), so that camera-major kernels form R once per camera (CamRcR) and
+// point-major ones per observation — the same operations either way.
+__device__ inline double lin_obs_rc(const DevProblem& P, const D3* R, const double* t, const double* Kd, int cidx,
+                                    bool cvar, bool pvar, double X0, double X1, double X2, float2 uv,
+                                    double (&out)[kJR], bool& fin, double* prf) {
   double q[3], dq[3][3], dX[3][3], iw = 1.0;   // dq/dw_k [k][row], dq/dX_col [col][row]
   if (cvar) {
-    D3 R[9];
-    angle_axis_to_R_d3_pre(cr.w, cr.th, R);
     D3 p[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const D3 a = R[i], b = R[3 + i], c = R[6 + i];
-      p[i] = mk(a.a * X0 + b.a * X1 + c.a * X2 + cr.t[i], a.d[0] * X0 + b.d[0] * X1 + c.d[0] * X2,
+      p[i] = mk(a.a * X0 + b.a * X1 + c.a * X2 + t[i], a.d[0] * X0 + b.d[0] * X1 + c.d[0] * X2,
                 a.d[1] * X0 + b.d[1] * X1 + c.d[1] * X2, a.d[2] * X0 + b.d[2] * X1 + c.d[2] * X2);
     }
 #pragma unroll
@@ -556,7 +596,7 @@ __device__ inline double lin_obs(const DevProblem& P, const CamRc& cr, bool cvar
         dX[col][row] = Kd[row] * R[col * 3].a + Kd[3 + row] * R[col * 3 + 1].a + Kd[6 + row] * R[col * 3 + 2].a;
     }
   } else {
-    const float* E = P.extr + 16 * cr.cidx;
+    const float* E = P.extr + 16 * cidx;
     double e3[4], KE[12];
 #pragma unroll
     for (int l = 0; l < 12; ++l) {
@@ -581,6 +621,7 @@ __device__ inline double lin_obs(const DevProblem& P, const CamRc& cr, bool cvar
   const double rho = huber(r0 * r0 + r1 * r1, P.huber_a, P.huber_b, &scale);
   const double f = iq * scale;
   fin = isfinite(r0) && isfinite(r1) && isfinite(f);
+  if (prf) { prf[0] = pr0; prf[1] = pr1; prf[2] = f; }
   if (cvar) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -609,6 +650,37 @@ __device__ inline double lin_obs(const DevProblem& P, const CamRc& cr, bool cvar
 #pragma unroll
   for (int k = 0; k < 18; ++k) fin = fin && isfinite(out[k]);
   return rho;
+}
+__device__ inline double lin_obs(const DevProblem& P, const CamRc& cr, bool cvar, bool pvar, double X0, double X1,
+                                 double X2, float2 uv, double (&out)[kJR], bool& fin, double* prf = nullptr) {
+  D3 R[9];
+  if (cvar) angle_axis_to_R_d3_pre(cr.w, cr.th, R);
+  return lin_obs_rc(P, R, cr.t, cr.Kd, cr.cidx, cvar, pvar, X0, X1, X2, uv, out, fin, prf);
+}
+// a compact camera with its dual Rodrigues formed (camera-major kernels)
+struct CamRcR {
+  D3 R[9];
+  double t[3], Kd[9];
+  int cidx;
+  bool v;
+  __device__ void make(const CamRc& c) {
+    if (c.v) angle_axis_to_R_d3_pre(c.w, c.th, R);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[k] = c.t[k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Kd[k] = c.Kd[k];
+    cidx = c.cidx;
+    v = c.v;
+  }
+  __device__ bool var() const { return v; }
+};
+__device__ inline double lin_obs(const DevProblem& P, const CamRcR& cr, bool cvar, bool pvar, double X0, double X1,
+                                 double X2, float2 uv, double (&out)[kJR], bool& fin, double* prf = nullptr) {
+  return lin_obs_rc(P, cr.R, cr.t, cr.Kd, cr.cidx, cvar, pvar, X0, X1, X2, uv, out, fin, prf);
+}
+// the compact record of camera c, unpacked (one 128-B line)
+__device__ inline CamRc cam_rc(const double* __restrict__ crec, int c) {
+  return cam_make(CamRcOf{crec, nullptr}, cam_pre(CamRcOf{crec, nullptr}, c));
 }
 
 // Wave body: every wave owns chunks of 64 consecutive observations (grid
@@ -1085,11 +1157,15 @@ __global__ __launch_bounds__(256) void k_cam_norms(DevProblem P, const double* _
 //   A = s Hpp s + D^2 (D = sqrt(diag / radius), ceres lm_diagonal_), L L^T = A,
 //   store L^-1 and u = L^-1 (s g)
 // ---------------------------------------------------------------------------
+// prec (optional, the camera-major W of ITERATIVE_SCHUR): one 128-B record
+// per point with what k_obs_w_cam gathers: X, the variable flag, s_p, L_p^-1
+constexpr int kPRec = 16;
 __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* __restrict__ Hpp,
                                                     const double* __restrict__ gp, const double* __restrict__ scale_p,
                                                     const double* __restrict__ diag_p, double radius,
                                                     double* __restrict__ Linv, double* __restrict__ u,
-                                                    double* __restrict__ part) {
+                                                    double* __restrict__ part, const double* __restrict__ pts,
+                                                    double* __restrict__ prec) {
   __shared__ double lds[16];
   double acc[1] = {0.0};
   const size_t np = (size_t)P.np;
@@ -1099,6 +1175,13 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
       for (int k = 0; k < 6; ++k) Linv[k * np + p] = 0.0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) u[4 * (size_t)p + k] = 0.0;
+      if (prec) {
+        double2* r = reinterpret_cast<double2*>(prec + (size_t)p * kPRec);
+        r[0] = make_double2(pts[3 * (size_t)p], pts[3 * (size_t)p + 1]);
+        r[1] = make_double2(pts[3 * (size_t)p + 2], 0.0);
+#pragma unroll
+        for (int k = 2; k < kPRec / 2; ++k) r[k] = make_double2(0.0, 0.0);
+      }
       continue;
     }
     double s[3], D2[3], gs[3];
@@ -1136,6 +1219,17 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
     u[4 * (size_t)p + 1] = i10 * gs[0] + i11 * gs[1];
     u[4 * (size_t)p + 2] = i20 * gs[0] + i21 * gs[1] + i22 * gs[2];
     u[4 * (size_t)p + 3] = 0.0;
+    if (prec) {
+      double2* r = reinterpret_cast<double2*>(prec + (size_t)p * kPRec);
+      r[0] = make_double2(pts[3 * (size_t)p], pts[3 * (size_t)p + 1]);
+      r[1] = make_double2(pts[3 * (size_t)p + 2], 1.0);
+      r[2] = make_double2(s[0], s[1]);
+      r[3] = make_double2(s[2], i00);
+      r[4] = make_double2(i10, i11);
+      r[5] = make_double2(i20, i21);
+      r[6] = make_double2(i22, 0.0);
+      r[7] = make_double2(0.0, 0.0);
+    }
     acc[0] += ok ? 0.0 : 1.0;
   }
   double out[1];
@@ -1507,6 +1601,7 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
 
 // compact W records (k_obs_w_rc<double, true>, described there): 16 doubles
 constexpr int kWcRec = 16;
+constexpr int kWcCams = kWcCamsHost;   // variable cameras k_schur_pairs_c's LDS table holds (72 KB)
 // the camera constants of the compact records: Jc's scaled translation
 // columns are f (A_row,k - pr_row B_k), A_row,k = s_{3+k} K_{3k+row},
 // B_k = s_{3+k} K_{3k+2}
@@ -1547,7 +1642,8 @@ __device__ inline void wc_rows(const WcRaw& w, const WcCam& m, double (&c0)[6], 
 // diagonal Schur blocks and rhs (local part): one workgroup per camera
 //   S_cc = -sum W W^T (lower 21) ; b_c = -sum W u_p
 // ---------------------------------------------------------------------------
-template <typename WT>
+// CM: W is the camera-major copy (row i of cam_op), streamed
+template <typename WT, bool CM = false>
 __global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const WT* __restrict__ W,
                                                         const double* __restrict__ u, double* __restrict__ S,
                                                         double* __restrict__ cpart) {
@@ -1573,7 +1669,7 @@ __global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const WT* 
   for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int2 op = P.cam_op[i];
     double w[18];
-    load_w18(W, (size_t)op.x, w);
+    load_w18(W, CM ? (size_t)i : (size_t)op.x, w);
     const double2 u01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
     add(w, u01.x, u01.y, u[4 * (size_t)op.y + 2]);
   }
@@ -1682,7 +1778,7 @@ __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4*
                                                        const double* __restrict__ scale_c, double* __restrict__ S) {
   // the camera constants of every variable camera in LDS (nvc <= 200 in the
   // J-free mode: 14.4 KB), read per pair (registers: 1 -> 2 waves per SIMD)
-  __shared__ WcCam ctab[kLinLdsCams];
+  __shared__ WcCam ctab[kWcCams];
   for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
   __syncthreads();
   constexpr int PL = kPairLanes, BPW = 64 / PL;
@@ -2002,16 +2098,20 @@ struct CamRegs {
 // l + LANES, ...; fixed-order xor fold inside the group); the next
 // observation's indices and pixel, and the group's next point, are loaded one
 // step ahead (clamped, unconditional loads)
-template <int NT, int LANES, bool LAZY = false>
+// TB: the camera source (nc > kLinLdsCams: no LDS copy) — 0 the LDS copy of
+// the records' lin tables, 1 rec is the global table gtbl (kGRec rows), 2 rec
+// is the compact records crec (k_cam_compact; the dual Rodrigues per
+// observation), gathered per observation
+template <int NT, int LANES, bool LAZY = false, int TB = 0>
 __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __restrict__ rec,
                                                   const double* __restrict__ pts, double* __restrict__ Hpp,
                                                   double* __restrict__ gp, double* __restrict__ scale_p,
                                                   double* __restrict__ diag_p, int compute_scale, double min_diag,
                                                   double max_diag, double* __restrict__ part) {
   __shared__ double lds[5 * 16];
-  __shared__ __attribute__((aligned(16))) double tbl[kLinLdsCams * kTblRec];
-  __shared__ float ktb[kLinLdsCams * 9];
-  fill_lin_table<NT>(P, rec, tbl, ktb);
+  __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
+  __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
+  if constexpr (!TB) fill_lin_table<NT>(P, rec, tbl, ktb);
   double acc[4] = {0.0, 0.0, 0.0, 0.0};   // cost, bad, gn2, xn2
   double gmax = 0.0;
   const size_t np = (size_t)P.np;
@@ -2044,7 +2144,13 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
       double out[kJR];
       bool fin;
       double rho;
-      if constexpr (LAZY) {   // table entries read from LDS at use (fewer registers)
+      if constexpr (TB == 1) {
+        const CamG cam{rec + (size_t)c * kGRec};
+        rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
+      } else if constexpr (TB == 2) {
+        const CamRc cam = cam_rc(rec, c);
+        rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
+      } else if constexpr (LAZY) {   // table entries read from LDS at use (fewer registers)
         const CamLdsLazy cam{tbl + c * kTblRec, ktb + c * 9};
         rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
       } else {
@@ -2119,15 +2225,19 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
 
 // Hcc (lower 21) and gc per variable camera, its observations in camera order
 // (k_cam_assemble's order: thread i takes i0 + tid, i0 + tid + NT, ...)
-template <int NT>
+// TB = 2: rec is the compact records crec (the camera's dual Rodrigues once
+// per workgroup: CamRcR), else the camera records (lin table in registers)
+template <int NT, int TB = 0>
 __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const double* __restrict__ rec,
                                                         const double* __restrict__ pts, double* __restrict__ cpart,
                                                         double* __restrict__ Hcc, double* __restrict__ gc) {
   __shared__ double lds[27 * 16];
   const int v = blockIdx.x;
   const int c = P.cam_of_vc[v];
-  CamRegs cam;
-  {
+  typename std::conditional<TB == 2, CamRcR, CamRegs>::type cam;
+  if constexpr (TB == 2) {
+    cam.make(cam_rc(rec, c));
+  } else {
     const double2* s2 = reinterpret_cast<const double2*>(rec + (size_t)c * kCamRec + kRecL);
 #pragma unroll
     for (int k = 0; k < kLin / 2; ++k) { const double2 u = s2[k]; cam.t[2 * k] = u.x; cam.t[2 * k + 1] = u.y; }
@@ -2185,7 +2295,10 @@ __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const doub
 // through the 2 x 2 inner matrices Z Z'^T (WcCam: the camera's K and
 // translation scalings).
 constexpr int kObsWRcWaves = 6;   // table + K + scales + 6 staging slots fit the 160 KB LDS
-template <typename WT, bool COMPACT = false>
+// TB (nc > kLinLdsCams, k_lin_point's camera sources): rec is the global
+// table gtbl (1) or the compact records crec (2); the camera scalings are
+// read from scale_c
+template <typename WT, bool COMPACT = false, int TB = 0>
 __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, const double* __restrict__ rec,
                                                                 const double* __restrict__ pts,
                                                                 const double* __restrict__ scale_c,
@@ -2194,16 +2307,18 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
   using V2 = typename std::conditional<sizeof(WT) == 8, double2, float2>::type;
   constexpr int WAVES = kObsWRcWaves, NT = 64 * WAVES;
   __shared__ double stage[WAVES * 64 * kStageLd];
-  __shared__ __attribute__((aligned(16))) double tbl[kLinLdsCams * kTblRec];
-  __shared__ float ktb[kLinLdsCams * 9];
-  __shared__ double sct[kLinLdsCams * 6];
-  fill_lin_table<NT>(P, rec, tbl, ktb);   // (ends with a barrier)
-  for (int e = threadIdx.x; e < P.nc * 6; e += NT) {
-    const int c = e / 6, a = e - 6 * c;
-    const int v = P.vc[c];
-    sct[e] = v >= 0 ? scale_c[(size_t)v * 6 + a] : 0.0;
+  __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
+  __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
+  __shared__ double sct[TB ? 1 : kLinLdsCams * 6];
+  if constexpr (!TB) {
+    fill_lin_table<NT>(P, rec, tbl, ktb);   // (ends with a barrier)
+    for (int e = threadIdx.x; e < P.nc * 6; e += NT) {
+      const int c = e / 6, a = e - 6 * c;
+      const int v = P.vc[c];
+      sct[e] = v >= 0 ? scale_c[(size_t)v * 6 + a] : 0.0;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   if (P.no == 0) return;   // (the clamped prefetch indices below need no >= 1)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double* st = stage + w * (64 * kStageLd);
@@ -2226,14 +2341,27 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
     const double s0 = scale_p[p], s1 = scale_p[np + p], s2 = scale_p[2 * np + p];
     const double i00 = Linv[p], i10 = Linv[np + p], i11 = Linv[2 * np + p];
     const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
-    const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
     double j[kJR];
     bool fin;
     double prf[3];
-    (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin, prf);
     double sc[6];
+    if constexpr (TB) {
+      if constexpr (TB == 1) {
+        const CamG cam{rec + (size_t)c * kGRec};
+        (void)lin_obs(P, cam, v >= 0, pv, X0, X1, X2, uv, j, fin, prf);
+      } else {
+        const CamRc cam = cam_rc(rec, c);
+        (void)lin_obs(P, cam, v >= 0, pv, X0, X1, X2, uv, j, fin, prf);
+      }
+      const double* sv = scale_c + (size_t)max(v, 0) * 6;   // (v < 0: the record is zero, !live)
 #pragma unroll
-    for (int a = 0; a < 6; ++a) sc[a] = sct[c * 6 + a];
+      for (int a = 0; a < 6; ++a) sc[a] = sv[a];
+    } else {
+      const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
+      (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin, prf);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) sc[a] = sct[c * 6 + a];
+    }
     const double jp0[3] = {j[12] * s0, j[13] * s1, j[14] * s2};
     const double jp1[3] = {j[15] * s0, j[16] * s1, j[17] * s2};
     constexpr int REC = COMPACT ? kWcRec : kWRec;
@@ -2288,6 +2416,74 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
       }
     }
     c = cn; p = pn; uv = uvn;
+  }
+}
+
+// Camera-major W (ITERATIVE_SCHUR, W.wcm): the same W_o as k_obs_w_rc, row
+// i of the cam_op order, so that the camera-side passes (the diagonal Schur
+// blocks and every CG iteration's camera pass) stream it instead of
+// gathering point-major records (random 72 / 144-B gathers from an array
+// past the Infinity Cache at C5).  One workgroup per camera slice, the
+// camera's table row in registers (k_cam_assemble_rc), the point's record
+// (k_point_elim's prec: one 128-B line) and pixel gathered per observation;
+// J by the same lin_obs on the same table values: bitwise k_obs_w_rc's W.
+template <int NT, typename WT, int TB = 0>
+__global__ __launch_bounds__(NT) void k_obs_w_cam(DevProblem P, const double* __restrict__ rec,
+                                                  const double* __restrict__ prec,
+                                                  const double* __restrict__ scale_c, WT* __restrict__ Wcm) {
+  const int v = blockIdx.x;
+  const int c = P.cam_of_vc[v];
+  typename std::conditional<TB == 2, CamRcR, CamRegs>::type cam;
+  if constexpr (TB == 2) {
+    cam.make(cam_rc(rec, c));
+  } else {
+    const double2* s2 = reinterpret_cast<const double2*>(rec + (size_t)c * kCamRec + kRecL);
+#pragma unroll
+    for (int k = 0; k < kLin / 2; ++k) { const double2 q = s2[k]; cam.t[2 * k] = q.x; cam.t[2 * k + 1] = q.y; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) cam.k[k] = (double)P.K[9 * c + k];   // float-valued (Matrix3f)
+  }
+  double sc[6];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) sc[a] = scale_c[(size_t)v * 6 + a];
+  int i0, i1;
+  cam_slice(P, v, i0, i1);
+  using V2 = typename std::conditional<sizeof(WT) == 8, double2, float2>::type;
+  for (int i = i0 + threadIdx.x; i < i1; i += NT) {
+    const int2 op = P.cam_op[i];
+    double r[kPRec];
+    {
+      const double2* q = reinterpret_cast<const double2*>(prec + (size_t)op.y * kPRec);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) { const double2 t = q[k]; r[2 * k] = t.x; r[2 * k + 1] = t.y; }
+    }
+    const bool pv = r[3] != 0.0;
+    double j[kJR];
+    bool fin;
+    (void)lin_obs(P, cam, true, pv, r[0], r[1], r[2], P.uv[op.x], j, fin);
+    const double s0 = r[4], s1 = r[5], s2 = r[6];
+    const double i00 = r[7], i10 = r[8], i11 = r[9], i20 = r[10], i21 = r[11], i22 = r[12];
+    const double jp0[3] = {j[12] * s0, j[13] * s1, j[14] * s2};
+    const double jp1[3] = {j[15] * s0, j[16] * s1, j[17] * s2};
+    double wv[kWRec];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {   // k_obs_w_rc's arithmetic
+      const double c0 = j[a] * sc[a], c1 = j[6 + a] * sc[a];
+      const double e0 = c0 * jp0[0] + c1 * jp1[0];
+      const double e1 = c0 * jp0[1] + c1 * jp1[1];
+      const double e2 = c0 * jp0[2] + c1 * jp1[2];
+      wv[a * 3 + 0] = pv ? e0 * i00 : 0.0;
+      wv[a * 3 + 1] = pv ? e0 * i10 + e1 * i11 : 0.0;
+      wv[a * 3 + 2] = pv ? e0 * i20 + e1 * i21 + e2 * i22 : 0.0;
+    }
+    V2* dst = reinterpret_cast<V2*>(Wcm + (size_t)i * kWRec);
+#pragma unroll
+    for (int k = 0; k < kWRec / 2; ++k) {
+      V2 t;
+      t.x = (WT)wv[2 * k];
+      t.y = (WT)wv[2 * k + 1];
+      dst[k] = t;
+    }
   }
 }
 
@@ -2374,7 +2570,10 @@ __global__ __launch_bounds__(NT) void k_cam_schur_diag_c(DevProblem P, const dou
 
 // model cost change + candidate cost with J recomputed at x (the lin table of
 // the linearisation point) beside the value-only candidate table
-template <int NT>
+// TB (nc > kLinLdsCams, k_lin_point's camera sources): rec is gtbl (1) or
+// crec (2), rec_c the global candidate table ctbl (k_cand_table), K from
+// gtbl / P.K
+template <int NT, int TB = 0>
 __global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double* __restrict__ rec,
                                                      const double* __restrict__ pts,
                                                      const double* __restrict__ delta_c,
@@ -2382,15 +2581,16 @@ __global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double*
                                                      const double* __restrict__ rec_c,
                                                      const double* __restrict__ pts_c, double* __restrict__ part) {
   __shared__ double lds[3 * 16];
-  __shared__ __attribute__((aligned(16))) double tbl[kLinLdsCams * kTblRec];
-  __shared__ float ktb[kLinLdsCams * 9];
-  __shared__ double ctb[kLinLdsCams * kCandRec];
-  fill_lin_table<NT>(P, rec, tbl, ktb);
-  {
+  __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
+  __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
+  __shared__ double ctb_s[TB ? 1 : kLinLdsCams * kCandRec];
+  if constexpr (!TB) {
+    fill_lin_table<NT>(P, rec, tbl, ktb);
     const int n = P.nc * kCandRec;
-    for (int e = threadIdx.x; e < n; e += NT) ctb[e] = cand_entry(P, rec_c, delta_c, e);
+    for (int e = threadIdx.x; e < n; e += NT) ctb_s[e] = cand_entry(P, rec_c, delta_c, e);
+    __syncthreads();
   }
-  __syncthreads();
+  const double* ctb = TB ? rec_c : ctb_s;
   double acc[3] = {0.0, 0.0, 0.0};  // mneg, ccost, cand_bad
   // the next observation's indices, pixel and point data are loaded one step
   // ahead (clamped, unconditional)
@@ -2423,14 +2623,26 @@ __global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double*
     load_in(o + ostep, nxt);
     const int c = cur.c;
     const float2 uv = cur.uv;
-    const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
     double j[kJR];
     bool fin;
-    (void)lin_obs(P, cam, cam.var(), cur.pv, cur.X[0], cur.X[1], cur.X[2], uv, j, fin);
+    const float* Kc;
+    if constexpr (TB == 1) {
+      const CamG cam{rec + (size_t)c * kGRec};
+      (void)lin_obs(P, cam, cam.var(), cur.pv, cur.X[0], cur.X[1], cur.X[2], uv, j, fin);
+      Kc = cam.Kf();
+    } else if constexpr (TB == 2) {
+      const CamRc cam = cam_rc(rec, c);
+      (void)lin_obs(P, cam, cam.var(), cur.pv, cur.X[0], cur.X[1], cur.X[2], uv, j, fin);
+      Kc = P.K + 9 * c;
+    } else {
+      const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
+      (void)lin_obs(P, cam, cam.var(), cur.pv, cur.X[0], cur.X[1], cur.X[2], uv, j, fin);
+      Kc = ktb + c * 9;
+    }
     const double dp0 = cur.dp[0], dp1 = cur.dp[1], dp2 = cur.dp[2];
     const double X0 = cur.Xc[0], X1 = cur.Xc[1], X2 = cur.Xc[2];
     const bool cfix = P.cam_fixed && P.cam_fixed[c];
-    const double* cr = ctb + c * kCandRec;
+    const double* cr = ctb + (size_t)c * kCandRec;
     // k_candidate_lds' arithmetic on the same values
     double jd0 = 0.0, jd1 = 0.0;
 #pragma unroll
@@ -2448,7 +2660,6 @@ __global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double*
       for (int i = 0; i < 4; ++i) ph[i] = X0 * cr[i] + X1 * cr[4 + i] + X2 * cr[8 + i] + cr[12 + i];
       pc[0] = ph[0] / ph[3]; pc[1] = ph[1] / ph[3]; pc[2] = ph[2] / ph[3];
     }
-    const float* Kc = ktb + c * 9;
     double q[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) q[i] = pc[0] * (double)Kc[i] + pc[1] * (double)Kc[3 + i] + pc[2] * (double)Kc[6 + i];
@@ -2480,7 +2691,9 @@ __global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double*
 //   pass 2  J d . (r + J d / 2) (Jc dc, Jp and r kept from pass 1 for the
 //           lane's first KC observations, J again past them) and the
 //           candidate residual at (camera', x'_p) per observation.
-template <int NT, int LANES, bool LAZY, int KC = 3>
+// TB (nc > kLinLdsCams, k_lin_point's camera sources): rec is gtbl (1) or
+// crec (2), rec_c the global candidate table ctbl (k_cand_table)
+template <int NT, int LANES, bool LAZY, int KC = 3, int TB = 0>
 __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double* __restrict__ rec,
                                                       const double* __restrict__ pts,
                                                       const double* __restrict__ delta_c,
@@ -2489,15 +2702,16 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
                                                       const double* __restrict__ scale_p, double* __restrict__ pts_c,
                                                       double* __restrict__ delta_p, double* __restrict__ part) {
   __shared__ double lds[5 * 16];
-  __shared__ __attribute__((aligned(16))) double tbl[kLinLdsCams * kTblRec];
-  __shared__ float ktb[kLinLdsCams * 9];
-  __shared__ double ctb[kLinLdsCams * kCandRec];
-  fill_lin_table<NT>(P, rec, tbl, ktb);
-  {
+  __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
+  __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
+  __shared__ double ctb_s[TB ? 1 : kLinLdsCams * kCandRec];
+  if constexpr (!TB) {
+    fill_lin_table<NT>(P, rec, tbl, ktb);
     const int n = P.nc * kCandRec;
-    for (int e = threadIdx.x; e < n; e += NT) ctb[e] = cand_entry(P, rec_c, delta_c, e);
+    for (int e = threadIdx.x; e < n; e += NT) ctb_s[e] = cand_entry(P, rec_c, delta_c, e);
+    __syncthreads();
   }
-  __syncthreads();
+  const double* ctb = TB ? rec_c : ctb_s;
   double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // step2, step_bad, mneg, ccost, cand_bad
   const size_t np = (size_t)P.np;
   const int sl = threadIdx.x & (LANES - 1);
@@ -2505,7 +2719,13 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
   const int lastp = max(P.np - 1, 0), lasto = max(P.no - 1, 0);
   auto lin = [&](int c, bool pv, double X0, double X1, double X2, float2 uv, double (&j)[kJR]) {
     bool fin;
-    if constexpr (LAZY) {
+    if constexpr (TB == 1) {
+      const CamG cam{rec + (size_t)c * kGRec};
+      (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
+    } else if constexpr (TB == 2) {
+      const CamRc cam = cam_rc(rec, c);
+      (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
+    } else if constexpr (LAZY) {
       const CamLdsLazy cam{tbl + c * kTblRec, ktb + c * 9};
       (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
     } else {
@@ -2543,7 +2763,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
           const float2 uvn = P.uv[on];
           double j[kJR];
           lin(c, true, X0, X1, X2, uv, j);
-          const double* dc = ctb + c * kCandRec + 16;   // the camera step (0 for a fixed camera)
+          const double* dc = ctb + (size_t)c * kCandRec + 16;   // the camera step (0 for a fixed camera)
           double t0 = 0.0, t1 = 0.0;
 #pragma unroll
           for (int a = 0; a < 6; ++a) { t0 += j[a] * dc[a]; t1 += j[6 + a] * dc[a]; }
@@ -2607,7 +2827,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
           const int cn = P.obs_cam[on];
           const float2 uvn = P.uv[on];
           const bool cfix = P.cam_fixed && P.cam_fixed[c];
-          const double* cr = ctb + c * kCandRec;
+          const double* cr = ctb + (size_t)c * kCandRec;
           // k_candidate_lds' arithmetic
           double jd0, jd1, jp[6], r0, r1;
           if (keep) {
@@ -2638,7 +2858,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
             for (int i = 0; i < 4; ++i) ph[i] = Xc[0] * cr[i] + Xc[1] * cr[4 + i] + Xc[2] * cr[8 + i] + cr[12 + i];
             pcand[0] = ph[0] / ph[3]; pcand[1] = ph[1] / ph[3]; pcand[2] = ph[2] / ph[3];
           }
-          const float* Kc = ktb + c * 9;
+          const float* Kc = TB == 1 ? CamG{rec + (size_t)c * kGRec}.Kf() : (TB == 2 ? P.K + 9 * c : ktb + c * 9);
           double q[3];
 #pragma unroll
           for (int i = 0; i < 3; ++i)
@@ -2694,11 +2914,21 @@ static int lds_grid(int n) {
   return g < 1 ? 1 : (g > n_cu ? n_cu : g);
 }
 
+// the J-free kernels read the LDS copy of the camera records' lin tables up
+// to kLinLdsCams cameras and the global table gtbl beyond
+// camera source of the J-free kernels: 0 the LDS copy of the records' lin
+// tables (nc <= kLinLdsCams), beyond: 1 the global table gtbl, 2 the compact
+// records crec (W.jtab)
+static int jr_tab(const DevProblem& P, const DevWork& W) { return W.jrfree && P.nc > kLinLdsCams ? W.jtab : 0; }
 void launch_lin_prep(const DevProblem& P, const DevWork& W, hipStream_t s) {
-  if (P.nc <= kLinLdsCams || lin_legacy())
-    launch_cam_prep(P, W.cams, W.rec, true, s);
-  else
+  const int tb = jr_tab(P, W);
+  if (tb == 2 || (P.nc > kLinLdsCams && !lin_legacy() && !W.jrfree)) {
     hipLaunchKernelGGL(k_cam_compact, dim3((P.nc + 255) / 256), dim3(256), 0, s, P, W.cams, W.crec);
+    return;
+  }
+  launch_cam_prep(P, W.cams, W.rec, true, s);
+  if (tb == 1)
+    hipLaunchKernelGGL(k_lin_gtbl, dim3((P.nc * kGRec + 255) / 256), dim3(256), 0, s, P, (const double*)W.rec, W.gtbl);
 }
 void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   // t0 / t1 (optional): start / stop of the kernel's execution, stamped by
@@ -2713,7 +2943,10 @@ void launch_linearize_jr(const DevProblem& P, const DevWork& W, hipStream_t s, h
                           P, (const double*)W.rec, (const double*)W.pts, W.JR, W.part);
     return;
   }
-  if (!lin_legacy()) {
+  // (J-free beyond kLinLdsCams cameras, ba_linearize's read-back: the
+  // global-record kernel below evaluates the same lin tables as gtbl holds,
+  // so the records are bitwise what the J-free consumers compute)
+  if (!lin_legacy() && (!W.jrfree || jr_tab(P, W) == 2)) {
     hipExtLaunchKernelGGL(k_linearize_rc, dim3(grid_for(P.no)), dim3(kThreads), 0, s, t0, t1, 0, P,
                           (const double*)W.crec, (const double*)W.pts, W.JR, W.part);
     return;
@@ -2736,12 +2969,26 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
     const int L = lanes == 2 || lanes == 8 ? lanes : 4;
     const int NT = nt == 512 ? 512 : 256;
     // two 74-KB-LDS workgroups per CU at most: a grid of that size, grid-stride
-    // over the points (no second round of table fills)
+    // over the points (no second round of table fills); the global-table
+    // variant has no table to fill: up to kMaxBlocks (its partials' slots)
     const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
-    const int g = std::max(1, std::min(want, 2 * lds_grid(1 << 30)));
+    const int tb = jr_tab(P, W);
+    const int g = std::max(1, std::min(want, tb ? kMaxBlocks : 2 * lds_grid(1 << 30)));
     using KF = void (*)(DevProblem, const double*, const double*, double*, double*, double*, double*, int, double,
                         double, double*);
     KF kern;
+    if (tb) {
+      if (tb == 1)
+        kern = NT == 512 ? (L == 2 ? k_lin_point<512, 2, false, 1> : (L == 8 ? k_lin_point<512, 8, false, 1> : k_lin_point<512, 4, false, 1>))
+                         : (L == 2 ? k_lin_point<256, 2, false, 1> : (L == 8 ? k_lin_point<256, 8, false, 1> : k_lin_point<256, 4, false, 1>));
+      else
+        kern = NT == 512 ? (L == 2 ? k_lin_point<512, 2, false, 2> : (L == 8 ? k_lin_point<512, 8, false, 2> : k_lin_point<512, 4, false, 2>))
+                         : (L == 2 ? k_lin_point<256, 2, false, 2> : (L == 8 ? k_lin_point<256, 8, false, 2> : k_lin_point<256, 4, false, 2>));
+      hipExtLaunchKernelGGL(kern, dim3(g), dim3(NT), 0, s, t0, t1, 0, P, (const double*)(tb == 1 ? W.gtbl : W.crec),
+                            (const double*)W.pts, W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag,
+                            max_diag, W.part);
+      return;
+    }
     if (NT == 256) {
       if (lazy) kern = L == 2 ? k_lin_point<256, 2, true> : (L == 8 ? k_lin_point<256, 8, true> : k_lin_point<256, 4, true>);
       else kern = L == 2 ? k_lin_point<256, 2> : (L == 8 ? k_lin_point<256, 8> : k_lin_point<256, 4>);
@@ -2771,7 +3018,10 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
     if (sp < 0) { const char* e = getenv("BA_CA_SPLIT"); sp = e ? atoi(e) : 1; }
     const int sl = std::max(1, std::min(sp, W.cam_split));
     const dim3 g(P.nvc, sl);
-    if (nt == 128)
+    if (jr_tab(P, W) == 2)   // (the compact records: the camera's dual Rodrigues once per workgroup)
+      hipLaunchKernelGGL((k_cam_assemble_rc<512, 2>), g, dim3(512), 0, s, P, (const double*)W.crec, (const double*)W.pts,
+                         W.cpart, W.Hcc, W.gc);
+    else if (nt == 128)
       hipLaunchKernelGGL(k_cam_assemble_rc<128>, g, dim3(128), 0, s, P, (const double*)W.rec, (const double*)W.pts,
                          W.cpart, W.Hcc, W.gc);
     else if (nt == 256)
@@ -2814,9 +3064,40 @@ void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale,
                      W.diag_c, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
 }
 void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
+  const bool cm = W.wcm && W.jrfree;
   hipLaunchKernelGGL(k_point_elim, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.Hpp, W.gp, W.scale_p, W.diag_p,
-                     radius, W.Linv, W.u, W.part);
+                     radius, W.Linv, W.u, W.part, (const double*)W.pts, cm ? W.prec : nullptr);
   if (P.no == 0) return;
+  const int tb = jr_tab(P, W);
+  if (cm && P.nvc > 0) {   // the camera-major copy (the point-major W below stays: the point passes read it)
+    const dim3 g(P.nvc, W.cam_split);
+    if (tb == 2) {
+      if (W.w32)
+        hipLaunchKernelGGL((k_obs_w_cam<256, float, 2>), g, dim3(256), 0, s, P, (const double*)W.crec,
+                           (const double*)W.prec, W.scale_c, W.Wcmf);
+      else
+        hipLaunchKernelGGL((k_obs_w_cam<256, double, 2>), g, dim3(256), 0, s, P, (const double*)W.crec,
+                           (const double*)W.prec, W.scale_c, W.Wcm);
+    } else {
+      if (W.w32)
+        hipLaunchKernelGGL((k_obs_w_cam<256, float>), g, dim3(256), 0, s, P, (const double*)W.rec,
+                           (const double*)W.prec, W.scale_c, W.Wcmf);
+      else
+        hipLaunchKernelGGL((k_obs_w_cam<256, double>), g, dim3(256), 0, s, P, (const double*)W.rec,
+                           (const double*)W.prec, W.scale_c, W.Wcm);
+    }
+  }
+  if (tb) {   // global camera source: 64.5 KB of staging LDS, two workgroups per CU
+    const int g = std::min(2 * lds_grid(1 << 30), std::max(1, (P.no + 64 * kObsWRcWaves - 1) / (64 * kObsWRcWaves)));
+    const double* src = tb == 1 ? W.gtbl : W.crec;
+    if (W.w32)
+      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<float, false, 1> : k_obs_w_rc<float, false, 2>), dim3(g),
+                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.Wf);
+    else
+      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, false, 1> : k_obs_w_rc<double, false, 2>), dim3(g),
+                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.W);
+    return;
+  }
   if (W.jrfree) {   // one 148-KB-LDS workgroup per CU
     const int g = lds_grid(P.no);
     if (W.w32)
@@ -2848,7 +3129,14 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
   static int dsplit = -1;   // diagnostics: BA_DIAG_SPLIT overrides the slice count
   if (dsplit < 0) { const char* e = getenv("BA_DIAG_SPLIT"); dsplit = e ? atoi(e) : 0; }
   const int sl = dsplit > 0 ? std::min(dsplit, kCamSplit) : W.cam_split;
-  if (W.w32)
+  if (W.wcm && W.jrfree) {
+    if (W.w32)
+      hipLaunchKernelGGL((k_cam_schur_diag<float, true>), dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wcmf, W.u, W.S,
+                         W.cpart);
+    else
+      hipLaunchKernelGGL((k_cam_schur_diag<double, true>), dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wcm, W.u, W.S,
+                         W.cpart);
+  } else if (W.w32)
     hipLaunchKernelGGL(k_cam_schur_diag<float>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wf, W.u, W.S, W.cpart);
   else if (W.wcompact) {
     // diagnostics: BA_DIAG_NT (64 / 128 / 256 threads), BA_DIAG_PREF (0 / 1)
@@ -2953,14 +3241,42 @@ bool point_step_fused() {
   return fused != 0;
 }
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
+  if (const int tb = jr_tab(P, W)) {
+    // global camera source: the candidate table (value-only records + the
+    // camera step) from k_cam_candidate's records, then the same kernels as
+    // below
+    hipLaunchKernelGGL(k_cand_table, dim3((P.nc * kCandRec + 255) / 256), dim3(256), 0, s, P, W.rec_c, W.delta_c,
+                       W.ctbl);
+    if (point_step_fused()) {
+      constexpr int NT = 512, L = 4;
+      const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
+      const int g = std::max(1, std::min(want, kMaxBlocks));
+      hipLaunchKernelGGL((tb == 1 ? k_point_step_rc<NT, L, false, 3, 1> : k_point_step_rc<NT, L, false, 3, 2>), dim3(g),
+                         dim3(NT), 0, s, P, (const double*)(tb == 1 ? W.gtbl : W.crec), (const double*)W.pts,
+                         W.delta_c, (const double*)W.ctbl, W.u, W.Linv, W.scale_p, W.pts_c, W.delta_p, W.part);
+      return;
+    }
+    if (W.w32)
+      hipLaunchKernelGGL(k_backsub<float>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c,
+                         W.delta_p, W.Wf, W.u, W.Linv, W.y, W.scale_p, W.part);
+    else
+      hipLaunchKernelGGL(k_backsub<double>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c,
+                         W.delta_p, W.W, W.u, W.Linv, W.y, W.scale_p, W.part);
+    const int g = std::max(1, std::min(kMaxBlocks, (P.no + 511) / 512));
+    hipLaunchKernelGGL((tb == 1 ? k_candidate_rc<512, 1> : k_candidate_rc<512, 2>), dim3(g), dim3(512), 0, s, P,
+                       (const double*)(tb == 1 ? W.gtbl : W.crec), (const double*)W.pts, W.delta_c, W.delta_p,
+                       (const double*)W.ctbl, W.pts_c, W.part);
+    return;
+  }
   if (W.jrfree) {
     // (BA_PSTEP_LAZY=1: lazy camera-table reads, diagnostics)
     static int lazy = -1;
     const bool fused = point_step_fused();
     if (lazy < 0) { const char* e = getenv("BA_PSTEP_LAZY"); lazy = e ? atoi(e) : 0; }
-    // (fp32 W storage keeps the W-based back substitution: the step then
-    // solves with the stored fp32 blocks, as the oracle's fp32-W mode does)
-    if (fused && !W.w32) {
+    // (fp32 W storage too: the back substitution is exact in fp64 from J,
+    // as the oracle's fp32-W mode restates it; only the matvec, the rhs and
+    // the preconditioner see the fp32 blocks)
+    if (fused) {
       constexpr int NT = 512, L = 4;
       const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
       const int g = std::max(1, std::min(want, lds_grid(1 << 30)));   // one 110-KB-LDS workgroup per CU

@@ -259,7 +259,9 @@ __global__ __launch_bounds__(256) void k_pcg_point(DevProblem P, const WT* __res
 // ---------------------------------------------------------------------------
 // matvec, camera pass: slice g of camera v: sum_{o in slice} W_o v_{p(o)}
 // ---------------------------------------------------------------------------
-template <typename WT>
+// CM: Wm is the camera-major copy (row i of cam_op, ba_kernels.hip
+// k_obs_w_cam), streamed; the same products in the same order
+template <typename WT, bool CM = false>
 __global__ __launch_bounds__(256) void k_pcg_cam(DevProblem P, const WT* __restrict__ Wm,
                                                  const double* __restrict__ vpt, double* __restrict__ tpart,
                                                  const double* __restrict__ st) {
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(256) void k_pcg_cam(DevProblem P, const WT* __restr
     const int2 op = P.cam_op[i];   // fixed points: W_o = 0, v_p = 0
     const int o = op.x, p = op.y;
     double wv[18];
-    load_w18(Wm, (size_t)o, wv);
+    load_w18(Wm, CM ? (size_t)i : (size_t)o, wv);
     const double u0 = vpt[3 * (size_t)p], u1 = vpt[3 * (size_t)p + 1], u2 = vpt[3 * (size_t)p + 2];
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[a] += wv[a * 3] * u0 + wv[a * 3 + 1] * u1 + wv[a * 3 + 2] * u2;
@@ -608,6 +610,18 @@ void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec,
     else
       hipLaunchKernelGGL(k_pcg_point_t<double>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.W, vec, W.tobs, st);
     hipLaunchKernelGGL(k_pcg_cam_t, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
+    return;
+  }
+  if (W.wcm && W.jrfree) {   // camera pass over the camera-major copy
+    if (W.w32) {
+      hipLaunchKernelGGL(k_pcg_point<float>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.Wf, vec, W.vpt, st);
+      hipLaunchKernelGGL((k_pcg_cam<float, true>), dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wcmf, W.vpt, W.tpart,
+                         st);
+    } else {
+      hipLaunchKernelGGL(k_pcg_point<double>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.W, vec, W.vpt, st);
+      hipLaunchKernelGGL((k_pcg_cam<double, true>), dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wcm, W.vpt, W.tpart,
+                         st);
+    }
     return;
   }
   if (W.w32) {

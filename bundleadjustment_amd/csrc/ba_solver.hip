@@ -112,9 +112,11 @@ struct ba_ctx {
   bool dup_diag = false;   // the dense pair list has diagonal blocks (duplicate observations)
   double* tobs_buf = nullptr;   // [no][6] ITERATIVE_SCHUR per-observation products (allocated on first use)
   int max_no = 0;               // largest observation count over the ranks (collective matvec-path choice)
+  int ncamobs = 0;              // observations of variable cameras (the cam_op list)
 
   // solver state
   std::vector<ba_iteration> log;
+  std::vector<double> bench_ms;   // host wall time of each iteration of the last ba_bench_iterations
   bool scale_valid = false;
   double t_lin = 0.0, t_solve = 0.0;
 
@@ -337,6 +339,7 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   for (int s = 0; s < no; ++s) if (vc[obs_cam[s]] >= 0) cam_off[vc[obs_cam[s]] + 1]++;
   for (int v = 0; v < nvc; ++v) cam_off[v + 1] += cam_off[v];
   std::vector<int> cam_obs(cam_off[nvc]);
+  ctx->ncamobs = cam_off[nvc];
   {
     std::vector<int> fill(cam_off.begin(), cam_off.end() - 1);
     for (int s = 0; s < no; ++s) if (vc[obs_cam[s]] >= 0) cam_obs[fill[vc[obs_cam[s]]]++] = s;
@@ -384,14 +387,22 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.rec_c = ctx->dalloc<double>((size_t)kCamRec * nc);
   W.crec = ctx->dalloc<double>((size_t)16 * nc);
   W.ctbl = ctx->dalloc<double>((size_t)22 * nc);
-  // J-free iteration where the camera table fits the LDS (nc <= 200): r and J
-  // are recomputed by every consumer and never stored; BA_JR=1 forces the
-  // JR-materialising kernels (A/B, diagnostics).  JR is then allocated only
-  // for ba_linearize's read-back.
+  // J-free iteration: r and J are recomputed by every consumer and never
+  // stored (camera tables in LDS up to 200 cameras, the L2-resident global
+  // table gtbl beyond); BA_JR=1 forces the JR-materialising kernels (A/B,
+  // diagnostics).  JR is then allocated only for ba_linearize's read-back.
   {
     const char* e = std::getenv("BA_JR");
-    W.jrfree = nc > 0 && nc <= bahip::kLinLdsCamsHost && !(e && e[0] == '1');
+    W.jrfree = nc > 0 && !(e && e[0] == '1');
   }
+  {
+    // beyond 200 cameras the J-free kernels gather the camera per
+    // observation: the compact 128-B records (2, default; the dual Rodrigues
+    // per observation) or the 384-B lin-table rows (1, BA_JTAB=1)
+    const char* e = std::getenv("BA_JTAB");
+    W.jtab = e && atoi(e) == 1 ? 1 : 2;
+  }
+  W.gtbl = W.jrfree && nc > bahip::kLinLdsCamsHost && W.jtab == 1 ? ctx->dalloc<double>((size_t)48 * nc) : nullptr;
   W.JR = W.jrfree ? nullptr : ctx->dalloc<double>((size_t)(bahip::jr_ja_host(nc) + 8) * no);   // JA [no][jr_ja] + JB [no][8] (ba_kernels.hip)
   W.delta_p = ctx->dalloc<double>(3 * (size_t)np);
   W.Hpp = ctx->dalloc<double>(6 * (size_t)np);
@@ -663,8 +674,9 @@ LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max
 
 struct StepResult { bool linear_ok; double mcc, cand_cost, step_norm; int ls_iters; };
 
-// DENSE_SCHUR: explicit reduced camera system + dense Cholesky
-void reduced_solve_dense(ba_ctx* ctx, double radius) {
+// DENSE_SCHUR: explicit reduced camera system (form_reduced_dense) + dense
+// Cholesky
+void form_reduced_dense(ba_ctx* ctx, double radius) {
   const hipStream_t s = ctx->stream;
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
@@ -691,7 +703,10 @@ void reduced_solve_dense(ba_ctx* ctx, double radius) {
     launch_pack_lower(P, W, false, s);
   }
   if (!fused_diag) launch_cam_add_diag(P, W, radius, s);   // (after the exchange)
-  launch_cholesky_solve2(P, W, ++ctx->chol_epoch, s);
+}
+void reduced_solve_dense(ba_ctx* ctx, double radius) {
+  form_reduced_dense(ctx, radius);
+  launch_cholesky_solve2(ctx->P, ctx->W, ++ctx->chol_epoch, ctx->stream);
 }
 
 // ITERATIVE_SCHUR: implicit Schur complement + PCG (ba_pcg.hip).  The host
@@ -714,7 +729,7 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
     const int force = fe ? atoi(fe) : -1;
     // (decided from the largest rank's shard: every rank runs the same path)
     const bool big = 144.0 * (double)ctx->max_no > 256.0 * 1024 * 1024;
-    const bool use_t = force >= 0 ? force != 0 : (!W.w32 && big);
+    const bool use_t = !W.wcm && (force >= 0 ? force != 0 : (!W.w32 && big));
     if (use_t && !ctx->tobs_buf) ctx->tobs_buf = ctx->dalloc<double>(6 * (size_t)std::max(ctx->no, 1));
     if (!use_t && ctx->tobs_buf) { ctx->dfree(ctx->tobs_buf); ctx->tobs_buf = nullptr; }   // 48 B/obs back
     W.tobs = use_t ? ctx->tobs_buf : nullptr;
@@ -760,22 +775,42 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
 
 // Trust-region step phase: enqueue (the PCG reads its state record between
 // batches of CG iterations) / read back.  Returns the linear-solver iterations.
-int step_enqueue(ba_ctx* ctx, double radius, const ba_options& o) {
-  const hipStream_t s = ctx->stream;
-  DevProblem& P = ctx->P;
+// the per-observation Schur blocks of a step: fp32 or fp64, compact records,
+// camera-major copies
+void step_w_storage(ba_ctx* ctx, const ba_options& o) {
   DevWork& W = ctx->W;
   W.w32 = o.precision == BA_MIXED_FP32;
   if (W.w32 && !W.Wf) W.Wf = ctx->dalloc<float>(18 * (size_t)ctx->no);
   if (!W.w32 && !W.W) W.W = ctx->dalloc<double>(18 * (size_t)ctx->no);
+  {
+    // ITERATIVE_SCHUR, J-free: a camera-major copy of W written beside the
+    // point-major one (k_obs_w_cam), streamed by the diagonal Schur blocks and
+    // by every CG iteration's camera pass.  BA_WCM=0 / 1 (read per solve)
+    // forces it off / on
+    const char* e = getenv("BA_WCM");
+    const int force = e ? atoi(e) : -1;
+    W.wcm = W.jrfree && o.linear_solver == BA_ITERATIVE_SCHUR && (force >= 0 ? force != 0 : true);
+    if (W.wcm) {
+      if (!W.prec) W.prec = ctx->dalloc<double>(16 * (size_t)std::max(ctx->np, 1));
+      if (W.w32 && !W.Wcmf) W.Wcmf = ctx->dalloc<float>(18 * (size_t)std::max(ctx->ncamobs, 1));
+      if (!W.w32 && !W.Wcm) W.Wcm = ctx->dalloc<double>(18 * (size_t)std::max(ctx->ncamobs, 1));
+    }
+  }
   {
     // compact W records (ba_kernels.hip k_obs_w_rc<double, true>): the
     // J-free fp64 DENSE_SCHUR iteration with the fused point step (the only
     // W readers are then k_cam_schur_diag_c and k_schur_pairs_c);
     // BA_WCOMPACT=0 (diagnostics, read per solve) keeps the 18-double blocks
     const char* e = getenv("BA_WCOMPACT");
-    W.wcompact = W.jrfree && !W.w32 && o.linear_solver == BA_DENSE_SCHUR && !(e && e[0] == '0') &&
-                 point_step_fused();
+    W.wcompact = W.jrfree && ctx->nvc <= bahip::kWcCamsHost && !W.w32 && o.linear_solver == BA_DENSE_SCHUR &&
+                 !(e && e[0] == '0') && point_step_fused();
   }
+}
+int step_enqueue(ba_ctx* ctx, double radius, const ba_options& o) {
+  const hipStream_t s = ctx->stream;
+  DevProblem& P = ctx->P;
+  DevWork& W = ctx->W;
+  step_w_storage(ctx, o);
   // (SL_CHOL_BAD is cleared by k_cam_add_diag / k_pcg_setup_fin, the first
   // kernels that may set it, so no separate memset per step)
   int ls_iters = 1;
@@ -1347,9 +1382,67 @@ int ba_solve_pose_batch(ba_ctx* ctx, const ba_pose_batch* b, const ba_options* o
   });
 }
 
+int ba_debug_blocks(ba_ctx* ctx, double radius, double* Hpp, double* gp, double* Hcc, double* gc, double* S,
+                    double* rhs, int* n_out) {
+  if (!ctx || !(radius > 0.0)) return BA_ERR_INVALID_ARGUMENT;
+  return guarded(ctx, [&] {
+    if (!ctx->have_problem) throw BaError{BA_ERR_NO_PROBLEM, "no problem"};
+    HIP_OK(hipSetDevice(ctx->device));
+    ba_options o;
+    ba_default_options(&o);   // DENSE_SCHUR, fp64
+    ctx->read_env();
+    // iteration 0's linearisation (Jacobi scaling from it), then the step's
+    // reduced system without its factorisation
+    const LinResult L = linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
+    if (!L.ok) throw BaError{BA_ERR_DEVICE, "linearisation not finite"};
+    step_w_storage(ctx, o);
+    form_reduced_dense(ctx, radius);
+    const hipStream_t st = ctx->stream;
+    const int np = ctx->np, nc = ctx->nc, nvc = ctx->nvc, n = ctx->n;
+    HIP_OK(hipStreamSynchronize(st));
+    if (Hpp || gp) {
+      std::vector<double> h(6 * (size_t)np), g(3 * (size_t)np);
+      HIP_OK(hipMemcpy(h.data(), ctx->W.Hpp, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+      HIP_OK(hipMemcpy(g.data(), ctx->W.gp, g.size() * sizeof(double), hipMemcpyDeviceToHost));
+      for (int p = 0; p < np; ++p) {   // (SoA [k][np] on the device; fixed points: not written)
+        const bool v = ctx->h_pt_var[p] != 0;
+        for (int k = 0; k < 6; ++k) if (Hpp) Hpp[6 * (size_t)p + k] = v ? h[(size_t)k * np + p] : 0.0;
+        for (int k = 0; k < 3; ++k) if (gp) gp[3 * (size_t)p + k] = v ? g[(size_t)k * np + p] : 0.0;
+      }
+    }
+    if (Hcc || gc) {
+      std::vector<double> h(27 * (size_t)std::max(nvc, 1));
+      if (nvc) HIP_OK(hipMemcpy(h.data(), ctx->W.Hcc, 27 * (size_t)nvc * sizeof(double), hipMemcpyDeviceToHost));
+      if (Hcc) std::fill(Hcc, Hcc + 21 * (size_t)nc, 0.0);
+      if (gc) std::fill(gc, gc + 6 * (size_t)nc, 0.0);
+      for (int v = 0; v < nvc; ++v) {
+        const int c = ctx->cam_of_vc[v];
+        for (int k = 0; k < 21; ++k) if (Hcc) Hcc[21 * (size_t)c + k] = h[21 * (size_t)v + k];
+        for (int k = 0; k < 6; ++k) if (gc) gc[6 * (size_t)c + k] = h[21 * (size_t)nvc + 6 * (size_t)v + k];
+      }
+    }
+    if (S || rhs) {
+      std::vector<double> m((size_t)(n + 1) * std::max(ctx->ld, 1));
+      if (n) HIP_OK(hipMemcpy(m.data(), ctx->W.S, m.size() * sizeof(double), hipMemcpyDeviceToHost));
+      for (int i = 0; i < n; ++i) {
+        if (S) for (int j = 0; j < n; ++j) S[(size_t)i * n + j] = j <= i ? m[(size_t)i * ctx->ld + j] : 0.0;
+        if (rhs) rhs[i] = m[(size_t)n * ctx->ld + i];
+      }
+    }
+    if (n_out) *n_out = n;
+  });
+}
+
 int ba_synchronize(ba_ctx* ctx) {
   if (!ctx) return BA_ERR_INVALID_ARGUMENT;
   return guarded(ctx, [&] { HIP_OK(hipStreamSynchronize(ctx->stream)); });
+}
+
+int ba_bench_iteration_times(ba_ctx* ctx, double* ms, int n) {
+  if (!ctx) return BA_ERR_INVALID_ARGUMENT;
+  const int m = (int)ctx->bench_ms.size();
+  for (int i = 0; i < std::min(n, m) && ms; ++i) ms[i] = ctx->bench_ms[i];
+  return m;
 }
 
 int ba_stream_copy(ba_ctx* ctx, size_t bytes, int reps, double* gbs) {
@@ -1398,6 +1491,8 @@ int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double ra
     const bool trj = ms_rj_kernel != nullptr;   // event pair around the r+J kernel
     HIP_OK(hipEventRecord(ctx->ev[0], ctx->stream));
     ctx->rj_slot = 0;
+    ctx->bench_ms.assign(iters, 0.0);
+    double th = now_s();
     if (spec) linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, trj, true);
     for (int i = 0; i < iters; ++i) {
       // the solver's steady state after an accepted step: the step, its
@@ -1413,6 +1508,11 @@ int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double ra
         linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, trj, true);
       }
       ctx->wait_scalars();
+      {   // (the iteration's record has arrived: its host wall time)
+        const double t = now_s();
+        ctx->bench_ms[i] = (t - th) * 1e3;
+        th = t;
+      }
       const StepResult st = step_result(ctx, ls);
       if (trj) {
         float rj = 0.0f;

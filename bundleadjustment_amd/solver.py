@@ -203,6 +203,26 @@ class Solver:
         self._check(self.lib.ba_linearize(self.h, _ptr(r), _ptr(J), C.byref(cost)), "ba_linearize")
         return r, J, cost.value
 
+    def debug_blocks(self, radius: float = 1e4, with_s: bool = True) -> dict:
+        """The blocks of one DENSE_SCHUR step at the current parameters
+        (iteration-0 Jacobi scaling, trust-region radius `radius`), as the
+        solve's own kernels form them (ba_debug_blocks): Hpp [n_pts, 6], gp
+        [n_pts, 3], Hcc [n_cams, 21] (lower, row-major), gc [n_cams, 6], and
+        with_s: the reduced system S [n, n] (lower triangle) and rhs [n]."""
+        p = self.problem
+        Hpp, gp = np.empty((p.n_pts, 6)), np.empty((p.n_pts, 3))
+        Hcc, gc = np.empty((p.n_cams, 21)), np.empty((p.n_cams, 6))
+        n = C.c_int(0)
+        if with_s:   # size of the variable-camera system: ask first (S, rhs NULL)
+            self._check(self.lib.ba_debug_blocks(self.h, float(radius), None, None, None, None, None, None,
+                                                 C.byref(n)), "ba_debug_blocks")
+        S = np.empty((n.value, n.value)) if with_s else None
+        rhs = np.empty(n.value) if with_s else None
+        self._check(self.lib.ba_debug_blocks(self.h, float(radius), _ptr(Hpp), _ptr(gp), _ptr(Hcc), _ptr(gc),
+                                             _ptr(S) if with_s else None, _ptr(rhs) if with_s else None,
+                                             C.byref(n)), "ba_debug_blocks")
+        return {"Hpp": Hpp, "gp": gp, "Hcc": Hcc, "gc": gc, "S": S, "rhs": rhs, "n": n.value}
+
     def prune(self, extr, cam_center, K, obs_cam, obs_X, obs_uv, obs_inv_sigma, obs_dist) -> np.ndarray:
         """pruneCorrespondences (Optimizer.cpp:6-79) on the device for a batch of
         (keyframe, keypoint) pairs; returns a uint8 ba_prune_result per pair."""
@@ -261,6 +281,15 @@ class Solver:
         if with_linear_iters:
             return ms.value, r, li.value
         return ms.value, r
+
+    def bench_iteration_times(self) -> np.ndarray:
+        """Host wall time (ms) of each LM iteration of the last
+        bench_iterations call (scalar record to scalar record)."""
+        n = self.lib.ba_bench_iteration_times(self.h, None, 0)
+        out = np.empty(max(n, 0))
+        if n > 0:
+            self.lib.ba_bench_iteration_times(self.h, _ptr(out), n)
+        return out
 
     def stream_copy(self, nbytes: int = 1 << 30, reps: int = 10) -> float:
         """Measured device copy bandwidth in GB/s (read + write bytes), the

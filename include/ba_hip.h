@@ -273,6 +273,27 @@ typedef struct {
 int ba_solve_pose_batch(ba_ctx* ctx, const ba_pose_batch* batch, const ba_options* opt, double* cams_out,
                         ba_summary* summaries);
 
+/* Test / inspection entry point: the state inside ceres::Solve's
+ * SchurComplementSolver (Optimizer.cpp:242, DENSE_SCHUR) for one step.
+ * Linearises at the current parameters with iteration-0 Jacobi scaling, then
+ * forms the reduced camera system at trust-region radius `radius` with the
+ * very kernels a solve's step runs (J-free consumers, compact or 18-double W
+ * records, LDS or global camera tables: whatever the problem size selects),
+ * without factoring it, and copies out (caller indices; any pointer may be
+ * NULL):
+ *   Hpp[6*n_pts]  J_p^T J_p per point (xx, xy, xz, yy, yz, zz; unscaled,
+ *                 Huber-corrected J; zero for constant points),
+ *   gp[3*n_pts]   J_p^T r,
+ *   Hcc[21*n_cams] J_c^T J_c (lower triangle, row-major: (a, b), b <= a),
+ *   gc[6*n_cams]  J_c^T r (zero for constant / unobserved cameras),
+ *   S[n*n]        the reduced system s_c (Hcc - sum W W^T) s_c + D^2 as the
+ *                 Cholesky receives it (row-major, lower triangle; upper 0),
+ *   rhs[n]        its right-hand side,
+ * with n = *n_out = 6 x the observed variable cameras in increasing camera
+ * index (Jacobi-scaled columns, as Ceres' DENSE_SCHUR forms them). */
+int ba_debug_blocks(ba_ctx* ctx, double radius, double* Hpp, double* gp, double* Hcc, double* gc, double* S,
+                    double* rhs, int* n_out);
+
 /* Blocks until all device work of the context is done. */
 int ba_synchronize(ba_ctx* ctx);
 
@@ -287,6 +308,13 @@ int ba_synchronize(ba_ctx* ctx);
  * ~5 us per iteration; bench.py times the kernel in a second pass). */
 int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double radius, double* ms_per_iter,
                         double* ms_rj_kernel, double* linear_iters);
+
+/* Host wall time (ms) of each LM iteration of the last ba_bench_iterations
+ * call: from one iteration's scalar record reaching the host to the next's
+ * (the first from the call's start).  Copies min(n, available) values and
+ * returns the number available (bench.py reports their median, BASELINE.md
+ * §2, beside the mean over the timed region). */
+int ba_bench_iteration_times(ba_ctx* ctx, double* ms, int n);
 
 /* Measured copy bandwidth of the context's device ("also
  * report a measured STREAM-copy figure" beside the 8 TB/s peak): a

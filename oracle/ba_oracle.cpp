@@ -1000,8 +1000,10 @@ static bool iterative_schur_solve(const Problem& P, const Schur& S, const std::v
 //   S x = (F'F + D_f^2) x - sum_p W_p W_p' x,   rhs = F'b - sum_o W_o u_p,
 //   u_p = L_p^-1 E_p' b,   back substitution y_e = L_p^-T (u_p - W_p' x),
 // and MIXED_FP32 means every W_o entry is rounded to float once and used
-// in that form in the matvec, the rhs, the SCHUR_JACOBI blocks and the back
-// substitution; all sums, the CG vectors and everything else stay fp64.
+// in that form in the matvec, the rhs and the SCHUR_JACOBI blocks; the back
+// substitution uses the unrounded W_o (the device recomputes it from J in
+// fp64: k_point_step_rc); all sums, the CG vectors and everything else stay
+// fp64.
 // The CG (termination rules, preconditioner inversion) is the one above.
 // ----------------------------------------------------------------------------
 static bool iterative_schur_solve_w(const Problem& P, const Schur& S, const std::vector<Lin>& L,
@@ -1054,7 +1056,7 @@ static bool iterative_schur_solve_w(const Problem& P, const Schur& S, const std:
     for (int a = 0; a < 3; ++a) u[(size_t)ip * 3 + a] = M[a * 3] * g[0] + M[a * 3 + 1] * g[1] + M[a * 3 + 2] * g[2];
   }
   // W_o (stored rounded) for residuals with a variable camera and point
-  std::vector<double> W((size_t)P.no * 18, 0.0);
+  std::vector<double> W((size_t)P.no * 18, 0.0), W64((size_t)P.no * 18, 0.0);   // (W64: unrounded)
   for (int o = 0; o < P.no; ++o) {
     if (P.type[o] != RB_ANGLE) continue;
     const int ip = vp[P.obs_pt[o]];
@@ -1065,8 +1067,11 @@ static bool iterative_schur_solve_w(const Problem& P, const Schur& S, const std:
     for (int a = 0; a < 6; ++a) {
       const double e[3] = {Jc[a] * Jp[0] + Jc[6 + a] * Jp[3], Jc[a] * Jp[1] + Jc[6 + a] * Jp[4],
                            Jc[a] * Jp[2] + Jc[6 + a] * Jp[5]};
-      for (int k = 0; k < 3; ++k)   // (e L^-T)_k = sum_t e_t M[k][t]
-        W[(size_t)o * 18 + a * 3 + k] = rnd(e[0] * M[k * 3] + e[1] * M[k * 3 + 1] + e[2] * M[k * 3 + 2]);
+      for (int k = 0; k < 3; ++k) {   // (e L^-T)_k = sum_t e_t M[k][t]
+        const double wv = e[0] * M[k * 3] + e[1] * M[k * 3 + 1] + e[2] * M[k * 3 + 2];
+        W64[(size_t)o * 18 + a * 3 + k] = wv;
+        W[(size_t)o * 18 + a * 3 + k] = rnd(wv);
+      }
     }
   }
   // A_f = F'F + D_f^2 per camera block, rhs
@@ -1151,12 +1156,12 @@ static bool iterative_schur_solve_w(const Problem& P, const Schur& S, const std:
   }
   std::vector<double> x(n, 0.0);
   if (!pcg_solve(rhs, schur_mul, Minv, nf, opt, x, cg_iterations)) return false;
-  // back substitution (scaled space), then the camera part
+  // back substitution (scaled space, the unrounded W), then the camera part
   for (int ip = 0; ip < npv; ++ip) {
     double w3[3] = {u[(size_t)ip * 3], u[(size_t)ip * 3 + 1], u[(size_t)ip * 3 + 2]};
     for (int o : S.pt_obs[ip]) {
       if (P.type[o] != RB_ANGLE) continue;
-      const double* w = &W[(size_t)o * 18];
+      const double* w = &W64[(size_t)o * 18];
       const double* xc = &x[6 * S.fidx[P.obs_cam[o]]];
       for (int k = 0; k < 3; ++k)
         for (int a = 0; a < 6; ++a) w3[k] -= w[a * 3 + k] * xc[a];

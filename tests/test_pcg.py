@@ -139,16 +139,27 @@ def compare(glog, olog, n, rtol=1e-9):
         assert g["trust_region_radius"] == pytest.approx(o["trust_region_radius"], rel=1e-9)
 
 
+# matvec forms of the implicit Schur complement: "auto" the default (the
+# J-free iteration's camera-major copy of W, k_obs_w_cam: the camera passes
+# stream it), "gather" the point-major W gathered in camera order
+# (BA_WCM=0), "t" the per-observation products (k_pcg_point_t / k_pcg_cam_t,
+# BA_WCM=0 BA_PCG_T=1)
+MATVECS = ["auto", "gather", "t"]
+
+
+def set_matvec(monkeypatch, mode):
+    if mode != "auto":
+        monkeypatch.setenv("BA_WCM", "0")
+        monkeypatch.setenv("BA_PCG_T", "1" if mode == "t" else "0")
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("pc", PRECONDITIONERS)
 @pytest.mark.parametrize("cfg,scale", [("c1", 1.0), ("c2", 0.2), ("c3", 0.01)])
-@pytest.mark.parametrize("pcg_t", ["auto", "1"])
-def test_gpu_iterative_matches_oracle(solver, oracle_lib, cfg, scale, pc, pcg_t, monkeypatch):
-    """pcg_t = "1" forces the per-observation product matvec (k_pcg_point_t /
-    k_pcg_cam_t), which the solver picks by itself only when the fp64 W
-    outgrows the Infinity Cache (C5-sized shards)."""
-    if pcg_t != "auto":
-        monkeypatch.setenv("BA_PCG_T", pcg_t)
+@pytest.mark.parametrize("mv", MATVECS)
+def test_gpu_iterative_matches_oracle(solver, oracle_lib, cfg, scale, pc, mv, monkeypatch):
+    """Every matvec form against the oracle."""
+    set_matvec(monkeypatch, mv)
     p = make_config(cfg, scale=scale)
     _, _, so, olog = oracle_lib.solve(p, oracle_opts(oracle_lib, pc, max_num_iterations=8))
     _, _, sg, glog = gpu_solve(solver, p, preconditioner_type=pc, max_num_iterations=8)
@@ -168,12 +179,11 @@ def test_gpu_iterative_reaches_dense_minimum(solver, pc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pcg_t", ["auto", "1"])
-def test_gpu_iterative_residual_reset_and_cap(solver, oracle_lib, pcg_t, monkeypatch):
+@pytest.mark.parametrize("mv", MATVECS)
+def test_gpu_iterative_residual_reset_and_cap(solver, oracle_lib, mv, monkeypatch):
     """Residual resets (r = b - S x every 10 CG iterations: a matvec of the
-    iterate) and the iteration cap, on both matvec forms."""
-    if pcg_t != "auto":
-        monkeypatch.setenv("BA_PCG_T", pcg_t)
+    iterate) and the iteration cap, on every matvec form."""
+    set_matvec(monkeypatch, mv)
     p = make_config("c2", scale=0.2)
     kw = dict(max_num_iterations=4, eta=1e-14, max_linear_solver_iterations=23)
     _, _, so, olog = oracle_lib.solve(p, oracle_opts(oracle_lib, "JACOBI", **kw))
@@ -279,14 +289,14 @@ def test_gpu_mixed_fp32_matches_fp64(solver, pc):
 @pytest.mark.gpu
 @pytest.mark.parametrize("pc", PRECONDITIONERS)
 @pytest.mark.parametrize("cfg,scale", [("c2", 0.2), ("c3", 0.01)])
-@pytest.mark.parametrize("pcg_t", ["auto", "1"])
-def test_gpu_mixed_fp32_matches_oracle_mixed(solver, oracle_lib, cfg, scale, pc, pcg_t, monkeypatch):
+@pytest.mark.parametrize("mv", MATVECS)
+def test_gpu_mixed_fp32_matches_oracle_mixed(solver, oracle_lib, cfg, scale, pc, mv, monkeypatch):
     """BA_MIXED_FP32 against the oracle's independent fp32-W restatement
-    (oracle precision 1): the same W entries rounded to float, so the
+    (oracle precision 1): the same W entries rounded to float in the matvec,
+    the rhs and the preconditioner, the back substitution in fp64, so the
     iterations match like the fp64 ones — cost 1e-9, identical decisions and
-    CG counts — on both matvec forms (BA_PCG_T=1 runs k_pcg_point_t<float>)."""
-    if pcg_t != "auto":
-        monkeypatch.setenv("BA_PCG_T", pcg_t)
+    CG counts — on every matvec form (mv "t" runs k_pcg_point_t<float>)."""
+    set_matvec(monkeypatch, mv)
     p = make_config(cfg, scale=scale)
     _, _, so, olog = oracle_lib.solve(p, oracle_opts(oracle_lib, pc, max_num_iterations=8, precision=1))
     _, _, sg, glog = gpu_solve(solver, p, preconditioner_type=pc, max_num_iterations=8, precision="MIXED_FP32")
@@ -304,11 +314,32 @@ def test_gpu_pcg_t_auto_threshold(solver, monkeypatch):
     p = make_config("c3", scale=2.0)
     assert 144 * p.n_obs > 256 * 2 ** 20
     kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=5)
+    monkeypatch.setenv("BA_WCM", "0")   # (the default camera-major copy has no product form)
     _, _, sa, la = gpu_solve(solver, p, **kw)
     monkeypatch.setenv("BA_PCG_T", "0")
     _, _, sb, lb = gpu_solve(solver, p, **kw)
     compare(la, lb, len(lb), rtol=1e-10)
     assert sa.final_cost == pytest.approx(sb.final_cost, rel=1e-10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
+@pytest.mark.parametrize("cfg,scale", [("c2", 0.2), ("c4", 0.01)])
+def test_gpu_camera_major_w_is_bitwise_the_gather(solver, cfg, scale, precision, monkeypatch):
+    """The camera-major copy of W (k_obs_w_cam) holds bitwise the point-major
+    records (the same lin_obs on the same table values) and the camera passes
+    read them in the same order: the whole trajectory is bitwise the gather
+    form's (also beyond 200 cameras: c4, global camera table)."""
+    p = make_config(cfg, scale=scale)
+    kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=6, precision=precision)
+    ca, xa, sa, la = gpu_solve(solver, p, **kw)
+    monkeypatch.setenv("BA_WCM", "0")
+    monkeypatch.setenv("BA_PCG_T", "0")
+    cb, xb, sb, lb = gpu_solve(solver, p, **kw)
+    assert sa.final_cost == sb.final_cost
+    assert [r["cost"] for r in la] == [r["cost"] for r in lb]
+    assert [r["linear_solver_iterations"] for r in la] == [r["linear_solver_iterations"] for r in lb]
+    assert np.array_equal(ca, cb) and np.array_equal(xa, xb)
 
 
 @pytest.mark.gpu
