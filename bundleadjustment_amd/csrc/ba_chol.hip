@@ -274,7 +274,7 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
     gran_store(yg + 2 * (size_t)(s0 + tid), val, epoch);
     y[s0 + tid] = val;
   }
-  if (tid == 0 && bad) scal[SL_CHOL_BAD] += 1.0;
+  if (tid == 0 && bad) scal[SL_CHOL_SPIN] += 1.0;   // (a granule that never came: not a pivot failure)
 }
 
 // Workgroups of k_back_flow the device holds at once (occupancy API x CUs).

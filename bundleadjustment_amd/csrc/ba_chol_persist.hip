@@ -30,8 +30,9 @@
 // (relaxed agent-scope loads + s_sleep), the workgroup barrier releases the
 // other waves, and EVERY load of handed-off bytes is a 16-B sc1 buffer load.
 // Flags carry the factorisation's epoch (never 0, never reset).  Spins are
-// bounded: a missing producer sets SL_CHOL_BAD (the step is then rejected as
-// a failed linear solve) instead of hanging the GPU.  Every workgroup of the
+// bounded: a missing producer (e.g. a grid that could not be resident beside
+// another process's work) sets SL_CHOL_SPIN instead of hanging the GPU; the
+// host then redoes the step with the per-step launches.  Every workgroup of the
 // grid must be resident at once: the host checks the occupancy first
 // (chol_persist_fits) and otherwise runs the per-step launches.
 #include "ba_chol.h"
@@ -267,7 +268,8 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   const Rsrc rV = make_rsrc(a.Vbuf, (size_t)(T + 1) * CB * CB * sizeof(double));
   unsigned* vflag = a.flags;
   unsigned* tflag = a.flags + T;
-  bool bad = false;
+  bool bad = false;    // a non-positive pivot
+  bool spin = false;   // a hand-off spin bound hit
 
   if (blockIdx.x == 0) {
     // ---------------- critical workgroup: the diagonal chain
@@ -333,13 +335,13 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         // it lands behind the panel GEMM
         const bool have_pref = pref_ok[0] == 1 && pref_ok[1] == 1;   // (read after the factor's last barrier)
         if (!have_pref) {
-          if (k >= 1) bad |= !wait_flag(&tflag[c * T + k], a.epoch);
+          if (k >= 1) spin |= !wait_flag(&tflag[c * T + k], a.epoch);
           const TileRegs tP = tile_fetch_sc1(rA, ld, s, kc, nrows, kc + kb);   // A_{c,k}
           tile_put(S3, tP);
         }
         // (its barrier also covers S3; the plain form is an LDS-only
         // barrier, so the diagonal tile's loads stay in flight across it)
-        if (c >= 2 && !have_diag) bad |= !wait_flag(&tflag[c * T + c], a.epoch);
+        if (c >= 2 && !have_diag) spin |= !wait_flag(&tflag[c * T + c], a.epoch);
         else lds_barrier();
         if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
         PSTAMP(c, 1);
@@ -386,6 +388,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
     PSTAMP(T - 1, 6);
     publish(&vflag[T - 1], a.epoch);
     if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
+    if (threadIdx.x == 0 && spin) atomicAdd(&a.scal[SL_CHOL_SPIN], 1.0);
 #ifdef BA_CHOL_STAMPS
     if (threadIdx.x == 0) g_stamp_on = 1;
 #endif
@@ -419,8 +422,8 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   auto stage_panels = [&](int k) {
     const int kc = k * CB, kb = min(CB, n - kc);
     if (k >= 1) {
-      bad |= !wait_flag(&tflag[I * T + k], a.epoch);
-      if (!diag) bad |= !wait_flag(&tflag[J * T + k], a.epoch);
+      spin |= !wait_flag(&tflag[I * T + k], a.epoch);
+      if (!diag) spin |= !wait_flag(&tflag[J * T + k], a.epoch);
     }
     const TileRegs tI = tile_fetch_sc1(rA, ld, r0, kc, nrows, kc + kb);        // A_{I,k}
     TileRegs tJ;
@@ -430,7 +433,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   };
   if (kmax >= 0) stage_panels(0);
   for (int k = 0; k <= kmax; ++k) {
-    bad |= !wait_flag(&vflag[k], a.epoch);
+    spin |= !wait_flag(&vflag[k], a.epoch);
     if (stamp && k == kmax) WSTAMP(J, 0);
     tile_put(S2, tile_fetch_sc1(rV, CB, k * CB, 0, (k + 1) * CB, CB));          // V_k (stored cleaned)
     __syncthreads();
@@ -499,6 +502,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   // through the same strip product; block row J has no rhs row here)
   if (I == J + 1) lds_to_global(S1, a.L, ld, c0, kmax * CB, CB, min(CB, n - kmax * CB));
   if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
+  if (threadIdx.x == 0 && spin) atomicAdd(&a.scal[SL_CHOL_SPIN], 1.0);
 }
 
 // grid of the persistent factorisation: 1 critical + one worker per tile

@@ -28,6 +28,7 @@ enum Slot {
   SL_ELIM_BAD,      // failed 3x3 point-block Cholesky count
   SL_GMAX_C, SL_GN2_C, SL_XN2_C, SL_STEP2_C,
   SL_CHOL_BAD,      // non-positive pivot in the reduced camera system
+  SL_CHOL_SPIN,     // a hand-off spin bound of the dataflow Cholesky / back substitution was hit (not a pivot failure)
   kNumSlots
 };
 
@@ -42,6 +43,7 @@ struct DevProblem {
   const int* pt_off;         // [np+1] CSR of observations by point
   const int* cam_off;        // [nvc+1] CSR of observations by active variable camera
   const int2* cam_op;        // [..] (sorted observation, its point) grouped by camera
+  const float2* uv_cm;       // [..] the pixel of each cam_op entry (camera-major copy of uv: streamed, not gathered)
   const int* vc;             // [nc] compact variable-camera index or -1
   const int* obs_vc;         // [no] vc of each observation's camera (one load instead of two dependent ones)
   const int* cam_of_vc;      // [nvc] camera id of a compact index
@@ -76,6 +78,8 @@ struct DevWork {
   double* Wcm;                       // [n_camobs][18] fp64
   float* Wcmf;                       // [n_camobs][18] fp32 (BA_MIXED_FP32)
   double* prec;                      // [np][16] point record for the camera-major W: X (3), var flag, s_p (3), L_p^-1 (6)
+  double* pxv;                       // [np][4] the linearisation point {X, var flag} (k_lin_point; camera-major gathers)
+  bool jdiag;                        // the diagonal Schur blocks J-free (k_cam_schur_diag_rc: prec gathered, W not read)
   float* Wf;                         // [no][18]  the same in fp32 (BA_MIXED_FP32)
   bool w32;                          // W blocks stored in Wf
   bool wcompact;                     // W as 128-B compact records (J-free fp64 DENSE_SCHUR; ba_kernels.hip)
@@ -107,6 +111,10 @@ struct DevWork {
   double* tpart;                     // [pcg_G][nvc][6] camera-side slices of one implicit matvec
   double* ppart;                     // [3][kMaxBlocks] per-block partials of the camera-side kernels
   int pcg_G;
+  const int2* pchunks;               // point-aligned observation chunks of <= 64 {start, end} (the PCG point pass)
+  const int* cam_pos;                // [no] camera-order position (cam_op index) of each observation, -1: fixed camera
+  bool tscat;                        // per-observation products stored in camera order (k_pcg_point_seg<.., SCAT>)
+  int npchunks;                      // 0: a point has more than 64 observations (value-pair point pass)
   bool pcg_folded;                   // exchange path: slices folded into slice 0 before the all-reduce
   const int* dup_off;                // [nvc+1] per variable camera: pairs of observations of one
   const int2* dup_pairs;             //   point by that camera (Schur-Jacobi diagonal cross terms)

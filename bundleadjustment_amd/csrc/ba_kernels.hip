@@ -1157,8 +1157,9 @@ __global__ __launch_bounds__(256) void k_cam_norms(DevProblem P, const double* _
 //   A = s Hpp s + D^2 (D = sqrt(diag / radius), ceres lm_diagonal_), L L^T = A,
 //   store L^-1 and u = L^-1 (s g)
 // ---------------------------------------------------------------------------
-// prec (optional, the camera-major W of ITERATIVE_SCHUR): one 128-B record
-// per point with what k_obs_w_cam gathers: X, the variable flag, s_p, L_p^-1
+// prec (optional: the camera-major J-free kernels of a step): one 128-B
+// record per point with what k_obs_w_cam / k_cam_schur_diag_rc gather: X, the
+// variable flag, s_p, L_p^-1, u_p
 constexpr int kPRec = 16;
 __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* __restrict__ Hpp,
                                                     const double* __restrict__ gp, const double* __restrict__ scale_p,
@@ -1215,9 +1216,12 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
     Linv[0 * np + p] = i00; Linv[1 * np + p] = i10; Linv[2 * np + p] = i11;
     Linv[3 * np + p] = i20; Linv[4 * np + p] = i21; Linv[5 * np + p] = i22;
     // u AoS [np][4] (one 32-B sector per point for the camera-side gathers)
-    u[4 * (size_t)p + 0] = i00 * gs[0];
-    u[4 * (size_t)p + 1] = i10 * gs[0] + i11 * gs[1];
-    u[4 * (size_t)p + 2] = i20 * gs[0] + i21 * gs[1] + i22 * gs[2];
+    const double u0 = i00 * gs[0];
+    const double u1 = i10 * gs[0] + i11 * gs[1];
+    const double u2 = i20 * gs[0] + i21 * gs[1] + i22 * gs[2];
+    u[4 * (size_t)p + 0] = u0;
+    u[4 * (size_t)p + 1] = u1;
+    u[4 * (size_t)p + 2] = u2;
     u[4 * (size_t)p + 3] = 0.0;
     if (prec) {
       double2* r = reinterpret_cast<double2*>(prec + (size_t)p * kPRec);
@@ -1227,8 +1231,8 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
       r[3] = make_double2(s[2], i00);
       r[4] = make_double2(i10, i11);
       r[5] = make_double2(i20, i21);
-      r[6] = make_double2(i22, 0.0);
-      r[7] = make_double2(0.0, 0.0);
+      r[6] = make_double2(i22, u0);
+      r[7] = make_double2(u1, u2);
     }
     acc[0] += ok ? 0.0 : 1.0;
   }
@@ -1642,9 +1646,10 @@ __device__ inline void wc_rows(const WcRaw& w, const WcCam& m, double (&c0)[6], 
 // diagonal Schur blocks and rhs (local part): one workgroup per camera
 //   S_cc = -sum W W^T (lower 21) ; b_c = -sum W u_p
 // ---------------------------------------------------------------------------
-// CM: W is the camera-major copy (row i of cam_op), streamed
-template <typename WT, bool CM = false>
-__global__ __launch_bounds__(256) void k_cam_schur_diag(DevProblem P, const WT* __restrict__ W,
+// CM: W is the camera-major copy (row i of cam_op), streamed.  NT threads per
+// camera slice
+template <typename WT, bool CM = false, int NT = 256>
+__global__ __launch_bounds__(NT) void k_cam_schur_diag(DevProblem P, const WT* __restrict__ W,
                                                         const double* __restrict__ u, double* __restrict__ S,
                                                         double* __restrict__ cpart) {
   __shared__ double lds[27 * 16];
@@ -1875,7 +1880,7 @@ __global__ __launch_bounds__(256) void k_cam_add_diag(DevProblem P, const double
   // k_cam_add_diag) must round identically
 #pragma clang fp contract(off)
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e == 0) scal[SL_CHOL_BAD] = 0.0;   // the Cholesky that follows flags failures here
+  if (e == 0) { scal[SL_CHOL_BAD] = 0.0; scal[SL_CHOL_SPIN] = 0.0; }   // the Cholesky that follows flags failures here
   if (e >= P.nvc * 27) return;
   const int v = e / 27, k = e - v * 27;
   const size_t ld = (size_t)P.ld;
@@ -1907,7 +1912,7 @@ __global__ __launch_bounds__(256) void k_cam_fold_diag(DevProblem P, const doubl
   // k_cam_add_diag) must round identically
 #pragma clang fp contract(off)
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e == 0) scal[SL_CHOL_BAD] = 0.0;   // the Cholesky that follows flags failures here
+  if (e == 0) { scal[SL_CHOL_BAD] = 0.0; scal[SL_CHOL_SPIN] = 0.0; }   // the Cholesky that follows flags failures here
   if (e >= P.nvc * 27) return;
   const int v = e / 27, k = e - v * 27;
   double acc = 0.0;
@@ -2103,11 +2108,14 @@ struct CamRegs {
 // is the compact records crec (k_cam_compact; the dual Rodrigues per
 // observation), gathered per observation
 template <int NT, int LANES, bool LAZY = false, int TB = 0>
+// pxv: the points as 32-B records {X, variable flag} for the camera-major
+// consumers (k_cam_assemble_rc: one sector per gathered point)
 __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __restrict__ rec,
                                                   const double* __restrict__ pts, double* __restrict__ Hpp,
                                                   double* __restrict__ gp, double* __restrict__ scale_p,
                                                   double* __restrict__ diag_p, int compute_scale, double min_diag,
-                                                  double max_diag, double* __restrict__ part) {
+                                                  double max_diag, double* __restrict__ part,
+                                                  double* __restrict__ pxv) {
   __shared__ double lds[5 * 16];
   __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
   __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
@@ -2206,6 +2214,11 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
         }
       }
     }
+    if (sl == 0) {
+      double2* d = reinterpret_cast<double2*>(pxv + 4 * (size_t)p);
+      d[0] = make_double2(X0, X1);
+      d[1] = make_double2(X2, pv ? 1.0 : 0.0);
+    }
     o0 = o0n; o1 = o1n;
     X0 = Y0; X1 = Y1; X2 = Y2;
     pv = pvn;
@@ -2226,10 +2239,12 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
 // Hcc (lower 21) and gc per variable camera, its observations in camera order
 // (k_cam_assemble's order: thread i takes i0 + tid, i0 + tid + NT, ...)
 // TB = 2: rec is the compact records crec (the camera's dual Rodrigues once
-// per workgroup: CamRcR), else the camera records (lin table in registers)
+// per workgroup: CamRcR), else the camera records (lin table in registers).
+// pxv: k_lin_point's 32-B point records {X, variable flag}; the pixels come
+// in camera order (uv_cm)
 template <int NT, int TB = 0>
 __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const double* __restrict__ rec,
-                                                        const double* __restrict__ pts, double* __restrict__ cpart,
+                                                        const double* __restrict__ pxv, double* __restrict__ cpart,
                                                         double* __restrict__ Hcc, double* __restrict__ gc) {
   __shared__ double lds[27 * 16];
   const int v = blockIdx.x;
@@ -2250,11 +2265,12 @@ __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const doub
   int i0, i1;
   cam_slice(P, v, i0, i1);
   for (int i = i0 + threadIdx.x; i < i1; i += NT) {
-    const int2 op = P.cam_op[i];
-    const int p = op.y;
+    const int p = P.cam_op[i].y;
+    const double2* xr = reinterpret_cast<const double2*>(pxv + 4 * (size_t)p);
+    const double2 x01 = xr[0], x2v = xr[1];
     double out[kJR];
     bool fin;
-    (void)lin_obs(P, cam, true, P.pt_var[p] != 0, pts[3 * p], pts[3 * p + 1], pts[3 * p + 2], P.uv[op.x], out, fin);
+    (void)lin_obs(P, cam, true, x2v.y != 0.0, x01.x, x01.y, x2v.x, P.uv_cm[i], out, fin);
     // cam_acc_jr on the record: Jc rows (0..11) and the residual (18, 19)
     const double rr[2] = {out[18], out[19]};
 #pragma unroll
@@ -2449,7 +2465,15 @@ __global__ __launch_bounds__(NT) void k_obs_w_cam(DevProblem P, const double* __
   int i0, i1;
   cam_slice(P, v, i0, i1);
   using V2 = typename std::conditional<sizeof(WT) == 8, double2, float2>::type;
-  for (int i = i0 + threadIdx.x; i < i1; i += NT) {
+  // each wave writes 64 consecutive rows through its LDS slot as contiguous
+  // wave stores (k_obs_w_rc's staging; a row-per-lane store of 72 / 144 B
+  // leaves every store instruction partial lines)
+  __shared__ double stage[(NT / 64) * 64 * kStageLd];
+  const int lane = threadIdx.x & 63, wv_ = threadIdx.x >> 6;
+  double* st = stage + wv_ * (64 * kStageLd);
+  for (int base = i0 + 64 * wv_; base < i1; base += NT) {   // (uniform per wave)
+    const int i = min(base + lane, i1 - 1);
+    const bool live = base + lane < i1;
     const int2 op = P.cam_op[i];
     double r[kPRec];
     {
@@ -2460,7 +2484,7 @@ __global__ __launch_bounds__(NT) void k_obs_w_cam(DevProblem P, const double* __
     const bool pv = r[3] != 0.0;
     double j[kJR];
     bool fin;
-    (void)lin_obs(P, cam, true, pv, r[0], r[1], r[2], P.uv[op.x], j, fin);
+    (void)lin_obs(P, cam, true, pv, r[0], r[1], r[2], P.uv_cm[i], j, fin);
     const double s0 = r[4], s1 = r[5], s2 = r[6];
     const double i00 = r[7], i10 = r[8], i11 = r[9], i20 = r[10], i21 = r[11], i22 = r[12];
     const double jp0[3] = {j[12] * s0, j[13] * s1, j[14] * s2};
@@ -2476,15 +2500,105 @@ __global__ __launch_bounds__(NT) void k_obs_w_cam(DevProblem P, const double* __
       wv[a * 3 + 1] = pv ? e0 * i10 + e1 * i11 : 0.0;
       wv[a * 3 + 2] = pv ? e0 * i20 + e1 * i21 + e2 * i22 : 0.0;
     }
-    V2* dst = reinterpret_cast<V2*>(Wcm + (size_t)i * kWRec);
 #pragma unroll
-    for (int k = 0; k < kWRec / 2; ++k) {
-      V2 t;
-      t.x = (WT)wv[2 * k];
-      t.y = (WT)wv[2 * k + 1];
-      dst[k] = t;
+    for (int k = 0; k < kWRec; ++k) st[lane * kStageLd + k] = live ? wv[k] : 0.0;
+    wave_lds_sync();
+    constexpr int NIT = kWRec / 2;
+    V2 ov[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int e = it * 64 + lane;
+      const int r = e / NIT, f = 2 * (e - r * NIT);
+      ov[it].x = (WT)st[r * kStageLd + f];
+      ov[it].y = (WT)st[r * kStageLd + f + 1];
+    }
+    wave_lds_sync();
+    V2* dst = reinterpret_cast<V2*>(Wcm + (size_t)base * kWRec);
+    const int nrec = min(64, i1 - base);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int e = it * 64 + lane;
+      if (e / NIT < nrec) dst[e] = ov[it];
     }
   }
+}
+
+// The diagonal Schur blocks and the reduced rhs per camera, J-free
+// (k_cam_schur_diag without W): the camera's table row (or its compact
+// record's dual Rodrigues) in registers, per observation the point's
+// 128-B record (prec: X, s_p, L_p^-1, u_p) and the pixel in camera order,
+// W_o formed as k_obs_w_rc forms it and consumed at once:
+//   -sum W W^T (lower 21), -sum W u_p (6).  W32: W_o rounded to fp32 first
+// (BA_MIXED_FP32: the preconditioner and the rhs see the stored fp32 blocks).
+// Replaces a 72 / 144-B gather per observation from the point-major W.
+template <int NT, int TB, bool W32>
+__global__ __launch_bounds__(NT) void k_cam_schur_diag_rc(DevProblem P, const double* __restrict__ rec,
+                                                          const double* __restrict__ prec,
+                                                          const double* __restrict__ scale_c,
+                                                          double* __restrict__ cpart) {
+  __shared__ double lds[27 * 16];
+  const int v = blockIdx.x;
+  const int c = P.cam_of_vc[v];
+  typename std::conditional<TB == 2, CamRcR, CamRegs>::type cam;
+  if constexpr (TB == 2) {
+    cam.make(cam_rc(rec, c));
+  } else {
+    const double2* s2 = reinterpret_cast<const double2*>(rec + (size_t)c * kCamRec + kRecL);
+#pragma unroll
+    for (int k = 0; k < kLin / 2; ++k) { const double2 q = s2[k]; cam.t[2 * k] = q.x; cam.t[2 * k + 1] = q.y; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) cam.k[k] = (double)P.K[9 * c + k];
+  }
+  double sc[6];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) sc[a] = scale_c[(size_t)v * 6 + a];
+  double acc[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+  int i0, i1;
+  cam_slice(P, v, i0, i1);
+  for (int i = i0 + threadIdx.x; i < i1; i += NT) {
+    const int p = P.cam_op[i].y;
+    double r[kPRec];
+    {
+      const double2* q = reinterpret_cast<const double2*>(prec + (size_t)p * kPRec);
+#pragma unroll
+      for (int k = 0; k < kPRec / 2; ++k) { const double2 t = q[k]; r[2 * k] = t.x; r[2 * k + 1] = t.y; }
+    }
+    const bool pv = r[3] != 0.0;
+    double j[kJR];
+    bool fin;
+    (void)lin_obs(P, cam, true, pv, r[0], r[1], r[2], P.uv_cm[i], j, fin);
+    const double s0 = r[4], s1 = r[5], s2 = r[6];
+    const double i00 = r[7], i10 = r[8], i11 = r[9], i20 = r[10], i21 = r[11], i22 = r[12];
+    const double jp0[3] = {j[12] * s0, j[13] * s1, j[14] * s2};
+    const double jp1[3] = {j[15] * s0, j[16] * s1, j[17] * s2};
+    double w[kWRec];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {   // k_obs_w_rc's arithmetic
+      const double c0 = j[a] * sc[a], c1 = j[6 + a] * sc[a];
+      const double e0 = c0 * jp0[0] + c1 * jp1[0];
+      const double e1 = c0 * jp0[1] + c1 * jp1[1];
+      const double e2 = c0 * jp0[2] + c1 * jp1[2];
+      double w0 = pv ? e0 * i00 : 0.0;
+      double w1 = pv ? e0 * i10 + e1 * i11 : 0.0;
+      double w2 = pv ? e0 * i20 + e1 * i21 + e2 * i22 : 0.0;
+      if constexpr (W32) { w0 = (double)(float)w0; w1 = (double)(float)w1; w2 = (double)(float)w2; }
+      w[a * 3 + 0] = w0; w[a * 3 + 1] = w1; w[a * 3 + 2] = w2;
+    }
+    const double u0 = r[13], u1 = r[14], u2 = r[15];
+    int t = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {   // k_cam_schur_diag's accumulation
+#pragma unroll
+      for (int b = 0; b <= a; ++b) acc[t++] += w[a * 3] * w[b * 3] + w[a * 3 + 1] * w[b * 3 + 1] + w[a * 3 + 2] * w[b * 3 + 2];
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] += w[a * 3] * u0 + w[a * 3 + 1] * u1 + w[a * 3 + 2] * u2;
+  }
+  double tot[27];
+  block_sum<27>(acc, lds, tot);
+  cam_slice_store(tot, cpart, v, P.nvc);
 }
 
 // k_cam_schur_diag on compact records:
@@ -2975,7 +3089,7 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
     const int tb = jr_tab(P, W);
     const int g = std::max(1, std::min(want, tb ? kMaxBlocks : 2 * lds_grid(1 << 30)));
     using KF = void (*)(DevProblem, const double*, const double*, double*, double*, double*, double*, int, double,
-                        double, double*);
+                        double, double*, double*);
     KF kern;
     if (tb) {
       if (tb == 1)
@@ -2986,7 +3100,7 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
                          : (L == 2 ? k_lin_point<256, 2, false, 2> : (L == 8 ? k_lin_point<256, 8, false, 2> : k_lin_point<256, 4, false, 2>));
       hipExtLaunchKernelGGL(kern, dim3(g), dim3(NT), 0, s, t0, t1, 0, P, (const double*)(tb == 1 ? W.gtbl : W.crec),
                             (const double*)W.pts, W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag,
-                            max_diag, W.part);
+                            max_diag, W.part, W.pxv);
       return;
     }
     if (NT == 256) {
@@ -2997,7 +3111,7 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
       else kern = L == 2 ? k_lin_point<512, 2> : (L == 8 ? k_lin_point<512, 8> : k_lin_point<512, 4>);
     }
     hipExtLaunchKernelGGL(kern, dim3(g), dim3(NT), 0, s, t0, t1, 0, P, (const double*)W.rec, (const double*)W.pts,
-                          W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
+                          W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag, max_diag, W.part, W.pxv);
     return;
   }
   const bool many = P.nc > kLinLdsCams;
@@ -3018,17 +3132,31 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
     if (sp < 0) { const char* e = getenv("BA_CA_SPLIT"); sp = e ? atoi(e) : 1; }
     const int sl = std::max(1, std::min(sp, W.cam_split));
     const dim3 g(P.nvc, sl);
-    if (jr_tab(P, W) == 2)   // (the compact records: the camera's dual Rodrigues once per workgroup)
-      hipLaunchKernelGGL((k_cam_assemble_rc<512, 2>), g, dim3(512), 0, s, P, (const double*)W.crec, (const double*)W.pts,
-                         W.cpart, W.Hcc, W.gc);
-    else if (nt == 128)
-      hipLaunchKernelGGL(k_cam_assemble_rc<128>, g, dim3(128), 0, s, P, (const double*)W.rec, (const double*)W.pts,
+    if (jr_tab(P, W) == 2) {
+      // (the compact records: the camera's dual Rodrigues once per
+      // workgroup).  Threads per camera by its observations (~8 per thread):
+      // at 10k cameras x 1250 observations a 512-thread workgroup had 2.4
+      // per thread and the per-workgroup setup and 27-value reduction
+      // dominated (C5 shard 642 us)
+      const int per = (int)std::max<long long>(1, (long long)P.no / std::max(P.nvc, 1));
+      const int t = per >= 8 * 512 ? 512 : (per >= 8 * 256 ? 256 : (per >= 8 * 128 ? 128 : 64));
+      const double* cr = W.crec;
+      if (t == 512)
+        hipLaunchKernelGGL((k_cam_assemble_rc<512, 2>), g, dim3(512), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
+      else if (t == 256)
+        hipLaunchKernelGGL((k_cam_assemble_rc<256, 2>), g, dim3(256), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
+      else if (t == 128)
+        hipLaunchKernelGGL((k_cam_assemble_rc<128, 2>), g, dim3(128), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
+      else
+        hipLaunchKernelGGL((k_cam_assemble_rc<64, 2>), g, dim3(64), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
+    } else if (nt == 128)
+      hipLaunchKernelGGL(k_cam_assemble_rc<128>, g, dim3(128), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
                          W.cpart, W.Hcc, W.gc);
     else if (nt == 256)
-      hipLaunchKernelGGL(k_cam_assemble_rc<256>, g, dim3(256), 0, s, P, (const double*)W.rec, (const double*)W.pts,
+      hipLaunchKernelGGL(k_cam_assemble_rc<256>, g, dim3(256), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
                          W.cpart, W.Hcc, W.gc);
     else
-      hipLaunchKernelGGL(k_cam_assemble_rc<512>, g, dim3(512), 0, s, P, (const double*)W.rec, (const double*)W.pts,
+      hipLaunchKernelGGL(k_cam_assemble_rc<512>, g, dim3(512), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
                          W.cpart, W.Hcc, W.gc);
     if (sl > 1)
       hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
@@ -3066,18 +3194,27 @@ void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale,
 void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
   const bool cm = W.wcm && W.jrfree;
   hipLaunchKernelGGL(k_point_elim, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.Hpp, W.gp, W.scale_p, W.diag_p,
-                     radius, W.Linv, W.u, W.part, (const double*)W.pts, cm ? W.prec : nullptr);
+                     radius, W.Linv, W.u, W.part, (const double*)W.pts, cm || W.jdiag ? W.prec : nullptr);
   if (P.no == 0) return;
   const int tb = jr_tab(P, W);
   if (cm && P.nvc > 0) {   // the camera-major copy (the point-major W below stays: the point passes read it)
     const dim3 g(P.nvc, W.cam_split);
     if (tb == 2) {
-      if (W.w32)
-        hipLaunchKernelGGL((k_obs_w_cam<256, float, 2>), g, dim3(256), 0, s, P, (const double*)W.crec,
-                           (const double*)W.prec, W.scale_c, W.Wcmf);
-      else
-        hipLaunchKernelGGL((k_obs_w_cam<256, double, 2>), g, dim3(256), 0, s, P, (const double*)W.crec,
-                           (const double*)W.prec, W.scale_c, W.Wcm);
+      // threads per camera slice by its observations (~8 per thread, as
+      // k_cam_assemble_rc)
+      const int per = (int)std::max<long long>(1, (long long)P.no / std::max(P.nvc * W.cam_split, 1));
+      const int t = per >= 8 * 256 ? 256 : (per >= 8 * 128 ? 128 : 64);
+      const double* cr = W.crec;
+      const double* pr = W.prec;
+      if (W.w32) {
+        if (t == 256) hipLaunchKernelGGL((k_obs_w_cam<256, float, 2>), g, dim3(256), 0, s, P, cr, pr, W.scale_c, W.Wcmf);
+        else if (t == 128) hipLaunchKernelGGL((k_obs_w_cam<128, float, 2>), g, dim3(128), 0, s, P, cr, pr, W.scale_c, W.Wcmf);
+        else hipLaunchKernelGGL((k_obs_w_cam<64, float, 2>), g, dim3(64), 0, s, P, cr, pr, W.scale_c, W.Wcmf);
+      } else {
+        if (t == 256) hipLaunchKernelGGL((k_obs_w_cam<256, double, 2>), g, dim3(256), 0, s, P, cr, pr, W.scale_c, W.Wcm);
+        else if (t == 128) hipLaunchKernelGGL((k_obs_w_cam<128, double, 2>), g, dim3(128), 0, s, P, cr, pr, W.scale_c, W.Wcm);
+        else hipLaunchKernelGGL((k_obs_w_cam<64, double, 2>), g, dim3(64), 0, s, P, cr, pr, W.scale_c, W.Wcm);
+      }
     } else {
       if (W.w32)
         hipLaunchKernelGGL((k_obs_w_cam<256, float>), g, dim3(256), 0, s, P, (const double*)W.rec,
@@ -3093,6 +3230,9 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
     if (W.w32)
       hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<float, false, 1> : k_obs_w_rc<float, false, 2>), dim3(g),
                          dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.Wf);
+    else if (W.wcompact)   // (DENSE_SCHUR up to kWcCams variable cameras: the compact records)
+      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, true, 1> : k_obs_w_rc<double, true, 2>), dim3(g),
+                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.W);
     else
       hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, false, 1> : k_obs_w_rc<double, false, 2>), dim3(g),
                          dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.W);
@@ -3129,14 +3269,37 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
   static int dsplit = -1;   // diagnostics: BA_DIAG_SPLIT overrides the slice count
   if (dsplit < 0) { const char* e = getenv("BA_DIAG_SPLIT"); dsplit = e ? atoi(e) : 0; }
   const int sl = dsplit > 0 ? std::min(dsplit, kCamSplit) : W.cam_split;
-  if (W.wcm && W.jrfree) {
-    if (W.w32)
-      hipLaunchKernelGGL((k_cam_schur_diag<float, true>), dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wcmf, W.u, W.S,
-                         W.cpart);
-    else
-      hipLaunchKernelGGL((k_cam_schur_diag<double, true>), dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wcm, W.u, W.S,
-                         W.cpart);
-  } else if (W.w32)
+  // threads per camera slice by its observations (~8 per thread): 256, or
+  // 128 at C5's 1250 observations per camera
+  const int per = (int)std::max<long long>(1, (long long)P.no / std::max(P.nvc * sl, 1));
+  const bool t128 = per < 8 * 256;
+  if (W.jdiag) {   // J-free (no W read): the camera's row in registers, the point records gathered
+    const dim3 g(P.nvc, sl);
+    const int tb = jr_tab(P, W) == 2 ? 2 : 0;
+    const double* src = tb == 2 ? (const double*)W.crec : (const double*)W.rec;
+    const double* pr = W.prec;
+#define BA_DIAG_RC(NT_, TB_, W32_) \
+    hipLaunchKernelGGL((k_cam_schur_diag_rc<NT_, TB_, W32_>), g, dim3(NT_), 0, s, P, src, pr, W.scale_c, W.cpart)
+    if (tb == 2) {
+      if (t128) { if (W.w32) BA_DIAG_RC(128, 2, true); else BA_DIAG_RC(128, 2, false); }
+      else { if (W.w32) BA_DIAG_RC(256, 2, true); else BA_DIAG_RC(256, 2, false); }
+    } else {
+      if (t128) { if (W.w32) BA_DIAG_RC(128, 0, true); else BA_DIAG_RC(128, 0, false); }
+      else { if (W.w32) BA_DIAG_RC(256, 0, true); else BA_DIAG_RC(256, 0, false); }
+    }
+#undef BA_DIAG_RC
+  } else if (W.wcm && W.jrfree) {
+    const dim3 g(P.nvc, sl);
+    if (W.w32) {
+      if (t128) hipLaunchKernelGGL((k_cam_schur_diag<float, true, 128>), g, dim3(128), 0, s, P, W.Wcmf, W.u, W.S, W.cpart);
+      else hipLaunchKernelGGL((k_cam_schur_diag<float, true>), g, dim3(kThreads), 0, s, P, W.Wcmf, W.u, W.S, W.cpart);
+    } else {
+      if (t128) hipLaunchKernelGGL((k_cam_schur_diag<double, true, 128>), g, dim3(128), 0, s, P, W.Wcm, W.u, W.S, W.cpart);
+      else hipLaunchKernelGGL((k_cam_schur_diag<double, true>), g, dim3(kThreads), 0, s, P, W.Wcm, W.u, W.S, W.cpart);
+    }
+  } else if (W.w32 && t128)
+    hipLaunchKernelGGL((k_cam_schur_diag<float, false, 128>), dim3(P.nvc, sl), dim3(128), 0, s, P, W.Wf, W.u, W.S, W.cpart);
+  else if (W.w32)
     hipLaunchKernelGGL(k_cam_schur_diag<float>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wf, W.u, W.S, W.cpart);
   else if (W.wcompact) {
     // diagnostics: BA_DIAG_NT (64 / 128 / 256 threads), BA_DIAG_PREF (0 / 1)

@@ -30,6 +30,12 @@ namespace bahip {
 
 constexpr int kPcgThreads = 1024;   // camera-side workgroup
 
+// LDS hand-off between the lanes of one wave (in-order DS operations)
+__device__ inline void wave_lds_sync_pcg() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ inline bool zero_or_inf(double x) { return x == 0.0 || isinf(x); }   // ceres IsZeroOrInfinity
 
 // lower-triangle index of (a, b), a >= b
@@ -339,6 +345,156 @@ __global__ __launch_bounds__(256) void k_pcg_cam_t(DevProblem P, const double* _
   }
 }
 
+// Point pass over point-aligned chunks of <= 64 observations, one wave per
+// chunk (ensure_pcg builds the chunk list; points with more than 64
+// observations keep k_pcg_point / k_pcg_point_t).  The chunk's W records
+// arrive as contiguous 8-B-per-lane wave loads (512 B per instruction)
+// through the wave's LDS slot; each lane then forms W_o^T x_c for its own
+// observation from LDS, and a segmented inclusive scan over the lanes (a
+// fixed order for a given layout) sums each point's run, whose last lane
+// stores v_p.  TOUT: every lane then takes its point's v_p back (shuffle
+// from the run's last lane) and forms t_o = W_o v_p, stored as contiguous
+// wave stores.  (k_pcg_point_t's value-pair loop issued ~4 loads per 8-16 B
+// of W and re-read every record for t_o: 3.4 TB/s at C4.)
+// SCAT (with TOUT): t_o is stored at its camera-order position cam_pos[o]
+// instead (one 48-B scattered store per observation), so that the camera
+// pass streams the products (k_pcg_cam_s) instead of gathering them.
+template <typename WT, bool TOUT, bool SCAT = false>
+__global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2* __restrict__ chunks, int nchunks,
+                                                       const WT* __restrict__ Wm, const double* __restrict__ xv,
+                                                       double* __restrict__ vpt, double* __restrict__ tobs,
+                                                       const int* __restrict__ cam_pos,
+                                                       const double* __restrict__ st) {
+  if (st[PS_DONE] != 0.0) return;
+  constexpr int REC = 18;
+  // fp64: 16-B units (a record is 9, 16-B aligned; the per-lane 144-B record
+  // reads from LDS are ds_read_b128 at 9 slots' stride: every 16-lane group
+  // hits 16 distinct slots).  fp32 (72-B records, 8-B aligned): 8-B units
+  using U = typename std::conditional<sizeof(WT) == 8, uint4, unsigned long long>::type;
+  constexpr int UN = REC * (int)sizeof(WT) / (int)sizeof(U);   // units per record: 9
+  __shared__ U stage[4][64 * UN];
+  __shared__ double tst[TOUT ? 4 : 1][TOUT ? 64 * 6 : 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int ch = blockIdx.x * 4 + w; ch < nchunks; ch += gridDim.x * 4) {   // (uniform per wave)
+    const int2 cr = chunks[ch];
+    const int o0 = cr.x, n = cr.y - cr.x;
+    const U* src = reinterpret_cast<const U*>(Wm + (size_t)o0 * REC);
+    const int nu = n * UN;
+#pragma unroll
+    for (int k = 0; k < UN; ++k) {
+      const int e = k * 64 + lane;
+      if (e < nu) stage[w][e] = src[e];
+    }
+    const bool live = lane < n;
+    const int o = o0 + min(lane, n - 1);
+    const int vc = P.obs_vc[o];
+    const int pt = live ? P.obs_pt[o] : -1;
+    const double2* xc = reinterpret_cast<const double2*>(xv + 6 * (size_t)max(vc, 0));
+    const double2 x01 = xc[0], x23 = xc[1], x45 = xc[2];
+    const double x[6] = {x01.x, x01.y, x23.x, x23.y, x45.x, x45.y};
+    wave_lds_sync_pcg();
+    double wr[REC];
+    {
+      const U* ru = &stage[w][0] + (size_t)min(lane, n - 1) * UN;
+      U ur[UN];
+#pragma unroll
+      for (int k = 0; k < UN; ++k) ur[k] = ru[k];
+      const WT* r = reinterpret_cast<const WT*>(ur);
+#pragma unroll
+      for (int k = 0; k < REC; ++k) wr[k] = (double)r[k];
+    }
+    double v[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      double a = 0.0;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) a += wr[b * 3 + k] * x[b];
+      v[k] = live ? a : 0.0;
+    }
+    // segmented inclusive scan: runs of equal pt (the chunk holds whole points)
+    const int ptp = __shfl_up(pt, 1, 64);
+    const bool head = lane == 0 || pt != ptp;
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long upto = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1);
+    const int s0 = 63 - __clzll(heads & upto);   // this lane's run head
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      double y[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) y[k] = __shfl_up(v[k], off, 64);
+      if (lane - off >= s0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) v[k] += y[k];
+      }
+    }
+    const unsigned long long after = heads & ~upto;   // heads past this lane
+    const int last = after ? __ffsll((long long)after) - 2 : n - 1;   // this run's last lane
+    if (live && lane == last) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) vpt[3 * (size_t)pt + k] = v[k];
+    }
+    if constexpr (TOUT && SCAT) {
+      double vp[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) vp[k] = __shfl(v[k], last, 64);
+      const int q = live ? cam_pos[o] : -1;   // (-1: a fixed camera, no camera-side entry)
+      if (q >= 0) {
+        double2* d = reinterpret_cast<double2*>(tobs + 6 * (size_t)q);
+#pragma unroll
+        for (int a = 0; a < 6; a += 2)
+          d[a / 2] = make_double2(wr[a * 3] * vp[0] + wr[a * 3 + 1] * vp[1] + wr[a * 3 + 2] * vp[2],
+                                  wr[a * 3 + 3] * vp[0] + wr[a * 3 + 4] * vp[1] + wr[a * 3 + 5] * vp[2]);
+      }
+    } else if constexpr (TOUT) {
+      double vp[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) vp[k] = __shfl(v[k], last, 64);
+      {   // (three 16-B LDS stores at 3 slots' stride: conflict-free)
+        double tv[6];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) tv[a] = wr[a * 3] * vp[0] + wr[a * 3 + 1] * vp[1] + wr[a * 3 + 2] * vp[2];
+        double2* td = reinterpret_cast<double2*>(&tst[w][lane * 6]);
+#pragma unroll
+        for (int a = 0; a < 3; ++a) td[a] = make_double2(tv[2 * a], tv[2 * a + 1]);
+      }
+      wave_lds_sync_pcg();
+      double2* dst = reinterpret_cast<double2*>(tobs + 6 * (size_t)o0);
+      const double2* tsrc = reinterpret_cast<const double2*>(&tst[w][0]);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int e = k * 64 + lane;
+        if (e < 3 * n) dst[e] = tsrc[e];
+      }
+    }
+    wave_lds_sync_pcg();   // (the slots are rewritten by the next chunk)
+  }
+}
+
+// camera pass over products stored in camera order (k_pcg_point_seg<.., SCAT>):
+// the same sums as k_pcg_cam_t in the same order, the reads contiguous
+__global__ __launch_bounds__(256) void k_pcg_cam_s(DevProblem P, const double* __restrict__ tcm,
+                                                   double* __restrict__ tpart, const double* __restrict__ st) {
+  if (st[PS_DONE] != 0.0) return;
+  __shared__ double lds[6 * 16];
+  const int v = blockIdx.x, g = blockIdx.y, G = gridDim.y;
+  const int a0 = P.cam_off[v], a1 = P.cam_off[v + 1];
+  const int len = (a1 - a0 + G - 1) / G;
+  const int i0 = min(a1, a0 + g * len), i1 = min(a1, i0 + len);
+  double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const double2* t = reinterpret_cast<const double2*>(tcm + 6 * (size_t)i);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { const double2 x = t[k]; acc[2 * k] += x.x; acc[2 * k + 1] += x.y; }
+  }
+  double tot[6];
+  block_sum<6>(acc, lds, tot);
+  if (threadIdx.x == 0) {
+    double* dst = tpart + ((size_t)g * P.nvc + v) * 6;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) dst[a] = tot[a];
+  }
+}
+
 // Sum of the G matvec slices of camera v entry a, in slice order (the same
 // order in k_pcg_tfold, so the exchange path, which folds the slices before
 // its all-reduce, rounds exactly like the single-rank path)
@@ -604,6 +760,47 @@ void launch_pcg_setup(const DevProblem& P, const DevWork& W, double radius, cons
 }
 void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s) {
   const double* st = W.scal + kNumSlots;
+  if (W.npchunks > 0) {   // point-aligned chunks of <= 64 observations (k_pcg_point_seg)
+    const int g = std::max(1, std::min((W.npchunks + 3) / 4, 16384));
+    if (W.tobs && W.tscat) {   // products scattered to camera order, streamed by the camera pass
+      if (W.w32)
+        hipLaunchKernelGGL((k_pcg_point_seg<float, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks,
+                           W.Wf, vec, W.vpt, W.tobs, W.cam_pos, st);
+      else
+        hipLaunchKernelGGL((k_pcg_point_seg<double, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks,
+                           W.W, vec, W.vpt, W.tobs, W.cam_pos, st);
+      hipLaunchKernelGGL(k_pcg_cam_s, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
+      return;
+    }
+    if (W.tobs) {
+      if (W.w32)
+        hipLaunchKernelGGL((k_pcg_point_seg<float, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks, W.Wf,
+                           vec, W.vpt, W.tobs, nullptr, st);
+      else
+        hipLaunchKernelGGL((k_pcg_point_seg<double, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks, W.W,
+                           vec, W.vpt, W.tobs, nullptr, st);
+      hipLaunchKernelGGL(k_pcg_cam_t, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
+      return;
+    }
+    const bool cm = W.wcm && W.jrfree;
+    if (W.w32) {
+      hipLaunchKernelGGL((k_pcg_point_seg<float, false>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks, W.Wf,
+                         vec, W.vpt, nullptr, nullptr, st);
+      if (cm)
+        hipLaunchKernelGGL((k_pcg_cam<float, true>), dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wcmf, W.vpt, W.tpart, st);
+      else
+        hipLaunchKernelGGL(k_pcg_cam<float>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wf, W.vpt, W.tpart, st);
+    } else {
+      hipLaunchKernelGGL((k_pcg_point_seg<double, false>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks, W.W,
+                         vec, W.vpt, nullptr, nullptr, st);
+      if (cm)
+        hipLaunchKernelGGL((k_pcg_cam<double, true>), dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wcm, W.vpt, W.tpart,
+                           st);
+      else
+        hipLaunchKernelGGL(k_pcg_cam<double>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.W, W.vpt, W.tpart, st);
+    }
+    return;
+  }
   if (W.tobs) {
     if (W.w32)
       hipLaunchKernelGGL(k_pcg_point_t<float>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.Wf, vec, W.tobs, st);

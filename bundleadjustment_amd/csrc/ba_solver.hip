@@ -359,6 +359,9 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
     std::vector<int2> cam_op(cam_obs.size());
     for (size_t i = 0; i < cam_obs.size(); ++i) cam_op[i] = make_int2(cam_obs[i], obs_pt[cam_obs[i]]);
     P.cam_op = ctx->upload(cam_op);
+    std::vector<float2> uv_cm(cam_obs.size());
+    for (size_t i = 0; i < cam_obs.size(); ++i) uv_cm[i] = uv[cam_obs[i]];
+    P.uv_cm = ctx->upload(uv_cm);
   }
   P.vc = ctx->upload(vc);
   {
@@ -405,6 +408,7 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.gtbl = W.jrfree && nc > bahip::kLinLdsCamsHost && W.jtab == 1 ? ctx->dalloc<double>((size_t)48 * nc) : nullptr;
   W.JR = W.jrfree ? nullptr : ctx->dalloc<double>((size_t)(bahip::jr_ja_host(nc) + 8) * no);   // JA [no][jr_ja] + JB [no][8] (ba_kernels.hip)
   W.delta_p = ctx->dalloc<double>(3 * (size_t)np);
+  W.pxv = ctx->dalloc<double>(4 * (size_t)np);
   W.Hpp = ctx->dalloc<double>(6 * (size_t)np);
   W.gp = ctx->dalloc<double>(3 * (size_t)np);
   W.scale_p = ctx->dalloc<double>(3 * (size_t)np);
@@ -502,10 +506,13 @@ void ensure_dense(ba_ctx* ctx) {
   {
     // persistent factorisation (one launch) when the per-step form would not
     // split and the whole grid is resident; BA_CHOL_PERSIST=0 forces the
-    // per-step launches (A/B)
+    // per-step launches (A/B).  Not with the host-staged transport: its ranks
+    // may share one GPU, and their persistent grids need not all fit at once
+    // (a spin bound would then be hit on some ranks only, and the ranks'
+    // steps would diverge)
     const int T = (ctx->n + 63) / 64, TR = (ctx->n + 1 + 63) / 64;
     const char* env = std::getenv("BA_CHOL_PERSIST");
-    W.chol_persist = ctx->n > 0 && T < bahip::chol_split_blocks() && !(env && env[0] == '0') &&
+    W.chol_persist = ctx->n > 0 && T < bahip::chol_split_blocks() && !(env && env[0] == '0') && !ctx->host_fn &&
                      bahip::chol_persist_fits(ctx->device, ctx->n);
     const size_t nf = (size_t)T + (size_t)TR * T;
     W.cflags = ctx->dalloc<unsigned>(nf);
@@ -598,6 +605,35 @@ void ensure_pcg(ba_ctx* ctx) {
   }
   W.dup_off = ctx->upload(dup_off);
   W.dup_pairs = ctx->upload(dup);
+  {
+    // point-aligned chunks of <= 64 observations for the PCG point pass
+    // (k_pcg_point_seg); BA_PCG_SEG=0 keeps the value-pair passes
+    const char* e = std::getenv("BA_PCG_SEG");
+    std::vector<int2> ch;
+    bool ok = !(e && e[0] == '0');
+    int start = 0;
+    for (int p = 0; p < np && ok; ++p) {
+      const int a = ctx->h_pt_off[p], b = ctx->h_pt_off[p + 1];
+      if (b - a > 64) { ok = false; break; }
+      if (b - start > 64) { ch.push_back(make_int2(start, a)); start = a; }
+    }
+    if (ok && ctx->no > start) ch.push_back(make_int2(start, ctx->no));
+    W.npchunks = ok ? (int)ch.size() : 0;
+    W.pchunks = ok && !ch.empty() ? ctx->upload(ch) : nullptr;
+    if (!W.pchunks) W.npchunks = 0;
+    // camera-order positions for the scattered products
+    std::vector<int> pos(std::max(ctx->no, 1), -1);
+    {
+      std::vector<int> fill(nvc + 1, 0);
+      // (cam_op is the observations of each variable camera in increasing
+      // sorted index: rebuild the same order)
+      std::vector<int> cnt(nvc + 1, 0);
+      for (int o = 0; o < ctx->no; ++o) { const int v = ctx->h_vc[ctx->h_obs_cam[o]]; if (v >= 0) cnt[v + 1]++; }
+      for (int v = 0; v < nvc; ++v) cnt[v + 1] += cnt[v];
+      for (int o = 0; o < ctx->no; ++o) { const int v = ctx->h_vc[ctx->h_obs_cam[o]]; if (v >= 0) pos[o] = cnt[v]++; }
+    }
+    W.cam_pos = ctx->upload(pos);
+  }
   HIP_OK(hipStreamSynchronize(ctx->stream));
   ctx->have_pcg = true;
 }
@@ -672,7 +708,7 @@ LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max
   return lin_result(ctx);
 }
 
-struct StepResult { bool linear_ok; double mcc, cand_cost, step_norm; int ls_iters; };
+struct StepResult { bool linear_ok; double mcc, cand_cost, step_norm; int ls_iters; bool spin; };
 
 // DENSE_SCHUR: explicit reduced camera system (form_reduced_dense) + dense
 // Cholesky
@@ -729,10 +765,16 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
     const int force = fe ? atoi(fe) : -1;
     // (decided from the largest rank's shard: every rank runs the same path)
     const bool big = 144.0 * (double)ctx->max_no > 256.0 * 1024 * 1024;
-    const bool use_t = !W.wcm && (force >= 0 ? force != 0 : (!W.w32 && big));
+    // (with the point-aligned chunks the products go to camera order and are
+    // streamed: then also for the fp32 W)
+    const bool use_t = !W.wcm && (force >= 0 ? force != 0 : big && (!W.w32 || W.npchunks > 0));
     if (use_t && !ctx->tobs_buf) ctx->tobs_buf = ctx->dalloc<double>(6 * (size_t)std::max(ctx->no, 1));
     if (!use_t && ctx->tobs_buf) { ctx->dfree(ctx->tobs_buf); ctx->tobs_buf = nullptr; }   // 48 B/obs back
     W.tobs = use_t ? ctx->tobs_buf : nullptr;
+    // the products in camera order (streamed camera pass): BA_TSCAT=0 / 1
+    // forces the gathered form / this one
+    const char* se = getenv("BA_TSCAT");
+    W.tscat = use_t && W.npchunks > 0 && (se ? atoi(se) != 0 : true);
   }
   PcgOpts po{o.eta, o.min_linear_solver_iterations, std::max(1, o.max_linear_solver_iterations),
              o.preconditioner_type == BA_SCHUR_JACOBI ? 1 : 0};
@@ -783,20 +825,6 @@ void step_w_storage(ba_ctx* ctx, const ba_options& o) {
   if (W.w32 && !W.Wf) W.Wf = ctx->dalloc<float>(18 * (size_t)ctx->no);
   if (!W.w32 && !W.W) W.W = ctx->dalloc<double>(18 * (size_t)ctx->no);
   {
-    // ITERATIVE_SCHUR, J-free: a camera-major copy of W written beside the
-    // point-major one (k_obs_w_cam), streamed by the diagonal Schur blocks and
-    // by every CG iteration's camera pass.  BA_WCM=0 / 1 (read per solve)
-    // forces it off / on
-    const char* e = getenv("BA_WCM");
-    const int force = e ? atoi(e) : -1;
-    W.wcm = W.jrfree && o.linear_solver == BA_ITERATIVE_SCHUR && (force >= 0 ? force != 0 : true);
-    if (W.wcm) {
-      if (!W.prec) W.prec = ctx->dalloc<double>(16 * (size_t)std::max(ctx->np, 1));
-      if (W.w32 && !W.Wcmf) W.Wcmf = ctx->dalloc<float>(18 * (size_t)std::max(ctx->ncamobs, 1));
-      if (!W.w32 && !W.Wcm) W.Wcm = ctx->dalloc<double>(18 * (size_t)std::max(ctx->ncamobs, 1));
-    }
-  }
-  {
     // compact W records (ba_kernels.hip k_obs_w_rc<double, true>): the
     // J-free fp64 DENSE_SCHUR iteration with the fused point step (the only
     // W readers are then k_cam_schur_diag_c and k_schur_pairs_c);
@@ -804,6 +832,27 @@ void step_w_storage(ba_ctx* ctx, const ba_options& o) {
     const char* e = getenv("BA_WCOMPACT");
     W.wcompact = W.jrfree && ctx->nvc <= bahip::kWcCamsHost && !W.w32 && o.linear_solver == BA_DENSE_SCHUR &&
                  !(e && e[0] == '0') && point_step_fused();
+  }
+  {
+    // ITERATIVE_SCHUR, J-free: a camera-major copy of W written beside the
+    // point-major one (k_obs_w_cam), streamed by the diagonal Schur blocks and
+    // by every CG iteration's camera pass.  Measured: the extra pass costs
+    // what the streamed camera passes save (C4 3.84 vs 4.51 ms, C5 shard
+    // 5.08 vs 5.17 ms without / with it: profiles/r04_v2_*), so off unless
+    // BA_WCM=1 (read per solve)
+    const char* e = getenv("BA_WCM");
+    const int force = e ? atoi(e) : -1;
+    W.wcm = W.jrfree && o.linear_solver == BA_ITERATIVE_SCHUR && (force >= 0 ? force != 0 : false);
+    // the diagonal Schur blocks J-free (k_cam_schur_diag_rc) where they would
+    // gather the 18-value W (ITERATIVE_SCHUR, or DENSE_SCHUR without compact
+    // records); BA_JDIAG=0 (read per solve) gathers W
+    const char* de = getenv("BA_JDIAG");
+    W.jdiag = W.jrfree && !W.wcm && !W.wcompact && !(de && de[0] == '0');
+    if ((W.wcm || W.jdiag) && !W.prec) W.prec = ctx->dalloc<double>(16 * (size_t)std::max(ctx->np, 1));
+    if (W.wcm) {
+      if (W.w32 && !W.Wcmf) W.Wcmf = ctx->dalloc<float>(18 * (size_t)std::max(ctx->ncamobs, 1));
+      if (!W.w32 && !W.Wcm) W.Wcm = ctx->dalloc<double>(18 * (size_t)std::max(ctx->ncamobs, 1));
+    }
   }
 }
 int step_enqueue(ba_ctx* ctx, double radius, const ba_options& o) {
@@ -843,6 +892,7 @@ StepResult step_result(ba_ctx* ctx, int ls_iters) {
   r.cand_cost = h[SL_CAND_BAD] > 0.0 || !std::isfinite(h[SL_CCOST]) ? std::numeric_limits<double>::max() : h[SL_CCOST];
   r.step_norm = std::sqrt(h[SL_STEP2_P] + h[SL_STEP2_C]);
   r.ls_iters = ls_iters;
+  r.spin = h[SL_CHOL_SPIN] != 0.0;
   return r;
 }
 
@@ -955,6 +1005,23 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
     }
     have_step = false;
     StepResult st = step_result(ctx, ls);
+    if (st.spin) {
+      // a hand-off of the persistent factorisation never came (its grid
+      // could not be fully resident, e.g. beside another process's kernels):
+      // not a pivot failure.  Redo the step with the per-step launches (and
+      // keep them for this context); the back substitution's own spins have
+      // no fallback.
+      // (with collectives the ranks could not agree on a redo: one process
+      // per GPU there, where the grid fits by construction)
+      if (!ctx->W.chol_persist || ctx->coll())
+        throw BaError{BA_ERR_DEVICE, "dense Cholesky: a hand-off spin bound was hit"};
+      ctx->W.chol_persist = false;
+      if (ctx->lin_at_cand) linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, false, true);
+      ls = step_enqueue(ctx, radius, o);
+      ctx->read_scalars();
+      st = step_result(ctx, ls);
+      if (st.spin) throw BaError{BA_ERR_DEVICE, "dense Cholesky: a hand-off spin bound was hit"};
+    }
     ctx->t_solve += now_s() - ts;
     it.linear_solver_iterations = st.ls_iters;
     const bool valid = st.linear_ok && st.mcc > 0.0;
@@ -1508,6 +1575,7 @@ int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double ra
         linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, trj, true);
       }
       ctx->wait_scalars();
+      if (ctx->h_scal[SL_CHOL_SPIN] != 0.0) throw BaError{BA_ERR_DEVICE, "dense Cholesky: a hand-off spin bound was hit"};
       {   // (the iteration's record has arrived: its host wall time)
         const double t = now_s();
         ctx->bench_ms[i] = (t - th) * 1e3;
