@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int i = h + 4 * q;
-      t += V[(size_t)j * CB + i] * ys[i];
+      t += (i <= j ? V[(size_t)j * CB + i] : 0.0) * ys[i];   // (V lower triangular; the persistent form leaves its upper blocks unwritten)
     }
     part[h][j] = t;
     __syncthreads();
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(256) void k_back_flow(const double* __restrict__ A,
   {
     const double* V = Vall + (size_t)K * CB * CB;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) vk[q] = V[(size_t)(h + 4 * q) * CB + j];
+    for (int q = 0; q < 16; ++q) vk[q] = h + 4 * q >= j ? V[(size_t)(h + 4 * q) * CB + j] : 0.0;   // (lower triangle only)
   }
   double acc = 0.0;
   for (int J = T - 1; J > K; --J) {

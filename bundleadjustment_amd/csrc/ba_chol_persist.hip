@@ -285,6 +285,22 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
     // never live across the loop's back edge.
     auto end_step = [&](int cp) {
       const int sp = cp * CB, bp = min(CB, n - sp), mp = min(CB, nrows - sp);
+      if (bp == CB) {
+        // a full block: only the lower block triangle (10 of 16 blocks) is
+        // read again — the panel products skip the upper blocks, k_back_flow
+        // masks them — and the diagonal blocks already hold exact zeros
+        // above the diagonal (diag_inverse16): no clean-up pass, 5 / 8 of
+        // the stores (the upper blocks' Vbuf entries stay stale, unread)
+        for (int e = ctid(); e < 10 * 16 * 8; e += 256) {
+          const int blk = e >> 7, rr = (e >> 3) & 15, cc = (e & 7) * 2;
+          const int bi = blk < 1 ? 0 : (blk < 3 ? 1 : (blk < 6 ? 2 : 3));
+          const int bj = blk - bi * (bi + 1) / 2;
+          const int i = 16 * bi + rr, j = 16 * bj + cc;
+          st_sc1(rV, ((size_t)cp * CB * CB + (size_t)i * CB + j) * sizeof(double), make_double2(S2[i][j], S2[i][j + 1]));
+        }
+        bad |= cw.bad != 0;
+        return;
+      }
       for (int e2 = ctid(); e2 < CB * CB / 2; e2 += 256) {
         const int i = (2 * e2) / CB, j = (2 * e2) % CB;
         double v[2];

@@ -375,16 +375,33 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
   __shared__ U stage[4][64 * UN];
   __shared__ double tst[TOUT ? 4 : 1][TOUT ? 64 * 6 : 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int ch = blockIdx.x * 4 + w; ch < nchunks; ch += gridDim.x * 4) {   // (uniform per wave)
-    const int2 cr = chunks[ch];
+  // the next chunk's W units are loaded one chunk ahead, into registers, so
+  // that their HBM latency runs under this chunk's arithmetic and scan
+  const int cstride = gridDim.x * 4;
+  auto fetch = [&](int c, U (&u)[UN], int2& crr) {
+    crr = chunks[c];
+    const U* src = reinterpret_cast<const U*>(Wm + (size_t)crr.x * REC);
+    const int nu = (crr.y - crr.x) * UN;
+#pragma unroll
+    for (int k = 0; k < UN; ++k) {
+      const int e = k * 64 + lane;
+      if (e < nu) u[k] = src[e];
+    }
+  };
+  int ch = blockIdx.x * 4 + w;
+  U nxt[UN];
+  int2 ncr = make_int2(0, 0);
+  if (ch < nchunks) fetch(ch, nxt, ncr);
+  for (; ch < nchunks; ch += cstride) {   // (uniform per wave)
+    const int2 cr = ncr;
     const int o0 = cr.x, n = cr.y - cr.x;
-    const U* src = reinterpret_cast<const U*>(Wm + (size_t)o0 * REC);
     const int nu = n * UN;
 #pragma unroll
     for (int k = 0; k < UN; ++k) {
       const int e = k * 64 + lane;
-      if (e < nu) stage[w][e] = src[e];
+      if (e < nu) stage[w][e] = nxt[k];
     }
+    if (ch + cstride < nchunks) fetch(ch + cstride, nxt, ncr);
     const bool live = lane < n;
     const int o = o0 + min(lane, n - 1);
     const int vc = P.obs_vc[o];
