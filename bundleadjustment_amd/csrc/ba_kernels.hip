@@ -1777,13 +1777,14 @@ __global__ __launch_bounds__(256) void k_schur_pairs(DevProblem P, const int4* _
 // with the camera constants re-read from LDS per pair to keep 2 waves per
 // SIMD: 168 vs 165 us, profiles/r03_v13_ab_pairs_ca.txt.)
 
+// (236 VGPRs: 2 waves per SIMD; forcing 3 or 4 spills 109 / 262 VGPRs)
 __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4* __restrict__ blocks,
                                                        const int* __restrict__ xoff, const int2* __restrict__ pairs,
                                                        const double* __restrict__ Wc,
                                                        const double* __restrict__ scale_c, double* __restrict__ S) {
-  // the camera constants of every variable camera in LDS (nvc <= 200 in the
-  // J-free mode: 14.4 KB), read per pair (registers: 1 -> 2 waves per SIMD)
-  __shared__ WcCam ctab[kWcCams];
+  // the camera constants of every variable camera in LDS (dynamic: 72 B per
+  // camera, 14.4 KB at 200 cameras), read per pair (registers)
+  extern __shared__ WcCam ctab[];
   for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
   __syncthreads();
   constexpr int PL = kPairLanes, BPW = 64 / PL;
@@ -2315,8 +2316,10 @@ constexpr int kObsWRcWaves = 6;   // table + K + scales + 6 staging slots fit th
 // table gtbl (1) or the compact records crec (2); the camera scalings are
 // read from scale_c
 template <typename WT, bool COMPACT = false, int TB = 0>
+// pxv: k_lin_point's 32-B point records {X, variable flag} (one aligned
+// 32-B read per observation instead of 24 B of X plus the flag byte)
 __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, const double* __restrict__ rec,
-                                                                const double* __restrict__ pts,
+                                                                const double* __restrict__ pxv,
                                                                 const double* __restrict__ scale_c,
                                                                 const double* __restrict__ scale_p,
                                                                 const double* __restrict__ Linv, WT* __restrict__ W) {
@@ -2351,9 +2354,11 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
     const int cn = P.obs_cam[ocn], pn = P.obs_pt[ocn];
     const float2 uvn = P.uv[ocn];
     const int v = P.vc[c];
-    const bool pv = P.pt_var[p] != 0;
+    const double2* xr = reinterpret_cast<const double2*>(pxv + 4 * (size_t)p);
+    const double2 x01 = xr[0], x2v = xr[1];
+    const bool pv = x2v.y != 0.0;
     const bool live = base + lane < P.no && v >= 0 && pv;
-    const double X0 = pts[3 * p], X1 = pts[3 * p + 1], X2 = pts[3 * p + 2];
+    const double X0 = x01.x, X1 = x01.y, X2 = x2v.x;
     const double s0 = scale_p[p], s1 = scale_p[np + p], s2 = scale_p[2 * np + p];
     const double i00 = Linv[p], i10 = Linv[np + p], i11 = Linv[2 * np + p];
     const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
@@ -3229,26 +3234,26 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
     const double* src = tb == 1 ? W.gtbl : W.crec;
     if (W.w32)
       hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<float, false, 1> : k_obs_w_rc<float, false, 2>), dim3(g),
-                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.Wf);
+                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
     else if (W.wcompact)   // (DENSE_SCHUR up to kWcCams variable cameras: the compact records)
       hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, true, 1> : k_obs_w_rc<double, true, 2>), dim3(g),
-                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.W);
+                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
     else
       hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, false, 1> : k_obs_w_rc<double, false, 2>), dim3(g),
-                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.W);
+                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
     return;
   }
   if (W.jrfree) {   // one 148-KB-LDS workgroup per CU
     const int g = lds_grid(P.no);
     if (W.w32)
       hipLaunchKernelGGL(k_obs_w_rc<float>, dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, (const double*)W.rec,
-                         (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.Wf);
+                         (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
     else if (W.wcompact)
       hipLaunchKernelGGL((k_obs_w_rc<double, true>), dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, (const double*)W.rec,
-                         (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.W);
+                         (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
     else
       hipLaunchKernelGGL(k_obs_w_rc<double>, dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, (const double*)W.rec,
-                         (const double*)W.pts, W.scale_c, W.scale_p, W.Linv, W.W);
+                         (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
     return;
   }
   const int g = lds_grid(P.no);
@@ -3347,7 +3352,8 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (grid > grid_cap) grid = grid_cap;
   grid = (grid + 7) / 8 * 8;   // k_schur_pairs' XCD ranges need a multiple of 8
   if (W.wcompact)
-    hipLaunchKernelGGL(k_schur_pairs_c, dim3(grid), dim3(256), 0, s, P, W.blocks, xoff, W.pairs, W.W, W.scale_c, W.S);
+    hipLaunchKernelGGL(k_schur_pairs_c, dim3(grid), dim3(256), sizeof(WcCam) * (size_t)P.nvc, s, P, W.blocks, xoff,
+                       W.pairs, W.W, W.scale_c, W.S);
   else
     hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, xoff, W.pairs, W.W, W.S);
 }

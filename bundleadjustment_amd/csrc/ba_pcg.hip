@@ -375,8 +375,11 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
   __shared__ U stage[4][64 * UN];
   __shared__ double tst[TOUT ? 4 : 1][TOUT ? 64 * 6 : 1];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  // the next chunk's W units are loaded one chunk ahead, into registers, so
-  // that their HBM latency runs under this chunk's arithmetic and scan
+  // fp32: the next chunk's W units are loaded one chunk ahead, into
+  // registers, so that their latency runs under this chunk's arithmetic and
+  // scan (C5 shard 4.20 -> 4.09 ms per LM iteration).  fp64: the 36 VGPRs
+  // this needs cost occupancy (C4 seg pass 300 -> 547 us): loaded in place
+  constexpr bool PF = sizeof(WT) == 4;
   const int cstride = gridDim.x * 4;
   auto fetch = [&](int c, U (&u)[UN], int2& crr) {
     crr = chunks[c];
@@ -389,19 +392,30 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
     }
   };
   int ch = blockIdx.x * 4 + w;
-  U nxt[UN];
+  U nxt[PF ? UN : 1];
   int2 ncr = make_int2(0, 0);
-  if (ch < nchunks) fetch(ch, nxt, ncr);
+  if constexpr (PF) {
+    if (ch < nchunks) fetch(ch, nxt, ncr);
+  }
   for (; ch < nchunks; ch += cstride) {   // (uniform per wave)
-    const int2 cr = ncr;
+    const int2 cr = PF ? ncr : chunks[ch];
     const int o0 = cr.x, n = cr.y - cr.x;
     const int nu = n * UN;
+    if constexpr (PF) {
 #pragma unroll
-    for (int k = 0; k < UN; ++k) {
-      const int e = k * 64 + lane;
-      if (e < nu) stage[w][e] = nxt[k];
+      for (int k = 0; k < UN; ++k) {
+        const int e = k * 64 + lane;
+        if (e < nu) stage[w][e] = nxt[k];
+      }
+      if (ch + cstride < nchunks) fetch(ch + cstride, nxt, ncr);
+    } else {
+      const U* src = reinterpret_cast<const U*>(Wm + (size_t)o0 * REC);
+#pragma unroll
+      for (int k = 0; k < UN; ++k) {
+        const int e = k * 64 + lane;
+        if (e < nu) stage[w][e] = src[e];
+      }
     }
-    if (ch + cstride < nchunks) fetch(ch + cstride, nxt, ncr);
     const bool live = lane < n;
     const int o = o0 + min(lane, n - 1);
     const int vc = P.obs_vc[o];

@@ -907,14 +907,20 @@ void accept_candidate(ba_ctx* ctx) {
 // the step's scalar record: it runs while the host reads the record and
 // decides, and it is the next iteration's linearisation when the step is
 // accepted (the common case).  A rejected step re-linearises at x
-// (ctx->lin_at_cand); the values are the same either way.  Single rank only
-// (the exchange path's collectives keep their order).  BA_SPEC_LIN=0: off.
+// (ctx->lin_at_cand); the values are the same either way.  With collectives
+// too: every rank enqueues the same linearisation (identical decisions), so
+// the all-reduces keep one order across the ranks.  BA_SPEC_LIN=0: off
+// (ba_ctx::read_env).
 void spec_lin_enqueue(ba_ctx* ctx, const ba_options& o) {
-  static const bool on = [] { const char* e = std::getenv("BA_SPEC_LIN"); return !(e && e[0] == '0'); }();
-  if (!on || ctx->coll()) return;
-  accept_candidate(ctx);   // (the kernels read W.cams / W.pts: point them at the candidate)
+  if (!ctx->spec_lin) return;
+  // the kernels read W.cams / W.pts: point them at the candidate for the
+  // enqueue only (restored on every exit, a throw included)
+  struct Swap {
+    ba_ctx* c;
+    explicit Swap(ba_ctx* x) : c(x) { accept_candidate(c); }
+    ~Swap() { accept_candidate(c); }
+  } swap(ctx);
   linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, false, true);
-  accept_candidate(ctx);
   ctx->lin_at_cand = true;
 }
 

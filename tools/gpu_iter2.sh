@@ -14,4 +14,11 @@ if [ "${TESTS:-1}" = "1" ]; then
 fi
 timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; python3 -c "import json; d=json.load(open('$OUT/bench.json')); print('c3', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])"; stop_on_fault $rc
+if [ "${PROF3:-1}" = "1" ]; then
+  export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c3 -o run -- \
+    python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_c3.json 2> $OUT/prof_c3.err
+  rc=$?; stop_on_fault $rc
+  echo "== c3"; python3 tools/kstats.py $OUT/prof_c3/run_kernel_stats.csv 12 | head -20
+fi
 bash tools/gpu_big.sh
