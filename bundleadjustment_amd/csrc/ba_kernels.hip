@@ -1870,6 +1870,135 @@ __global__ __launch_bounds__(256) void k_schur_pairs_c(DevProblem P, const int4*
   }
 }
 
+// k_schur_pairs_c with the two records of every pair gathered into LDS by
+// LDS-DMA (global_load_lds_dwordx4) instead of per-lane 16-B register loads.
+// A per-lane record load touches 64 different lines per wave-instruction (8
+// instructions per record); here 8 lanes fetch one record's eight 16-B
+// pieces, so an instruction covers 8 whole lines.  The pieces land
+// lane-linear (record q at q * 128 B), with the piece order XOR-swizzled by
+// (q >> 1) & 7 through the SOURCE address, so that the per-lane record reads
+// (ds_read_b128, 16-lane groups) are conflict-free.  One buffer per wave:
+// the next pair's records are requested right after this pair's are read out
+// of LDS, and arrive during its arithmetic.  Same lanes, pairs, products and
+// reduction as k_schur_pairs_c: bitwise the same S.
+__device__ __forceinline__ void glds16(const double* src, double* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+constexpr int kPairsDmaLds = 4 * 2 * 64 * kWcRec * (int)sizeof(double);   // 64 KB: 4 waves x (row, partner) x 64 records
+
+__global__ __launch_bounds__(256) void k_schur_pairs_cd(DevProblem P, const int4* __restrict__ blocks,
+                                                        const int* __restrict__ xoff, const int2* __restrict__ pairs,
+                                                        const double* __restrict__ Wc,
+                                                        const double* __restrict__ scale_c, double* __restrict__ S) {
+  extern __shared__ double dsm[];
+  WcCam* ctab = reinterpret_cast<WcCam*>(dsm + kPairsDmaLds / (int)sizeof(double));
+  for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
+  __syncthreads();
+  constexpr int PL = kPairLanes, BPW = 64 / PL;
+  const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
+  const int xcd = blockIdx.x & 7, wx = blockIdx.x >> 3, nwx = gridDim.x >> 3;
+  const int r0 = xoff[xcd], r1 = xoff[xcd + 1];
+  const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  double* rbuf = dsm + (size_t)wv * 2 * 64 * kWcRec;   // row camera's records [64][16]
+  double* pbuf = rbuf + 64 * kWcRec;                    // partner records
+  const int swr = (lane >> 1) & 7;                      // this lane's record: piece p at slot p ^ swr
+  const size_t ld = (size_t)P.ld;
+  // the 8 DMA pieces of this lane: record q = (lane >> 3) + 8 i, source piece
+  // (lane & 7) ^ ((q >> 1) & 7), destination slot lane & 7
+  auto issue = [&](int2 pr) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = (lane >> 3) + 8 * i;
+      const int ra = __shfl(pr.x, q), rb = __shfl(pr.y, q);
+      const int sp = 2 * ((lane & 7) ^ ((q >> 1) & 7));
+      glds16(Wc + (size_t)ra * kWcRec + sp, rbuf + i * 128);
+      glds16(Wc + (size_t)rb * kWcRec + sp, pbuf + i * 128);
+    }
+  };
+  auto read_rec = [&](const double* buf) {
+    WcRaw w;
+    const double* r = buf + lane * kWcRec;
+#pragma unroll
+    for (int p = 0; p < kWcRec / 2; ++p) {
+      const double2 t = *reinterpret_cast<const double2*>(r + 2 * (p ^ swr));
+      w.r[2 * p] = t.x;
+      w.r[2 * p + 1] = t.y;
+    }
+    return w;
+  };
+  for (int base = r0 + (wx * nwv + wv) * BPW; base < r1; base += nwx * nwv * BPW) {
+    const int bi = base + sub;
+    const bool live = bi < r1;
+    const int4 blk = live ? blocks[bi] : make_int4(0, 0, 0, 0);
+    const WcCam& mI = ctab[blk.x];
+    const WcCam& mJ = ctab[blk.y];
+    double acc[36];
+#pragma unroll
+    for (int k = 0; k < 36; ++k) acc[k] = 0.0;
+    // pairs per lane, wave maximum (the loop below is wave-uniform)
+    const int len = blk.w - blk.z;
+    int nit = len > sl ? (len - sl + PL - 1) / PL : 0;
+#pragma unroll
+    for (int x = 32; x >= 1; x >>= 1) nit = max(nit, __shfl_xor(nit, x));
+    int e = blk.z + sl;
+    int2 pr = e < blk.w ? pairs[e] : make_int2(0, 0);
+    int2 pn = e + PL < blk.w ? pairs[e + PL] : make_int2(0, 0);
+    if (nit > 0) issue(pr);
+    for (int t = 0; t < nit; ++t, e += PL) {
+      // this pair's DMA has landed (the compiler does not order LDS reads
+      // after an LDS-DMA on its own)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const WcRaw wa = read_rec(rbuf);
+      const WcRaw wb = read_rec(pbuf);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the buffers are refilled
+      if (t + 1 < nit) {
+        issue(pn);
+        pn = e + 2 * PL < blk.w ? pairs[e + 2 * PL] : make_int2(0, 0);
+      }
+      if (e < blk.w) {
+        double ca0[6], ca1[6], cb0[6], cb1[6];
+        wc_rows(wa, mI, ca0, ca1);
+        wc_rows(wb, mJ, cb0, cb1);
+        const double* za0 = wa.r + 9;
+        const double* za1 = wa.r + 12;
+        const double* zb0 = wb.r + 9;
+        const double* zb1 = wb.r + 12;
+        const double m00 = za0[0] * zb0[0] + za0[1] * zb0[1] + za0[2] * zb0[2];
+        const double m01 = za0[0] * zb1[0] + za0[1] * zb1[1] + za0[2] * zb1[2];
+        const double m10 = za1[0] * zb0[0] + za1[1] * zb0[1] + za1[2] * zb0[2];
+        const double m11 = za1[0] * zb1[0] + za1[1] * zb1[1] + za1[2] * zb1[2];
+        double n0[6], n1[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          n0[j] = m00 * cb0[j] + m01 * cb1[j];
+          n1[j] = m10 * cb0[j] + m11 * cb1[j];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+          for (int j = 0; j < 6; ++j) acc[i * 6 + j] += ca0[i] * n0[j] + ca1[i] * n1[j];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 36; ++k) {
+      double v = acc[k];
+#pragma unroll
+      for (int x = PL / 2; x >= 1; x >>= 1) v += __shfl_xor(v, x, PL);
+      acc[k] = v;
+    }
+    if (live) {
+      const int I = blk.x, Jb = blk.y;
+#pragma unroll
+      for (int k = 0; k < 36; ++k) {
+        if ((k % PL) != sl) continue;
+        const int i = k / 6, j = k % 6;
+        if (I != Jb) S[(size_t)(6 * I + i) * ld + 6 * Jb + j] = -acc[k];
+        else if (j <= i) S[(size_t)(6 * I + i) * ld + 6 * I + j] -= acc[k];  // duplicate obs of one point by one camera
+      }
+    }
+  }
+}
+
 // S_cc += s Hcc s + D^2 ;  b_c += s * g_c      (after any cross-rank reduction)
 // one thread per (camera, entry): 21 lower entries of the diagonal block and
 // 6 rhs entries (a thread per camera serialised ~50 dependent accesses)
@@ -3351,8 +3480,17 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (grid == 0) return;
   if (grid > grid_cap) grid = grid_cap;
   grid = (grid + 7) / 8 * 8;   // k_schur_pairs' XCD ranges need a multiple of 8
-  if (W.wcompact)
-    hipLaunchKernelGGL(k_schur_pairs_c, dim3(grid), dim3(256), sizeof(WcCam) * (size_t)P.nvc, s, P, W.blocks, xoff,
+  // BA_PAIRS_DMA=1: the LDS-DMA gather form (two workgroups per CU while its
+  // 64 KB + the camera constants fit half the LDS)
+  // (read per launch: tests compare both forms in one process)
+  const char* dma_env = getenv("BA_PAIRS_DMA");
+  const int dma = dma_env ? atoi(dma_env) : 0;
+  const size_t ctab_bytes = sizeof(WcCam) * (size_t)P.nvc;
+  if (W.wcompact && dma && kPairsDmaLds + ctab_bytes <= 80 * 1024)
+    hipLaunchKernelGGL(k_schur_pairs_cd, dim3(grid), dim3(256), kPairsDmaLds + ctab_bytes, s, P, W.blocks, xoff,
+                       W.pairs, W.W, W.scale_c, W.S);
+  else if (W.wcompact)
+    hipLaunchKernelGGL(k_schur_pairs_c, dim3(grid), dim3(256), ctab_bytes, s, P, W.blocks, xoff,
                        W.pairs, W.W, W.scale_c, W.S);
   else
     hipLaunchKernelGGL(k_schur_pairs, dim3(grid), dim3(256), 0, s, P, W.blocks, xoff, W.pairs, W.W, W.S);

@@ -771,12 +771,14 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
     if (use_t && !ctx->tobs_buf) ctx->tobs_buf = ctx->dalloc<double>(6 * (size_t)std::max(ctx->no, 1));
     if (!use_t && ctx->tobs_buf) { ctx->dfree(ctx->tobs_buf); ctx->tobs_buf = nullptr; }   // 48 B/obs back
     W.tobs = use_t ? ctx->tobs_buf : nullptr;
-    // the products in camera order (streamed camera pass) for the fp64 W
-    // (C4 3.53 vs 3.56 ms); with the fp32 W the 48-B scattered stores cost
-    // more than the gathers they save (C5 shard 4.41 vs 4.20 ms,
-    // profiles/r04_v4_jdiag_tscat_ab.txt).  BA_TSCAT=0 / 1 forces it off / on
+    // the products in camera order (streamed camera pass, BA_TSCAT=1): off
+    // by default.  fp32 W: the 48-B scattered stores cost more than the
+    // gathers they save (C5 shard 4.41 vs 4.20 ms,
+    // profiles/r04_v4_jdiag_tscat_ab.txt); fp64 W: within the spread between
+    // boxes (C4 3.53 vs 3.56 ms on one box, 3.76 vs 3.60 ms on another,
+    // profiles/r04_v6_tscat_ab.txt)
     const char* se = getenv("BA_TSCAT");
-    W.tscat = use_t && W.npchunks > 0 && (se ? atoi(se) != 0 : !W.w32);
+    W.tscat = use_t && W.npchunks > 0 && se && atoi(se) != 0;
   }
   PcgOpts po{o.eta, o.min_linear_solver_iterations, std::max(1, o.max_linear_solver_iterations),
              o.preconditioner_type == BA_SCHUR_JACOBI ? 1 : 0};

@@ -84,3 +84,19 @@ def test_jfree_blocks_and_reduced_system_match_oracle(oracle_lib, cfg, scale):
     d = np.arange(n)
     assert np.allclose(got["S"][d, d], lhs[d, d], rtol=1e-11, atol=0), "S diagonal"
     close_to_scale(got["rhs"], rhs, 1e-10, "rhs")
+
+
+@pytest.mark.timeout(600)
+def test_pair_pass_dma_gather_is_bitwise_the_register_gather(monkeypatch):
+    """k_schur_pairs_cd (records gathered into LDS by LDS-DMA, BA_PAIRS_DMA=1)
+    forms the same products in the same order as k_schur_pairs_c: S and the
+    rhs must agree bitwise (C3 camera count: the LDS form's size limit)."""
+    p = make_config("c3", scale=0.2)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("BA_PAIRS_DMA", mode)
+        with Solver(0) as s:
+            s.set_problem(p)
+            out[mode] = s.debug_blocks(1e4)
+    assert np.array_equal(out["0"]["S"], out["1"]["S"])
+    assert np.array_equal(out["0"]["rhs"], out["1"]["rhs"])
