@@ -2816,6 +2816,95 @@ __global__ __launch_bounds__(NT) void k_cam_schur_diag_c(DevProblem P, const dou
   cam_slice_store(tot, cpart, v, P.nvc);
 }
 
+// k_cam_schur_diag_c with the compact records and u gathered into LDS by
+// LDS-DMA (as k_schur_pairs_cd: 8 lanes per 128-B record, 2 per 32-B u
+// record, pieces XOR-swizzled through the source address), one wave per
+// workgroup.  The next round's observation indices are loaded one round
+// ahead, its DMA issued right after this round's records are read out of
+// LDS.  The same adds per lane in the same order: bitwise k_cam_schur_diag_c.
+__global__ __launch_bounds__(64) void k_cam_schur_diag_cd(DevProblem P, const double* __restrict__ Wc,
+                                                          const double* __restrict__ scale_c,
+                                                          const double* __restrict__ u, double* __restrict__ cpart) {
+  __shared__ double lds[27 * 16];
+  __shared__ __attribute__((aligned(16))) double rbuf[64 * kWcRec];
+  __shared__ __attribute__((aligned(16))) double ubuf[64 * 4];
+  const int v = blockIdx.x;
+  WcCam m;
+  m.load(P, scale_c, v);
+  double acc[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+  int i0, i1;
+  cam_slice(P, v, i0, i1);
+  const int lane = threadIdx.x;
+  const int swr = (lane >> 1) & 7;
+  auto issue = [&](int2 op) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = (lane >> 3) + 8 * k;
+      const int oq = __shfl(op.x, q);
+      glds16(Wc + (size_t)oq * kWcRec + 2 * ((lane & 7) ^ ((q >> 1) & 7)), rbuf + k * 128);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = (lane >> 1) + 32 * k;
+      const int pq = __shfl(op.y, q);
+      glds16(u + 4 * (size_t)pq + 2 * (lane & 1), ubuf + k * 128);
+    }
+  };
+  const int nr = (i1 - i0 + 63) >> 6;   // rounds (uniform)
+  int i = i0 + lane;
+  int2 op = i < i1 ? P.cam_op[i] : make_int2(0, 0);
+  int2 opn = i + 64 < i1 ? P.cam_op[i + 64] : make_int2(0, 0);
+  if (nr > 0) issue(op);
+  for (int r = 0; r < nr; ++r, i += 64) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this round's DMA has landed
+    WcRaw w;
+    const double* rr = rbuf + lane * kWcRec;
+#pragma unroll
+    for (int p = 0; p < kWcRec / 2; ++p) {
+      const double2 t = *reinterpret_cast<const double2*>(rr + 2 * (p ^ swr));
+      w.r[2 * p] = t.x;
+      w.r[2 * p + 1] = t.y;
+    }
+    const double2 u01 = *reinterpret_cast<const double2*>(ubuf + 4 * lane);
+    const double u2 = ubuf[4 * lane + 2];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the refill
+    if (r + 1 < nr) {
+      issue(opn);
+      opn = i + 128 < i1 ? P.cam_op[i + 128] : make_int2(0, 0);
+    }
+    if (i < i1) {
+      double c0[6], c1[6];
+      wc_rows(w, m, c0, c1);
+      const double* z0 = w.r + 9;
+      const double* z1 = w.r + 12;
+      const double m00 = z0[0] * z0[0] + z0[1] * z0[1] + z0[2] * z0[2];
+      const double m01 = z0[0] * z1[0] + z0[1] * z1[1] + z0[2] * z1[2];
+      const double m11 = z1[0] * z1[0] + z1[1] * z1[1] + z1[2] * z1[2];
+      const double zu0 = z0[0] * u01.x + z0[1] * u01.y + z0[2] * u2;
+      const double zu1 = z1[0] * u01.x + z1[1] * u01.y + z1[2] * u2;
+      double n0[6], n1[6];
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        n0[b] = m00 * c0[b] + m01 * c1[b];
+        n1[b] = m01 * c0[b] + m11 * c1[b];
+      }
+      int t = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+#pragma unroll
+        for (int b = 0; b <= a; ++b) acc[t++] += c0[a] * n0[b] + c1[a] * n1[b];
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) acc[21 + a] += c0[a] * zu0 + c1[a] * zu1;
+    }
+  }
+  double tot[27];
+  block_sum<27>(acc, lds, tot);
+  cam_slice_store(tot, cpart, v, P.nvc);
+}
+
 // model cost change + candidate cost with J recomputed at x (the lin table of
 // the linearisation point) beside the value-only candidate table
 // TB (nc > kLinLdsCams, k_lin_point's camera sources): rec is gtbl (1) or
@@ -3445,7 +3534,12 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
     if (nt < 0) { const char* e = getenv("BA_DIAG_NT"); nt = e ? atoi(e) : 64; }
     if (pref < 0) { const char* e = getenv("BA_DIAG_PREF"); pref = e ? atoi(e) : 0; }
     const dim3 g(P.nvc, sl);
-    if (nt == 64)
+    // BA_DIAG_DMA=0: the register-gather form (read per launch: A/B in one process)
+    const char* de = getenv("BA_DIAG_DMA");
+    const bool dma = !(de && de[0] == '0');
+    if (nt == 64 && dma && !pref)
+      hipLaunchKernelGGL(k_cam_schur_diag_cd, g, dim3(64), 0, s, P, W.W, W.scale_c, W.u, W.cpart);
+    else if (nt == 64)
       hipLaunchKernelGGL((pref ? k_cam_schur_diag_c<64, true> : k_cam_schur_diag_c<64, false>), g, dim3(64), 0, s, P,
                          W.W, W.scale_c, W.u, W.cpart);
     else if (nt == 128)
@@ -3480,11 +3574,12 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (grid == 0) return;
   if (grid > grid_cap) grid = grid_cap;
   grid = (grid + 7) / 8 * 8;   // k_schur_pairs' XCD ranges need a multiple of 8
-  // BA_PAIRS_DMA=1: the LDS-DMA gather form (two workgroups per CU while its
-  // 64 KB + the camera constants fit half the LDS)
-  // (read per launch: tests compare both forms in one process)
+  // the LDS-DMA gather form while its 64 KB + the camera constants fit half
+  // the LDS (two workgroups per CU): C3 159 -> 121 us, 1409-1424 -> 1487-1503
+  // M-obs/s (profiles/r04_v7_ab_pairs_dma.txt).  BA_PAIRS_DMA=0: the register
+  // form (read per launch: tests compare both forms in one process)
   const char* dma_env = getenv("BA_PAIRS_DMA");
-  const int dma = dma_env ? atoi(dma_env) : 0;
+  const int dma = dma_env ? atoi(dma_env) : 1;
   const size_t ctab_bytes = sizeof(WcCam) * (size_t)P.nvc;
   if (W.wcompact && dma && kPairsDmaLds + ctab_bytes <= 80 * 1024)
     hipLaunchKernelGGL(k_schur_pairs_cd, dim3(grid), dim3(256), kPairsDmaLds + ctab_bytes, s, P, W.blocks, xoff,

@@ -87,14 +87,16 @@ def test_jfree_blocks_and_reduced_system_match_oracle(oracle_lib, cfg, scale):
 
 
 @pytest.mark.timeout(600)
-def test_pair_pass_dma_gather_is_bitwise_the_register_gather(monkeypatch):
-    """k_schur_pairs_cd (records gathered into LDS by LDS-DMA, BA_PAIRS_DMA=1)
-    forms the same products in the same order as k_schur_pairs_c: S and the
-    rhs must agree bitwise (C3 camera count: the LDS form's size limit)."""
+@pytest.mark.parametrize("switch", ["BA_PAIRS_DMA", "BA_DIAG_DMA"])
+def test_dma_gathers_are_bitwise_the_register_gathers(monkeypatch, switch):
+    """k_schur_pairs_cd / k_cam_schur_diag_cd (compact records gathered into
+    LDS by LDS-DMA, the defaults) form the same products in the same order as
+    k_schur_pairs_c / k_cam_schur_diag_c (register gathers, switch=0): S and
+    the rhs must agree bitwise (C3 camera count: the LDS form's size limit)."""
     p = make_config("c3", scale=0.2)
     out = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("BA_PAIRS_DMA", mode)
+        monkeypatch.setenv(switch, mode)
         with Solver(0) as s:
             s.set_problem(p)
             out[mode] = s.debug_blocks(1e4)
