@@ -345,6 +345,67 @@ __global__ __launch_bounds__(256) void k_pcg_cam_t(DevProblem P, const double* _
   }
 }
 
+// k_pcg_cam_t with the 48-B products gathered into LDS by LDS-DMA: a round of
+// 64 observations is 192 16-B pieces, three wave-instructions whose lane l
+// fetches piece (l + 64 k) mod 3 of record (l + 64 k) / 3, so the records
+// land contiguously (record q at 48 q B) and an instruction touches ~21
+// records instead of 64; each lane then reads its record with three
+// conflict-free ds_read_b128 (stride 12 dwords).  Thread t still sums the
+// observations i0 + t + 256 j in order: bitwise k_pcg_cam_t.
+__device__ __forceinline__ void glds16p(const double* src, double* lds_dst) {
+  __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+__global__ __launch_bounds__(256) void k_pcg_cam_td(DevProblem P, const double* __restrict__ tobs,
+                                                    double* __restrict__ tpart, const double* __restrict__ st) {
+  if (st[PS_DONE] != 0.0) return;
+  __shared__ double lds[6 * 16];
+  __shared__ __attribute__((aligned(16))) double tb[4][64 * 6];
+  const int v = blockIdx.x, g = blockIdx.y, G = gridDim.y;
+  const int a0 = P.cam_off[v], a1 = P.cam_off[v + 1];
+  const int len = (a1 - a0 + G - 1) / G;
+  const int i0 = min(a1, a0 + g * len), i1 = min(a1, i0 + len);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* buf = tb[w];
+  auto issue = [&](int o) {   // o: this lane's observation (any valid index when unused)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int e = lane + 64 * k, q = e / 3, pc = e - 3 * q;
+      const int oq = __shfl(o, q);
+      glds16p(tobs + 6 * (size_t)oq + 2 * pc, buf + 128 * k);
+    }
+  };
+  double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  // rounds of this wave: observations i0 + 64 w + lane + 256 r
+  const int first = i0 + 64 * w;
+  const int nr = first < i1 ? (i1 - first + 255) / 256 : 0;   // (uniform per wave)
+  int i = first + lane;
+  int on = i < i1 ? P.cam_op[i].x : 0;
+  if (nr > 0) issue(on);
+  on = i + 256 < i1 ? P.cam_op[i + 256].x : 0;
+  for (int r = 0; r < nr; ++r, i += 256) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this round's DMA has landed
+    const double2* t = reinterpret_cast<const double2*>(buf + 6 * lane);
+    const double2 x0 = t[0], x1 = t[1], x2 = t[2];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the refill
+    if (r + 1 < nr) {
+      issue(on);
+      on = i + 512 < i1 ? P.cam_op[i + 512].x : 0;
+    }
+    if (i < i1) {
+      acc[0] += x0.x; acc[1] += x0.y;
+      acc[2] += x1.x; acc[3] += x1.y;
+      acc[4] += x2.x; acc[5] += x2.y;
+    }
+  }
+  double tot[6];
+  block_sum<6>(acc, lds, tot);
+  if (threadIdx.x == 0) {
+    double* dst = tpart + ((size_t)g * P.nvc + v) * 6;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) dst[a] = tot[a];
+  }
+}
+
 // Point pass over point-aligned chunks of <= 64 observations, one wave per
 // chunk (ensure_pcg builds the chunk list; points with more than 64
 // observations keep k_pcg_point / k_pcg_point_t).  The chunk's W records
@@ -810,7 +871,12 @@ void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec,
       else
         hipLaunchKernelGGL((k_pcg_point_seg<double, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks, W.W,
                            vec, W.vpt, W.tobs, nullptr, st);
-      hipLaunchKernelGGL(k_pcg_cam_t, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
+      // BA_CAMT_DMA=0: the register-gather camera pass (read per launch)
+      const char* ce = getenv("BA_CAMT_DMA");
+      if (ce && ce[0] == '0')
+        hipLaunchKernelGGL(k_pcg_cam_t, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
+      else
+        hipLaunchKernelGGL(k_pcg_cam_td, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
       return;
     }
     const bool cm = W.wcm && W.jrfree;

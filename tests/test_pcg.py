@@ -142,12 +142,13 @@ def compare(glog, olog, n, rtol=1e-9):
 # matvec forms of the implicit Schur complement: "auto" the solver's choice
 # by size; "gather" the point-major W gathered in camera order (BA_PCG_T=0);
 # "t" the per-observation products t_o = W_o v_p scattered to camera order
-# and streamed by the camera pass (BA_PCG_T=1); "t_gather" the products in
-# point order, gathered (BA_TSCAT=0); "pairs" the value-pair point passes
-# k_pcg_point / k_pcg_point_t instead of the point-aligned chunks
-# (BA_PCG_SEG=0, BA_PCG_T=1); "wcm" the camera-major copy of W (k_obs_w_cam,
-# BA_WCM=1: the camera passes stream it)
-MATVECS = ["auto", "gather", "t", "t_gather", "pairs", "wcm"]
+# and streamed by the camera pass (BA_PCG_T=1, BA_TSCAT=1); "t_gather" the
+# products in point order, gathered into LDS by LDS-DMA (BA_TSCAT=0, the
+# default); "t_gather_reg" the same with register gathers (BA_CAMT_DMA=0);
+# "pairs" the value-pair point passes k_pcg_point / k_pcg_point_t instead of
+# the point-aligned chunks (BA_PCG_SEG=0, BA_PCG_T=1); "wcm" the camera-major
+# copy of W (k_obs_w_cam, BA_WCM=1: the camera passes stream it)
+MATVECS = ["auto", "gather", "t", "t_gather", "t_gather_reg", "pairs", "wcm"]
 
 
 def set_matvec(monkeypatch, mode):
@@ -156,10 +157,28 @@ def set_matvec(monkeypatch, mode):
     elif mode != "auto":
         monkeypatch.setenv("BA_WCM", "0")
         monkeypatch.setenv("BA_PCG_T", "0" if mode == "gather" else "1")
-        if mode == "t_gather":
-            monkeypatch.setenv("BA_TSCAT", "0")
+        monkeypatch.setenv("BA_TSCAT", "1" if mode == "t" else "0")
+        if mode == "t_gather_reg":
+            monkeypatch.setenv("BA_CAMT_DMA", "0")
         if mode == "pairs":
             monkeypatch.setenv("BA_PCG_SEG", "0")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
+def test_gpu_camera_pass_dma_gather_is_bitwise_the_register_gather(solver, precision, monkeypatch):
+    """k_pcg_cam_td (the products gathered into LDS by LDS-DMA) sums the same
+    values per thread in the same order as k_pcg_cam_t: the same trajectory
+    bitwise (C4 camera count, the compact camera records)."""
+    p = make_config("c4", scale=0.01)
+    kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=6, precision=precision)
+    set_matvec(monkeypatch, "t_gather")
+    ca, xa, sa, la = gpu_solve(solver, p, **kw)
+    monkeypatch.setenv("BA_CAMT_DMA", "0")
+    cb, xb, sb, lb = gpu_solve(solver, p, **kw)
+    assert [it["cost"] for it in la] == [it["cost"] for it in lb]
+    assert sa.final_cost == sb.final_cost
+    assert np.array_equal(ca, cb) and np.array_equal(xa, xb)
 
 
 @pytest.mark.gpu
