@@ -2477,7 +2477,36 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
   int oc = min(base + lane, P.no - 1);
   int c = P.obs_cam[oc], p = P.obs_pt[oc];
   float2 uv = P.uv[oc];
+  // TB 3: the compact records (TB 2) gathered by LDS-DMA into the wave's
+  // staging slot, 8 lanes per 128-B record (pieces XOR-swizzled through the
+  // source address, as k_schur_pairs_cd): a wave-instruction touches 8
+  // records instead of 64.  The next chunk's records are requested after
+  // this chunk's W records have left the slot, ahead of their stores
+  constexpr int NST = (COMPACT ? kWcRec : kWRec) / 2;   // store instructions per chunk
+  auto crec_issue = [&](int cc) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = (lane >> 3) + 8 * k;
+      const int cq = __shfl(cc, q);
+      glds16(rec + (size_t)cq * kCRec + 2 * ((lane & 7) ^ ((q >> 1) & 7)), st + k * 128);
+    }
+  };
+  if constexpr (TB == 3) {
+    crec_issue(c);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the first chunk's; later ones: below)
+  }
   for (; base < P.no; base += step) {
+    CamRcPre crp;
+    if constexpr (TB == 3) {
+      // this chunk's records have landed; the previous chunk's NST stores,
+      // issued after them, may still be in flight (in-order completion; only
+      // a full chunk is followed by a request, and it stores NST times)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+      const int swr = (lane >> 1) & 7;
+#pragma unroll
+      for (int k = 0; k < kCRec / 2; ++k) crp.v[k] = *reinterpret_cast<const double2*>(st + lane * kCRec + 2 * (k ^ swr));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // out of the slot before the W staging
+    }
     const int nb = base + step;
     const int ocn = min(nb + lane, P.no - 1);
     const int cn = P.obs_cam[ocn], pn = P.obs_pt[ocn];
@@ -2498,6 +2527,9 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
     if constexpr (TB) {
       if constexpr (TB == 1) {
         const CamG cam{rec + (size_t)c * kGRec};
+        (void)lin_obs(P, cam, v >= 0, pv, X0, X1, X2, uv, j, fin, prf);
+      } else if constexpr (TB == 3) {
+        const CamRc cam = cam_make(CamRcOf{rec, nullptr}, crp);
         (void)lin_obs(P, cam, v >= 0, pv, X0, X1, X2, uv, j, fin, prf);
       } else {
         const CamRc cam = cam_rc(rec, c);
@@ -2553,6 +2585,10 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
       ov[it].y = (WT)st[r * kStageLd + f + 1];
     }
     wave_lds_sync();
+    if constexpr (TB == 3) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the W records are out of the slot
+      if (nb < P.no) crec_issue(cn);
+    }
     V2* dst = reinterpret_cast<V2*>(W + (size_t)base * REC);
     const int nrec = min(64, P.no - base);
     if (nrec == 64) {
@@ -3450,15 +3486,21 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
   if (tb) {   // global camera source: 64.5 KB of staging LDS, two workgroups per CU
     const int g = std::min(2 * lds_grid(1 << 30), std::max(1, (P.no + 64 * kObsWRcWaves - 1) / (64 * kObsWRcWaves)));
     const double* src = tb == 1 ? W.gtbl : W.crec;
+    // compact records by LDS-DMA (TB 3) unless BA_CREC_DMA=0 (read per launch)
+    const char* de = getenv("BA_CREC_DMA");
+    const bool dma = tb == 2 && !(de && de[0] == '0');
     if (W.w32)
-      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<float, false, 1> : k_obs_w_rc<float, false, 2>), dim3(g),
-                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
+      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<float, false, 1> : dma ? k_obs_w_rc<float, false, 3> : k_obs_w_rc<float, false, 2>),
+                         dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv,
+                         W.Wf);
     else if (W.wcompact)   // (DENSE_SCHUR up to kWcCams variable cameras: the compact records)
-      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, true, 1> : k_obs_w_rc<double, true, 2>), dim3(g),
-                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
+      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, true, 1> : dma ? k_obs_w_rc<double, true, 3> : k_obs_w_rc<double, true, 2>),
+                         dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv,
+                         W.W);
     else
-      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, false, 1> : k_obs_w_rc<double, false, 2>), dim3(g),
-                         dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
+      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, false, 1> : dma ? k_obs_w_rc<double, false, 3> : k_obs_w_rc<double, false, 2>),
+                         dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv,
+                         W.W);
     return;
   }
   if (W.jrfree) {   // one 148-KB-LDS workgroup per CU

@@ -166,6 +166,23 @@ def set_matvec(monkeypatch, mode):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
+def test_gpu_camera_record_dma_is_bitwise_the_register_gather(solver, precision, monkeypatch):
+    """k_obs_w_rc with the compact camera records gathered by LDS-DMA (TB 3,
+    the default beyond 200 cameras) runs the same lin_obs on the same record
+    values as the per-lane register gather (BA_CREC_DMA=0): the same
+    trajectory bitwise."""
+    p = make_config("c4", scale=0.01)
+    kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=6, precision=precision)
+    ca, xa, sa, la = gpu_solve(solver, p, **kw)
+    monkeypatch.setenv("BA_CREC_DMA", "0")
+    cb, xb, sb, lb = gpu_solve(solver, p, **kw)
+    assert [it["cost"] for it in la] == [it["cost"] for it in lb]
+    assert sa.final_cost == sb.final_cost
+    assert np.array_equal(ca, cb) and np.array_equal(xa, xb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
 def test_gpu_camera_pass_dma_gather_is_bitwise_the_register_gather(solver, precision, monkeypatch):
     """k_pcg_cam_td (the products gathered into LDS by LDS-DMA) sums the same
     values per thread in the same order as k_pcg_cam_t: the same trajectory
