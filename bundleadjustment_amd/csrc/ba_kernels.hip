@@ -2366,6 +2366,162 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
   }
 }
 
+// k_lin_point<.., TB 2> with the compact camera records gathered by LDS-DMA
+// (8 lanes per 128-B record, a wave-instruction touching 8 records instead of
+// 64; pieces XOR-swizzled through the source address as in k_schur_pairs_cd)
+// one observation round ahead — across point boundaries too: the last round
+// of a point requests the first cameras of the lane's next point.  The DMA
+// needs every lane of the wave, so the point and observation loops run in
+// wave-uniform rounds (a lane past its point's observations, or past the
+// points, computes nothing).  Per lane the same lin_obs on the same record
+// values and the same accumulation order: bitwise k_lin_point<.., 2>.
+template <int NT, int LANES>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_lin_point_d(DevProblem P, const double* __restrict__ crec,
+                                                    const double* __restrict__ pts, double* __restrict__ Hpp,
+                                                    double* __restrict__ gp, double* __restrict__ scale_p,
+                                                    double* __restrict__ diag_p, int compute_scale, double min_diag,
+                                                    double max_diag, double* __restrict__ part,
+                                                    double* __restrict__ pxv) {
+  __shared__ double lds[5 * 16];
+  __shared__ __attribute__((aligned(16))) double cbuf[NT / 64][64 * kCRec];
+  const int lane = threadIdx.x & 63;
+  double* cb = cbuf[threadIdx.x >> 6];
+  const int swr = (lane >> 1) & 7;
+  auto issue = [&](int cc) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = (lane >> 3) + 8 * k;
+      const int cq = __shfl(cc, q);
+      glds16(crec + (size_t)cq * kCRec + 2 * ((lane & 7) ^ ((q >> 1) & 7)), cb + k * 128);
+    }
+  };
+  auto fetch = [&]() {
+    CamRcPre q;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this round's records have landed
+#pragma unroll
+    for (int k = 0; k < kCRec / 2; ++k) q.v[k] = *reinterpret_cast<const double2*>(cb + lane * kCRec + 2 * (k ^ swr));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the next request
+    return q;
+  };
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};   // cost, bad, gn2, xn2
+  double gmax = 0.0;
+  const size_t np = (size_t)P.np;
+  const int sl = threadIdx.x & (LANES - 1);
+  const int g0 = (blockIdx.x * NT + threadIdx.x) / LANES, gs = gridDim.x * NT / LANES;
+  const int lastp = max(P.np - 1, 0), lasto = max(P.no - 1, 0);
+  if (P.np > 0 && P.no > 0) {
+    int p = g0;
+    int pc = min(p, lastp);
+    int o0 = P.pt_off[pc], o1 = P.pt_off[pc + 1];
+    double X0 = pts[3 * pc], X1 = pts[3 * pc + 1], X2 = pts[3 * pc + 2];
+    bool pv = P.pt_var[pc] != 0;
+    int c = P.obs_cam[min(o0 + sl, lasto)];
+    float2 uv = P.uv[min(o0 + sl, lasto)];
+    issue(c);
+    while (__any(p < P.np)) {   // wave-uniform point rounds
+      const bool livep = p < P.np;
+      const int pn = min(p + gs, lastp);
+      const int o0n = P.pt_off[pn], o1n = P.pt_off[pn + 1];
+      const double Y0 = pts[3 * pn], Y1 = pts[3 * pn + 1], Y2 = pts[3 * pn + 2];
+      const bool pvn = P.pt_var[pn] != 0;
+      const int onp = min(o0n + sl, lasto);   // the next point's first observation of this lane
+      const int cnp = P.obs_cam[onp];
+      const float2 uvnp = P.uv[onp];
+      double H[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+      int cnt = livep && o1 - o0 > sl ? (o1 - o0 - sl + LANES - 1) / LANES : 0;
+#pragma unroll
+      for (int x = 32; x >= 1; x >>= 1) cnt = max(cnt, __shfl_xor(cnt, x));
+      int o = o0 + sl;
+      if (cnt == 0) {   // (keep one request in flight: the next point's)
+        (void)fetch();
+        issue(cnp);
+        uv = uvnp;
+      }
+      for (int t = 0; t < cnt; ++t) {
+        const CamRcPre q = fetch();
+        const bool more = t + 1 < cnt;
+        const int on = min(o + LANES, lasto);
+        const int cn = more ? P.obs_cam[on] : cnp;
+        const float2 uvn = more ? P.uv[on] : uvnp;
+        issue(cn);
+        if (livep && o < o1) {
+          const CamRc cam = cam_make(CamRcOf{crec, nullptr}, q);
+          double out[kJR];
+          bool fin;
+          const double rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
+          acc[0] += 0.5 * rho;
+          acc[1] += fin ? 0.0 : 1.0;
+          const double jp[2][3] = {{out[12], out[13], out[14]}, {out[15], out[16], out[17]}};
+          const double rr[2] = {out[18], out[19]};
+#pragma unroll
+          for (int row = 0; row < 2; ++row) {
+            const double a = jp[row][0], b = jp[row][1], cc = jp[row][2];
+            H[0] += a * a; H[1] += a * b; H[2] += a * cc; H[3] += b * b; H[4] += b * cc; H[5] += cc * cc;
+            g[0] += a * rr[row]; g[1] += b * rr[row]; g[2] += cc * rr[row];
+          }
+        }
+        uv = uvn;
+        o += LANES;
+      }
+      if (livep && pv) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+#pragma unroll
+          for (int x = LANES / 2; x >= 1; x >>= 1) H[k] += __shfl_xor(H[k], x, LANES);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+#pragma unroll
+          for (int x = LANES / 2; x >= 1; x >>= 1) g[k] += __shfl_xor(g[k], x, LANES);
+        }
+        if (sl == 0) {
+#pragma unroll
+          for (int k = 0; k < 6; ++k) Hpp[k * np + p] = H[k];
+          const double hd[3] = {H[0], H[3], H[5]};
+          const double Xk[3] = {X0, X1, X2};
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            gp[k * np + p] = g[k];
+            double s;
+            if (compute_scale) {
+              s = 1.0 / (1.0 + sqrt(hd[k]));
+              scale_p[k * np + p] = s;
+            } else {
+              s = scale_p[k * np + p];
+            }
+            diag_p[k * np + p] = fmin(fmax(hd[k] * s * s, min_diag), max_diag);
+            const double x = Xk[k];
+            const double d = x - (x + (-g[k]));
+            gmax = fmax(gmax, fabs(d));
+            acc[2] += d * d;
+            acc[3] += x * x;
+          }
+        }
+      }
+      if (livep && sl == 0) {
+        double2* d = reinterpret_cast<double2*>(pxv + 4 * (size_t)p);
+        d[0] = make_double2(X0, X1);
+        d[1] = make_double2(X2, pv ? 1.0 : 0.0);
+      }
+      o0 = o0n; o1 = o1n;
+      X0 = Y0; X1 = Y1; X2 = Y2;
+      pv = pvn;
+      p += gs;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last (unread) request
+  }
+  double tot[4];
+  block_sum<4>(acc, lds, tot);
+  const double m = block_max1(gmax, lds + 64);
+  if (threadIdx.x == 0) {
+    part_of(part, SL_COST)[blockIdx.x] = tot[0];
+    part_of(part, SL_LIN_BAD)[blockIdx.x] = tot[1];
+    part_of(part, SL_GN2_P)[blockIdx.x] = tot[2];
+    part_of(part, SL_XN2_P)[blockIdx.x] = tot[3];
+    part_of(part, SL_GMAX_P)[blockIdx.x] = m;
+  }
+}
+
 // Hcc (lower 21) and gc per variable camera, its observations in camera order
 // (k_cam_assemble's order: thread i takes i0 + tid, i0 + tid + NT, ...)
 // TB = 2: rec is the compact records crec (the camera's dual Rodrigues once
@@ -3328,6 +3484,18 @@ void launch_linearize_jr(const DevProblem& P, const DevWork& W, hipStream_t s, h
   hipLaunchKernelGGL(k_linearize, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.rec, W.pts, W.JR, W.part);
   if (t1) (void)hipEventRecord(t1, s);
 }
+// compact camera records gathered by LDS-DMA in the point-major kernels
+// beyond 200 cameras; BA_CREC_DMA=0: per-lane register gathers (read per
+// launch: tests compare both forms in one process)
+static bool crec_dma() {
+  const char* e = getenv("BA_CREC_DMA");
+  return !(e && e[0] == '0');
+}
+// k_lin_point_d (BA_LP_DMA=1; with BA_CREC_DMA)
+static bool lp_dma() {
+  const char* e = getenv("BA_LP_DMA");
+  return crec_dma() && e && e[0] == '1';
+}
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
                            double max_diag, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   if (W.jrfree) {   // r, J, cost and the point blocks in one pass (J never materialised)
@@ -3354,10 +3522,15 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
       if (tb == 1)
         kern = NT == 512 ? (L == 2 ? k_lin_point<512, 2, false, 1> : (L == 8 ? k_lin_point<512, 8, false, 1> : k_lin_point<512, 4, false, 1>))
                          : (L == 2 ? k_lin_point<256, 2, false, 1> : (L == 8 ? k_lin_point<256, 8, false, 1> : k_lin_point<256, 4, false, 1>));
+      else if (lp_dma())   // (LDS-DMA camera records: 2 lanes per point, 256 threads)
+        kern = k_lin_point_d<256, 2>;
       else
         kern = NT == 512 ? (L == 2 ? k_lin_point<512, 2, false, 2> : (L == 8 ? k_lin_point<512, 8, false, 2> : k_lin_point<512, 4, false, 2>))
                          : (L == 2 ? k_lin_point<256, 2, false, 2> : (L == 8 ? k_lin_point<256, 8, false, 2> : k_lin_point<256, 4, false, 2>));
-      hipExtLaunchKernelGGL(kern, dim3(g), dim3(NT), 0, s, t0, t1, 0, P, (const double*)(tb == 1 ? W.gtbl : W.crec),
+      const bool dma = tb == 2 && lp_dma();
+      const int nt_l = dma ? 256 : NT;
+      const int g_l = dma ? std::max(1, std::min((int)std::min<long long>(((long long)P.np * 2 + 255) / 256, 1LL << 30), kMaxBlocks)) : g;
+      hipExtLaunchKernelGGL(kern, dim3(g_l), dim3(nt_l), 0, s, t0, t1, 0, P, (const double*)(tb == 1 ? W.gtbl : W.crec),
                             (const double*)W.pts, W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag,
                             max_diag, W.part, W.pxv);
       return;
@@ -3486,9 +3659,8 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
   if (tb) {   // global camera source: 64.5 KB of staging LDS, two workgroups per CU
     const int g = std::min(2 * lds_grid(1 << 30), std::max(1, (P.no + 64 * kObsWRcWaves - 1) / (64 * kObsWRcWaves)));
     const double* src = tb == 1 ? W.gtbl : W.crec;
-    // compact records by LDS-DMA (TB 3) unless BA_CREC_DMA=0 (read per launch)
-    const char* de = getenv("BA_CREC_DMA");
-    const bool dma = tb == 2 && !(de && de[0] == '0');
+    // compact records by LDS-DMA (TB 3) unless BA_CREC_DMA=0
+    const bool dma = tb == 2 && crec_dma();
     if (W.w32)
       hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<float, false, 1> : dma ? k_obs_w_rc<float, false, 3> : k_obs_w_rc<float, false, 2>),
                          dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv,

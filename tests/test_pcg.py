@@ -166,15 +166,17 @@ def set_matvec(monkeypatch, mode):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
-def test_gpu_camera_record_dma_is_bitwise_the_register_gather(solver, precision, monkeypatch):
-    """k_obs_w_rc with the compact camera records gathered by LDS-DMA (TB 3,
-    the default beyond 200 cameras) runs the same lin_obs on the same record
-    values as the per-lane register gather (BA_CREC_DMA=0): the same
-    trajectory bitwise."""
+@pytest.mark.parametrize("switch,on,off", [("BA_CREC_DMA", "1", "0"), ("BA_LP_DMA", "1", "0")])
+def test_gpu_camera_record_dma_is_bitwise_the_register_gather(solver, precision, switch, on, off, monkeypatch):
+    """The point-major kernels beyond 200 cameras with the compact camera
+    records gathered by LDS-DMA (k_obs_w_rc TB 3: BA_CREC_DMA; k_lin_point_d:
+    BA_LP_DMA) run the same lin_obs on the same record values as the per-lane
+    register gathers: the same trajectory bitwise."""
     p = make_config("c4", scale=0.01)
     kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=6, precision=precision)
+    monkeypatch.setenv(switch, on)
     ca, xa, sa, la = gpu_solve(solver, p, **kw)
-    monkeypatch.setenv("BA_CREC_DMA", "0")
+    monkeypatch.setenv(switch, off)
     cb, xb, sb, lb = gpu_solve(solver, p, **kw)
     assert [it["cost"] for it in la] == [it["cost"] for it in lb]
     assert sa.final_cost == sb.final_cost
