@@ -264,10 +264,16 @@ def main():
             raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a {world}-rank run "
                              f"as {args.gpus} GPU(s)")
     device = local_rank if args.device is None else args.device
+    # the JSON line is the only thing a rank writes to stdout: native
+    # libraries print there too (RCCL's version banner at communicator
+    # creation), so fd 1 goes to stderr and the line to a copy of the original
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     if os.environ.get("BA_BENCH_DRYRUN") == "1":
         if os.environ.get("BA_BENCH_DRYRUN_FAIL_RANK") == str(rank):
             raise SystemExit(3)
-        print(dry_run_line(args, rank, world, local_rank, device), flush=True)
+        print(dry_run_line(args, rank, world, local_rank, device), file=json_out, flush=True)
         if rank != 0:   # a surviving rank of a failed launch is terminated by the parent
             time.sleep(float(os.environ.get("BA_BENCH_DRYRUN_SLEEP", "0")))
         return
@@ -438,7 +444,7 @@ def main():
             "iteration_roofline": iteration_roofline,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     solver.close()
     if host_ar is not None:
         import torch.distributed as dist
