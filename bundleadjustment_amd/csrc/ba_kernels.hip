@@ -3491,10 +3491,12 @@ static bool crec_dma() {
   const char* e = getenv("BA_CREC_DMA");
   return !(e && e[0] == '0');
 }
-// k_lin_point_d (BA_LP_DMA=1; with BA_CREC_DMA)
+// k_lin_point_d (with BA_CREC_DMA; BA_LP_DMA=0 alone turns it off): C5 shard
+// 386.5 -> 331.3 us, 3183 -> 3235 M-obs/s; C4 2883 -> 2896
+// (profiles/r04_v11_ab_lp_dma.txt)
 static bool lp_dma() {
   const char* e = getenv("BA_LP_DMA");
-  return crec_dma() && e && e[0] == '1';
+  return crec_dma() && !(e && e[0] == '0');
 }
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
                            double max_diag, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
