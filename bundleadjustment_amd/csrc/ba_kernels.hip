@@ -3234,6 +3234,8 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
   __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
   __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
   __shared__ double ctb_s[TB ? 1 : kLinLdsCams * kCandRec];
+  // TB 3: pass 1's compact camera records by LDS-DMA (k_lin_point_d's rounds)
+  __shared__ __attribute__((aligned(16))) double cbuf[TB == 3 ? NT / 64 : 1][TB == 3 ? 64 * kCRec : 2];
   if constexpr (!TB) {
     fill_lin_table<NT>(P, rec, tbl, ktb);
     const int n = P.nc * kCandRec;
@@ -3251,7 +3253,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
     if constexpr (TB == 1) {
       const CamG cam{rec + (size_t)c * kGRec};
       (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
-    } else if constexpr (TB == 2) {
+    } else if constexpr (TB == 2 || TB == 3) {
       const CamRc cam = cam_rc(rec, c);
       (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
     } else if constexpr (LAZY) {
@@ -3262,13 +3264,40 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
       (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
     }
   };
+  const int lane = threadIdx.x & 63;
+  double* cb = cbuf[TB == 3 ? (int)(threadIdx.x >> 6) : 0];
+  auto issue = [&](int cc) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = (lane >> 3) + 8 * k;
+      const int cq = __shfl(cc, q);
+      glds16(rec + (size_t)cq * kCRec + 2 * ((lane & 7) ^ ((q >> 1) & 7)), cb + k * 128);
+    }
+  };
+  auto fetch = [&]() {
+    CamRcPre q;
+    const int swr = (lane >> 1) & 7;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < kCRec / 2; ++k) q.v[k] = *reinterpret_cast<const double2*>(cb + lane * kCRec + 2 * (k ^ swr));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return q;
+  };
   int p = P.np > 0 ? g0 : P.np;
   if (P.np > 0) {
     int pc = min(p, lastp);
     int o0 = P.pt_off[pc], o1 = P.pt_off[pc + 1];
     double X0 = pts[3 * pc], X1 = pts[3 * pc + 1], X2 = pts[3 * pc + 2];
     bool pv = P.pt_var[pc] != 0;
-    for (; p < P.np; p += gs) {   // uniform inside a lane group
+    // TB 3: the lane's camera whose record is in flight (the point's first)
+    int cdma = 0;
+    if constexpr (TB == 3) {
+      cdma = P.obs_cam[min(o0 + sl, lasto)];
+      issue(cdma);
+    }
+    // TB 3: wave-uniform point rounds (the DMA needs every lane)
+    for (; TB == 3 ? __any(p < P.np) != 0 : p < P.np; p += gs) {   // uniform inside a lane group
+      const bool livep = TB != 3 || p < P.np;
       const int pn = min(p + gs, lastp);
       const int o0n = P.pt_off[pn], o1n = P.pt_off[pn + 1];
       const double Y0 = pts[3 * pn], Y1 = pts[3 * pn + 1], Y2 = pts[3 * pn + 2];
@@ -3279,7 +3308,76 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
       // past them (points with more than LANES * KC observations) and for
       // fixed points (no pass 1)
       double kc[KC][10];
-      if (pv) {
+      if constexpr (TB == 3) {
+        // pass 1 in wave-uniform rounds, the records one round ahead (the
+        // point's last round requests the lane's next point's first camera)
+        const bool act1 = livep && pv;
+        double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+        int o = o0 + sl;
+        float2 uv = P.uv[min(o, lasto)];
+        int cnt = act1 && o1 - o0 > sl ? (o1 - o0 - sl + LANES - 1) / LANES : 0;
+#pragma unroll
+        for (int x = 32; x >= 1; x >>= 1) cnt = max(cnt, __shfl_xor(cnt, x));
+        const int cnp = P.obs_cam[min(o0n + sl, lasto)];
+        if (cnt == 0) {
+          (void)fetch();
+          issue(cnp);
+          cdma = cnp;
+        }
+        auto round = [&](double (&keep)[10], bool store, bool more) {
+          const CamRcPre q = fetch();
+          const int on = min(o + LANES, lasto);
+          const int cn = more ? P.obs_cam[on] : cnp;
+          const float2 uvn = P.uv[on];
+          if (act1 && o < o1) {
+            const CamRc cam = cam_make(CamRcOf{rec, nullptr}, q);
+            double j[kJR];
+            bool fin;
+            (void)lin_obs(P, cam, cam.var(), true, X0, X1, X2, uv, j, fin);
+            const double* dc = ctb + (size_t)cdma * kCandRec + 16;
+            double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+            for (int a = 0; a < 6; ++a) { t0 += j[a] * dc[a]; t1 += j[6 + a] * dc[a]; }
+            v0 += j[12] * t0 + j[15] * t1;
+            v1 += j[13] * t0 + j[16] * t1;
+            v2 += j[14] * t0 + j[17] * t1;
+            if (store) {
+              keep[0] = t0; keep[1] = t1;
+#pragma unroll
+              for (int k = 0; k < 8; ++k) keep[2 + k] = j[12 + k];
+            }
+          }
+          // the next round's records (after the arithmetic: the request's
+          // addresses then do not share the registers of lin_obs)
+          issue(cn);
+          cdma = cn;
+          uv = uvn;
+          o += LANES;
+        };
+#pragma unroll
+        for (int t = 0; t < KC; ++t)
+          if (t < cnt) round(kc[t], true, t + 1 < cnt);
+        for (int t = KC; t < cnt; ++t) round(kc[0], false, t + 1 < cnt);
+        if (act1) {
+#pragma unroll
+          for (int x = LANES / 2; x >= 1; x >>= 1) {
+            v0 += __shfl_xor(v0, x, LANES);
+            v1 += __shfl_xor(v1, x, LANES);
+            v2 += __shfl_xor(v2, x, LANES);
+          }
+          const double s0 = scale_p[p], s1 = scale_p[np + p], s2 = scale_p[2 * np + p];
+          const double i00 = Linv[p], i10 = Linv[np + p], i11 = Linv[2 * np + p];
+          const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
+          const double z0 = s0 * v0, z1 = s1 * v1, z2 = s2 * v2;
+          const double w0 = u[4 * p] + i00 * z0;
+          const double w1 = u[4 * p + 1] + (i10 * z0 + i11 * z1);
+          const double w2 = u[4 * p + 2] + (i20 * z0 + i21 * z1 + i22 * z2);
+          const double yp[3] = {i00 * w0 + i10 * w1 + i20 * w2, i11 * w1 + i21 * w2, i22 * w2};
+          const double sp[3] = {s0, s1, s2};
+#pragma unroll
+          for (int k = 0; k < 3; ++k) dX[k] = (-yp[k]) * sp[k];
+        }
+      } else if (pv) {
         // pass 1: v = sum Jp^T (Jc dc)
         double v0 = 0.0, v1 = 0.0, v2 = 0.0;
         int o = o0 + sl;
@@ -3331,7 +3429,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
         for (int k = 0; k < 3; ++k) dX[k] = (-yp[k]) * sp[k];
       }
       const double Xc[3] = {X0 + dX[0], X1 + dX[1], X2 + dX[2]};
-      if (sl == 0) {
+      if (livep && sl == 0) {
         const double Xk[3] = {X0, X1, X2};
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -3345,7 +3443,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
         }
       }
       // pass 2: model cost change and candidate cost per observation
-      {
+      if (livep) {
         int o = o0 + sl;
         int oc = min(o, lasto);
         int c = P.obs_cam[oc];
@@ -3387,7 +3485,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
             for (int i = 0; i < 4; ++i) ph[i] = Xc[0] * cr[i] + Xc[1] * cr[4 + i] + Xc[2] * cr[8 + i] + cr[12 + i];
             pcand[0] = ph[0] / ph[3]; pcand[1] = ph[1] / ph[3]; pcand[2] = ph[2] / ph[3];
           }
-          const float* Kc = TB == 1 ? CamG{rec + (size_t)c * kGRec}.Kf() : (TB == 2 ? P.K + 9 * c : ktb + c * 9);
+          const float* Kc = TB == 1 ? CamG{rec + (size_t)c * kGRec}.Kf() : (TB >= 2 ? P.K + 9 * c : ktb + c * 9);
           double q[3];
 #pragma unroll
           for (int i = 0; i < 3; ++i)
@@ -3413,6 +3511,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
       X0 = Y0; X1 = Y1; X2 = Y2;
       pv = pvn;
     }
+    if constexpr (TB == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last (unread) request
   }
   double tot[5];
   block_sum<5>(acc, lds, tot);
@@ -3869,7 +3968,12 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
       constexpr int NT = 512, L = 4;
       const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
       const int g = std::max(1, std::min(want, kMaxBlocks));
-      hipLaunchKernelGGL((tb == 1 ? k_point_step_rc<NT, L, false, 3, 1> : k_point_step_rc<NT, L, false, 3, 2>), dim3(g),
+      // TB 3: pass 1's compact records by LDS-DMA (BA_PS_DMA=0: register gathers)
+      const char* pe = getenv("BA_PS_DMA");
+      const bool dma = tb == 2 && P.no > 0 && crec_dma() && !(pe && pe[0] == '0');
+      hipLaunchKernelGGL((tb == 1 ? k_point_step_rc<NT, L, false, 3, 1>
+                                  : dma ? k_point_step_rc<NT, L, false, 3, 3> : k_point_step_rc<NT, L, false, 3, 2>),
+                         dim3(g),
                          dim3(NT), 0, s, P, (const double*)(tb == 1 ? W.gtbl : W.crec), (const double*)W.pts,
                          W.delta_c, (const double*)W.ctbl, W.u, W.Linv, W.scale_p, W.pts_c, W.delta_p, W.part);
       return;

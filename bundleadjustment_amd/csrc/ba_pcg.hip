@@ -624,6 +624,11 @@ __global__ __launch_bounds__(256) void k_pcg_tfold(int nvc, int G, double* __res
 //   NO_CONVERGENCE; then iteration it+1 begins: z = M r, rho' = r.z,
 //   beta = rho' / rho (zero or inf: FAILURE), p = z + beta p.
 // ---------------------------------------------------------------------------
+// nvc <= kPcgThreads: one camera per thread, its vectors held in registers
+// across the phases (every load issued at the start, each vector stored once;
+// the per-phase re-reads of the loop form cost a dependent L2 round trip per
+// phase: C4 shard 15.4 us per launch).  The same operations per camera in the
+// same order and the same workgroup sums: bitwise the loop form.
 __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(DevProblem P, int mode, int it, PcgOpts o, int G,
                                                             const double* __restrict__ Adiag,
                                                             const double* __restrict__ Minv,
@@ -636,14 +641,24 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(DevProblem P, int mo
   double* st = scal + kNumSlots;
   if (st[PS_DONE] != 0.0) return;
   const int nvc = P.nvc;
+  const int v = threadIdx.x;
+  const bool on = v < nvc;
+  const size_t o6 = 6 * (size_t)(on ? v : 0);
+  double pv[6] = {0, 0, 0, 0, 0, 0}, xv[6] = {0, 0, 0, 0, 0, 0};
+  double rv[6] = {0, 0, 0, 0, 0, 0}, bv[6] = {0, 0, 0, 0, 0, 0};
+  if (on) {
+    load6(p + o6, pv);
+    load6(x + o6, xv);
+    load6(b + o6, bv);
+    if (mode != 2) load6(r + o6, rv);
+  }
   double alpha;
   if (mode != 2) {
     double acc[1] = {0.0};
-    for (int v = threadIdx.x; v < nvc; v += blockDim.x) {
-      double pv[6], qv[6];
-      load6(p + 6 * (size_t)v, pv);
+    double qv[6] = {0, 0, 0, 0, 0, 0};
+    if (on) {
       schur_row(Adiag, tpart, G, nvc, v, pv, qv);
-      store6(q + 6 * (size_t)v, qv);
+      store6(q + o6, qv);
 #pragma unroll
       for (int a = 0; a < 6; ++a) acc[0] += pv[a] * qv[a];
     }
@@ -652,32 +667,31 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(DevProblem P, int mo
     if (pq <= 0.0 || isinf(pq)) { pcg_stop(st, scal, PCG_NO_CONVERGENCE, it); return; }
     alpha = rho / pq;
     if (isinf(alpha) || isnan(alpha)) { pcg_stop(st, scal, PCG_FAILURE, it); return; }
-    for (int v = threadIdx.x; v < nvc; v += blockDim.x)
+    if (on) {
 #pragma unroll
-      for (int a = 0; a < 6; ++a) x[6 * (size_t)v + a] = x[6 * (size_t)v + a] + alpha * p[6 * (size_t)v + a];
+      for (int a = 0; a < 6; ++a) xv[a] = xv[a] + alpha * pv[a];
+      store6(x + o6, xv);
+    }
     if (mode == 1) {
       if (threadIdx.x == 0) st[PS_ALPHA] = alpha;
       return;
     }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) rv[a] = rv[a] - alpha * qv[a];
   } else {
     alpha = st[PS_ALPHA];
-  }
-  double acc[1] = {0.0};
-  for (int v = threadIdx.x; v < nvc; v += blockDim.x) {
-    double rv[6], xv[6];
-    load6(x + 6 * (size_t)v, xv);
-    if (mode == 2) {
+    if (on) {
       double sx[6];
       schur_row(Adiag, tpart, G, nvc, v, xv, sx);
 #pragma unroll
-      for (int a = 0; a < 6; ++a) rv[a] = b[6 * (size_t)v + a] - sx[a];
-    } else {
-#pragma unroll
-      for (int a = 0; a < 6; ++a) rv[a] = r[6 * (size_t)v + a] - alpha * q[6 * (size_t)v + a];
+      for (int a = 0; a < 6; ++a) rv[a] = bv[a] - sx[a];
     }
-    store6(r + 6 * (size_t)v, rv);
+  }
+  double acc[1] = {0.0};
+  if (on) {
+    store6(r + o6, rv);
 #pragma unroll
-    for (int a = 0; a < 6; ++a) acc[0] += xv[a] * (b[6 * (size_t)v + a] + rv[a]);
+    for (int a = 0; a < 6; ++a) acc[0] += xv[a] * (bv[a] + rv[a]);
   }
   block_allsum<1>(acc, lds);
   const double Q1 = -1.0 * acc[0];
@@ -687,11 +701,10 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(DevProblem P, int mo
   if (it >= o.max_iter) { pcg_stop(st, scal, PCG_NO_CONVERGENCE, it); return; }
   // iteration it + 1
   double racc[1] = {0.0};
-  for (int v = threadIdx.x; v < nvc; v += blockDim.x) {
-    double rv[6], zv[6];
-    load6(r + 6 * (size_t)v, rv);
+  double zv[6] = {0, 0, 0, 0, 0, 0};
+  if (on) {
     mat6_mul(Minv + (size_t)v * 36, rv, zv);
-    store6(z + 6 * (size_t)v, zv);
+    store6(z + o6, zv);
 #pragma unroll
     for (int a = 0; a < 6; ++a) racc[0] += rv[a] * zv[a];
   }
@@ -700,9 +713,11 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(DevProblem P, int mo
   if (zero_or_inf(rho_new) || isnan(rho_new)) { pcg_stop(st, scal, PCG_FAILURE, it + 1); return; }
   const double beta = rho_new / rho;
   if (zero_or_inf(beta)) { pcg_stop(st, scal, PCG_FAILURE, it + 1); return; }
-  for (int v = threadIdx.x; v < nvc; v += blockDim.x)
+  if (on) {
 #pragma unroll
-    for (int a = 0; a < 6; ++a) p[6 * (size_t)v + a] = z[6 * (size_t)v + a] + beta * p[6 * (size_t)v + a];
+    for (int a = 0; a < 6; ++a) pv[a] = zv[a] + beta * pv[a];
+    store6(p + o6, pv);
+  }
   if (threadIdx.x == 0) {
     st[PS_RHO] = rho_new;
     st[PS_Q0] = Q1;

@@ -756,18 +756,19 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
   DevWork& W = ctx->W;
   ensure_pcg(ctx);
   {
-    // per-observation products (k_pcg_point_t / k_pcg_cam_t) when the fp64 W
-    // outgrows the 256-MiB Infinity Cache: the camera pass then gathers 48 B
-    // per observation from HBM instead of 144 + 24 B (C5 shard +2.7 %; below
-    // the cache, e.g. C3 and the C4 shard, the W gathers hit it and the extra
-    // pass loses ~0.7 %).  BA_PCG_T=0 / 1 (diagnostics) forces it off / on.
+    // per-observation products t_o = W_o v_p: the camera pass then reads 48 B
+    // per observation instead of gathering 144 + 24 B.  With the point-aligned
+    // chunks (k_pcg_point_seg forms t_o from the W it has just staged, the
+    // camera pass gathers them by LDS-DMA) always: C4 shard 1998-2029 ->
+    // 2091-2098 M-obs/s (profiles/r04_v13_ab_pcg_t_c4shard.txt).  Without
+    // them (k_pcg_point_t re-reads W) only when the fp64 W outgrows the
+    // 256-MiB Infinity Cache (C5 shard +2.7 %; below it the extra pass lost
+    // ~0.7 %).  BA_PCG_T=0 / 1 (diagnostics) forces it off / on.
     const char* fe = getenv("BA_PCG_T");   // (read per solve: tests switch it)
     const int force = fe ? atoi(fe) : -1;
     // (decided from the largest rank's shard: every rank runs the same path)
     const bool big = 144.0 * (double)ctx->max_no > 256.0 * 1024 * 1024;
-    // (with the point-aligned chunks the products go to camera order and are
-    // streamed: then also for the fp32 W)
-    const bool use_t = !W.wcm && (force >= 0 ? force != 0 : big && (!W.w32 || W.npchunks > 0));
+    const bool use_t = !W.wcm && (force >= 0 ? force != 0 : W.npchunks > 0 || (big && !W.w32));
     if (use_t && !ctx->tobs_buf) ctx->tobs_buf = ctx->dalloc<double>(6 * (size_t)std::max(ctx->no, 1));
     if (!use_t && ctx->tobs_buf) { ctx->dfree(ctx->tobs_buf); ctx->tobs_buf = nullptr; }   // 48 B/obs back
     W.tobs = use_t ? ctx->tobs_buf : nullptr;
