@@ -1886,17 +1886,67 @@ __device__ __forceinline__ void glds16(const double* src, double* lds_dst) {
 }
 constexpr int kPairsDmaLds = 4 * 2 * 64 * kWcRec * (int)sizeof(double);   // 64 KB: 4 waves x (row, partner) x 64 records
 
+// S_cc = s Hcc s + D^2 - (the G slices of -sum W W^T), b_c likewise: entry e
+// = (camera, 27 entries) (k_cam_fold_diag, or the extra workgroups of the
+// pair pass's launch)
+__device__ __forceinline__ void cam_fold_diag_entry(const DevProblem& P, const double* __restrict__ cpart, int nsl,
+                                                    const double* __restrict__ Hcc, const double* __restrict__ gc,
+                                                    const double* __restrict__ scale_c,
+                                                    const double* __restrict__ diag_c, double radius,
+                                                    double* __restrict__ S, double* __restrict__ scal, int e) {
+  // no fma contraction: the fused and the exchange path (k_cam_fold +
+  // k_cam_add_diag) must round identically
+#pragma clang fp contract(off)
+  if (e == 0) { scal[SL_CHOL_BAD] = 0.0; scal[SL_CHOL_SPIN] = 0.0; }   // the Cholesky that follows flags failures here
+  if (e >= P.nvc * 27) return;
+  const int v = e / 27, k = e - v * 27;
+  double acc = 0.0;
+  for (int sl = 0; sl < nsl; ++sl) acc += cpart[((size_t)sl * P.nvc + v) * 27 + k];
+  const size_t ld = (size_t)P.ld;
+  if (k < 21) {
+    int a = 0;
+    while ((a + 1) * (a + 2) / 2 <= k) ++a;
+    const int b = k - a * (a + 1) / 2;
+    double h = Hcc[(size_t)v * 21 + k] * scale_c[(size_t)v * 6 + a] * scale_c[(size_t)v * 6 + b];
+    if (a == b) {
+      const double D = sqrt(diag_c[(size_t)v * 6 + a] / radius);
+      h += D * D;
+    }
+    S[(size_t)(6 * v + a) * ld + 6 * v + b] = -acc + h;
+  } else {
+    const int a = k - 21;
+    S[(size_t)P.n * ld + 6 * v + a] = -acc + gc[(size_t)v * 6 + a] * scale_c[(size_t)v * 6 + a];
+  }
+}
+// FoldArgs (nsl > 0): workgroups past pgrid run the diagonal fold
+// (cam_fold_diag_entry) instead of pairs — independent of the pairs (other S
+// blocks) when no point has two observations by one camera
+struct FoldArgs {
+  const double* cpart;
+  int nsl;
+  const double* Hcc;
+  const double* gc;
+  const double* diag_c;
+  double radius;
+  double* scal;
+};
 __global__ __launch_bounds__(256) void k_schur_pairs_cd(DevProblem P, const int4* __restrict__ blocks,
                                                         const int* __restrict__ xoff, const int2* __restrict__ pairs,
                                                         const double* __restrict__ Wc,
-                                                        const double* __restrict__ scale_c, double* __restrict__ S) {
+                                                        const double* __restrict__ scale_c, double* __restrict__ S,
+                                                        int pgrid, FoldArgs fa) {
+  if ((int)blockIdx.x >= pgrid) {
+    cam_fold_diag_entry(P, fa.cpart, fa.nsl, fa.Hcc, fa.gc, scale_c, fa.diag_c, fa.radius, S, fa.scal,
+                        ((int)blockIdx.x - pgrid) * blockDim.x + threadIdx.x);
+    return;
+  }
   extern __shared__ double dsm[];
   WcCam* ctab = reinterpret_cast<WcCam*>(dsm + kPairsDmaLds / (int)sizeof(double));
   for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
   __syncthreads();
   constexpr int PL = kPairLanes, BPW = 64 / PL;
   const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
-  const int xcd = blockIdx.x & 7, wx = blockIdx.x >> 3, nwx = gridDim.x >> 3;
+  const int xcd = blockIdx.x & 7, wx = blockIdx.x >> 3, nwx = pgrid >> 3;
   const int r0 = xoff[xcd], r1 = xoff[xcd + 1];
   const int wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   double* rbuf = dsm + (size_t)wv * 2 * 64 * kWcRec;   // row camera's records [64][16]
@@ -2038,30 +2088,7 @@ __global__ __launch_bounds__(256) void k_cam_fold_diag(DevProblem P, const doubl
                                                        const double* __restrict__ scale_c,
                                                        const double* __restrict__ diag_c, double radius,
                                                        double* __restrict__ S, double* __restrict__ scal) {
-  // no fma contraction: the fused and the exchange path (k_cam_fold +
-  // k_cam_add_diag) must round identically
-#pragma clang fp contract(off)
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e == 0) { scal[SL_CHOL_BAD] = 0.0; scal[SL_CHOL_SPIN] = 0.0; }   // the Cholesky that follows flags failures here
-  if (e >= P.nvc * 27) return;
-  const int v = e / 27, k = e - v * 27;
-  double acc = 0.0;
-  for (int sl = 0; sl < nsl; ++sl) acc += cpart[((size_t)sl * P.nvc + v) * 27 + k];
-  const size_t ld = (size_t)P.ld;
-  if (k < 21) {
-    int a = 0;
-    while ((a + 1) * (a + 2) / 2 <= k) ++a;
-    const int b = k - a * (a + 1) / 2;
-    double h = Hcc[(size_t)v * 21 + k] * scale_c[(size_t)v * 6 + a] * scale_c[(size_t)v * 6 + b];
-    if (a == b) {
-      const double D = sqrt(diag_c[(size_t)v * 6 + a] / radius);
-      h += D * D;
-    }
-    S[(size_t)(6 * v + a) * ld + 6 * v + b] = -acc + h;
-  } else {
-    const int a = k - 21;
-    S[(size_t)P.n * ld + 6 * v + a] = -acc + gc[(size_t)v * 6 + a] * scale_c[(size_t)v * 6 + a];
-  }
+  cam_fold_diag_entry(P, cpart, nsl, Hcc, gc, scale_c, diag_c, radius, S, scal, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -3802,11 +3829,16 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
       hipLaunchKernelGGL((k_obs_w<false, double>), dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.W);
   }
 }
-void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact, double radius) {
-  if (P.nvc == 0) return;
-  static int dsplit = -1;   // diagnostics: BA_DIAG_SPLIT overrides the slice count
+// camera slices of the diagonal pass (BA_DIAG_SPLIT: diagnostics)
+int cam_split_count(const DevWork& W) {
+  static int dsplit = -1;
   if (dsplit < 0) { const char* e = getenv("BA_DIAG_SPLIT"); dsplit = e ? atoi(e) : 0; }
-  const int sl = dsplit > 0 ? std::min(dsplit, kCamSplit) : W.cam_split;
+  return dsplit > 0 ? std::min(dsplit, kCamSplit) : W.cam_split;
+}
+void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact, double radius,
+                           bool skip_fold) {
+  if (P.nvc == 0) return;
+  const int sl = cam_split_count(W);
   // threads per camera slice by its observations (~8 per thread): 256, or
   // 128 at C5's 1250 observations per camera
   const int per = (int)std::max<long long>(1, (long long)P.no / std::max(P.nvc * sl, 1));
@@ -3866,6 +3898,7 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
   }
   else
     hipLaunchKernelGGL(k_cam_schur_diag<double>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.W, W.u, W.S, W.cpart);
+  if (skip_fold) return;   // (the pair pass's launch folds: launch_schur_pairs)
   if (!compact && radius > 0.0) {   // single rank: the LM diagonal goes in with the fold
     hipLaunchKernelGGL(k_cam_fold_diag, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, W.Hcc,
                        W.gc, W.scale_c, W.diag_c, radius, W.S, W.scal);
@@ -3875,7 +3908,15 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
                      compact ? 2 : 1, W.Hcc,
                      W.gc, compact ? compact : W.S);
 }
-void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
+// the diagonal fold (k_cam_fold_diag) can ride in the pair pass's launch
+bool pairs_take_fold(const DevProblem& P, const DevWork& W) {
+  const char* dma_env = getenv("BA_PAIRS_DMA");
+  const int dma = dma_env ? atoi(dma_env) : 1;
+  const char* fe = getenv("BA_FOLD_IN_PAIRS");
+  return W.nblocks > 0 && W.wcompact && dma && kPairsDmaLds + sizeof(WcCam) * (size_t)P.nvc <= 80 * 1024 &&
+         !(fe && fe[0] == '0');
+}
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius) {
   if (W.nblocks == 0) return;
   static int grid_cap = 0;
   if (grid_cap == 0) {
@@ -3896,9 +3937,16 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s) {
   const char* dma_env = getenv("BA_PAIRS_DMA");
   const int dma = dma_env ? atoi(dma_env) : 1;
   const size_t ctab_bytes = sizeof(WcCam) * (size_t)P.nvc;
-  if (W.wcompact && dma && kPairsDmaLds + ctab_bytes <= 80 * 1024)
-    hipLaunchKernelGGL(k_schur_pairs_cd, dim3(grid), dim3(256), kPairsDmaLds + ctab_bytes, s, P, W.blocks, xoff,
-                       W.pairs, W.W, W.scale_c, W.S);
+  if (W.wcompact && dma && kPairsDmaLds + ctab_bytes <= 80 * 1024) {
+    FoldArgs fa{W.cpart, 0, W.Hcc, W.gc, W.diag_c, fold_radius, W.scal};
+    int fgrid = 0;
+    if (fold_radius > 0.0) {   // the diagonal fold rides in this launch
+      fa.nsl = cam_split_count(W);
+      fgrid = (P.nvc * 27 + 255) / 256;
+    }
+    hipLaunchKernelGGL(k_schur_pairs_cd, dim3(grid + fgrid), dim3(256), kPairsDmaLds + ctab_bytes, s, P, W.blocks,
+                       xoff, W.pairs, W.W, W.scale_c, W.S, grid, fa);
+  }
   else if (W.wcompact)
     hipLaunchKernelGGL(k_schur_pairs_c, dim3(grid), dim3(256), ctab_bytes, s, P, W.blocks, xoff,
                        W.pairs, W.W, W.scale_c, W.S);

@@ -725,8 +725,11 @@ void form_reduced_dense(ba_ctx* ctx, double radius) {
   // single rank, no diagonal pair blocks: the LM diagonal goes in with the
   // fold (same operation order as the exchange path's, bitwise)
   const bool fused_diag = !ctx->coll() && !ctx->dup_diag;
-  launch_cam_schur_diag(P, W, s, nullptr, fused_diag ? radius : 0.0);
-  launch_schur_pairs(P, W, s);
+  // ... and that fold rides in the pair pass's launch when it can (one
+  // launch fewer; the fold writes only the diagonal blocks and the rhs)
+  const bool fold_in_pairs = fused_diag && radius > 0.0 && pairs_take_fold(P, W);
+  launch_cam_schur_diag(P, W, s, nullptr, fused_diag ? radius : 0.0, fold_in_pairs);
+  launch_schur_pairs(P, W, s, fold_in_pairs ? radius : 0.0);
   if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
   if (ctx->coll()) {
     // only the lower triangle and the rhs row of S carry data: all-reduce
