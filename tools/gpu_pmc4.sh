@@ -9,7 +9,10 @@ mkdir -p gpurun_out
 OUT=gpurun_out
 export TMPDIR=/tmp
 SQSET="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU"
-for w in "c3" "c4s --workload c4 --scale 0.125" "c5s --workload c5 --scale 0.125"; do
+# WL: the workloads (default all three), e.g. WL="c3"
+WL=${WL:-"c3,c4s --workload c4 --scale 0.125,c5s --workload c5 --scale 0.125"}
+IFS=, read -ra WLS <<< "$WL"
+for w in "${WLS[@]}"; do
   set -- $w; tag=$1; shift
   for pass in FETCH_SIZE WRITE_SIZE SQ; do
     ctr=$pass; [ $pass = SQ ] && ctr=$SQSET
