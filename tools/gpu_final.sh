@@ -14,7 +14,6 @@ timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/
 rc=$?; tail -2 $OUT/smoke.log; stop_on_fault $rc
 timeout -k 10 600 python3 -u bench.py > $OUT/final_bench.json 2> $OUT/final_bench.err
 rc=$?; python3 -c "import json; d=json.load(open('$OUT/final_bench.json')); print('c3', d['value'], d['ms_per_step'], d.get('ms_per_step_median'), d['roofline']['frac'], d['cpu_baseline']['value'])"; stop_on_fault $rc
-PROF3=1 TESTS=0 bash -c 'true'
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c3 -o run -- \
   python3 -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_c3.json 2> $OUT/prof_c3.err
