@@ -90,6 +90,7 @@ struct DevWork {
   double* Vbuf;                      // [ceil(n/64)][64][64] inverses of the diagonal Cholesky blocks
   double* yg;                        // [n][2] back-substitution hand-off granules {y, epoch} (zeroed once)
   unsigned* cflags;                  // [T + TR*T] persistent-Cholesky hand-off flags (epoch-tagged, zeroed once)
+  unsigned* dcnt = nullptr;          // [nvc] per-camera slice tickets of the diagonal pass in the pair launch
   bool chol_persist;                 // the factorisation runs as one persistent launch (ba_chol_persist.hip)
   const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}, camera rows interleaved over the XCDs
   const int* xoff;                   // [9] k_schur_pairs* block range of XCD x: [xoff[x], xoff[x+1])
@@ -148,8 +149,10 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
 // rank): add s Hcc s + D^2 and s g_c in the same pass (no launch_cam_add_diag)
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact = nullptr,
                            double radius = 0.0, bool skip_fold = false);
-void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius = 0.0);
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius = 0.0,
+                        bool with_diag = false);
 bool pairs_take_fold(const DevProblem& P, const DevWork& W);
+bool pairs_take_diag(const DevProblem& P, const DevWork& W);
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
 // ba_chol.hip; epoch: per-context launch counter (>= 1) tagging the
 // back substitution's hand-off flags

@@ -1886,6 +1886,95 @@ __device__ __forceinline__ void glds16(const double* src, double* lds_dst) {
 }
 constexpr int kPairsDmaLds = 4 * 2 * 64 * kWcRec * (int)sizeof(double);   // 64 KB: 4 waves x (row, partner) x 64 records
 
+// one camera slice (v, slice g of G) by one wave: the per-lane sums
+__device__ __forceinline__ void diag_cd_wave(const DevProblem& P, const double* __restrict__ Wc,
+                                             const double* __restrict__ scale_c, const double* __restrict__ u,
+                                             int v, int g, int G, double* rbuf, double* ubuf, double (&acc)[27]) {
+  WcCam m;
+  m.load(P, scale_c, v);
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
+  const int a0 = P.cam_off[v], a1 = P.cam_off[v + 1];
+  const int len = (a1 - a0 + G - 1) / G;
+  const int i0 = min(a1, a0 + g * len), i1 = min(a1, i0 + len);
+  const int lane = threadIdx.x & 63;
+  const int swr = (lane >> 1) & 7;
+  auto issue = [&](int2 op) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = (lane >> 3) + 8 * k;
+      const int oq = __shfl(op.x, q);
+      glds16(Wc + (size_t)oq * kWcRec + 2 * ((lane & 7) ^ ((q >> 1) & 7)), rbuf + k * 128);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = (lane >> 1) + 32 * k;
+      const int pq = __shfl(op.y, q);
+      glds16(u + 4 * (size_t)pq + 2 * (lane & 1), ubuf + k * 128);
+    }
+  };
+  const int nr = (i1 - i0 + 63) >> 6;   // rounds (uniform)
+  int i = i0 + lane;
+  int2 op = i < i1 ? P.cam_op[i] : make_int2(0, 0);
+  int2 opn = i + 64 < i1 ? P.cam_op[i + 64] : make_int2(0, 0);
+  if (nr > 0) issue(op);
+  for (int r = 0; r < nr; ++r, i += 64) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this round's DMA has landed
+    WcRaw w;
+    const double* rr = rbuf + lane * kWcRec;
+#pragma unroll
+    for (int p = 0; p < kWcRec / 2; ++p) {
+      const double2 t = *reinterpret_cast<const double2*>(rr + 2 * (p ^ swr));
+      w.r[2 * p] = t.x;
+      w.r[2 * p + 1] = t.y;
+    }
+    const double2 u01 = *reinterpret_cast<const double2*>(ubuf + 4 * lane);
+    const double u2 = ubuf[4 * lane + 2];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the refill
+    if (r + 1 < nr) {
+      issue(opn);
+      opn = i + 128 < i1 ? P.cam_op[i + 128] : make_int2(0, 0);
+    }
+    if (i < i1) {
+      double c0[6], c1[6];
+      wc_rows(w, m, c0, c1);
+      const double* z0 = w.r + 9;
+      const double* z1 = w.r + 12;
+      const double m00 = z0[0] * z0[0] + z0[1] * z0[1] + z0[2] * z0[2];
+      const double m01 = z0[0] * z1[0] + z0[1] * z1[1] + z0[2] * z1[2];
+      const double m11 = z1[0] * z1[0] + z1[1] * z1[1] + z1[2] * z1[2];
+      const double zu0 = z0[0] * u01.x + z0[1] * u01.y + z0[2] * u2;
+      const double zu1 = z1[0] * u01.x + z1[1] * u01.y + z1[2] * u2;
+      double n0[6], n1[6];
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        n0[b] = m00 * c0[b] + m01 * c1[b];
+        n1[b] = m01 * c0[b] + m11 * c1[b];
+      }
+      int t = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+#pragma unroll
+        for (int b = 0; b <= a; ++b) acc[t++] += c0[a] * n0[b] + c1[a] * n1[b];
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) acc[21 + a] += c0[a] * zu0 + c1[a] * zu1;
+    }
+  }
+}
+__global__ __launch_bounds__(64) void k_cam_schur_diag_cd(DevProblem P, const double* __restrict__ Wc,
+                                                          const double* __restrict__ scale_c,
+                                                          const double* __restrict__ u, double* __restrict__ cpart) {
+  __shared__ double lds[27 * 16];
+  __shared__ __attribute__((aligned(16))) double rbuf[64 * kWcRec];
+  __shared__ __attribute__((aligned(16))) double ubuf[64 * 4];
+  double acc[27];
+  diag_cd_wave(P, Wc, scale_c, u, blockIdx.x, blockIdx.y, gridDim.y, rbuf, ubuf, acc);
+  double tot[27];
+  block_sum<27>(acc, lds, tot);
+  cam_slice_store(tot, cpart, blockIdx.x, P.nvc);
+}
+
 // S_cc = s Hcc s + D^2 - (the G slices of -sum W W^T), b_c likewise: entry e
 // = (camera, 27 entries) (k_cam_fold_diag, or the extra workgroups of the
 // pair pass's launch)
@@ -1922,25 +2011,60 @@ __device__ __forceinline__ void cam_fold_diag_entry(const DevProblem& P, const d
 // (cam_fold_diag_entry) instead of pairs — independent of the pairs (other S
 // blocks) when no point has two observations by one camera
 struct FoldArgs {
-  const double* cpart;
+  double* cpart;
   int nsl;
   const double* Hcc;
   const double* gc;
   const double* diag_c;
   double radius;
   double* scal;
+  // diag: the diagonal pass rides in the launch as well (workgroups past
+  // pgrid: four camera slices each, one per wave); the last slice of a
+  // camera to finish folds it (per-camera ticket)
+  int diag;
+  const double* u;
+  unsigned* dcnt;
 };
 __global__ __launch_bounds__(256) void k_schur_pairs_cd(DevProblem P, const int4* __restrict__ blocks,
                                                         const int* __restrict__ xoff, const int2* __restrict__ pairs,
                                                         const double* __restrict__ Wc,
                                                         const double* __restrict__ scale_c, double* __restrict__ S,
                                                         int pgrid, FoldArgs fa) {
+  extern __shared__ double dsm[];
   if ((int)blockIdx.x >= pgrid) {
-    cam_fold_diag_entry(P, fa.cpart, fa.nsl, fa.Hcc, fa.gc, scale_c, fa.diag_c, fa.radius, S, fa.scal,
-                        ((int)blockIdx.x - pgrid) * blockDim.x + threadIdx.x);
+    if (!fa.diag) {
+      cam_fold_diag_entry(P, fa.cpart, fa.nsl, fa.Hcc, fa.gc, scale_c, fa.diag_c, fa.radius, S, fa.scal,
+                          ((int)blockIdx.x - pgrid) * blockDim.x + threadIdx.x);
+      return;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int item = ((int)blockIdx.x - pgrid) * 4 + wv;
+    if (item >= P.nvc * fa.nsl) return;
+    const int v = item / fa.nsl, g = item - v * fa.nsl;
+    double* rb = dsm + (size_t)wv * (64 * kWcRec + 64 * 4);
+    double acc[27];
+    diag_cd_wave(P, Wc, scale_c, fa.u, v, g, fa.nsl, rb, rb + 64 * kWcRec, acc);
+    // k_cam_schur_diag_cd's single-wave block_sum: the wave sum, then 0 + it
+    double tot[27];
+#pragma unroll
+    for (int k = 0; k < 27; ++k) tot[k] = 0.0 + wave_sum(acc[k]);
+    unsigned t = 0;
+    if (lane == 0) {
+      double* dst = fa.cpart + ((size_t)g * P.nvc + v) * 27;
+#pragma unroll
+      for (int k = 0; k < 27; ++k) dst[k] = tot[k];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the slice before the ticket
+      t = __hip_atomic_fetch_add(&fa.dcnt[v], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (t != (unsigned)fa.nsl - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every slice of camera v after it
+    if (lane < 27)
+      cam_fold_diag_entry(P, fa.cpart, fa.nsl, fa.Hcc, fa.gc, scale_c, fa.diag_c, fa.radius, S, fa.scal,
+                          v * 27 + lane);
+    if (lane == 0) fa.dcnt[v] = 0u;   // (the next launch's ticket; ordered by the launch boundary)
     return;
   }
-  extern __shared__ double dsm[];
   WcCam* ctab = reinterpret_cast<WcCam*>(dsm + kPairsDmaLds / (int)sizeof(double));
   for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
   __syncthreads();
@@ -3041,88 +3165,6 @@ __global__ __launch_bounds__(NT) void k_cam_schur_diag_c(DevProblem P, const dou
 // workgroup.  The next round's observation indices are loaded one round
 // ahead, its DMA issued right after this round's records are read out of
 // LDS.  The same adds per lane in the same order: bitwise k_cam_schur_diag_c.
-__global__ __launch_bounds__(64) void k_cam_schur_diag_cd(DevProblem P, const double* __restrict__ Wc,
-                                                          const double* __restrict__ scale_c,
-                                                          const double* __restrict__ u, double* __restrict__ cpart) {
-  __shared__ double lds[27 * 16];
-  __shared__ __attribute__((aligned(16))) double rbuf[64 * kWcRec];
-  __shared__ __attribute__((aligned(16))) double ubuf[64 * 4];
-  const int v = blockIdx.x;
-  WcCam m;
-  m.load(P, scale_c, v);
-  double acc[27];
-#pragma unroll
-  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
-  int i0, i1;
-  cam_slice(P, v, i0, i1);
-  const int lane = threadIdx.x;
-  const int swr = (lane >> 1) & 7;
-  auto issue = [&](int2 op) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int q = (lane >> 3) + 8 * k;
-      const int oq = __shfl(op.x, q);
-      glds16(Wc + (size_t)oq * kWcRec + 2 * ((lane & 7) ^ ((q >> 1) & 7)), rbuf + k * 128);
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int q = (lane >> 1) + 32 * k;
-      const int pq = __shfl(op.y, q);
-      glds16(u + 4 * (size_t)pq + 2 * (lane & 1), ubuf + k * 128);
-    }
-  };
-  const int nr = (i1 - i0 + 63) >> 6;   // rounds (uniform)
-  int i = i0 + lane;
-  int2 op = i < i1 ? P.cam_op[i] : make_int2(0, 0);
-  int2 opn = i + 64 < i1 ? P.cam_op[i + 64] : make_int2(0, 0);
-  if (nr > 0) issue(op);
-  for (int r = 0; r < nr; ++r, i += 64) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this round's DMA has landed
-    WcRaw w;
-    const double* rr = rbuf + lane * kWcRec;
-#pragma unroll
-    for (int p = 0; p < kWcRec / 2; ++p) {
-      const double2 t = *reinterpret_cast<const double2*>(rr + 2 * (p ^ swr));
-      w.r[2 * p] = t.x;
-      w.r[2 * p + 1] = t.y;
-    }
-    const double2 u01 = *reinterpret_cast<const double2*>(ubuf + 4 * lane);
-    const double u2 = ubuf[4 * lane + 2];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the refill
-    if (r + 1 < nr) {
-      issue(opn);
-      opn = i + 128 < i1 ? P.cam_op[i + 128] : make_int2(0, 0);
-    }
-    if (i < i1) {
-      double c0[6], c1[6];
-      wc_rows(w, m, c0, c1);
-      const double* z0 = w.r + 9;
-      const double* z1 = w.r + 12;
-      const double m00 = z0[0] * z0[0] + z0[1] * z0[1] + z0[2] * z0[2];
-      const double m01 = z0[0] * z1[0] + z0[1] * z1[1] + z0[2] * z1[2];
-      const double m11 = z1[0] * z1[0] + z1[1] * z1[1] + z1[2] * z1[2];
-      const double zu0 = z0[0] * u01.x + z0[1] * u01.y + z0[2] * u2;
-      const double zu1 = z1[0] * u01.x + z1[1] * u01.y + z1[2] * u2;
-      double n0[6], n1[6];
-#pragma unroll
-      for (int b = 0; b < 6; ++b) {
-        n0[b] = m00 * c0[b] + m01 * c1[b];
-        n1[b] = m01 * c0[b] + m11 * c1[b];
-      }
-      int t = 0;
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-#pragma unroll
-        for (int b = 0; b <= a; ++b) acc[t++] += c0[a] * n0[b] + c1[a] * n1[b];
-      }
-#pragma unroll
-      for (int a = 0; a < 6; ++a) acc[21 + a] += c0[a] * zu0 + c1[a] * zu1;
-    }
-  }
-  double tot[27];
-  block_sum<27>(acc, lds, tot);
-  cam_slice_store(tot, cpart, v, P.nvc);
-}
 
 // model cost change + candidate cost with J recomputed at x (the lin table of
 // the linearisation point) beside the value-only candidate table
@@ -3916,7 +3958,16 @@ bool pairs_take_fold(const DevProblem& P, const DevWork& W) {
   return W.nblocks > 0 && W.wcompact && dma && kPairsDmaLds + sizeof(WcCam) * (size_t)P.nvc <= 80 * 1024 &&
          !(fe && fe[0] == '0');
 }
-void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius) {
+// the diagonal pass itself can ride there too (BA_DIAG_IN_PAIRS=1)
+bool pairs_take_diag(const DevProblem& P, const DevWork& W) {
+  const char* e = getenv("BA_DIAG_IN_PAIRS");
+  const char* de = getenv("BA_DIAG_DMA");
+  const char* ne = getenv("BA_DIAG_NT");
+  const char* pe = getenv("BA_DIAG_PREF");
+  return pairs_take_fold(P, W) && W.dcnt && e && e[0] == '1' && !(de && de[0] == '0') && !(ne && atoi(ne) != 64) &&
+         !(pe && atoi(pe) != 0) && 4 * (64 * kWcRec + 64 * 4) * (int)sizeof(double) <= kPairsDmaLds;
+}
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius, bool with_diag) {
   if (W.nblocks == 0) return;
   static int grid_cap = 0;
   if (grid_cap == 0) {
@@ -3938,11 +3989,15 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, do
   const int dma = dma_env ? atoi(dma_env) : 1;
   const size_t ctab_bytes = sizeof(WcCam) * (size_t)P.nvc;
   if (W.wcompact && dma && kPairsDmaLds + ctab_bytes <= 80 * 1024) {
-    FoldArgs fa{W.cpart, 0, W.Hcc, W.gc, W.diag_c, fold_radius, W.scal};
+    FoldArgs fa{W.cpart, 0, W.Hcc, W.gc, W.diag_c, fold_radius, W.scal, 0, W.u, W.dcnt};
     int fgrid = 0;
     if (fold_radius > 0.0) {   // the diagonal fold rides in this launch
       fa.nsl = cam_split_count(W);
       fgrid = (P.nvc * 27 + 255) / 256;
+      if (with_diag) {   // ... and the diagonal pass (four slices per workgroup)
+        fa.diag = 1;
+        fgrid = (P.nvc * fa.nsl + 3) / 4;
+      }
     }
     hipLaunchKernelGGL(k_schur_pairs_cd, dim3(grid + fgrid), dim3(256), kPairsDmaLds + ctab_bytes, s, P, W.blocks,
                        xoff, W.pairs, W.W, W.scale_c, W.S, grid, fa);

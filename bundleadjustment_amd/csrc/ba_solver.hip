@@ -517,6 +517,8 @@ void ensure_dense(ba_ctx* ctx) {
     const size_t nf = (size_t)T + (size_t)TR * T;
     W.cflags = ctx->dalloc<unsigned>(nf);
     HIP_OK(hipMemsetAsync(W.cflags, 0, sizeof(unsigned) * std::max<size_t>(nf, 1), ctx->stream));
+    W.dcnt = ctx->dalloc<unsigned>(std::max(nvc, 1));
+    HIP_OK(hipMemsetAsync(W.dcnt, 0, sizeof(unsigned) * std::max(nvc, 1), ctx->stream));
   }
   W.Spk = nullptr;
   // diagonal pair blocks (a point observed twice by one camera) update the
@@ -728,8 +730,10 @@ void form_reduced_dense(ba_ctx* ctx, double radius) {
   // ... and that fold rides in the pair pass's launch when it can (one
   // launch fewer; the fold writes only the diagonal blocks and the rhs)
   const bool fold_in_pairs = fused_diag && radius > 0.0 && pairs_take_fold(P, W);
-  launch_cam_schur_diag(P, W, s, nullptr, fused_diag ? radius : 0.0, fold_in_pairs);
-  launch_schur_pairs(P, W, s, fold_in_pairs ? radius : 0.0);
+  // (BA_DIAG_IN_PAIRS=1: the diagonal pass too, its fold by per-camera tickets)
+  const bool diag_in_pairs = fold_in_pairs && pairs_take_diag(P, W);
+  if (!diag_in_pairs) launch_cam_schur_diag(P, W, s, nullptr, fused_diag ? radius : 0.0, fold_in_pairs);
+  launch_schur_pairs(P, W, s, fold_in_pairs ? radius : 0.0, diag_in_pairs);
   if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
   if (ctx->coll()) {
     // only the lower triangle and the rhs row of S carry data: all-reduce
