@@ -2684,11 +2684,17 @@ __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const doub
                                                         const double* __restrict__ pxv, double* __restrict__ cpart,
                                                         double* __restrict__ Hcc, double* __restrict__ gc) {
   __shared__ double lds[27 * 16];
+  // TB 2: the camera's dual Rodrigues and K once per workgroup, in LDS and
+  // read at use (uniform broadcasts; an opaque per-observation offset keeps
+  // the reads from being hoisted into registers: 196 -> fewer VGPRs, more
+  // waves per SIMD)
+  __shared__ CamRcR scam;
   const int v = blockIdx.x;
   const int c = P.cam_of_vc[v];
-  typename std::conditional<TB == 2, CamRcR, CamRegs>::type cam;
+  CamRegs cam;
   if constexpr (TB == 2) {
-    cam.make(cam_rc(rec, c));
+    if (threadIdx.x == 0) scam.make(cam_rc(rec, c));
+    __syncthreads();
   } else {
     const double2* s2 = reinterpret_cast<const double2*>(rec + (size_t)c * kCamRec + kRecL);
 #pragma unroll
@@ -2707,7 +2713,14 @@ __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const doub
     const double2 x01 = xr[0], x2v = xr[1];
     double out[kJR];
     bool fin;
-    (void)lin_obs(P, cam, true, x2v.y != 0.0, x01.x, x01.y, x2v.x, P.uv_cm[i], out, fin);
+    if constexpr (TB == 2) {
+      int zo = 0;
+      asm volatile("" : "+v"(zo));
+      const CamRcR& cl = *reinterpret_cast<const CamRcR*>(reinterpret_cast<const char*>(&scam) + zo);
+      (void)lin_obs(P, cl, true, x2v.y != 0.0, x01.x, x01.y, x2v.x, P.uv_cm[i], out, fin);
+    } else {
+      (void)lin_obs(P, cam, true, x2v.y != 0.0, x01.x, x01.y, x2v.x, P.uv_cm[i], out, fin);
+    }
     // cam_acc_jr on the record: Jc rows (0..11) and the residual (18, 19)
     const double rr[2] = {out[18], out[19]};
 #pragma unroll
@@ -3016,6 +3029,8 @@ __global__ __launch_bounds__(NT) void k_cam_schur_diag_rc(DevProblem P, const do
   __shared__ double lds[27 * 16];
   const int v = blockIdx.x;
   const int c = P.cam_of_vc[v];
+  // (the camera in registers: its LDS form, as k_cam_assemble_rc's, drops
+  // 244 -> 204 VGPRs, still two waves per SIMD; three spill 35)
   typename std::conditional<TB == 2, CamRcR, CamRegs>::type cam;
   if constexpr (TB == 2) {
     cam.make(cam_rc(rec, c));
