@@ -4086,9 +4086,10 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
       constexpr int NT = 512, L = 4;
       const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
       const int g = std::max(1, std::min(want, kMaxBlocks));
-      // TB 3: pass 1's compact records by LDS-DMA (BA_PS_DMA=0: register gathers)
+      // TB 3: pass 1's compact records by LDS-DMA (BA_PS_DMA=1; the variant
+      // spills ~50 VGPRs, so it is opt-in until measured)
       const char* pe = getenv("BA_PS_DMA");
-      const bool dma = tb == 2 && P.no > 0 && crec_dma() && !(pe && pe[0] == '0');
+      const bool dma = tb == 2 && P.no > 0 && crec_dma() && pe && pe[0] == '1';
       hipLaunchKernelGGL((tb == 1 ? k_point_step_rc<NT, L, false, 3, 1>
                                   : dma ? k_point_step_rc<NT, L, false, 3, 3> : k_point_step_rc<NT, L, false, 3, 2>),
                          dim3(g),
