@@ -558,15 +558,40 @@ __device__ __forceinline__ void factor_invert_impl(double (*T)[LDP], double (*X)
   __syncthreads();
   CHOL_STAMP(2);
   int last = 0;
+  // one trailing-update tile (ti, ts) -= (sub-panel c0 columns) products
+  auto upd_tile = [&](int ti, int ts, int c0) {
+    d4 acc = tile_load(T, 16 * ti, 16 * ts);
+    acc = mfma_tile<16>(acc, T, 16 * ti, c0, T, 16 * ts, c0, -1.0);
+    tile_store(T, 16 * ti, 16 * ts, acc);
+  };
   auto subpanel = [&](const int p) {
     const int c0 = 16 * p;
     last = p;
     if (w == 0) panel_sweep(T, W, c0, b, m);
     else if (w == 1 && p > 0) inverse_rowblock(T, W.rsv, X, Z, p - 1, b, 1);
     else if (p == 0 && Pc != nullptr) mfma_xxT_rest(Pc, T);
-    else if (p >= 1) hook(p);
+    else if (p >= 1) {
+      // FULL: sub-panel 0's updates of tiles (3, 2) and (3, 3), which only
+      // sub-panels 2 and 3 read, run here beside the sweep of sub-panel 1
+      // (waves 2, 3) instead of as a second round before it; each tile
+      // still takes its sub-panel-0 update before its sub-panel-1 one
+      if constexpr (FULL) {
+        if (p == 1) upd_tile(3, w == 2 ? 2 : 3, 0);
+      }
+      hook(p);
+    }
     CHOL_STAMP(10 + 2 * p);
     __syncthreads();
+    if constexpr (FULL) {
+      if (p == 0) {   // the tiles the next sweeps read first: one round
+        const int ti = w == 0 ? 1 : (w == 1 ? 2 : (w == 2 ? 2 : 3));
+        const int ts = w == 2 ? 2 : 1;
+        upd_tile(ti, ts, c0);
+        __syncthreads();
+        CHOL_STAMP(11 + 2 * p);
+        return;
+      }
+    }
     // trailing update of the remaining sub-panels: tiles (i, s), p < s <= i
     {
       const int nt = 3 - p;                  // tile rows below the sub-panel
