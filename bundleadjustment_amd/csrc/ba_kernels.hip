@@ -2673,6 +2673,56 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   }
 }
 
+// k_cam_norms folded into the camera assembly's launch (single rank, one
+// workgroup per camera): every workgroup takes a ticket after an agent-scope
+// release of its Hcc / gc; the last one acquires and forms the Jacobi
+// scalings, the LM diagonal and the camera-side norms of all cameras (the
+// per-camera arithmetic of k_cam_norms; one partial per slot)
+// (NormArgs: ba_kernels.h)
+__device__ inline void cam_norms_last(const DevProblem& P, const NormArgs& na, const double* __restrict__ Hcc,
+                                      const double* __restrict__ gc, double* lds) {
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this camera's blocks before the ticket
+    const unsigned t = __hip_atomic_fetch_add(na.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    lds[0] = t == gridDim.x - 1 ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  const bool last = lds[0] != 0.0;
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every camera's blocks after it
+  double acc[2] = {0.0, 0.0};
+  double gmax = 0.0;
+  for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) {
+    const int c = P.cam_of_vc[v];
+    for (int a = 0; a < 6; ++a) {
+      const double h = Hcc[(size_t)v * 21 + tri(a, a)];
+      double s;
+      if (na.compute_scale) {
+        s = 1.0 / (1.0 + sqrt(h));
+        na.scale_c[(size_t)v * 6 + a] = s;
+      } else {
+        s = na.scale_c[(size_t)v * 6 + a];
+      }
+      na.diag_c[(size_t)v * 6 + a] = fmin(fmax(h * s * s, na.min_diag), na.max_diag);
+      const double x = na.cams[6 * c + a], g = gc[(size_t)v * 6 + a];
+      const double d = x - (x + (-g));
+      gmax = fmax(gmax, fabs(d));
+      acc[0] += d * d;
+      acc[1] += x * x;
+    }
+  }
+  double out[2];
+  block_sum<2>(acc, lds, out);
+  const double m = block_max1(gmax, lds + 32);
+  if (threadIdx.x == 0) {
+    part_of(na.part, SL_GN2_C)[0] = out[0];
+    part_of(na.part, SL_XN2_C)[0] = out[1];
+    part_of(na.part, SL_GMAX_C)[0] = m;
+    *na.ticket = 0u;   // (the next launch's; ordered by the launch boundary)
+  }
+}
+
 // Hcc (lower 21) and gc per variable camera, its observations in camera order
 // (k_cam_assemble's order: thread i takes i0 + tid, i0 + tid + NT, ...)
 // TB = 2: rec is the compact records crec (the camera's dual Rodrigues once
@@ -2682,7 +2732,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 template <int NT, int TB = 0>
 __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const double* __restrict__ rec,
                                                         const double* __restrict__ pxv, double* __restrict__ cpart,
-                                                        double* __restrict__ Hcc, double* __restrict__ gc) {
+                                                        double* __restrict__ Hcc, double* __restrict__ gc,
+                                                        NormArgs na) {
   __shared__ double lds[27 * 16];
   // TB 2: the camera's dual Rodrigues and K once per workgroup, in LDS and
   // read at use (uniform broadcasts; an opaque per-observation offset keeps
@@ -2744,6 +2795,7 @@ __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const doub
 #pragma unroll
       for (int k = 0; k < 6; ++k) gc[(size_t)v * 6 + k] = out27[21 + k];
     }
+    if (na.ticket) cam_norms_last(P, na, Hcc, gc, lds);
     return;
   }
   cam_slice_store(out27, cpart, v, P.nvc);
@@ -3737,9 +3789,11 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
                      dim3(kThreads), 0, s, P, W.JR, W.pts, W.Hpp, W.gp,
                      W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
 }
-void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
+void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s, const NormArgs* norms) {
   if (P.nvc == 0) return;
   if (W.jrfree) {
+    NormArgs na{};
+    if (norms) na = *norms;
     // diagnostics: BA_CA_NT (128 / 256 / 512 threads), BA_CA_SPLIT (workgroups
     // per camera, <= W.cam_split; > 1 adds the ordered slice fold).  One
     // 512-thread workgroup per camera measured best: 30.6 us vs 37 / 49 us at
@@ -3749,6 +3803,7 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
     if (sp < 0) { const char* e = getenv("BA_CA_SPLIT"); sp = e ? atoi(e) : 1; }
     const int sl = std::max(1, std::min(sp, W.cam_split));
     const dim3 g(P.nvc, sl);
+    if (sl > 1) na.ticket = nullptr;   // (the launch_cam_norms caller checks cam_norms_fused)
     if (jr_tab(P, W) == 2) {
       // (the compact records: the camera's dual Rodrigues once per
       // workgroup).  Threads per camera by its observations (~8 per thread):
@@ -3759,22 +3814,22 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
       const int t = per >= 8 * 512 ? 512 : (per >= 8 * 256 ? 256 : (per >= 8 * 128 ? 128 : 64));
       const double* cr = W.crec;
       if (t == 512)
-        hipLaunchKernelGGL((k_cam_assemble_rc<512, 2>), g, dim3(512), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
+        hipLaunchKernelGGL((k_cam_assemble_rc<512, 2>), g, dim3(512), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc, na);
       else if (t == 256)
-        hipLaunchKernelGGL((k_cam_assemble_rc<256, 2>), g, dim3(256), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
+        hipLaunchKernelGGL((k_cam_assemble_rc<256, 2>), g, dim3(256), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc, na);
       else if (t == 128)
-        hipLaunchKernelGGL((k_cam_assemble_rc<128, 2>), g, dim3(128), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
+        hipLaunchKernelGGL((k_cam_assemble_rc<128, 2>), g, dim3(128), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc, na);
       else
-        hipLaunchKernelGGL((k_cam_assemble_rc<64, 2>), g, dim3(64), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
+        hipLaunchKernelGGL((k_cam_assemble_rc<64, 2>), g, dim3(64), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc, na);
     } else if (nt == 128)
       hipLaunchKernelGGL(k_cam_assemble_rc<128>, g, dim3(128), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
-                         W.cpart, W.Hcc, W.gc);
+                         W.cpart, W.Hcc, W.gc, na);
     else if (nt == 256)
       hipLaunchKernelGGL(k_cam_assemble_rc<256>, g, dim3(256), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
-                         W.cpart, W.Hcc, W.gc);
+                         W.cpart, W.Hcc, W.gc, na);
     else
       hipLaunchKernelGGL(k_cam_assemble_rc<512>, g, dim3(512), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
-                         W.cpart, W.Hcc, W.gc);
+                         W.cpart, W.Hcc, W.gc, na);
     if (sl > 1)
       hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
                          nullptr);
@@ -3802,6 +3857,12 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (sl > 1)
     hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
                        nullptr);
+}
+bool cam_norms_fused(const DevWork& W) {
+  static int sp = -1;
+  if (sp < 0) { const char* e = getenv("BA_CA_SPLIT"); sp = e ? atoi(e) : 1; }
+  const char* fe = getenv("BA_NORMS_FUSED");
+  return W.jrfree && W.aticket && std::max(1, std::min(sp, W.cam_split)) == 1 && !(fe && fe[0] == '0');
 }
 void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
                       hipStream_t s) {

@@ -108,3 +108,24 @@ def test_dma_gathers_are_bitwise_the_register_gathers(monkeypatch, switch, cfg):
             out[mode] = s.debug_blocks(1e4)
     assert np.array_equal(out["0"]["S"], out["1"]["S"])
     assert np.array_equal(out["0"]["rhs"], out["1"]["rhs"])
+
+
+@pytest.mark.timeout(600)
+def test_camera_norms_in_the_assembly_launch_are_bitwise_the_separate_launch(monkeypatch):
+    """The camera-side Jacobi scalings, LM diagonal and norms formed by the
+    camera assembly's last workgroup (BA_NORMS_FUSED, the default) equal those
+    of the separate k_cam_norms launch at C3 (one partial either way): the
+    same solve, bitwise."""
+    from bundleadjustment_amd import Options
+    p = make_config("c3", scale=0.2)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("BA_NORMS_FUSED", mode)
+        with Solver(0) as s:
+            s.set_problem(p)
+            summ = s.solve(Options(max_num_iterations=5))
+            cams, pts = s.params()
+            res[mode] = (summ.final_cost, [(it["cost"], it["gradient_norm"]) for it in s.iteration_log()], cams, pts)
+    assert res["0"][0] == res["1"][0]
+    assert res["0"][1] == res["1"][1]
+    assert np.array_equal(res["0"][2], res["1"][2]) and np.array_equal(res["0"][3], res["1"][3])
