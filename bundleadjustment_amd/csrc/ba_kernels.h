@@ -90,8 +90,6 @@ struct DevWork {
   double* Vbuf;                      // [ceil(n/64)][64][64] inverses of the diagonal Cholesky blocks
   double* yg;                        // [n][2] back-substitution hand-off granules {y, epoch} (zeroed once)
   unsigned* cflags;                  // [T + TR*T] persistent-Cholesky hand-off flags (epoch-tagged, zeroed once)
-  unsigned* dcnt = nullptr;          // [nvc] per-camera slice tickets of the diagonal pass in the pair launch
-  unsigned* aticket = nullptr;       // the camera assembly's ticket (k_cam_norms folded into its launch)
   bool chol_persist;                 // the factorisation runs as one persistent launch (ba_chol_persist.hip)
   const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}, camera rows interleaved over the XCDs
   const int* xoff;                   // [9] k_schur_pairs* block range of XCD x: [xoff[x], xoff[x+1])
@@ -141,18 +139,7 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
 // the JR-writing linearisation (launch_linearize in JR mode; ba_linearize's read-back in J-free mode)
 void launch_linearize_jr(const DevProblem& P, const DevWork& W, hipStream_t s, hipEvent_t t0 = nullptr,
                          hipEvent_t t1 = nullptr);
-// k_cam_norms' arguments when it runs inside the camera assembly's launch
-struct NormArgs {
-  const double* cams;
-  double* scale_c;
-  double* diag_c;
-  int compute_scale;
-  double min_diag, max_diag;
-  double* part;
-  unsigned* ticket;   // nullptr: k_cam_norms runs as its own launch
-};
-void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s, const NormArgs* norms = nullptr);
-bool cam_norms_fused(const DevWork& W);
+void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
                       hipStream_t s);
 void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);  // + W = E L^-T
@@ -161,10 +148,8 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
 // rank): add s Hcc s + D^2 and s g_c in the same pass (no launch_cam_add_diag)
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact = nullptr,
                            double radius = 0.0, bool skip_fold = false);
-void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius = 0.0,
-                        bool with_diag = false);
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius = 0.0);
 bool pairs_take_fold(const DevProblem& P, const DevWork& W);
-bool pairs_take_diag(const DevProblem& P, const DevWork& W);
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
 // ba_chol.hip; epoch: per-context launch counter (>= 1) tagging the
 // back substitution's hand-off flags

@@ -2011,60 +2011,25 @@ __device__ __forceinline__ void cam_fold_diag_entry(const DevProblem& P, const d
 // (cam_fold_diag_entry) instead of pairs — independent of the pairs (other S
 // blocks) when no point has two observations by one camera
 struct FoldArgs {
-  double* cpart;
+  const double* cpart;
   int nsl;
   const double* Hcc;
   const double* gc;
   const double* diag_c;
   double radius;
   double* scal;
-  // diag: the diagonal pass rides in the launch as well (workgroups past
-  // pgrid: four camera slices each, one per wave); the last slice of a
-  // camera to finish folds it (per-camera ticket)
-  int diag;
-  const double* u;
-  unsigned* dcnt;
 };
 __global__ __launch_bounds__(256) void k_schur_pairs_cd(DevProblem P, const int4* __restrict__ blocks,
                                                         const int* __restrict__ xoff, const int2* __restrict__ pairs,
                                                         const double* __restrict__ Wc,
                                                         const double* __restrict__ scale_c, double* __restrict__ S,
                                                         int pgrid, FoldArgs fa) {
-  extern __shared__ double dsm[];
   if ((int)blockIdx.x >= pgrid) {
-    if (!fa.diag) {
-      cam_fold_diag_entry(P, fa.cpart, fa.nsl, fa.Hcc, fa.gc, scale_c, fa.diag_c, fa.radius, S, fa.scal,
-                          ((int)blockIdx.x - pgrid) * blockDim.x + threadIdx.x);
-      return;
-    }
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int item = ((int)blockIdx.x - pgrid) * 4 + wv;
-    if (item >= P.nvc * fa.nsl) return;
-    const int v = item / fa.nsl, g = item - v * fa.nsl;
-    double* rb = dsm + (size_t)wv * (64 * kWcRec + 64 * 4);
-    double acc[27];
-    diag_cd_wave(P, Wc, scale_c, fa.u, v, g, fa.nsl, rb, rb + 64 * kWcRec, acc);
-    // k_cam_schur_diag_cd's single-wave block_sum: the wave sum, then 0 + it
-    double tot[27];
-#pragma unroll
-    for (int k = 0; k < 27; ++k) tot[k] = 0.0 + wave_sum(acc[k]);
-    unsigned t = 0;
-    if (lane == 0) {
-      double* dst = fa.cpart + ((size_t)g * P.nvc + v) * 27;
-#pragma unroll
-      for (int k = 0; k < 27; ++k) dst[k] = tot[k];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the slice before the ticket
-      t = __hip_atomic_fetch_add(&fa.dcnt[v], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    t = __builtin_amdgcn_readfirstlane(t);
-    if (t != (unsigned)fa.nsl - 1) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every slice of camera v after it
-    if (lane < 27)
-      cam_fold_diag_entry(P, fa.cpart, fa.nsl, fa.Hcc, fa.gc, scale_c, fa.diag_c, fa.radius, S, fa.scal,
-                          v * 27 + lane);
-    if (lane == 0) fa.dcnt[v] = 0u;   // (the next launch's ticket; ordered by the launch boundary)
+    cam_fold_diag_entry(P, fa.cpart, fa.nsl, fa.Hcc, fa.gc, scale_c, fa.diag_c, fa.radius, S, fa.scal,
+                        ((int)blockIdx.x - pgrid) * blockDim.x + threadIdx.x);
     return;
   }
+  extern __shared__ double dsm[];
   WcCam* ctab = reinterpret_cast<WcCam*>(dsm + kPairsDmaLds / (int)sizeof(double));
   for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
   __syncthreads();
@@ -2673,56 +2638,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   }
 }
 
-// k_cam_norms folded into the camera assembly's launch (single rank, one
-// workgroup per camera): every workgroup takes a ticket after an agent-scope
-// release of its Hcc / gc; the last one acquires and forms the Jacobi
-// scalings, the LM diagonal and the camera-side norms of all cameras (the
-// per-camera arithmetic of k_cam_norms; one partial per slot)
-// (NormArgs: ba_kernels.h)
-__device__ inline void cam_norms_last(const DevProblem& P, const NormArgs& na, const double* __restrict__ Hcc,
-                                      const double* __restrict__ gc, double* lds) {
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this camera's blocks before the ticket
-    const unsigned t = __hip_atomic_fetch_add(na.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    lds[0] = t == gridDim.x - 1 ? 1.0 : 0.0;
-  }
-  __syncthreads();
-  const bool last = lds[0] != 0.0;
-  __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every camera's blocks after it
-  double acc[2] = {0.0, 0.0};
-  double gmax = 0.0;
-  for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) {
-    const int c = P.cam_of_vc[v];
-    for (int a = 0; a < 6; ++a) {
-      const double h = Hcc[(size_t)v * 21 + tri(a, a)];
-      double s;
-      if (na.compute_scale) {
-        s = 1.0 / (1.0 + sqrt(h));
-        na.scale_c[(size_t)v * 6 + a] = s;
-      } else {
-        s = na.scale_c[(size_t)v * 6 + a];
-      }
-      na.diag_c[(size_t)v * 6 + a] = fmin(fmax(h * s * s, na.min_diag), na.max_diag);
-      const double x = na.cams[6 * c + a], g = gc[(size_t)v * 6 + a];
-      const double d = x - (x + (-g));
-      gmax = fmax(gmax, fabs(d));
-      acc[0] += d * d;
-      acc[1] += x * x;
-    }
-  }
-  double out[2];
-  block_sum<2>(acc, lds, out);
-  const double m = block_max1(gmax, lds + 32);
-  if (threadIdx.x == 0) {
-    part_of(na.part, SL_GN2_C)[0] = out[0];
-    part_of(na.part, SL_XN2_C)[0] = out[1];
-    part_of(na.part, SL_GMAX_C)[0] = m;
-    *na.ticket = 0u;   // (the next launch's; ordered by the launch boundary)
-  }
-}
-
 // Hcc (lower 21) and gc per variable camera, its observations in camera order
 // (k_cam_assemble's order: thread i takes i0 + tid, i0 + tid + NT, ...)
 // TB = 2: rec is the compact records crec (the camera's dual Rodrigues once
@@ -2732,8 +2647,7 @@ __device__ inline void cam_norms_last(const DevProblem& P, const NormArgs& na, c
 template <int NT, int TB = 0>
 __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const double* __restrict__ rec,
                                                         const double* __restrict__ pxv, double* __restrict__ cpart,
-                                                        double* __restrict__ Hcc, double* __restrict__ gc,
-                                                        NormArgs na) {
+                                                        double* __restrict__ Hcc, double* __restrict__ gc) {
   __shared__ double lds[27 * 16];
   // TB 2: the camera's dual Rodrigues and K once per workgroup, in LDS and
   // read at use (uniform broadcasts; an opaque per-observation offset keeps
@@ -2795,7 +2709,6 @@ __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const doub
 #pragma unroll
       for (int k = 0; k < 6; ++k) gc[(size_t)v * 6 + k] = out27[21 + k];
     }
-    if (na.ticket) cam_norms_last(P, na, Hcc, gc, lds);
     return;
   }
   cam_slice_store(out27, cpart, v, P.nvc);
@@ -3370,8 +3283,6 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
   __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
   __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
   __shared__ double ctb_s[TB ? 1 : kLinLdsCams * kCandRec];
-  // TB 3: pass 1's compact camera records by LDS-DMA (k_lin_point_d's rounds)
-  __shared__ __attribute__((aligned(16))) double cbuf[TB == 3 ? NT / 64 : 1][TB == 3 ? 64 * kCRec : 2];
   if constexpr (!TB) {
     fill_lin_table<NT>(P, rec, tbl, ktb);
     const int n = P.nc * kCandRec;
@@ -3389,7 +3300,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
     if constexpr (TB == 1) {
       const CamG cam{rec + (size_t)c * kGRec};
       (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
-    } else if constexpr (TB == 2 || TB == 3) {
+    } else if constexpr (TB == 2) {
       const CamRc cam = cam_rc(rec, c);
       (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
     } else if constexpr (LAZY) {
@@ -3400,40 +3311,13 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
       (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
     }
   };
-  const int lane = threadIdx.x & 63;
-  double* cb = cbuf[TB == 3 ? (int)(threadIdx.x >> 6) : 0];
-  auto issue = [&](int cc) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int q = (lane >> 3) + 8 * k;
-      const int cq = __shfl(cc, q);
-      glds16(rec + (size_t)cq * kCRec + 2 * ((lane & 7) ^ ((q >> 1) & 7)), cb + k * 128);
-    }
-  };
-  auto fetch = [&]() {
-    CamRcPre q;
-    const int swr = (lane >> 1) & 7;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int k = 0; k < kCRec / 2; ++k) q.v[k] = *reinterpret_cast<const double2*>(cb + lane * kCRec + 2 * (k ^ swr));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    return q;
-  };
   int p = P.np > 0 ? g0 : P.np;
   if (P.np > 0) {
     int pc = min(p, lastp);
     int o0 = P.pt_off[pc], o1 = P.pt_off[pc + 1];
     double X0 = pts[3 * pc], X1 = pts[3 * pc + 1], X2 = pts[3 * pc + 2];
     bool pv = P.pt_var[pc] != 0;
-    // TB 3: the lane's camera whose record is in flight (the point's first)
-    int cdma = 0;
-    if constexpr (TB == 3) {
-      cdma = P.obs_cam[min(o0 + sl, lasto)];
-      issue(cdma);
-    }
-    // TB 3: wave-uniform point rounds (the DMA needs every lane)
-    for (; TB == 3 ? __any(p < P.np) != 0 : p < P.np; p += gs) {   // uniform inside a lane group
-      const bool livep = TB != 3 || p < P.np;
+    for (; p < P.np; p += gs) {   // uniform inside a lane group
       const int pn = min(p + gs, lastp);
       const int o0n = P.pt_off[pn], o1n = P.pt_off[pn + 1];
       const double Y0 = pts[3 * pn], Y1 = pts[3 * pn + 1], Y2 = pts[3 * pn + 2];
@@ -3444,76 +3328,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
       // past them (points with more than LANES * KC observations) and for
       // fixed points (no pass 1)
       double kc[KC][10];
-      if constexpr (TB == 3) {
-        // pass 1 in wave-uniform rounds, the records one round ahead (the
-        // point's last round requests the lane's next point's first camera)
-        const bool act1 = livep && pv;
-        double v0 = 0.0, v1 = 0.0, v2 = 0.0;
-        int o = o0 + sl;
-        float2 uv = P.uv[min(o, lasto)];
-        int cnt = act1 && o1 - o0 > sl ? (o1 - o0 - sl + LANES - 1) / LANES : 0;
-#pragma unroll
-        for (int x = 32; x >= 1; x >>= 1) cnt = max(cnt, __shfl_xor(cnt, x));
-        const int cnp = P.obs_cam[min(o0n + sl, lasto)];
-        if (cnt == 0) {
-          (void)fetch();
-          issue(cnp);
-          cdma = cnp;
-        }
-        auto round = [&](double (&keep)[10], bool store, bool more) {
-          const CamRcPre q = fetch();
-          const int on = min(o + LANES, lasto);
-          const int cn = more ? P.obs_cam[on] : cnp;
-          const float2 uvn = P.uv[on];
-          if (act1 && o < o1) {
-            const CamRc cam = cam_make(CamRcOf{rec, nullptr}, q);
-            double j[kJR];
-            bool fin;
-            (void)lin_obs(P, cam, cam.var(), true, X0, X1, X2, uv, j, fin);
-            const double* dc = ctb + (size_t)cdma * kCandRec + 16;
-            double t0 = 0.0, t1 = 0.0;
-#pragma unroll
-            for (int a = 0; a < 6; ++a) { t0 += j[a] * dc[a]; t1 += j[6 + a] * dc[a]; }
-            v0 += j[12] * t0 + j[15] * t1;
-            v1 += j[13] * t0 + j[16] * t1;
-            v2 += j[14] * t0 + j[17] * t1;
-            if (store) {
-              keep[0] = t0; keep[1] = t1;
-#pragma unroll
-              for (int k = 0; k < 8; ++k) keep[2 + k] = j[12 + k];
-            }
-          }
-          // the next round's records (after the arithmetic: the request's
-          // addresses then do not share the registers of lin_obs)
-          issue(cn);
-          cdma = cn;
-          uv = uvn;
-          o += LANES;
-        };
-#pragma unroll
-        for (int t = 0; t < KC; ++t)
-          if (t < cnt) round(kc[t], true, t + 1 < cnt);
-        for (int t = KC; t < cnt; ++t) round(kc[0], false, t + 1 < cnt);
-        if (act1) {
-#pragma unroll
-          for (int x = LANES / 2; x >= 1; x >>= 1) {
-            v0 += __shfl_xor(v0, x, LANES);
-            v1 += __shfl_xor(v1, x, LANES);
-            v2 += __shfl_xor(v2, x, LANES);
-          }
-          const double s0 = scale_p[p], s1 = scale_p[np + p], s2 = scale_p[2 * np + p];
-          const double i00 = Linv[p], i10 = Linv[np + p], i11 = Linv[2 * np + p];
-          const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
-          const double z0 = s0 * v0, z1 = s1 * v1, z2 = s2 * v2;
-          const double w0 = u[4 * p] + i00 * z0;
-          const double w1 = u[4 * p + 1] + (i10 * z0 + i11 * z1);
-          const double w2 = u[4 * p + 2] + (i20 * z0 + i21 * z1 + i22 * z2);
-          const double yp[3] = {i00 * w0 + i10 * w1 + i20 * w2, i11 * w1 + i21 * w2, i22 * w2};
-          const double sp[3] = {s0, s1, s2};
-#pragma unroll
-          for (int k = 0; k < 3; ++k) dX[k] = (-yp[k]) * sp[k];
-        }
-      } else if (pv) {
+      if (pv) {
         // pass 1: v = sum Jp^T (Jc dc)
         double v0 = 0.0, v1 = 0.0, v2 = 0.0;
         int o = o0 + sl;
@@ -3565,7 +3380,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
         for (int k = 0; k < 3; ++k) dX[k] = (-yp[k]) * sp[k];
       }
       const double Xc[3] = {X0 + dX[0], X1 + dX[1], X2 + dX[2]};
-      if (livep && sl == 0) {
+      if (sl == 0) {
         const double Xk[3] = {X0, X1, X2};
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -3579,7 +3394,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
         }
       }
       // pass 2: model cost change and candidate cost per observation
-      if (livep) {
+      {
         int o = o0 + sl;
         int oc = min(o, lasto);
         int c = P.obs_cam[oc];
@@ -3621,7 +3436,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
             for (int i = 0; i < 4; ++i) ph[i] = Xc[0] * cr[i] + Xc[1] * cr[4 + i] + Xc[2] * cr[8 + i] + cr[12 + i];
             pcand[0] = ph[0] / ph[3]; pcand[1] = ph[1] / ph[3]; pcand[2] = ph[2] / ph[3];
           }
-          const float* Kc = TB == 1 ? CamG{rec + (size_t)c * kGRec}.Kf() : (TB >= 2 ? P.K + 9 * c : ktb + c * 9);
+          const float* Kc = TB == 1 ? CamG{rec + (size_t)c * kGRec}.Kf() : (TB == 2 ? P.K + 9 * c : ktb + c * 9);
           double q[3];
 #pragma unroll
           for (int i = 0; i < 3; ++i)
@@ -3647,7 +3462,6 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
       X0 = Y0; X1 = Y1; X2 = Y2;
       pv = pvn;
     }
-    if constexpr (TB == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last (unread) request
   }
   double tot[5];
   block_sum<5>(acc, lds, tot);
@@ -3789,11 +3603,9 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
                      dim3(kThreads), 0, s, P, W.JR, W.pts, W.Hpp, W.gp,
                      W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
 }
-void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s, const NormArgs* norms) {
+void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
   if (W.jrfree) {
-    NormArgs na{};
-    if (norms) na = *norms;
     // diagnostics: BA_CA_NT (128 / 256 / 512 threads), BA_CA_SPLIT (workgroups
     // per camera, <= W.cam_split; > 1 adds the ordered slice fold).  One
     // 512-thread workgroup per camera measured best: 30.6 us vs 37 / 49 us at
@@ -3803,7 +3615,6 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s, c
     if (sp < 0) { const char* e = getenv("BA_CA_SPLIT"); sp = e ? atoi(e) : 1; }
     const int sl = std::max(1, std::min(sp, W.cam_split));
     const dim3 g(P.nvc, sl);
-    if (sl > 1) na.ticket = nullptr;   // (the launch_cam_norms caller checks cam_norms_fused)
     if (jr_tab(P, W) == 2) {
       // (the compact records: the camera's dual Rodrigues once per
       // workgroup).  Threads per camera by its observations (~8 per thread):
@@ -3814,22 +3625,22 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s, c
       const int t = per >= 8 * 512 ? 512 : (per >= 8 * 256 ? 256 : (per >= 8 * 128 ? 128 : 64));
       const double* cr = W.crec;
       if (t == 512)
-        hipLaunchKernelGGL((k_cam_assemble_rc<512, 2>), g, dim3(512), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc, na);
+        hipLaunchKernelGGL((k_cam_assemble_rc<512, 2>), g, dim3(512), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
       else if (t == 256)
-        hipLaunchKernelGGL((k_cam_assemble_rc<256, 2>), g, dim3(256), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc, na);
+        hipLaunchKernelGGL((k_cam_assemble_rc<256, 2>), g, dim3(256), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
       else if (t == 128)
-        hipLaunchKernelGGL((k_cam_assemble_rc<128, 2>), g, dim3(128), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc, na);
+        hipLaunchKernelGGL((k_cam_assemble_rc<128, 2>), g, dim3(128), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
       else
-        hipLaunchKernelGGL((k_cam_assemble_rc<64, 2>), g, dim3(64), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc, na);
+        hipLaunchKernelGGL((k_cam_assemble_rc<64, 2>), g, dim3(64), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
     } else if (nt == 128)
       hipLaunchKernelGGL(k_cam_assemble_rc<128>, g, dim3(128), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
-                         W.cpart, W.Hcc, W.gc, na);
+                         W.cpart, W.Hcc, W.gc);
     else if (nt == 256)
       hipLaunchKernelGGL(k_cam_assemble_rc<256>, g, dim3(256), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
-                         W.cpart, W.Hcc, W.gc, na);
+                         W.cpart, W.Hcc, W.gc);
     else
       hipLaunchKernelGGL(k_cam_assemble_rc<512>, g, dim3(512), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
-                         W.cpart, W.Hcc, W.gc, na);
+                         W.cpart, W.Hcc, W.gc);
     if (sl > 1)
       hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
                          nullptr);
@@ -3857,12 +3668,6 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s, c
   if (sl > 1)
     hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
                        nullptr);
-}
-bool cam_norms_fused(const DevWork& W) {
-  static int sp = -1;
-  if (sp < 0) { const char* e = getenv("BA_CA_SPLIT"); sp = e ? atoi(e) : 1; }
-  const char* fe = getenv("BA_NORMS_FUSED");
-  return W.jrfree && W.aticket && std::max(1, std::min(sp, W.cam_split)) == 1 && !(fe && fe[0] == '0');
 }
 void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
                       hipStream_t s) {
@@ -4034,16 +3839,7 @@ bool pairs_take_fold(const DevProblem& P, const DevWork& W) {
   return W.nblocks > 0 && W.wcompact && dma && kPairsDmaLds + sizeof(WcCam) * (size_t)P.nvc <= 80 * 1024 &&
          !(fe && fe[0] == '0');
 }
-// the diagonal pass itself can ride there too (BA_DIAG_IN_PAIRS=1)
-bool pairs_take_diag(const DevProblem& P, const DevWork& W) {
-  const char* e = getenv("BA_DIAG_IN_PAIRS");
-  const char* de = getenv("BA_DIAG_DMA");
-  const char* ne = getenv("BA_DIAG_NT");
-  const char* pe = getenv("BA_DIAG_PREF");
-  return pairs_take_fold(P, W) && W.dcnt && e && e[0] == '1' && !(de && de[0] == '0') && !(ne && atoi(ne) != 64) &&
-         !(pe && atoi(pe) != 0) && 4 * (64 * kWcRec + 64 * 4) * (int)sizeof(double) <= kPairsDmaLds;
-}
-void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius, bool with_diag) {
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius) {
   if (W.nblocks == 0) return;
   static int grid_cap = 0;
   if (grid_cap == 0) {
@@ -4065,15 +3861,11 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, do
   const int dma = dma_env ? atoi(dma_env) : 1;
   const size_t ctab_bytes = sizeof(WcCam) * (size_t)P.nvc;
   if (W.wcompact && dma && kPairsDmaLds + ctab_bytes <= 80 * 1024) {
-    FoldArgs fa{W.cpart, 0, W.Hcc, W.gc, W.diag_c, fold_radius, W.scal, 0, W.u, W.dcnt};
+    FoldArgs fa{W.cpart, 0, W.Hcc, W.gc, W.diag_c, fold_radius, W.scal};
     int fgrid = 0;
     if (fold_radius > 0.0) {   // the diagonal fold rides in this launch
       fa.nsl = cam_split_count(W);
       fgrid = (P.nvc * 27 + 255) / 256;
-      if (with_diag) {   // ... and the diagonal pass (four slices per workgroup)
-        fa.diag = 1;
-        fgrid = (P.nvc * fa.nsl + 3) / 4;
-      }
     }
     hipLaunchKernelGGL(k_schur_pairs_cd, dim3(grid + fgrid), dim3(256), kPairsDmaLds + ctab_bytes, s, P, W.blocks,
                        xoff, W.pairs, W.W, W.scale_c, W.S, grid, fa);
@@ -4147,13 +3939,7 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
       constexpr int NT = 512, L = 4;
       const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
       const int g = std::max(1, std::min(want, kMaxBlocks));
-      // TB 3: pass 1's compact records by LDS-DMA (BA_PS_DMA=1; the variant
-      // spills ~50 VGPRs, so it is opt-in until measured)
-      const char* pe = getenv("BA_PS_DMA");
-      const bool dma = tb == 2 && P.no > 0 && crec_dma() && pe && pe[0] == '1';
-      hipLaunchKernelGGL((tb == 1 ? k_point_step_rc<NT, L, false, 3, 1>
-                                  : dma ? k_point_step_rc<NT, L, false, 3, 3> : k_point_step_rc<NT, L, false, 3, 2>),
-                         dim3(g),
+      hipLaunchKernelGGL((tb == 1 ? k_point_step_rc<NT, L, false, 3, 1> : k_point_step_rc<NT, L, false, 3, 2>), dim3(g),
                          dim3(NT), 0, s, P, (const double*)(tb == 1 ? W.gtbl : W.crec), (const double*)W.pts,
                          W.delta_c, (const double*)W.ctbl, W.u, W.Linv, W.scale_p, W.pts_c, W.delta_p, W.part);
       return;

@@ -430,8 +430,6 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.Wf = nullptr;
   W.y = ctx->dalloc<double>(std::max(ctx->n, 1));
   W.part = ctx->dalloc<double>((size_t)kNumSlots * kMaxBlocks);
-  W.aticket = ctx->dalloc<unsigned>(1);
-  HIP_OK(hipMemsetAsync(W.aticket, 0, sizeof(unsigned), ctx->stream));
   W.cam_split = nvc > 0 ? std::min(kCamSplit, std::max(1, 2048 / nvc)) : 1;
   W.cpart = ctx->dalloc<double>((size_t)W.cam_split * 27 * std::max(nvc, 1));
 
@@ -519,8 +517,6 @@ void ensure_dense(ba_ctx* ctx) {
     const size_t nf = (size_t)T + (size_t)TR * T;
     W.cflags = ctx->dalloc<unsigned>(nf);
     HIP_OK(hipMemsetAsync(W.cflags, 0, sizeof(unsigned) * std::max<size_t>(nf, 1), ctx->stream));
-    W.dcnt = ctx->dalloc<unsigned>(std::max(nvc, 1));
-    HIP_OK(hipMemsetAsync(W.dcnt, 0, sizeof(unsigned) * std::max(nvc, 1), ctx->stream));
   }
   W.Spk = nullptr;
   // diagonal pair blocks (a point observed twice by one camera) update the
@@ -668,11 +664,7 @@ void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double 
   launch_linearize(P, W, s, e0, e1);
   // (J-free: the timed residual + Jacobian kernel is k_lin_point, launched here)
   launch_point_assemble(P, W, compute_scale, min_diag, max_diag, s, W.jrfree ? e0 : nullptr, W.jrfree ? e1 : nullptr);
-  // (single rank: the camera norms run inside the assembly's launch, by its
-  // last workgroup)
-  const bool fuse_norms = !ctx->coll() && cam_norms_fused(W);
-  const NormArgs na{W.cams, W.scale_c, W.diag_c, compute_scale ? 1 : 0, min_diag, max_diag, W.part, W.aticket};
-  launch_cam_assemble(P, W, s, fuse_norms ? &na : nullptr);
+  launch_cam_assemble(P, W, s);
   // point-side scalars: folded here when they must be all-reduced before
   // cam_norms, else together with the camera-side ones (one launch less)
   const uint32_t lin_sum = bit(SL_COST) | bit(SL_LIN_BAD) | bit(SL_GN2_P) | bit(SL_XN2_P);
@@ -682,7 +674,7 @@ void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double 
     ctx->allreduce(W.Hcc, 27 * (size_t)ctx->nvc + SL_GMAX_P);
     ctx->allreduce(W.scal + SL_GMAX_P, 1, ncclMax);
   }
-  if (!fuse_norms) launch_cam_norms(P, W, compute_scale, min_diag, max_diag, s);
+  launch_cam_norms(P, W, compute_scale, min_diag, max_diag, s);
   const uint32_t sum_mask = bit(SL_GN2_C) | bit(SL_XN2_C) | (ctx->coll() ? 0u : lin_sum);
   const uint32_t max_mask = bit(SL_GMAX_C) | (ctx->coll() ? 0u : bit(SL_GMAX_P));
   if (defer_reduce && !ctx->coll()) {
@@ -736,10 +728,8 @@ void form_reduced_dense(ba_ctx* ctx, double radius) {
   // ... and that fold rides in the pair pass's launch when it can (one
   // launch fewer; the fold writes only the diagonal blocks and the rhs)
   const bool fold_in_pairs = fused_diag && radius > 0.0 && pairs_take_fold(P, W);
-  // (BA_DIAG_IN_PAIRS=1: the diagonal pass too, its fold by per-camera tickets)
-  const bool diag_in_pairs = fold_in_pairs && pairs_take_diag(P, W);
-  if (!diag_in_pairs) launch_cam_schur_diag(P, W, s, nullptr, fused_diag ? radius : 0.0, fold_in_pairs);
-  launch_schur_pairs(P, W, s, fold_in_pairs ? radius : 0.0, diag_in_pairs);
+  launch_cam_schur_diag(P, W, s, nullptr, fused_diag ? radius : 0.0, fold_in_pairs);
+  launch_schur_pairs(P, W, s, fold_in_pairs ? radius : 0.0);
   if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
   if (ctx->coll()) {
     // only the lower triangle and the rhs row of S carry data: all-reduce

@@ -88,7 +88,7 @@ def test_jfree_blocks_and_reduced_system_match_oracle(oracle_lib, cfg, scale):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("switch,cfg", [("BA_PAIRS_DMA", "c3"), ("BA_DIAG_DMA", "c3"), ("BA_CREC_DMA", "c4"),
-                                        ("BA_FOLD_IN_PAIRS", "c3"), ("BA_DIAG_IN_PAIRS", "c3")])
+                                        ("BA_FOLD_IN_PAIRS", "c3")])
 def test_dma_gathers_are_bitwise_the_register_gathers(monkeypatch, switch, cfg):
     """k_schur_pairs_cd / k_cam_schur_diag_cd (compact records gathered into
     LDS by LDS-DMA, the defaults) form the same products in the same order as
@@ -96,9 +96,8 @@ def test_dma_gathers_are_bitwise_the_register_gathers(monkeypatch, switch, cfg):
     the rhs must agree bitwise (C3 camera count: the LDS form's size limit).
     BA_CREC_DMA: the compact W records of the C4 shard from camera records
     gathered by LDS-DMA (k_obs_w_rc TB 3) or per lane (TB 2).
-    BA_FOLD_IN_PAIRS / BA_DIAG_IN_PAIRS: the diagonal fold (and the diagonal
-    pass, folded by per-camera tickets) as extra workgroups of the pair
-    pass's launch or as launches of their own."""
+    BA_FOLD_IN_PAIRS: the diagonal fold as extra workgroups of the pair
+    pass's launch or as a launch of its own."""
     p = make_config(cfg, scale=0.2 if cfg == "c3" else 0.02)
     out = {}
     for mode in ("0", "1"):
@@ -109,23 +108,3 @@ def test_dma_gathers_are_bitwise_the_register_gathers(monkeypatch, switch, cfg):
     assert np.array_equal(out["0"]["S"], out["1"]["S"])
     assert np.array_equal(out["0"]["rhs"], out["1"]["rhs"])
 
-
-@pytest.mark.timeout(600)
-def test_camera_norms_in_the_assembly_launch_are_bitwise_the_separate_launch(monkeypatch):
-    """The camera-side Jacobi scalings, LM diagonal and norms formed by the
-    camera assembly's last workgroup (BA_NORMS_FUSED, the default) equal those
-    of the separate k_cam_norms launch at C3 (one partial either way): the
-    same solve, bitwise."""
-    from bundleadjustment_amd import Options
-    p = make_config("c3", scale=0.2)
-    res = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("BA_NORMS_FUSED", mode)
-        with Solver(0) as s:
-            s.set_problem(p)
-            summ = s.solve(Options(max_num_iterations=5))
-            cams, pts = s.params()
-            res[mode] = (summ.final_cost, [(it["cost"], it["gradient_norm"]) for it in s.iteration_log()], cams, pts)
-    assert res["0"][0] == res["1"][0]
-    assert res["0"][1] == res["1"][1]
-    assert np.array_equal(res["0"][2], res["1"][2]) and np.array_equal(res["0"][3], res["1"][3])

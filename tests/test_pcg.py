@@ -166,13 +166,12 @@ def set_matvec(monkeypatch, mode):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
-@pytest.mark.parametrize("switch,on,off", [("BA_CREC_DMA", "1", "0"), ("BA_LP_DMA", "1", "0"), ("BA_PS_DMA", "1", "0")])
+@pytest.mark.parametrize("switch,on,off", [("BA_CREC_DMA", "1", "0"), ("BA_LP_DMA", "1", "0")])
 def test_gpu_camera_record_dma_is_bitwise_the_register_gather(solver, precision, switch, on, off, monkeypatch):
     """The point-major kernels beyond 200 cameras with the compact camera
     records gathered by LDS-DMA (k_obs_w_rc TB 3: BA_CREC_DMA; k_lin_point_d:
-    BA_LP_DMA; k_point_step_rc TB 3: BA_PS_DMA) run the same lin_obs on the
-    same record values as the per-lane register gathers: the same trajectory
-    bitwise."""
+    BA_LP_DMA) run the same lin_obs on the same record values as the per-lane
+    register gathers: the same trajectory bitwise."""
     p = make_config("c4", scale=0.01)
     kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=6, precision=precision)
     monkeypatch.setenv(switch, on)
