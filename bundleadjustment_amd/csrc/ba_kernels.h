@@ -114,6 +114,9 @@ struct DevWork {
   const int2* pchunks;               // point-aligned observation chunks of <= 64 {start, end} (the PCG point pass)
   const int* cam_pos;                // [no] camera-order position (cam_op index) of each observation, -1: fixed camera
   bool tscat;                        // per-observation products stored in camera order (k_pcg_point_seg<.., SCAT>)
+  // ITERATIVE_SCHUR point-pass records in the 16-value rank-2 form
+  // (k_obs_w_rc<.., PC>, k_pcg_point_seg<.., PC>; step_w_storage decides)
+  bool pcgc = false;
   int npchunks;                      // 0: a point has more than 64 observations (value-pair point pass)
   bool pcg_folded;                   // exchange path: slices folded into slice 0 before the all-reduce
   const int* dup_off;                // [nvc+1] per variable camera: pairs of observations of one
@@ -142,7 +145,20 @@ void launch_linearize_jr(const DevProblem& P, const DevWork& W, hipStream_t s, h
 void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s);
 void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
                       hipStream_t s);
-void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);  // + W = E L^-T
+// the camera-side norms pass (k_cam_norms) as extra workgroups of another launch
+struct NormsFold {
+  const double* cams;
+  const double* Hcc;
+  const double* gc;
+  double* scale_c;
+  double* diag_c;
+  int compute_scale;
+  double min_diag, max_diag;
+};
+NormsFold norms_fold(const DevWork& W, bool compute_scale, double min_diag, double max_diag);
+// + W = E L^-T; nf: k_cam_norms rides in the point elimination's launch
+void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s,
+                       const NormsFold* nf = nullptr);
 // compact != nullptr: write the diagonal blocks + rhs to compact[nvc][27]
 // instead of the dense S (ITERATIVE_SCHUR); radius > 0 (dense, single
 // rank): add s Hcc s + D^2 and s g_c in the same pass (no launch_cam_add_diag)
@@ -178,6 +194,7 @@ void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipSt
 void launch_reduce_publish(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, double* host, int n,
                            unsigned* host_seq, unsigned seq, unsigned* ticket, hipStream_t s);
 int back_flow_capacity(int device);
+bool obs_w_pc_ok(const DevProblem& P, const DevWork& W);   // k_obs_w_rc has the PCG record form for this source
 bool point_step_fused();                      // J-free back substitution fused with the candidate (BA_PSTEP)
 bool chol_persist_fits(int device, int n);   // every workgroup of k_chol_persist resident at once
 int chol_split_blocks();                     // block columns from which the split step form is used   // resident k_back_flow workgroups (-1: query failed)

@@ -1116,14 +1116,17 @@ __global__ __launch_bounds__(NT) void k_cam_assemble(DevProblem P, const double*
 
 __device__ inline int tri(int a, int b) { return a * (a + 1) / 2 + b; }  // a >= b
 
-__global__ __launch_bounds__(256) void k_cam_norms(DevProblem P, const double* __restrict__ cams, const double* __restrict__ Hcc,
-                                                   const double* __restrict__ gc, double* __restrict__ scale_c,
-                                                   double* __restrict__ diag_c, int compute_scale, double min_diag,
-                                                   double max_diag, double* __restrict__ part) {
+// (bx, nbx: this workgroup's index and the workgroup count of the pass, so
+// that the pass can ride in another kernel's launch: k_point_elim_norms)
+__device__ __forceinline__ void cam_norms_body(const DevProblem& P, const double* __restrict__ cams,
+                                               const double* __restrict__ Hcc, const double* __restrict__ gc,
+                                               double* __restrict__ scale_c, double* __restrict__ diag_c,
+                                               int compute_scale, double min_diag, double max_diag,
+                                               double* __restrict__ part, int bx, int nbx) {
   __shared__ double lds[3 * 16];
   double acc[2] = {0.0, 0.0};
   double gmax = 0.0;
-  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < P.nvc; v += gridDim.x * blockDim.x) {
+  for (int v = bx * blockDim.x + threadIdx.x; v < P.nvc; v += nbx * blockDim.x) {
     const int c = P.cam_of_vc[v];
     for (int a = 0; a < 6; ++a) {
       const double h = Hcc[(size_t)v * 21 + tri(a, a)];
@@ -1146,10 +1149,16 @@ __global__ __launch_bounds__(256) void k_cam_norms(DevProblem P, const double* _
   block_sum<2>(acc, lds, out);
   const double m = block_max1(gmax, lds + 32);
   if (threadIdx.x == 0) {
-    part_of(part, SL_GN2_C)[blockIdx.x] = out[0];
-    part_of(part, SL_XN2_C)[blockIdx.x] = out[1];
-    part_of(part, SL_GMAX_C)[blockIdx.x] = m;
+    part_of(part, SL_GN2_C)[bx] = out[0];
+    part_of(part, SL_XN2_C)[bx] = out[1];
+    part_of(part, SL_GMAX_C)[bx] = m;
   }
+}
+__global__ __launch_bounds__(256) void k_cam_norms(DevProblem P, const double* __restrict__ cams, const double* __restrict__ Hcc,
+                                                   const double* __restrict__ gc, double* __restrict__ scale_c,
+                                                   double* __restrict__ diag_c, int compute_scale, double min_diag,
+                                                   double max_diag, double* __restrict__ part) {
+  cam_norms_body(P, cams, Hcc, gc, scale_c, diag_c, compute_scale, min_diag, max_diag, part, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -1161,16 +1170,16 @@ __global__ __launch_bounds__(256) void k_cam_norms(DevProblem P, const double* _
 // record per point with what k_obs_w_cam / k_cam_schur_diag_rc gather: X, the
 // variable flag, s_p, L_p^-1, u_p
 constexpr int kPRec = 16;
-__global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* __restrict__ Hpp,
-                                                    const double* __restrict__ gp, const double* __restrict__ scale_p,
-                                                    const double* __restrict__ diag_p, double radius,
-                                                    double* __restrict__ Linv, double* __restrict__ u,
-                                                    double* __restrict__ part, const double* __restrict__ pts,
-                                                    double* __restrict__ prec) {
+__device__ __forceinline__ void point_elim_body(const DevProblem& P, const double* __restrict__ Hpp,
+                                                const double* __restrict__ gp, const double* __restrict__ scale_p,
+                                                const double* __restrict__ diag_p, double radius,
+                                                double* __restrict__ Linv, double* __restrict__ u,
+                                                double* __restrict__ part, const double* __restrict__ pts,
+                                                double* __restrict__ prec, int bx, int nbx) {
   __shared__ double lds[16];
   double acc[1] = {0.0};
   const size_t np = (size_t)P.np;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P.np; p += gridDim.x * blockDim.x) {
+  for (int p = bx * blockDim.x + threadIdx.x; p < P.np; p += nbx * blockDim.x) {
     if (!P.pt_var[p]) {   // zeros: the camera-side gathers then need no point flag (W_o = 0 there too)
 #pragma unroll
       for (int k = 0; k < 6; ++k) Linv[k * np + p] = 0.0;
@@ -1238,7 +1247,34 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
   }
   double out[1];
   block_sum<1>(acc, lds, out);
-  if (threadIdx.x == 0) part_of(part, SL_ELIM_BAD)[blockIdx.x] = out[0];
+  if (threadIdx.x == 0) part_of(part, SL_ELIM_BAD)[bx] = out[0];
+}
+__global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* __restrict__ Hpp,
+                                                    const double* __restrict__ gp, const double* __restrict__ scale_p,
+                                                    const double* __restrict__ diag_p, double radius,
+                                                    double* __restrict__ Linv, double* __restrict__ u,
+                                                    double* __restrict__ part, const double* __restrict__ pts,
+                                                    double* __restrict__ prec) {
+  point_elim_body(P, Hpp, gp, scale_p, diag_p, radius, Linv, u, part, pts, prec, blockIdx.x, gridDim.x);
+}
+// k_point_elim with the camera-side norms of the linearisation it follows
+// (k_cam_norms) as the last nbn workgroups of the same launch: the two
+// passes share no data (point blocks vs camera blocks, distinct scalar
+// slots), and the norms' slots are folded only with the step's scalars
+// (single rank, deferred fold).  One ~6-us launch fewer per LM iteration;
+// each workgroup runs exactly the arithmetic of its separate launch.
+__global__ __launch_bounds__(256) void k_point_elim_norms(DevProblem P, const double* __restrict__ Hpp,
+                                                          const double* __restrict__ gp,
+                                                          const double* __restrict__ scale_p,
+                                                          const double* __restrict__ diag_p, double radius,
+                                                          double* __restrict__ Linv, double* __restrict__ u,
+                                                          double* __restrict__ part, const double* __restrict__ pts,
+                                                          double* __restrict__ prec, int nbp, NormsFold nf) {
+  if ((int)blockIdx.x < nbp)
+    point_elim_body(P, Hpp, gp, scale_p, diag_p, radius, Linv, u, part, pts, prec, blockIdx.x, nbp);
+  else
+    cam_norms_body(P, nf.cams, nf.Hcc, nf.gc, nf.scale_c, nf.diag_c, nf.compute_scale, nf.min_diag, nf.max_diag, part,
+                   blockIdx.x - nbp, gridDim.x - nbp);
 }
 
 // ---------------------------------------------------------------------------
@@ -2725,11 +2761,18 @@ __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const doub
 // k_schur_pairs_c) gather one line per observation and form their products
 // through the 2 x 2 inner matrices Z Z'^T (WcCam: the camera's K and
 // translation scalings).
+//
+// PC (ITERATIVE_SCHUR, intrinsics without skew: K01 = K10 = K20 = K21 = 0):
+// the same rank-2 form for the PCG point pass, self-contained — c's scaled
+// rotation columns, the four nonzero scaled translation entries c0[3],
+// c0[5], c1[4], c1[5] (c0[4] = (K01 - pr0 K21) f and c1[3] = (K10 - pr1 K20)
+// f are exact zeros there), then Z: 16 values, one 128-B line (fp64) instead
+// of 144 B, with no per-camera constants to gather (k_pcg_point_seg<.., PC>)
 constexpr int kObsWRcWaves = 6;   // table + K + scales + 6 staging slots fit the 160 KB LDS
 // TB (nc > kLinLdsCams, k_lin_point's camera sources): rec is the global
 // table gtbl (1) or the compact records crec (2); the camera scalings are
 // read from scale_c
-template <typename WT, bool COMPACT = false, int TB = 0>
+template <typename WT, bool COMPACT = false, int TB = 0, bool PC = false>
 // pxv: k_lin_point's 32-B point records {X, variable flag} (one aligned
 // 32-B read per observation instead of 24 B of X plus the flag byte)
 __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, const double* __restrict__ rec,
@@ -2767,7 +2810,8 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
   // source address, as k_schur_pairs_cd): a wave-instruction touches 8
   // records instead of 64.  The next chunk's records are requested after
   // this chunk's W records have left the slot, ahead of their stores
-  constexpr int NST = (COMPACT ? kWcRec : kWRec) / 2;   // store instructions per chunk
+  static_assert(!(COMPACT && PC), "one record form");
+  constexpr int NST = (COMPACT || PC ? kWcRec : kWRec) / 2;   // store instructions per chunk
   auto crec_issue = [&](int cc) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -2831,9 +2875,23 @@ __global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, co
     }
     const double jp0[3] = {j[12] * s0, j[13] * s1, j[14] * s2};
     const double jp1[3] = {j[15] * s0, j[16] * s1, j[17] * s2};
-    constexpr int REC = COMPACT ? kWcRec : kWRec;
+    constexpr int REC = COMPACT || PC ? kWcRec : kWRec;
     double wv[REC];
-    if constexpr (COMPACT) {
+    if constexpr (PC) {
+      const double z[6] = {jp0[0] * i00, jp0[0] * i10 + jp0[1] * i11, jp0[0] * i20 + jp0[1] * i21 + jp0[2] * i22,
+                           jp1[0] * i00, jp1[0] * i10 + jp1[1] * i11, jp1[0] * i20 + jp1[1] * i21 + jp1[2] * i22};
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        wv[a] = live ? j[a] * sc[a] : 0.0;
+        wv[3 + a] = live ? j[6 + a] * sc[a] : 0.0;
+      }
+      wv[6] = live ? j[3] * sc[3] : 0.0;
+      wv[7] = live ? j[5] * sc[5] : 0.0;
+      wv[8] = live ? j[10] * sc[4] : 0.0;
+      wv[9] = live ? j[11] * sc[5] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) wv[10 + k] = live ? z[k] : 0.0;
+    } else if constexpr (COMPACT) {
       const double z[6] = {jp0[0] * i00, jp0[0] * i10 + jp0[1] * i11, jp0[0] * i20 + jp0[1] * i21 + jp0[2] * i22,
                            jp1[0] * i00, jp1[0] * i10 + jp1[1] * i11, jp1[0] * i20 + jp1[1] * i21 + jp1[2] * i22};
 #pragma unroll
@@ -3508,6 +3566,14 @@ void launch_lin_prep(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (tb == 1)
     hipLaunchKernelGGL(k_lin_gtbl, dim3((P.nc * kGRec + 255) / 256), dim3(256), 0, s, P, (const double*)W.rec, W.gtbl);
 }
+// the W writers that have a 16-value PCG record form (k_obs_w_rc<.., PC>):
+// the LDS camera table (TB 0) and the DMA-gathered compact records (TB 3)
+static bool crec_dma();
+bool obs_w_pc_ok(const DevProblem& P, const DevWork& W) {
+  if (!W.jrfree) return false;
+  const int tb = jr_tab(P, W);
+  return tb == 0 || (tb == 2 && crec_dma());
+}
 void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   // t0 / t1 (optional): start / stop of the kernel's execution, stamped by
   // hipExtLaunchKernel itself (no separate event records around the launch)
@@ -3669,15 +3735,25 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
     hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
                        nullptr);
 }
+NormsFold norms_fold(const DevWork& W, bool compute_scale, double min_diag, double max_diag) {
+  return NormsFold{W.cams, W.Hcc, W.gc, W.scale_c, W.diag_c, compute_scale ? 1 : 0, min_diag, max_diag};
+}
 void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag, double max_diag,
                       hipStream_t s) {
   hipLaunchKernelGGL(k_cam_norms, dim3(grid_for(P.nvc)), dim3(kThreads), 0, s, P, W.cams, W.Hcc, W.gc, W.scale_c,
                      W.diag_c, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
 }
-void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
+void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s, const NormsFold* nf) {
   const bool cm = W.wcm && W.jrfree;
-  hipLaunchKernelGGL(k_point_elim, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.Hpp, W.gp, W.scale_p, W.diag_p,
-                     radius, W.Linv, W.u, W.part, (const double*)W.pts, cm || W.jdiag ? W.prec : nullptr);
+  double* prec = cm || W.jdiag ? W.prec : nullptr;
+  if (nf) {
+    const int nbp = grid_for(P.np);
+    hipLaunchKernelGGL(k_point_elim_norms, dim3(nbp + grid_for(P.nvc)), dim3(kThreads), 0, s, P, W.Hpp, W.gp,
+                       W.scale_p, W.diag_p, radius, W.Linv, W.u, W.part, (const double*)W.pts, prec, nbp, *nf);
+  } else {
+    hipLaunchKernelGGL(k_point_elim, dim3(grid_for(P.np)), dim3(kThreads), 0, s, P, W.Hpp, W.gp, W.scale_p, W.diag_p,
+                       radius, W.Linv, W.u, W.part, (const double*)W.pts, prec);
+  }
   if (P.no == 0) return;
   const int tb = jr_tab(P, W);
   if (cm && P.nvc > 0) {   // the camera-major copy (the point-major W below stays: the point passes read it)
@@ -3712,7 +3788,14 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
     const double* src = tb == 1 ? W.gtbl : W.crec;
     // compact records by LDS-DMA (TB 3) unless BA_CREC_DMA=0
     const bool dma = tb == 2 && crec_dma();
-    if (W.w32)
+    if (W.pcgc && dma) {   // (the host enables the PCG records only with the DMA gathers)
+      if (W.w32)
+        hipLaunchKernelGGL((k_obs_w_rc<float, false, 3, true>), dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src,
+                           (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
+      else
+        hipLaunchKernelGGL((k_obs_w_rc<double, false, 3, true>), dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src,
+                           (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
+    } else if (W.w32)
       hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<float, false, 1> : dma ? k_obs_w_rc<float, false, 3> : k_obs_w_rc<float, false, 2>),
                          dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv,
                          W.Wf);
@@ -3728,7 +3811,13 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
   }
   if (W.jrfree) {   // one 148-KB-LDS workgroup per CU
     const int g = lds_grid(P.no);
-    if (W.w32)
+    if (W.pcgc && W.w32)
+      hipLaunchKernelGGL((k_obs_w_rc<float, false, 0, true>), dim3(g), dim3(64 * kObsWRcWaves), 0, s, P,
+                         (const double*)W.rec, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
+    else if (W.pcgc)
+      hipLaunchKernelGGL((k_obs_w_rc<double, false, 0, true>), dim3(g), dim3(64 * kObsWRcWaves), 0, s, P,
+                         (const double*)W.rec, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
+    else if (W.w32)
       hipLaunchKernelGGL(k_obs_w_rc<float>, dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, (const double*)W.rec,
                          (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
     else if (W.wcompact)

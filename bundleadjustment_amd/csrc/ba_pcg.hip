@@ -420,22 +420,38 @@ __global__ __launch_bounds__(256) void k_pcg_cam_td(DevProblem P, const double* 
 // SCAT (with TOUT): t_o is stored at its camera-order position cam_pos[o]
 // instead (one 48-B scattered store per observation), so that the camera
 // pass streams the products (k_pcg_cam_s) instead of gathering them.
-template <typename WT, bool TOUT, bool SCAT = false>
+// PC: the 16-value rank-2 records of k_obs_w_rc<.., PC> (W_o = c^T Z: c's
+// scaled rotation columns, its four nonzero translation entries, Z):
+// W_o^T x = Z^T (c x), W_o v = c^T (Z v).  A record is 8 units (8 units of
+// 16 B fp64, of 8 B fp32): at that even stride the per-lane record reads
+// would conflict, so the units of record r sit XOR-swizzled in the slot
+// (unit k at k ^ ((r >> SH) & 7), SH = 1 fp64 / 2 fp32: the records of one
+// LDS row pass then cover distinct banks).
+template <typename WT, bool TOUT, bool SCAT = false, bool PC = false>
 __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2* __restrict__ chunks, int nchunks,
                                                        const WT* __restrict__ Wm, const double* __restrict__ xv,
                                                        double* __restrict__ vpt, double* __restrict__ tobs,
                                                        const int* __restrict__ cam_pos,
                                                        const double* __restrict__ st) {
+  static_assert(!PC || (TOUT && !SCAT), "rank-2 records: the point-order products");
   if (st[PS_DONE] != 0.0) return;
-  constexpr int REC = 18;
+  constexpr int REC = PC ? 16 : 18;
   // fp64: 16-B units (a record is 9, 16-B aligned; the per-lane 144-B record
   // reads from LDS are ds_read_b128 at 9 slots' stride: every 16-lane group
   // hits 16 distinct slots).  fp32 (72-B records, 8-B aligned): 8-B units
   using U = typename std::conditional<sizeof(WT) == 8, uint4, unsigned long long>::type;
-  constexpr int UN = REC * (int)sizeof(WT) / (int)sizeof(U);   // units per record: 9
-  __shared__ U stage[4][64 * UN];
-  __shared__ double tst[TOUT ? 4 : 1][TOUT ? 64 * 6 : 1];
+  constexpr int UN = REC * (int)sizeof(WT) / (int)sizeof(U);   // units per record: 9 (PC: 8)
+  constexpr int SH = sizeof(WT) == 8 ? 1 : 2;
+  // the slot position of unit e of the chunk (identity unless PC)
+  auto spos = [](int e) { return PC ? (e & ~7) | ((e & 7) ^ ((e >> (3 + SH)) & 7)) : e; };
+  __shared__ __attribute__((aligned(16))) U stage[4][64 * UN];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the products leave through the wave's own slot: its records are in
+  // registers by then (LDS operations of a wave complete in order), so the
+  // slot is free, and without a second array 4 (fp64 18-value: 4, was 3)
+  // workgroups fit a CU's LDS
+  static_assert(64 * UN * sizeof(U) >= 64 * 6 * sizeof(double), "products fit the slot");
+  double* tstw = reinterpret_cast<double*>(&stage[w][0]);
   // fp32: the next chunk's W units are loaded one chunk ahead, into
   // registers, so that their latency runs under this chunk's arithmetic and
   // scan (C5 shard 4.20 -> 4.09 ms per LM iteration).  fp64: the 36 VGPRs
@@ -466,7 +482,7 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
 #pragma unroll
       for (int k = 0; k < UN; ++k) {
         const int e = k * 64 + lane;
-        if (e < nu) stage[w][e] = nxt[k];
+        if (e < nu) stage[w][spos(e)] = nxt[k];
       }
       if (ch + cstride < nchunks) fetch(ch + cstride, nxt, ncr);
     } else {
@@ -474,7 +490,7 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
 #pragma unroll
       for (int k = 0; k < UN; ++k) {
         const int e = k * 64 + lane;
-        if (e < nu) stage[w][e] = src[e];
+        if (e < nu) stage[w][spos(e)] = src[e];
       }
     }
     const bool live = lane < n;
@@ -487,21 +503,30 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
     wave_lds_sync_pcg();
     double wr[REC];
     {
-      const U* ru = &stage[w][0] + (size_t)min(lane, n - 1) * UN;
+      const int rl = min(lane, n - 1);
+      const U* ru = &stage[w][0] + (size_t)rl * UN;
       U ur[UN];
 #pragma unroll
-      for (int k = 0; k < UN; ++k) ur[k] = ru[k];
+      for (int k = 0; k < UN; ++k) ur[k] = ru[PC ? k ^ ((rl >> SH) & 7) : k];
       const WT* r = reinterpret_cast<const WT*>(ur);
 #pragma unroll
       for (int k = 0; k < REC; ++k) wr[k] = (double)r[k];
     }
     double v[3];
+    if constexpr (PC) {
+      // y = c x (c0[4] = c1[3] = 0), v = Z^T y
+      const double y0 = wr[0] * x[0] + wr[1] * x[1] + wr[2] * x[2] + wr[6] * x[3] + wr[7] * x[5];
+      const double y1 = wr[3] * x[0] + wr[4] * x[1] + wr[5] * x[2] + wr[8] * x[4] + wr[9] * x[5];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      double a = 0.0;
+      for (int k = 0; k < 3; ++k) v[k] = live ? wr[10 + k] * y0 + wr[13 + k] * y1 : 0.0;
+    } else {
 #pragma unroll
-      for (int b = 0; b < 6; ++b) a += wr[b * 3 + k] * x[b];
-      v[k] = live ? a : 0.0;
+      for (int k = 0; k < 3; ++k) {
+        double a = 0.0;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) a += wr[b * 3 + k] * x[b];
+        v[k] = live ? a : 0.0;
+      }
     }
     // segmented inclusive scan: runs of equal pt (the chunk holds whole points)
     const int ptp = __shfl_up(pt, 1, 64);
@@ -543,15 +568,25 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
       for (int k = 0; k < 3; ++k) vp[k] = __shfl(v[k], last, 64);
       {   // (three 16-B LDS stores at 3 slots' stride: conflict-free)
         double tv[6];
+        if constexpr (PC) {   // q = Z v_p, t_o = c^T q
+          const double q0 = wr[10] * vp[0] + wr[11] * vp[1] + wr[12] * vp[2];
+          const double q1 = wr[13] * vp[0] + wr[14] * vp[1] + wr[15] * vp[2];
 #pragma unroll
-        for (int a = 0; a < 6; ++a) tv[a] = wr[a * 3] * vp[0] + wr[a * 3 + 1] * vp[1] + wr[a * 3 + 2] * vp[2];
-        double2* td = reinterpret_cast<double2*>(&tst[w][lane * 6]);
+          for (int a = 0; a < 3; ++a) tv[a] = wr[a] * q0 + wr[3 + a] * q1;
+          tv[3] = wr[6] * q0;
+          tv[4] = wr[8] * q1;
+          tv[5] = wr[7] * q0 + wr[9] * q1;
+        } else {
+#pragma unroll
+          for (int a = 0; a < 6; ++a) tv[a] = wr[a * 3] * vp[0] + wr[a * 3 + 1] * vp[1] + wr[a * 3 + 2] * vp[2];
+        }
+        double2* td = reinterpret_cast<double2*>(&tstw[lane * 6]);
 #pragma unroll
         for (int a = 0; a < 3; ++a) td[a] = make_double2(tv[2 * a], tv[2 * a + 1]);
       }
       wave_lds_sync_pcg();
       double2* dst = reinterpret_cast<double2*>(tobs + 6 * (size_t)o0);
-      const double2* tsrc = reinterpret_cast<const double2*>(&tst[w][0]);
+      const double2* tsrc = reinterpret_cast<const double2*>(&tstw[0]);
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const int e = k * 64 + lane;
@@ -880,7 +915,13 @@ void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec,
       return;
     }
     if (W.tobs) {
-      if (W.w32)
+      if (W.pcgc && W.w32)   // (the 16-value rank-2 records)
+        hipLaunchKernelGGL((k_pcg_point_seg<float, true, false, true>), dim3(g), dim3(256), 0, s, P, W.pchunks,
+                           W.npchunks, W.Wf, vec, W.vpt, W.tobs, nullptr, st);
+      else if (W.pcgc)
+        hipLaunchKernelGGL((k_pcg_point_seg<double, true, false, true>), dim3(g), dim3(256), 0, s, P, W.pchunks,
+                           W.npchunks, W.W, vec, W.vpt, W.tobs, nullptr, st);
+      else if (W.w32)
         hipLaunchKernelGGL((k_pcg_point_seg<float, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks, W.Wf,
                            vec, W.vpt, W.tobs, nullptr, st);
       else

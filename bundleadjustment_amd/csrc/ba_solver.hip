@@ -109,7 +109,25 @@ struct ba_ctx {
   // scalar slots whose fold a linearisation left to the step enqueued right
   // behind it (single rank: one k_reduce for both records)
   uint32_t pend_sum = 0, pend_max = 0;
+  // the camera-side norms pass of such a linearisation, left to ride in the
+  // step's point-elimination launch (launch_point_elim's NormsFold)
+  bool norms_pend = false;
+  bahip::NormsFold norms_args{};
+  // a pending norms pass as its own launch (before any fold of its slots)
+  void flush_norms() {
+    if (!norms_pend) return;
+    norms_pend = false;
+    bahip::launch_cam_norms(P, W, norms_args.compute_scale != 0, norms_args.min_diag, norms_args.max_diag, stream);
+  }
+  const bahip::NormsFold* take_norms() {
+    if (!norms_pend) return nullptr;
+    norms_pend = false;
+    return &norms_args;
+  }
+  void clear_pending() { pend_sum = pend_max = 0; norms_pend = false; }
   bool dup_diag = false;   // the dense pair list has diagonal blocks (duplicate observations)
+  bool k_plain = false;    // every camera's K without skew, row 2 = (0, 0, k22) (set_problem)
+  size_t pcg_ndup = 0;     // ITERATIVE_SCHUR duplicate (camera, point) pairs (ensure_pcg)
   double* tobs_buf = nullptr;   // [no][6] ITERATIVE_SCHUR per-observation products (allocated on first use)
   int max_no = 0;               // largest observation count over the ranks (collective matvec-path choice)
   int ncamobs = 0;              // observations of variable cameras (the cam_op list)
@@ -215,6 +233,7 @@ struct ba_ctx {
   }
   void publish_scalars() {
     const size_t cnt = kNumSlots + kPcgState;
+    flush_norms();
     if (!scal_spin()) {
       if (pend_sum | pend_max) bahip::launch_reduce(W, pend_sum, pend_max, stream);
       pend_sum = pend_max = 0;
@@ -373,6 +392,11 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   P.cam_fixed = ctx->upload(ctx->cam_fixed_h);
   P.pt_var = ctx->upload(pt_var);
   P.K = ctx->upload(std::vector<float>(pb->K, pb->K + 9 * (size_t)nc));
+  ctx->k_plain = true;   // no skew, row 2 = (0, 0, k22): the 16-value PCG records apply
+  for (int c = 0; c < nc; ++c) {
+    const float* k = pb->K + 9 * (size_t)c;   // column-major
+    if (k[1] != 0.0f || k[2] != 0.0f || k[3] != 0.0f || k[5] != 0.0f) ctx->k_plain = false;
+  }
   {
     std::vector<float> ex(16 * (size_t)nc, 0.0f);
     if (pb->cam_fixed_extr)
@@ -605,6 +629,7 @@ void ensure_pcg(ba_ctx* ctx) {
   }
   W.dup_off = ctx->upload(dup_off);
   W.dup_pairs = ctx->upload(dup);
+  ctx->pcg_ndup = dup.size();
   {
     // point-aligned chunks of <= 64 observations for the PCG point pass
     // (k_pcg_point_seg); BA_PCG_SEG=0 keeps the value-pair passes
@@ -674,7 +699,17 @@ void linearize_enqueue(ba_ctx* ctx, bool compute_scale, double min_diag, double 
     ctx->allreduce(W.Hcc, 27 * (size_t)ctx->nvc + SL_GMAX_P);
     ctx->allreduce(W.scal + SL_GMAX_P, 1, ncclMax);
   }
-  launch_cam_norms(P, W, compute_scale, min_diag, max_diag, s);
+  // deferred fold (single rank): the norms ride in the step's point
+  // elimination (BA_NORMS_FOLD=0: their own launch here)
+  const char* nfe = getenv("BA_NORMS_FOLD");   // (read per call: tests switch it)
+  const bool norms_fold_on = !(nfe && nfe[0] == '0');
+  if (defer_reduce && !ctx->coll() && norms_fold_on) {
+    ctx->norms_pend = true;
+    ctx->norms_args = norms_fold(W, compute_scale, min_diag, max_diag);
+  } else {
+    ctx->norms_pend = false;
+    launch_cam_norms(P, W, compute_scale, min_diag, max_diag, s);
+  }
   const uint32_t sum_mask = bit(SL_GN2_C) | bit(SL_XN2_C) | (ctx->coll() ? 0u : lin_sum);
   const uint32_t max_mask = bit(SL_GMAX_C) | (ctx->coll() ? 0u : bit(SL_GMAX_P));
   if (defer_reduce && !ctx->coll()) {
@@ -702,7 +737,7 @@ LinResult linearize(ba_ctx* ctx, bool compute_scale, double min_diag, double max
   // a fresh start (solve / bench entry): folds still pending belong to work
   // an earlier call abandoned (e.g. the speculative linearisation behind a
   // solve's last step) and must not be folded into this record
-  ctx->pend_sum = ctx->pend_max = 0;
+  ctx->clear_pending();
   linearize_enqueue(ctx, compute_scale, min_diag, max_diag);
   ctx->read_scalars();
   return lin_result(ctx);
@@ -721,7 +756,7 @@ void form_reduced_dense(ba_ctx* ctx, double radius) {
     if (W.s_memset) HIP_OK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)(ctx->n + 1) * ctx->ld, s));
     else launch_zero_blocks(P, W, s);
   }
-  launch_point_elim(P, W, radius, s);
+  launch_point_elim(P, W, radius, s, ctx->take_norms());
   // single rank, no diagonal pair blocks: the LM diagonal goes in with the
   // fold (same operation order as the exchange path's, bitwise)
   const bool fused_diag = !ctx->coll() && !ctx->dup_diag;
@@ -786,7 +821,7 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
   }
   PcgOpts po{o.eta, o.min_linear_solver_iterations, std::max(1, o.max_linear_solver_iterations),
              o.preconditioner_type == BA_SCHUR_JACOBI ? 1 : 0};
-  launch_point_elim(P, W, radius, s);
+  launch_point_elim(P, W, radius, s, ctx->take_norms());
   launch_cam_schur_diag(P, W, s, W.Sd);
   if (po.schur_jacobi) launch_pcg_dup(P, W, s);
   if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
@@ -857,6 +892,21 @@ void step_w_storage(ba_ctx* ctx, const ba_options& o) {
     const char* de = getenv("BA_JDIAG");
     W.jdiag = W.jrfree && !W.wcm && !W.wcompact && !(de && de[0] == '0');
     if ((W.wcm || W.jdiag) && !W.prec) W.prec = ctx->dalloc<double>(16 * (size_t)std::max(ctx->np, 1));
+    // the PCG point pass over the 16-value rank-2 records (k_obs_w_rc<.., PC>:
+    // 128 B per observation fp64, 64 B fp32): only where nothing else reads
+    // W — the diagonal blocks J-free, the fused point step, the products t_o
+    // in point order (no scatter), no duplicate (camera, point) pairs, every
+    // point in the point-aligned chunks — and K without skew.  BA_PCG_PC=0
+    // (read per solve) keeps the 18-value records
+    W.pcgc = false;
+    const char* pe = getenv("BA_PCG_PC");
+    const char* te = getenv("BA_PCG_T");
+    const char* se = getenv("BA_TSCAT");
+    if (!(pe && pe[0] == '0') && o.linear_solver == BA_ITERATIVE_SCHUR && W.jdiag && ctx->k_plain &&
+        point_step_fused() && obs_w_pc_ok(ctx->P, W) && !(te && te[0] == '0') && !(se && atoi(se) != 0)) {
+      ensure_pcg(ctx);
+      W.pcgc = W.npchunks > 0 && ctx->pcg_ndup == 0;
+    }
     if (W.wcm) {
       if (W.w32 && !W.Wcmf) W.Wcmf = ctx->dalloc<float>(18 * (size_t)std::max(ctx->ncamobs, 1));
       if (!W.w32 && !W.Wcm) W.Wcm = ctx->dalloc<double>(18 * (size_t)std::max(ctx->ncamobs, 1));
@@ -999,7 +1049,7 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
   // a step enqueued right behind the last accepted step's linearisation
   // (its record arrived with the linearisation's): used if the solve goes on
   bool have_step = false;
-  ctx->pend_sum = ctx->pend_max = 0;   // (an earlier solve may have thrown between the two enqueues)
+  ctx->clear_pending();   // (an earlier solve may have thrown between the two enqueues)
   int spec_ls = 0;
   while (can_continue()) {
     const double ti = now_s();
@@ -1076,6 +1126,7 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
       if (spec) {
         spec_ls = step_enqueue(ctx, radius, o);
       } else if (ctx->pend_sum | ctx->pend_max) {
+        ctx->flush_norms();
         launch_reduce(ctx->W, ctx->pend_sum, ctx->pend_max, ctx->stream);
         ctx->pend_sum = ctx->pend_max = 0;
       }
@@ -1563,7 +1614,7 @@ int ba_bench_iterations(ba_ctx* ctx, const ba_options* opt, int iters, double ra
     ba_options o;
     if (opt) o = *opt; else ba_default_options(&o);
     check_options(o);
-    ctx->pend_sum = ctx->pend_max = 0;
+    ctx->clear_pending();
     if (!ctx->scale_valid) linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
     double rj_total = 0.0;
     long ls_total = 0;

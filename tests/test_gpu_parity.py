@@ -306,9 +306,11 @@ def test_persistent_cholesky_is_bitwise_the_per_step_form(monkeypatch, cfg, scal
 # speculative linearisation (BA_SPEC_LIN: the linearisation at a step's
 # candidate is enqueued behind the step's scalar record; a rejected or invalid
 # step re-linearises at x) and the spin-published scalar record
-# (BA_SCAL_SPIN): pure orchestration, so every on/off combination must give
-# the bitwise-identical trajectory.  The tolerances are switched off so the
-# solve runs into the late iterations where steps get rejected.
+# (BA_SCAL_SPIN), and the camera-side norms pass riding in the step's point
+# elimination launch (BA_NORMS_FOLD): pure orchestration, so every on/off
+# combination must give the bitwise-identical trajectory.  The tolerances are
+# switched off so the solve runs into the late iterations where steps get
+# rejected.
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("solver_type", ["DENSE_SCHUR", "ITERATIVE_SCHUR"])
 def test_speculative_linearisation_and_spin_are_bitwise_neutral(monkeypatch, solver_type):
@@ -318,17 +320,21 @@ def test_speculative_linearisation_and_spin_are_bitwise_neutral(monkeypatch, sol
     runs = {}
     for spec in ("0", "1"):
         for spin in ("0", "1"):
-            monkeypatch.setenv("BA_SPEC_LIN", spec)
-            monkeypatch.setenv("BA_SCAL_SPIN", spin)
-            with Solver(0) as s:
-                runs[spec + spin] = run_gpu(s, p, opts)
-    ref = runs["11"]
+            for fold in ("0", "1"):
+                monkeypatch.setenv("BA_SPEC_LIN", spec)
+                monkeypatch.setenv("BA_SCAL_SPIN", spin)
+                monkeypatch.setenv("BA_NORMS_FOLD", fold)
+                with Solver(0) as s:
+                    runs[spec + spin + fold] = run_gpu(s, p, opts)
+    ref = runs["111"]
     assert any(not r["step_is_successful"] for r in ref[3]), "no rejected step: the test does not exercise the path"
     for k, r in runs.items():
         assert np.array_equal(ref[0], r[0]) and np.array_equal(ref[1], r[1]), k
         assert [x["cost"] for x in ref[3]] == [x["cost"] for x in r[3]], k
         assert [x["step_is_successful"] for x in ref[3]] == [x["step_is_successful"] for x in r[3]], k
         assert [x["step_is_valid"] for x in ref[3]] == [x["step_is_valid"] for x in r[3]], k
+        assert [x["gradient_max_norm"] for x in ref[3]] == [x["gradient_max_norm"] for x in r[3]], k
+        assert [x["gradient_norm"] for x in ref[3]] == [x["gradient_norm"] for x in r[3]], k
 
 
 # ---------------------------------------------------------------------------

@@ -147,13 +147,17 @@ def compare(glog, olog, n, rtol=1e-9):
 # default); "t_gather_reg" the same with register gathers (BA_CAMT_DMA=0);
 # "pairs" the value-pair point passes k_pcg_point / k_pcg_point_t instead of
 # the point-aligned chunks (BA_PCG_SEG=0, BA_PCG_T=1); "wcm" the camera-major
-# copy of W (k_obs_w_cam, BA_WCM=1: the camera passes stream it)
-MATVECS = ["auto", "gather", "t", "t_gather", "t_gather_reg", "pairs", "wcm"]
+# copy of W (k_obs_w_cam, BA_WCM=1: the camera passes stream it); "w18" the
+# point-aligned chunks over the 18-value W records instead of the 16-value
+# rank-2 ones the default picks (BA_PCG_PC=0)
+MATVECS = ["auto", "gather", "t", "t_gather", "t_gather_reg", "pairs", "wcm", "w18"]
 
 
 def set_matvec(monkeypatch, mode):
     if mode == "wcm":
         monkeypatch.setenv("BA_WCM", "1")
+    elif mode == "w18":
+        monkeypatch.setenv("BA_PCG_PC", "0")
     elif mode != "auto":
         monkeypatch.setenv("BA_WCM", "0")
         monkeypatch.setenv("BA_PCG_T", "0" if mode == "gather" else "1")
@@ -171,9 +175,11 @@ def test_gpu_camera_record_dma_is_bitwise_the_register_gather(solver, precision,
     """The point-major kernels beyond 200 cameras with the compact camera
     records gathered by LDS-DMA (k_obs_w_rc TB 3: BA_CREC_DMA; k_lin_point_d:
     BA_LP_DMA) run the same lin_obs on the same record values as the per-lane
-    register gathers: the same trajectory bitwise."""
+    register gathers: the same trajectory bitwise.  (The 18-value PCG
+    records in both runs: the register-gather W kernel has no 16-value form.)"""
     p = make_config("c4", scale=0.01)
     kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=6, precision=precision)
+    monkeypatch.setenv("BA_PCG_PC", "0")
     monkeypatch.setenv(switch, on)
     ca, xa, sa, la = gpu_solve(solver, p, **kw)
     monkeypatch.setenv(switch, off)
@@ -198,6 +204,31 @@ def test_gpu_camera_pass_dma_gather_is_bitwise_the_register_gather(solver, preci
     assert [it["cost"] for it in la] == [it["cost"] for it in lb]
     assert sa.final_cost == sb.final_cost
     assert np.array_equal(ca, cb) and np.array_equal(xa, xb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
+@pytest.mark.parametrize("cfg,scale", [("c3", 0.01), ("c4", 0.01)])
+def test_gpu_rank2_pcg_records_track_the_full_records(solver, cfg, scale, precision, monkeypatch):
+    """The PCG point pass over the 16-value rank-2 records (k_obs_w_rc<.., PC>:
+    W_o = c^T Z with c's four nonzero translation entries; the default where
+    it applies) against the 18-value records (BA_PCG_PC=0): the same products
+    up to rounding (they associate differently), so fp64 costs to 1e-10 and
+    the same CG counts — at <= 200 cameras (LDS camera table) and beyond (the
+    DMA-gathered camera records).  fp32 W rounds c and Z instead of their
+    product: costs to 1e-6 there."""
+    p = make_config(cfg, scale=scale)
+    kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=6, precision=precision)
+    ca, xa, sa, la = gpu_solve(solver, p, **kw)
+    monkeypatch.setenv("BA_PCG_PC", "0")
+    cb, xb, sb, lb = gpu_solve(solver, p, **kw)
+    rel = 1e-10 if precision == "FP64" else 1e-6
+    assert len(la) == len(lb)
+    for a, b in zip(la, lb):
+        assert a["cost"] == pytest.approx(b["cost"], rel=rel)
+    if precision == "FP64":
+        assert [r["linear_solver_iterations"] for r in la] == [r["linear_solver_iterations"] for r in lb]
+    assert sa.final_cost == pytest.approx(sb.final_cost, rel=rel)
 
 
 @pytest.mark.gpu
