@@ -1258,7 +1258,8 @@ __global__ __launch_bounds__(256) void k_point_elim(DevProblem P, const double* 
   point_elim_body(P, Hpp, gp, scale_p, diag_p, radius, Linv, u, part, pts, prec, blockIdx.x, gridDim.x);
 }
 // k_point_elim with the camera-side norms of the linearisation it follows
-// (k_cam_norms) as the last nbn workgroups of the same launch: the two
+// (k_cam_norms) as the first workgroups of the same launch (dispatched
+// first: the norms' serial camera loop runs beside the points): the two
 // passes share no data (point blocks vs camera blocks, distinct scalar
 // slots), and the norms' slots are folded only with the step's scalars
 // (single rank, deferred fold).  One ~6-us launch fewer per LM iteration;
@@ -1270,11 +1271,12 @@ __global__ __launch_bounds__(256) void k_point_elim_norms(DevProblem P, const do
                                                           double* __restrict__ Linv, double* __restrict__ u,
                                                           double* __restrict__ part, const double* __restrict__ pts,
                                                           double* __restrict__ prec, int nbp, NormsFold nf) {
-  if ((int)blockIdx.x < nbp)
-    point_elim_body(P, Hpp, gp, scale_p, diag_p, radius, Linv, u, part, pts, prec, blockIdx.x, nbp);
-  else
+  const int nbn = (int)gridDim.x - nbp;
+  if ((int)blockIdx.x < nbn)
     cam_norms_body(P, nf.cams, nf.Hcc, nf.gc, nf.scale_c, nf.diag_c, nf.compute_scale, nf.min_diag, nf.max_diag, part,
-                   blockIdx.x - nbp, gridDim.x - nbp);
+                   blockIdx.x, nbn);
+  else
+    point_elim_body(P, Hpp, gp, scale_p, diag_p, radius, Linv, u, part, pts, prec, blockIdx.x - nbn, nbp);
 }
 
 // ---------------------------------------------------------------------------

@@ -823,7 +823,7 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
              o.preconditioner_type == BA_SCHUR_JACOBI ? 1 : 0};
   launch_point_elim(P, W, radius, s, ctx->take_norms());
   launch_cam_schur_diag(P, W, s, W.Sd);
-  if (po.schur_jacobi) launch_pcg_dup(P, W, s);
+  if (po.schur_jacobi && ctx->pcg_ndup > 0) launch_pcg_dup(P, W, s);   // (this rank's duplicate pairs)
   if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
   // exchange path: one 6 nvc vector per matvec crosses the ranks (the
   // camera slices are folded first, in the order the single-rank update
