@@ -2774,16 +2774,22 @@ constexpr int kObsWRcWaves = 6;   // table + K + scales + 6 staging slots fit th
 // TB (nc > kLinLdsCams, k_lin_point's camera sources): rec is the global
 // table gtbl (1) or the compact records crec (2); the camera scalings are
 // read from scale_c
-template <typename WT, bool COMPACT = false, int TB = 0, bool PC = false>
+// WAVES: waves per workgroup.  The LDS-table form (TB 0) holds one 148-KB
+// workgroup per CU: 6.  The global-source forms need ~230 VGPRs (two waves per
+// SIMD): a 6-wave workgroup then leaves a CU at one workgroup, 6 waves, where
+// two 4-wave workgroups fill its 8 slots (kObsWRcWavesG; C5 shard +0.9 %,
+// C4 unchanged: profiles/r04_v18_obsw_waves_ab.txt)
+constexpr int kObsWRcWavesG = 4;
+template <typename WT, bool COMPACT = false, int TB = 0, bool PC = false, int WAVES = kObsWRcWaves>
 // pxv: k_lin_point's 32-B point records {X, variable flag} (one aligned
 // 32-B read per observation instead of 24 B of X plus the flag byte)
-__global__ __launch_bounds__(64 * kObsWRcWaves) void k_obs_w_rc(DevProblem P, const double* __restrict__ rec,
+__global__ __launch_bounds__(64 * WAVES) void k_obs_w_rc(DevProblem P, const double* __restrict__ rec,
                                                                 const double* __restrict__ pxv,
                                                                 const double* __restrict__ scale_c,
                                                                 const double* __restrict__ scale_p,
                                                                 const double* __restrict__ Linv, WT* __restrict__ W) {
   using V2 = typename std::conditional<sizeof(WT) == 8, double2, float2>::type;
-  constexpr int WAVES = kObsWRcWaves, NT = 64 * WAVES;
+  constexpr int NT = 64 * WAVES;
   __shared__ double stage[WAVES * 64 * kStageLd];
   __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
   __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
@@ -3786,29 +3792,46 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
     }
   }
   if (tb) {   // global camera source: 64.5 KB of staging LDS, two workgroups per CU
-    const int g = std::min(2 * lds_grid(1 << 30), std::max(1, (P.no + 64 * kObsWRcWaves - 1) / (64 * kObsWRcWaves)));
+    // (BA_OBSW_WAVES=6, diagnostics, read per launch: the 6-wave form of
+    // the default DMA-gathered kernels)
+    const char* we = getenv("BA_OBSW_WAVES");
+    const bool w6 = we && atoi(we) == 6 && tb == 2 && crec_dma();
+    constexpr int WG = kObsWRcWavesG;
+    const int wv = w6 ? kObsWRcWaves : WG;
+    const int g = std::min(2 * lds_grid(1 << 30), std::max(1, (P.no + 64 * wv - 1) / (64 * wv)));
     const double* src = tb == 1 ? W.gtbl : W.crec;
     // compact records by LDS-DMA (TB 3) unless BA_CREC_DMA=0
     const bool dma = tb == 2 && crec_dma();
+    const dim3 b(64 * wv);
     if (W.pcgc && dma) {   // (the host enables the PCG records only with the DMA gathers)
       if (W.w32)
-        hipLaunchKernelGGL((k_obs_w_rc<float, false, 3, true>), dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src,
-                           (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
+        hipLaunchKernelGGL((w6 ? k_obs_w_rc<float, false, 3, true, kObsWRcWaves> : k_obs_w_rc<float, false, 3, true, WG>),
+                           dim3(g), b, 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
       else
-        hipLaunchKernelGGL((k_obs_w_rc<double, false, 3, true>), dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src,
+        hipLaunchKernelGGL((w6 ? k_obs_w_rc<double, false, 3, true, kObsWRcWaves> : k_obs_w_rc<double, false, 3, true, WG>),
+                           dim3(g), b, 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
+    } else if (w6) {
+      if (W.w32)
+        hipLaunchKernelGGL((k_obs_w_rc<float, false, 3, false, kObsWRcWaves>), dim3(g), b, 0, s, P, src,
+                           (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
+      else if (W.wcompact)
+        hipLaunchKernelGGL((k_obs_w_rc<double, true, 3, false, kObsWRcWaves>), dim3(g), b, 0, s, P, src,
+                           (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
+      else
+        hipLaunchKernelGGL((k_obs_w_rc<double, false, 3, false, kObsWRcWaves>), dim3(g), b, 0, s, P, src,
                            (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
     } else if (W.w32)
-      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<float, false, 1> : dma ? k_obs_w_rc<float, false, 3> : k_obs_w_rc<float, false, 2>),
-                         dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv,
-                         W.Wf);
+      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<float, false, 1, false, WG>
+                                  : dma ? k_obs_w_rc<float, false, 3, false, WG> : k_obs_w_rc<float, false, 2, false, WG>),
+                         dim3(g), b, 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
     else if (W.wcompact)   // (DENSE_SCHUR up to kWcCams variable cameras: the compact records)
-      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, true, 1> : dma ? k_obs_w_rc<double, true, 3> : k_obs_w_rc<double, true, 2>),
-                         dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv,
-                         W.W);
+      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, true, 1, false, WG>
+                                  : dma ? k_obs_w_rc<double, true, 3, false, WG> : k_obs_w_rc<double, true, 2, false, WG>),
+                         dim3(g), b, 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
     else
-      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, false, 1> : dma ? k_obs_w_rc<double, false, 3> : k_obs_w_rc<double, false, 2>),
-                         dim3(g), dim3(64 * kObsWRcWaves), 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv,
-                         W.W);
+      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, false, 1, false, WG>
+                                  : dma ? k_obs_w_rc<double, false, 3, false, WG> : k_obs_w_rc<double, false, 2, false, WG>),
+                         dim3(g), b, 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
     return;
   }
   if (W.jrfree) {   // one 148-KB-LDS workgroup per CU
