@@ -2872,9 +2872,12 @@ __global__ __launch_bounds__(64 * WAVES) void k_obs_w_rc(DevProblem P, const dou
         const CamRc cam = cam_rc(rec, c);
         (void)lin_obs(P, cam, v >= 0, pv, X0, X1, X2, uv, j, fin, prf);
       }
-      const double* sv = scale_c + (size_t)max(v, 0) * 6;   // (v < 0: the record is zero, !live)
+      // (v < 0: the record is zero, !live).  Three 16-B gathers, not six
+      // 8-B ones: each touches a random camera's line per lane, so the
+      // instruction count is what the address path pays for
+      const double2* sv = reinterpret_cast<const double2*>(scale_c + (size_t)max(v, 0) * 6);
 #pragma unroll
-      for (int a = 0; a < 6; ++a) sc[a] = sv[a];
+      for (int a = 0; a < 3; ++a) { const double2 x = sv[a]; sc[2 * a] = x.x; sc[2 * a + 1] = x.y; }
     } else {
       const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
       (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin, prf);
@@ -3348,14 +3351,21 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
   __shared__ double lds[5 * 16];
   __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
   __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
-  __shared__ double ctb_s[TB ? 1 : kLinLdsCams * kCandRec];
+  __shared__ __attribute__((aligned(16))) double ctb_s[TB ? 2 : kLinLdsCams * kCandRec];
   if constexpr (!TB) {
     fill_lin_table<NT>(P, rec, tbl, ktb);
     const int n = P.nc * kCandRec;
     for (int e = threadIdx.x; e < n; e += NT) ctb_s[e] = cand_entry(P, rec_c, delta_c, e);
     __syncthreads();
   }
+  // the candidate rows (176 B, 16-B aligned) are read as 16-B pieces: beyond
+  // 200 cameras each per-lane read touches a random camera's line, so the
+  // number of read instructions is what the address path pays for
   const double* ctb = TB ? rec_c : ctb_s;
+  auto row16 = [&](int c, int k0, double* dst, int n2) {   // entries k0 .. k0 + 2 n2 - 1 of row c
+    const double2* s2 = reinterpret_cast<const double2*>(ctb + (size_t)c * kCandRec + k0);
+    for (int k = 0; k < n2; ++k) { const double2 x = s2[k]; dst[2 * k] = x.x; dst[2 * k + 1] = x.y; }
+  };
   double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // step2, step_bad, mneg, ccost, cand_bad
   const size_t np = (size_t)P.np;
   const int sl = threadIdx.x & (LANES - 1);
@@ -3407,7 +3417,8 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
           const float2 uvn = P.uv[on];
           double j[kJR];
           lin(c, true, X0, X1, X2, uv, j);
-          const double* dc = ctb + (size_t)c * kCandRec + 16;   // the camera step (0 for a fixed camera)
+          double dc[6];   // the camera step (0 for a fixed camera)
+          row16(c, 16, dc, 3);
           double t0 = 0.0, t1 = 0.0;
 #pragma unroll
           for (int a = 0; a < 6; ++a) { t0 += j[a] * dc[a]; t1 += j[6 + a] * dc[a]; }
@@ -3471,7 +3482,6 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
           const int cn = P.obs_cam[on];
           const float2 uvn = P.uv[on];
           const bool cfix = P.cam_fixed && P.cam_fixed[c];
-          const double* cr = ctb + (size_t)c * kCandRec;
           // k_candidate_lds' arithmetic
           double jd0, jd1, jp[6], r0, r1;
           if (keep) {
@@ -3483,8 +3493,10 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
             double j[kJR];
             lin(c, pv, X0, X1, X2, uv, j);
             jd0 = 0.0; jd1 = 0.0;
+            double dc[6];
+            row16(c, 16, dc, 3);
 #pragma unroll
-            for (int a2 = 0; a2 < 6; ++a2) { jd0 += j[a2] * cr[16 + a2]; jd1 += j[6 + a2] * cr[16 + a2]; }
+            for (int a2 = 0; a2 < 6; ++a2) { jd0 += j[a2] * dc[a2]; jd1 += j[6 + a2] * dc[a2]; }
 #pragma unroll
             for (int k = 0; k < 6; ++k) jp[k] = j[12 + k];
             r0 = j[18]; r1 = j[19];
@@ -3494,15 +3506,35 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
           const double mneg = jd0 * (r0 + jd0 / 2.0) + jd1 * (r1 + jd1 / 2.0);
           double pcand[3];
           if (!cfix) {
+            double cr[12];
+            row16(c, 0, cr, 6);
 #pragma unroll
             for (int i = 0; i < 3; ++i) pcand[i] = cr[i] * Xc[0] + cr[3 + i] * Xc[1] + cr[6 + i] * Xc[2] + cr[9 + i];
           } else {
+            double cr[16];
+            row16(c, 0, cr, 8);
             double ph[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) ph[i] = Xc[0] * cr[i] + Xc[1] * cr[4 + i] + Xc[2] * cr[8 + i] + cr[12 + i];
             pcand[0] = ph[0] / ph[3]; pcand[1] = ph[1] / ph[3]; pcand[2] = ph[2] / ph[3];
           }
-          const float* Kc = TB == 1 ? CamG{rec + (size_t)c * kGRec}.Kf() : (TB == 2 ? P.K + 9 * c : ktb + c * 9);
+          // TB 2: K from the compact record (the same floats as P.K, packed
+          // two per double at kCRecK: three 16-B reads instead of nine 4-B)
+          float kq[12];
+          if constexpr (TB == 2) {
+            const double2* s2 = reinterpret_cast<const double2*>(rec + (size_t)c * kCRec + kCRecK);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              const double2 x = s2[k];
+              const unsigned long long a = __builtin_bit_cast(unsigned long long, x.x);
+              const unsigned long long b = __builtin_bit_cast(unsigned long long, x.y);
+              kq[4 * k] = __builtin_bit_cast(float, (unsigned)a);
+              kq[4 * k + 1] = __builtin_bit_cast(float, (unsigned)(a >> 32));
+              kq[4 * k + 2] = __builtin_bit_cast(float, (unsigned)b);
+              kq[4 * k + 3] = __builtin_bit_cast(float, (unsigned)(b >> 32));
+            }
+          }
+          const float* Kc = TB == 1 ? CamG{rec + (size_t)c * kGRec}.Kf() : (TB == 2 ? kq : ktb + c * 9);
           double q[3];
 #pragma unroll
           for (int i = 0; i < 3; ++i)
