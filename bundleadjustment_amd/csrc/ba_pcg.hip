@@ -433,7 +433,7 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
                                                        double* __restrict__ vpt, double* __restrict__ tobs,
                                                        const int* __restrict__ cam_pos,
                                                        const double* __restrict__ st) {
-  static_assert(!PC || (TOUT && !SCAT), "rank-2 records: the point-order products");
+  static_assert(!PC || TOUT, "rank-2 records: the products");
   if (st[PS_DONE] != 0.0) return;
   constexpr int REC = PC ? 16 : 18;
   // fp64: 16-B units (a record is 9, 16-B aligned; the per-lane 144-B record
@@ -557,10 +557,18 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
       const int q = live ? cam_pos[o] : -1;   // (-1: a fixed camera, no camera-side entry)
       if (q >= 0) {
         double2* d = reinterpret_cast<double2*>(tobs + 6 * (size_t)q);
+        if constexpr (PC) {   // q = Z v_p, t_o = c^T q (as the point-order form)
+          const double q0 = wr[10] * vp[0] + wr[11] * vp[1] + wr[12] * vp[2];
+          const double q1 = wr[13] * vp[0] + wr[14] * vp[1] + wr[15] * vp[2];
+          d[0] = make_double2(wr[0] * q0 + wr[3] * q1, wr[1] * q0 + wr[4] * q1);
+          d[1] = make_double2(wr[2] * q0 + wr[5] * q1, wr[6] * q0);
+          d[2] = make_double2(wr[8] * q1, wr[7] * q0 + wr[9] * q1);
+        } else {
 #pragma unroll
-        for (int a = 0; a < 6; a += 2)
-          d[a / 2] = make_double2(wr[a * 3] * vp[0] + wr[a * 3 + 1] * vp[1] + wr[a * 3 + 2] * vp[2],
-                                  wr[a * 3 + 3] * vp[0] + wr[a * 3 + 4] * vp[1] + wr[a * 3 + 5] * vp[2]);
+          for (int a = 0; a < 6; a += 2)
+            d[a / 2] = make_double2(wr[a * 3] * vp[0] + wr[a * 3 + 1] * vp[1] + wr[a * 3 + 2] * vp[2],
+                                    wr[a * 3 + 3] * vp[0] + wr[a * 3 + 4] * vp[1] + wr[a * 3 + 5] * vp[2]);
+        }
       }
     } else if constexpr (TOUT) {
       double vp[3];
@@ -905,7 +913,13 @@ void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec,
   if (W.npchunks > 0) {   // point-aligned chunks of <= 64 observations (k_pcg_point_seg)
     const int g = std::max(1, std::min((W.npchunks + 3) / 4, 16384));
     if (W.tobs && W.tscat) {   // products scattered to camera order, streamed by the camera pass
-      if (W.w32)
+      if (W.pcgc && W.w32)
+        hipLaunchKernelGGL((k_pcg_point_seg<float, true, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks,
+                           W.npchunks, W.Wf, vec, W.vpt, W.tobs, W.cam_pos, st);
+      else if (W.pcgc)
+        hipLaunchKernelGGL((k_pcg_point_seg<double, true, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks,
+                           W.npchunks, W.W, vec, W.vpt, W.tobs, W.cam_pos, st);
+      else if (W.w32)
         hipLaunchKernelGGL((k_pcg_point_seg<float, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks,
                            W.Wf, vec, W.vpt, W.tobs, W.cam_pos, st);
       else

@@ -895,15 +895,15 @@ void step_w_storage(ba_ctx* ctx, const ba_options& o) {
     // the PCG point pass over the 16-value rank-2 records (k_obs_w_rc<.., PC>:
     // 128 B per observation fp64, 64 B fp32): only where nothing else reads
     // W — the diagonal blocks J-free, the fused point step, the products t_o
-    // in point order (no scatter), no duplicate (camera, point) pairs, every
-    // point in the point-aligned chunks — and K without skew.  BA_PCG_PC=0
+    // (point order, or scattered to camera order with BA_TSCAT=1), no
+    // duplicate (camera, point) pairs, every point in the point-aligned
+    // chunks — and K without skew.  BA_PCG_PC=0
     // (read per solve) keeps the 18-value records
     W.pcgc = false;
     const char* pe = getenv("BA_PCG_PC");
     const char* te = getenv("BA_PCG_T");
-    const char* se = getenv("BA_TSCAT");
     if (!(pe && pe[0] == '0') && o.linear_solver == BA_ITERATIVE_SCHUR && W.jdiag && ctx->k_plain &&
-        point_step_fused() && obs_w_pc_ok(ctx->P, W) && !(te && te[0] == '0') && !(se && atoi(se) != 0)) {
+        point_step_fused() && obs_w_pc_ok(ctx->P, W) && !(te && te[0] == '0')) {
       ensure_pcg(ctx);
       W.pcgc = W.npchunks > 0 && ctx->pcg_ndup == 0;
     }
