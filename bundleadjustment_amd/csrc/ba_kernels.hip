@@ -1177,73 +1177,89 @@ __device__ __forceinline__ void point_elim_body(const DevProblem& P, const doubl
                                                 double* __restrict__ part, const double* __restrict__ pts,
                                                 double* __restrict__ prec, int bx, int nbx) {
   __shared__ double lds[16];
+  // prec: the wave's 64 records leave through LDS as contiguous 1 KiB wave
+  // stores (a 128-B record per lane is store-issue bound); row stride 17
+  __shared__ double pst[(kThreads / 64) * 64 * (kPRec + 1)];
   double acc[1] = {0.0};
   const size_t np = (size_t)P.np;
-  for (int p = bx * blockDim.x + threadIdx.x; p < P.np; p += nbx * blockDim.x) {
-    if (!P.pt_var[p]) {   // zeros: the camera-side gathers then need no point flag (W_o = 0 there too)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* ps = pst + w * 64 * (kPRec + 1);
+  for (int pb = bx * blockDim.x; pb < P.np; pb += nbx * blockDim.x) {   // (uniform in the workgroup)
+    const int p = pb + threadIdx.x;
+    double rv[kPRec];
+    if (p < P.np && !P.pt_var[p]) {   // zeros: the camera-side gathers then need no point flag (W_o = 0 there too)
 #pragma unroll
       for (int k = 0; k < 6; ++k) Linv[k * np + p] = 0.0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) u[4 * (size_t)p + k] = 0.0;
       if (prec) {
-        double2* r = reinterpret_cast<double2*>(prec + (size_t)p * kPRec);
-        r[0] = make_double2(pts[3 * (size_t)p], pts[3 * (size_t)p + 1]);
-        r[1] = make_double2(pts[3 * (size_t)p + 2], 0.0);
+        rv[0] = pts[3 * (size_t)p]; rv[1] = pts[3 * (size_t)p + 1]; rv[2] = pts[3 * (size_t)p + 2];
 #pragma unroll
-        for (int k = 2; k < kPRec / 2; ++k) r[k] = make_double2(0.0, 0.0);
+        for (int k = 3; k < kPRec; ++k) rv[k] = 0.0;
       }
-      continue;
-    }
-    double s[3], D2[3], gs[3];
+    } else if (p < P.np) {
+      double s[3], D2[3], gs[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      s[k] = scale_p[k * np + p];
-      const double D = sqrt(diag_p[k * np + p] / radius);
-      D2[k] = D * D;
-      gs[k] = gp[k * np + p] * s[k];
+      for (int k = 0; k < 3; ++k) {
+        s[k] = scale_p[k * np + p];
+        const double D = sqrt(diag_p[k * np + p] / radius);
+        D2[k] = D * D;
+        gs[k] = gp[k * np + p] * s[k];
+      }
+      const double h00 = Hpp[0 * np + p] * s[0] * s[0] + D2[0];
+      const double h10 = Hpp[1 * np + p] * s[0] * s[1];
+      const double h20 = Hpp[2 * np + p] * s[0] * s[2];
+      const double h11 = Hpp[3 * np + p] * s[1] * s[1] + D2[1];
+      const double h21 = Hpp[4 * np + p] * s[1] * s[2];
+      const double h22 = Hpp[5 * np + p] * s[2] * s[2] + D2[2];
+      bool ok = h00 > 0.0;
+      const double l00 = sqrt(h00);
+      const double l10 = h10 / l00, l20 = h20 / l00;
+      const double d11 = h11 - l10 * l10;
+      ok = ok && d11 > 0.0;
+      const double l11 = sqrt(d11);
+      const double l21 = (h21 - l20 * l10) / l11;
+      const double d22 = h22 - l20 * l20 - l21 * l21;
+      ok = ok && d22 > 0.0;
+      const double l22 = sqrt(d22);
+      const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+      const double i10 = -(l10 * i00) * i11;
+      const double i21 = -(l21 * i11) * i22;
+      const double i20 = -(l20 * i00 + l21 * i10) * i22;
+      Linv[0 * np + p] = i00; Linv[1 * np + p] = i10; Linv[2 * np + p] = i11;
+      Linv[3 * np + p] = i20; Linv[4 * np + p] = i21; Linv[5 * np + p] = i22;
+      // u AoS [np][4] (one 32-B sector per point for the camera-side gathers)
+      const double u0 = i00 * gs[0];
+      const double u1 = i10 * gs[0] + i11 * gs[1];
+      const double u2 = i20 * gs[0] + i21 * gs[1] + i22 * gs[2];
+      u[4 * (size_t)p + 0] = u0;
+      u[4 * (size_t)p + 1] = u1;
+      u[4 * (size_t)p + 2] = u2;
+      u[4 * (size_t)p + 3] = 0.0;
+      if (prec) {
+        rv[0] = pts[3 * (size_t)p]; rv[1] = pts[3 * (size_t)p + 1]; rv[2] = pts[3 * (size_t)p + 2]; rv[3] = 1.0;
+        rv[4] = s[0]; rv[5] = s[1]; rv[6] = s[2]; rv[7] = i00;
+        rv[8] = i10; rv[9] = i11; rv[10] = i20; rv[11] = i21;
+        rv[12] = i22; rv[13] = u0; rv[14] = u1; rv[15] = u2;
+      }
+      acc[0] += ok ? 0.0 : 1.0;
     }
-    const double h00 = Hpp[0 * np + p] * s[0] * s[0] + D2[0];
-    const double h10 = Hpp[1 * np + p] * s[0] * s[1];
-    const double h20 = Hpp[2 * np + p] * s[0] * s[2];
-    const double h11 = Hpp[3 * np + p] * s[1] * s[1] + D2[1];
-    const double h21 = Hpp[4 * np + p] * s[1] * s[2];
-    const double h22 = Hpp[5 * np + p] * s[2] * s[2] + D2[2];
-    bool ok = h00 > 0.0;
-    const double l00 = sqrt(h00);
-    const double l10 = h10 / l00, l20 = h20 / l00;
-    const double d11 = h11 - l10 * l10;
-    ok = ok && d11 > 0.0;
-    const double l11 = sqrt(d11);
-    const double l21 = (h21 - l20 * l10) / l11;
-    const double d22 = h22 - l20 * l20 - l21 * l21;
-    ok = ok && d22 > 0.0;
-    const double l22 = sqrt(d22);
-    const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
-    const double i10 = -(l10 * i00) * i11;
-    const double i21 = -(l21 * i11) * i22;
-    const double i20 = -(l20 * i00 + l21 * i10) * i22;
-    Linv[0 * np + p] = i00; Linv[1 * np + p] = i10; Linv[2 * np + p] = i11;
-    Linv[3 * np + p] = i20; Linv[4 * np + p] = i21; Linv[5 * np + p] = i22;
-    // u AoS [np][4] (one 32-B sector per point for the camera-side gathers)
-    const double u0 = i00 * gs[0];
-    const double u1 = i10 * gs[0] + i11 * gs[1];
-    const double u2 = i20 * gs[0] + i21 * gs[1] + i22 * gs[2];
-    u[4 * (size_t)p + 0] = u0;
-    u[4 * (size_t)p + 1] = u1;
-    u[4 * (size_t)p + 2] = u2;
-    u[4 * (size_t)p + 3] = 0.0;
-    if (prec) {
-      double2* r = reinterpret_cast<double2*>(prec + (size_t)p * kPRec);
-      r[0] = make_double2(pts[3 * (size_t)p], pts[3 * (size_t)p + 1]);
-      r[1] = make_double2(pts[3 * (size_t)p + 2], 1.0);
-      r[2] = make_double2(s[0], s[1]);
-      r[3] = make_double2(s[2], i00);
-      r[4] = make_double2(i10, i11);
-      r[5] = make_double2(i20, i21);
-      r[6] = make_double2(i22, u0);
-      r[7] = make_double2(u1, u2);
+    if (prec) {   // (uniform)
+      if (p < P.np) {
+#pragma unroll
+        for (int k = 0; k < kPRec; ++k) ps[lane * (kPRec + 1) + k] = rv[k];
+      }
+      wave_lds_sync();
+      const int p0 = pb + w * 64;   // the wave's first point
+      const int nrec = min(64, P.np - p0);
+      double2* dst = reinterpret_cast<double2*>(prec + (size_t)max(p0, 0) * kPRec);
+#pragma unroll
+      for (int it = 0; it < kPRec / 2; ++it) {
+        const int e = it * 64 + lane, r = e >> 3, f = 2 * (e & 7);
+        if (r < nrec) dst[e] = make_double2(ps[r * (kPRec + 1) + f], ps[r * (kPRec + 1) + f + 1]);
+      }
+      wave_lds_sync();
     }
-    acc[0] += ok ? 0.0 : 1.0;
   }
   double out[1];
   block_sum<1>(acc, lds, out);
