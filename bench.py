@@ -58,18 +58,38 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(config: str, kernel: str = "k_linearize"):
-    """Per-launch HBM bytes of the residual+Jacobian kernel from the committed
-    rocprofv3 PMC summary (profiles/), corrected per MI355X_MICROARCH.md
-    (FETCH_SIZE x2 on gfx950), or None."""
-    f = ROOT / "profiles" / f"pmc_{config}.json"
-    if not f.exists():
+def pmc_record(config: str, kernel: str, n_obs: int, scale: float = 1.0):
+    """Per-launch HBM bytes (and VALU instructions, when recorded) of the
+    residual+Jacobian kernel from a committed rocprofv3 PMC summary
+    (profiles/pmc_<config>*.json, tools/pmc_summary.py: separate FETCH_SIZE /
+    WRITE_SIZE passes, FETCH_SIZE x2 per MI355X_MICROARCH.md's gfx950
+    correction).  A summary measured on a problem of another size (its
+    "_problem" n_obs) is scaled linearly in the observations and says so; a
+    summary without a recorded size counts only for the full-size c3 run it
+    was taken on.  None when no summary covers the kernel."""
+    best = None
+    for f in sorted((ROOT / "profiles").glob(f"pmc_{config}*.json")):
+        try:
+            d = json.loads(f.read_text())
+            k = d[kernel]
+            n_at = (d.get("_problem") or {}).get("n_obs")
+            if n_at is None and not (config == "c3" and scale == 1.0 and f.name == "pmc_c3.json"):
+                continue
+            n_at = n_at or n_obs
+            cand = (abs(n_at - n_obs), f.name, k, n_at)
+        except Exception:
+            continue
+        if best is None or cand[0] < best[0]:
+            best = cand
+    if best is None:
         return None
-    try:
-        d = json.loads(f.read_text())
-        return float(d[kernel]["hbm_bytes_per_launch"])
-    except Exception:
-        return None
+    _, name, k, n_at = best
+    f = n_obs / n_at
+    rec = {"hbm_bytes_per_launch": float(k["hbm_bytes_per_launch"]) * f,
+           "source": f"profiles/{name}" + ("" if n_at == n_obs else f" (measured at {n_at} obs, scaled x{f:.4g})")}
+    if k.get("valu_insts_per_launch"):
+        rec["valu_insts_per_launch"] = float(k["valu_insts_per_launch"]) * f
+    return rec
 
 
 def uid_path(world: int) -> Path:
@@ -217,7 +237,7 @@ def dry_run_line(args, rank, world, local_rank, device):
     run, without any GPU call."""
     return json.dumps({"dry_run": True, "rank": rank, "world": world, "local_rank": local_rank, "device": device,
                        "workload": args.workload, "transport": args.transport, "steps": args.steps,
-                       "warmup": args.warmup})
+                       "warmup": args.warmup, "mode": args.mode})
 
 
 def main():
@@ -243,11 +263,19 @@ def main():
     ap.add_argument("--preconditioner", default="SCHUR_JACOBI", choices=["JACOBI", "SCHUR_JACOBI"])
     ap.add_argument("--precision", default=None, choices=["FP64", "MIXED_FP32"],
                     help="MIXED_FP32: fp32 storage of the per-observation Schur blocks (iterative only)")
+    ap.add_argument("--mode", default=None, choices=["fixed", "trajectory"],
+                    help="fixed: every step re-linearises at x0 and takes a trial step at the initial radius "
+                         "(identical work per step; default for c3, whose DENSE_SCHUR step does not depend on the "
+                         "radius); trajectory: ONE ba_solve from x0 for exactly K LM iterations with Ceres' radius "
+                         "schedule (accepted and rejected steps, the CG counts the radius implies; default for "
+                         "c4 / c5)")
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit(f"--gpus must be >= 1 (got {args.gpus})")
     if args.workload is None:
         args.workload = "c3" if args.gpus == 1 else "c4"
+    if args.mode is None:
+        args.mode = "trajectory" if args.workload in STRONG else "fixed"
 
     if args.workload in STRONG and 8 % args.gpus != 0:
         raise SystemExit(f"--workload {args.workload}: the 8 point blocks need a rank count dividing 8 "
@@ -319,27 +347,73 @@ def main():
     iterative = lin == "iterative"
     opts = Options(linear_solver_type="ITERATIVE_SCHUR" if iterative else "DENSE_SCHUR",
                    preconditioner_type=args.preconditioner, precision=precision)
-    # warmup (first call also computes the Jacobi scaling, as LM iteration 0 does)
-    solver.bench_iterations(max(1, args.warmup), options=opts)
-    barrier()
-    solver.synchronize()
-    # the timed region carries no event pair around the r+J kernel (each
-    # pair's packets idle the device ~5 us per LM iteration); the kernel is
-    # timed with HIP events on its stream in a second pass of the same K
-    # iterations right after (BENCH_RJ_IN_LOOP=1: both in one pass, A/B)
+    trajectory = None
     rj_in_loop = os.environ.get("BENCH_RJ_IN_LOOP") == "1"
-    t0 = time.perf_counter()
-    ms_dev, ms_rj, cg_iters = solver.bench_iterations(args.steps, options=opts, with_linear_iters=True,
-                                                      time_rj=rj_in_loop)
-    solver.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
-    # per-iteration host wall times of the timed region (the
-    # median of >= 10 iterations after 2 warm-ups), reported beside the mean
-    it_ms = solver.bench_iteration_times()
-    if not rj_in_loop:
-        _, ms_rj = solver.bench_iterations(args.steps, options=opts)
+    if args.mode == "trajectory":
+        # ONE solve from x0 for exactly K LM iterations: Ceres' radius
+        # schedule (x3 per good step, /2, /4 ... per rejected one), so each
+        # step's CG count is the one its radius implies (2-7 on this
+        # generator) and rejected steps skip the re-linearisation.  The
+        # termination tests are off so that K iterations run; nothing else
+        # differs from ba_solve with configureSolver's options.
+        import dataclasses
+        x0c, x0p = solver.problem.cams.copy(), solver.problem.pts.copy()
+        topts = dataclasses.replace(opts, max_num_iterations=args.steps, function_tolerance=0.0,
+                                    gradient_tolerance=0.0, parameter_tolerance=0.0)
+        # warmup: a W-iteration solve (buffers, Jacobi scaling), then back to x0
+        solver.solve(dataclasses.replace(topts, max_num_iterations=max(1, args.warmup)))
+        solver.set_params(x0c, x0p)
         barrier()
+        solver.synchronize()
+        t0 = time.perf_counter()
+        summ = solver.solve(topts)
+        solver.synchronize()
+        barrier()
+        dt = time.perf_counter() - t0
+        tlog = solver.iteration_log()[1:]          # [0] is the initial linearisation
+        it_ms = np.array([r["iteration_time_s"] * 1e3 for r in tlog])
+        cg = [int(r["linear_solver_iterations"]) for r in tlog]
+        cg_iters = float(np.mean(cg)) if cg else 0.0
+        # where Ceres' default function tolerance (1e-6 relative cost change)
+        # would have ended the solve
+        stop = next((i + 1 for i, r in enumerate(tlog) if r["step_is_successful"]
+                     and abs(r["cost_change"]) <= 1e-6 * (r["cost"] + r["cost_change"])), None)
+        trajectory = {"lm_iterations": summ.num_iterations, "successful_steps": summ.num_successful_steps,
+                      "unsuccessful_steps": summ.num_unsuccessful_steps,
+                      "initial_cost": summ.initial_cost, "final_cost": summ.final_cost,
+                      "linear_solver_iterations": cg,
+                      "iteration_ms": [round(float(x), 4) for x in it_ms],
+                      "ceres_default_function_tolerance_stop": stop,
+                      "note": "one ba_solve from x0 (termination tests off, Ceres' radius schedule); ms_per_step "
+                              "= the solve's wall time / its LM iterations, initial linearisation included"}
+        steps_done = summ.num_iterations
+        ms_dev = dt / max(steps_done, 1) * 1e3
+        # the r+J kernel's launch time does not depend on the radius: timed in
+        # a short fixed-radius pass after the solve
+        _, ms_rj = solver.bench_iterations(min(args.steps, 10), options=opts)
+        barrier()
+    else:
+        # warmup (first call also computes the Jacobi scaling, as LM iteration 0 does)
+        solver.bench_iterations(max(1, args.warmup), options=opts)
+        barrier()
+        solver.synchronize()
+        # the timed region carries no event pair around the r+J kernel (each
+        # pair's packets idle the device ~5 us per LM iteration); the kernel is
+        # timed with HIP events on its stream in a second pass of the same K
+        # iterations right after (BENCH_RJ_IN_LOOP=1: both in one pass, A/B)
+        t0 = time.perf_counter()
+        ms_dev, ms_rj, cg_iters = solver.bench_iterations(args.steps, options=opts, with_linear_iters=True,
+                                                          time_rj=rj_in_loop)
+        solver.synchronize()
+        barrier()
+        dt = time.perf_counter() - t0
+        steps_done = args.steps
+        # per-iteration host wall times of the timed region (the
+        # median of >= 10 iterations after 2 warm-ups), reported beside the mean
+        it_ms = solver.bench_iteration_times()
+        if not rj_in_loop:
+            _, ms_rj = solver.bench_iterations(args.steps, options=opts)
+            barrier()
 
     n_obs_total = problem.n_obs
     n_pts_total = problem.n_pts
@@ -352,7 +426,11 @@ def main():
 
     # algorithmic bytes of the residual+Jacobian kernel per launch:
     #   176 B/obs (uv 8 + two int32 idx 8 + r 16 + J 144) + 24 B/point + 48 B/camera
-    B_rj = 176.0 * problem.n_obs + 24.0 * problem.n_pts + 48.0 * problem.n_cams
+    # and, with fp32 storage (MIXED_FP32, the C5 configuration), §8d's
+    #   96 B/obs (r 8 + J 72 + uv 8 + idx 8) + 12 B/point + 24 B/camera
+    mixed = precision == "MIXED_FP32"
+    N, Pn, Cn = float(problem.n_obs), float(problem.n_pts), float(problem.n_cams)
+    B_rj = (96.0 * N + 12.0 * Pn + 24.0 * Cn) if mixed else (176.0 * N + 24.0 * Pn + 48.0 * Cn)
     achieved = B_rj / (ms_rj * 1e-3) / 1e9
     # J-free iteration (libba_hip's default, BA_JR unset): the timed kernel is
     # k_lin_point, which forms r and J in registers and reduces them into the
@@ -360,20 +438,42 @@ def main():
     # the L2-resident global table beyond); SURVEY.md §8d prices such a fused
     # kernel against the unfused B_rj, labelled "effective"
     jrfree = os.environ.get("BA_JR") != "1"
-    traffic = pmc_traffic(cfg, "k_lin_point" if jrfree else "k_linearize") if not strong and args.scale == 1.0 else None
+    kname = ("k_lin_point" if problem.n_cams <= 200 else "k_lin_point_d") if jrfree else "k_linearize"
+    pmc = pmc_record(cfg, kname, problem.n_obs, args.scale)
+    traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     # measured copy bandwidth of this GPU (reported beside the
     # vendor peak, which stays the denominator of `frac`): 1 GiB non-temporal
     # 16-B copy, 10 launches, after the timed region
     copy_gbs = solver.stream_copy(1 << 30, 10)
-    roofline = {"kernel": ("k_lin_point (residual + Jacobian + Huber + point blocks; J not materialised)" if jrfree
+    roofline = {"kernel": (f"{kname} (residual + Jacobian + Huber + point blocks; J not materialised)" if jrfree
                            else "k_linearize (residual+Jacobian)"),
                 "effective": jrfree,
                 "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "algorithmic_bytes": B_rj, "avg_launch_ms": round(ms_rj, 5),
+                "traffic": traffic, "algorithmic_bytes": B_rj,
+                "algorithmic_formula": ("96 N + 12 P + 24 C (fp32 r + J storage, SURVEY.md §8d)" if mixed
+                                        else "176 N + 24 P + 48 C (fp64 r + J, SURVEY.md §8d)"),
+                "avg_launch_ms": round(ms_rj, 5),
                 "timing": ("HIP events around every launch, in the timed region" if rj_in_loop else
-                           "HIP events around every launch, in a second pass of the same K LM iterations"),
+                           "HIP events around every launch, in a second pass of the same K LM iterations"
+                           if args.mode == "fixed" else
+                           "HIP events around every launch, in a fixed-radius pass after the trajectory"),
                 "measured_copy": round(copy_gbs, 1), "frac_of_copy": round(achieved / copy_gbs, 4)}
+    if jrfree:
+        roofline["effective_note"] = (
+            "J is never stored: the kernel moves far fewer bytes than the unfused B_rj it is priced against, so "
+            "'achieved' and 'frac_of_copy' (> 1 possible) are bookkeeping, not a bandwidth claim; the kernel's "
+            "real HBM rate is 'real'")
+    if pmc:
+        real = pmc["hbm_bytes_per_launch"] / (ms_rj * 1e-3) / 1e9
+        roofline["real"] = {"hbm_bytes_per_launch": pmc["hbm_bytes_per_launch"], "achieved": round(real, 1),
+                            "frac": round(real / HBM_PEAK_GBS, 4), "source": pmc["source"]}
+        if pmc.get("valu_insts_per_launch"):
+            # fp64 VALU issue: a wave64 fp64 instruction holds its SIMD's 16
+            # fp64 lanes 4 cycles; 4 SIMDs x 256 CUs at the 2.4 GHz peak clock
+            busy = pmc["valu_insts_per_launch"] * 4.0 / (ms_rj * 1e-3 * 2.4e9 * 1024.0)
+            roofline["real"]["valu_insts_per_launch"] = pmc["valu_insts_per_launch"]
+            roofline["real"]["valu_busy_frac_est"] = round(busy, 4)
 
     # whole-iteration figure (reported beside the kernel line):
     # B_iter = 176N (r+J) + 160N (r, J re-read for assembly) + 144N (W write)
@@ -381,8 +481,7 @@ def main():
     # + C (48 + 216) + 16 (6C)^2 (dense S formed and factored) or 2 x 144N per
     # CG iteration (implicit Schur); W terms 72N with fp32 W storage.  Per
     # rank, over the rank's device time per LM iteration.
-    wb = 72.0 if precision == "MIXED_FP32" else 144.0
-    N, Pn, Cn = float(problem.n_obs), float(problem.n_pts), float(problem.n_cams)
+    wb = 72.0 if mixed else 144.0
     B_iter = (176.0 + 160.0 + 2.0 * wb + 16.0) * N + 168.0 * Pn + 264.0 * Cn
     B_iter += 2.0 * wb * N * cg_iters if iterative else 16.0 * (6.0 * Cn) ** 2
     it_ach = B_iter / (ms_dev * 1e-3) / 1e9
@@ -403,7 +502,7 @@ def main():
             log(f"cpu baseline skipped: {problem.n_obs} observations")
 
     if rank == 0:
-        ms_step = dt / args.steps * 1e3
+        ms_step = dt / steps_done * 1e3
         mixed = precision == "MIXED_FP32"
         if strong:
             workload = (f"{cfg.upper()}: one {CONFIGS[cfg]['n_cams']} cams x {n_pts_total} pts x {n_obs_total} obs "
@@ -420,10 +519,10 @@ def main():
             solver_s = "LM + DENSE_SCHUR, fp64"
         out = {
             "metric": "M-obs/s per LM iteration (residual+Jacobian+Schur)",
-            "value": round(n_obs_total * args.steps / dt / 1e6, 2),
+            "value": round(n_obs_total * steps_done / dt / 1e6, 2),
             "unit": "M-obs/s",
             "n_gpus": world,
-            "steps": args.steps,
+            "steps": steps_done,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "ms_per_step_median": round(float(np.median(it_ms)), 4) if len(it_ms) else None,
@@ -443,7 +542,10 @@ def main():
             "roofline": roofline,
             "iteration_roofline": iteration_roofline,
             "cpu_baseline": cpu,
+            "mode": args.mode,
         }
+        if trajectory is not None:
+            out["trajectory"] = trajectory
         print(json.dumps(out), file=json_out, flush=True)
     solver.close()
     if host_ar is not None:

@@ -60,9 +60,7 @@ struct DevWork {
   double* rec;   double* rec_c;      // camera records at x / x'
   double* crec;                      // [nc][16] compact camera records (w, t, K, flag, theta terms) for > kLinLdsCams cameras
   double* ctbl;                      // [nc][22] candidate camera table for > kLinLdsCams cameras
-  double* gtbl;                      // [nc][48] global lin table of the J-free kernels beyond kLinLdsCams cameras (ba_kernels.hip kGRec)
-  bool jrfree;                       // J-free iteration: consumers recompute J, JR unused (camera table in LDS up to kLinLdsCams cameras, gtbl / crec beyond)
-  int jtab;                          // camera source of the J-free kernels beyond kLinLdsCams cameras: 1 gtbl, 2 crec
+  bool jrfree;                       // J-free iteration: consumers recompute J, JR unused (camera table in LDS up to kLinLdsCams cameras, crec beyond)
   double* JR;                        // JA [no][JA] (Jc rows 0..1; JA = 14 beyond kLinLdsCams cameras: + r again), then JB [no][8] (Jp rows 3+3, r 2)
   double* delta_p;                   // [np][3] point step (scaled back)
   double* Hpp;   double* gp;         // [6][np], [3][np]
@@ -72,12 +70,7 @@ struct DevWork {
   double* scale_c; double* diag_c;   // [nvc][6]
   double* delta_c;                   // [nvc][6]
   double* W;                         // [no][18]  (E L^-T per observation), fp64
-  // camera-major copies of W (ITERATIVE_SCHUR, W.wcm): row i = the i-th entry
-  // of cam_op, so the camera-side passes stream instead of gathering
-  bool wcm;
-  double* Wcm;                       // [n_camobs][18] fp64
-  float* Wcmf;                       // [n_camobs][18] fp32 (BA_MIXED_FP32)
-  double* prec;                      // [np][16] point record for the camera-major W: X (3), var flag, s_p (3), L_p^-1 (6)
+  double* prec;                      // [np][16] point record of the J-free diagonal blocks: X (3), var flag, s_p (3), L_p^-1 (6), u_p
   double* pxv;                       // [np][4] the linearisation point {X, var flag} (k_lin_point; camera-major gathers)
   bool jdiag;                        // the diagonal Schur blocks J-free (k_cam_schur_diag_rc: prec gathered, W not read)
   float* Wf;                         // [no][18]  the same in fp32 (BA_MIXED_FP32)
@@ -112,8 +105,6 @@ struct DevWork {
   double* ppart;                     // [3][kMaxBlocks] per-block partials of the camera-side kernels
   int pcg_G;
   const int2* pchunks;               // point-aligned observation chunks of <= 64 {start, end} (the PCG point pass)
-  const int* cam_pos;                // [no] camera-order position (cam_op index) of each observation, -1: fixed camera
-  bool tscat;                        // per-observation products stored in camera order (k_pcg_point_seg<.., SCAT>)
   // ITERATIVE_SCHUR point-pass records in the 16-value rank-2 form
   // (k_obs_w_rc<.., PC>, k_pcg_point_seg<.., PC>; step_w_storage decides)
   bool pcgc = false;
@@ -195,7 +186,6 @@ void launch_reduce_publish(const DevWork& W, uint32_t sum_mask, uint32_t max_mas
                            unsigned* host_seq, unsigned seq, unsigned* ticket, hipStream_t s);
 int back_flow_capacity(int device);
 bool obs_w_pc_ok(const DevProblem& P, const DevWork& W);   // k_obs_w_rc has the PCG record form for this source
-bool point_step_fused();                      // J-free back substitution fused with the candidate (BA_PSTEP)
 bool chol_persist_fits(int device, int n);   // every workgroup of k_chol_persist resident at once
 int chol_split_blocks();                     // block columns from which the split step form is used   // resident k_back_flow workgroups (-1: query failed)
 constexpr int kLinLdsCamsHost = 200;   // = kLinLdsCams (ba_kernels.hip): cameras the LDS camera table holds

@@ -265,19 +265,8 @@ __device__ inline void jr_chunk_stage(double* st, int lane, const double2 (&t)[J
 // linearisation: one thread per observation (sorted by point)
 // ---------------------------------------------------------------------------
 // Camera access for the linearisation: the K-folded table (kRecL, 40
-// doubles, read as 20 16-B loads) and K (float-valued) — either the global
-// records or the block's LDS copy of the camera table.
-struct CamGlobal {
-  const double* r;
-  bool v;
-  __device__ bool var() const { return v; }
-  __device__ void load(double (&t)[kLin]) const {
-    const double2* s = reinterpret_cast<const double2*>(r + kRecL);
-#pragma unroll
-    for (int k = 0; k < kLin / 2; ++k) { const double2 u = s[k]; t[2 * k] = u.x; t[2 * k + 1] = u.y; }
-  }
-  __device__ double K(int k) const { return r[kRecK + k]; }
-};
+// doubles, read as 20 16-B loads) and K (float-valued) from the block's LDS
+// copy of the camera table.
 // LDS row: lin table (40) + variable flag (slot 40) + pad; stride 42 doubles
 // keeps rows 16-B aligned and spreads random cameras over the 16 bank
 // groups of ds_read_b128
@@ -293,69 +282,13 @@ struct CamLds {
   }
   __device__ double K(int i) const { return (double)k[i]; }
 };
-// same rows, read element-wise where used (the compiler schedules and pairs
-// the LDS reads; fewer live registers than the 40-double preload)
-struct CamLdsLazy {
-  const double* r;
-  const float* k;
-  struct Row {
-    const double* r;
-    __device__ double operator[](int i) const { return r[i]; }
-  };
-  __device__ bool var() const { return r[kLin] != 0.0; }
-  __device__ Row row() const { return Row{r}; }
-  __device__ double K(int i) const { return (double)k[i]; }
-};
-
-// Many cameras (nc > kLinLdsCams) in the J-free iteration: the same table
-// rows in global memory, one 384-B row (three whole cache lines) per camera:
-//   [0..39] the lin table, [40] the variable flag, [41..45] K as 9 floats
-// C4 (1k cameras): 384 KB, C5 (10k): 3.8 MB — L2-resident, gathered per
-// observation by the point-major kernels (the same values as the LDS rows,
-// so the same arithmetic as the <= 200-camera kernels)
-constexpr int kGRec = 48;
-constexpr int kGRecK = 41;
-struct CamG {
-  const double* r;
-  __device__ bool var() const { return r[kLin] != 0.0; }
-  __device__ void load(double (&t)[kLin]) const {
-    const double2* s = reinterpret_cast<const double2*>(r);
-#pragma unroll
-    for (int k = 0; k < kLin / 2; ++k) { const double2 u = s[k]; t[2 * k] = u.x; t[2 * k + 1] = u.y; }
-  }
-  __device__ double K(int i) const { return (double)reinterpret_cast<const float*>(r + kGRecK)[i]; }
-  __device__ const float* Kf() const { return reinterpret_cast<const float*>(r + kGRecK); }
-};
-// gtbl from the camera records (thread per entry)
-__global__ __launch_bounds__(256) void k_lin_gtbl(DevProblem P, const double* __restrict__ rec,
-                                                  double* __restrict__ gtbl) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= P.nc * kGRec) return;
-  const int c = e / kGRec, k = e - c * kGRec;
-  const double* r = rec + (size_t)c * kCamRec;
-  double v = 0.0;
-  if (k < kLin) {
-    v = r[kRecL + k];
-  } else if (k == kLin) {
-    v = P.vc[c] >= 0 ? 1.0 : 0.0;
-  } else if (k < kGRecK + 5) {
-    const int i = 2 * (k - kGRecK);
-    const float lo = (float)r[kRecK + i], hi = i + 1 < 9 ? (float)r[kRecK + i + 1] : 0.0f;
-    v = __builtin_bit_cast(double, ((unsigned long long)__builtin_bit_cast(unsigned, hi) << 32) |
-                                       __builtin_bit_cast(unsigned, lo));
-  }
-  gtbl[e] = v;
-}
-
-// camera row as an indexable value: a register copy (CamGlobal, CamLds, CamG)
-// or an LDS view (CamLdsLazy)
+// camera row as an indexable value: a register copy
 struct RowRegs {
   double t[kLin];
   __device__ double operator[](int i) const { return t[i]; }
 };
 template <class Cam>
 __device__ inline RowRegs cam_row(const Cam& cr) { RowRegs R; cr.load(R.t); return R; }
-__device__ inline CamLdsLazy::Row cam_row(const CamLdsLazy& cr) { return cr.row(); }
 
 // Many cameras (nc > kLinLdsCams): the 704-B camera records no longer fit the
 // LDS and, past ~5k cameras, not even one XCD's L2 (C5: 7 MB of records,
@@ -867,22 +800,6 @@ __device__ inline void lin_waves(const DevProblem& P, const double* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void k_linearize(DevProblem P, const double* __restrict__ rec,
-                                                   const double* __restrict__ pts, double* __restrict__ JR,
-                                                   double* __restrict__ part) {
-  __shared__ double lds[2 * 16];
-  __shared__ double stage[4 * 64 * kStageLd];
-  double acc[2] = {0.0, 0.0};  // cost, bad
-  lin_waves<jr_ja(true), 4, 64>(P, pts, JR, stage,
-                                [&](int c) { return CamGlobal{rec + (size_t)c * kCamRec, P.vc[c] >= 0}; }, acc);
-  double tot[2];
-  block_sum<2>(acc, lds, tot);
-  if (threadIdx.x == 0) {
-    part_of(part, SL_COST)[blockIdx.x] = tot[0];
-    part_of(part, SL_LIN_BAD)[blockIdx.x] = tot[1];
-  }
-}
-
 __global__ __launch_bounds__(256) void k_linearize_rc(DevProblem P, const double* __restrict__ crec,
                                                       const double* __restrict__ pts, double* __restrict__ JR,
                                                       double* __restrict__ part) {
@@ -946,7 +863,7 @@ __device__ inline void fill_lin_table(const DevProblem& P, const double* __restr
 // NT threads per block (one block per CU: the camera table fills most of
 // the LDS), stage rows ROWS per wave.
 // HOOK: the table fill runs after the first chunks' loads are issued
-template <int NT, int ROWS, int MODE = 0, bool LAZY = false, bool HOOK = false>
+template <int NT, int ROWS, int MODE = 0, bool HOOK = false>
 __global__ __launch_bounds__(NT) void k_linearize_lds_t(DevProblem P, const double* __restrict__ rec,
                                                         const double* __restrict__ pts, double* __restrict__ JR,
                                                         double* __restrict__ part) {
@@ -956,10 +873,7 @@ __global__ __launch_bounds__(NT) void k_linearize_lds_t(DevProblem P, const doub
   __shared__ float ktb[kLinLdsCams * 9];
   if (!HOOK) fill_lin_table<NT>(P, rec, tbl, ktb);
   double acc[2] = {0.0, 0.0};
-  auto cam_of = [&](int c) {
-    if constexpr (LAZY) return CamLdsLazy{tbl + c * kTblRec, ktb + c * 9};
-    else return CamLds{tbl + c * kTblRec, ktb + c * 9};
-  };
+  auto cam_of = [&](int c) { return CamLds{tbl + c * kTblRec, ktb + c * 9}; };
   auto init = [&] { if (HOOK) fill_lin_table<NT>(P, rec, tbl, ktb); };
   if (MODE != 3) lin_waves<jr_ja(false), NT / 64, ROWS, decltype(cam_of), MODE>(P, pts, JR, stage, cam_of, acc, init);
   double tot[2];
@@ -1700,9 +1614,8 @@ __device__ inline void wc_rows(const WcRaw& w, const WcCam& m, double (&c0)[6], 
 // diagonal Schur blocks and rhs (local part): one workgroup per camera
 //   S_cc = -sum W W^T (lower 21) ; b_c = -sum W u_p
 // ---------------------------------------------------------------------------
-// CM: W is the camera-major copy (row i of cam_op), streamed.  NT threads per
-// camera slice
-template <typename WT, bool CM = false, int NT = 256>
+// NT threads per camera slice
+template <typename WT, int NT = 256>
 __global__ __launch_bounds__(NT) void k_cam_schur_diag(DevProblem P, const WT* __restrict__ W,
                                                         const double* __restrict__ u, double* __restrict__ S,
                                                         double* __restrict__ cpart) {
@@ -1728,7 +1641,7 @@ __global__ __launch_bounds__(NT) void k_cam_schur_diag(DevProblem P, const WT* _
   for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int2 op = P.cam_op[i];
     double w[18];
-    load_w18(W, CM ? (size_t)i : (size_t)op.x, w);
+    load_w18(W, (size_t)op.x, w);
     const double2 u01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
     add(w, u01.x, u01.y, u[4 * (size_t)op.y + 2]);
   }
@@ -2363,12 +2276,6 @@ __global__ __launch_bounds__(64) void k_reduce(double* __restrict__ part, double
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-// diagnostics: BA_LIN_LEGACY=1 -> the global-record linearisation beyond 200 cameras
-static bool lin_legacy() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("BA_LIN_LEGACY"); v = e && atoi(e) ? 1 : 0; }
-  return v != 0;
-}
 // ---------------------------------------------------------------------------
 // J-free iteration (nc <= kLinLdsCams, the camera table fits the LDS).
 //
@@ -2383,7 +2290,8 @@ static bool lin_legacy() {
 //                     LM diagonal, gradient norms (k_linearize + k_point_assemble)
 //   k_cam_assemble_rc Hcc / gc per camera, the camera's table row in registers
 //   k_obs_w_rc        W_o = s_c Jc^T Jp s_p L_p^-T
-//   k_candidate_rc    model cost change J d . (r + J d / 2) and candidate cost
+//   k_point_step_rc   back substitution, model cost change J d . (r + J d / 2)
+//                     and candidate cost
 // Per point / camera the sums run in the order of the JR kernels they replace.
 // ---------------------------------------------------------------------------
 // a variable camera's table row held in registers (the camera of a whole
@@ -2402,12 +2310,9 @@ struct CamRegs {
 // LANES lanes per point (lane l of a group takes the point's observations l,
 // l + LANES, ...; fixed-order xor fold inside the group); the next
 // observation's indices and pixel, and the group's next point, are loaded one
-// step ahead (clamped, unconditional loads)
-// TB: the camera source (nc > kLinLdsCams: no LDS copy) — 0 the LDS copy of
-// the records' lin tables, 1 rec is the global table gtbl (kGRec rows), 2 rec
-// is the compact records crec (k_cam_compact; the dual Rodrigues per
-// observation), gathered per observation
-template <int NT, int LANES, bool LAZY = false, int TB = 0>
+// step ahead (clamped, unconditional loads).  The cameras from the LDS copy
+// of the records' lin tables (nc <= kLinLdsCams; beyond: k_lin_point_d)
+template <int NT, int LANES>
 // pxv: the points as 32-B records {X, variable flag} for the camera-major
 // consumers (k_cam_assemble_rc: one sector per gathered point)
 __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __restrict__ rec,
@@ -2417,9 +2322,9 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
                                                   double max_diag, double* __restrict__ part,
                                                   double* __restrict__ pxv) {
   __shared__ double lds[5 * 16];
-  __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
-  __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
-  if constexpr (!TB) fill_lin_table<NT>(P, rec, tbl, ktb);
+  __shared__ __attribute__((aligned(16))) double tbl[kLinLdsCams * kTblRec];
+  __shared__ float ktb[kLinLdsCams * 9];
+  fill_lin_table<NT>(P, rec, tbl, ktb);
   double acc[4] = {0.0, 0.0, 0.0, 0.0};   // cost, bad, gn2, xn2
   double gmax = 0.0;
   const size_t np = (size_t)P.np;
@@ -2451,20 +2356,8 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
       const float2 uvn = P.uv[on];
       double out[kJR];
       bool fin;
-      double rho;
-      if constexpr (TB == 1) {
-        const CamG cam{rec + (size_t)c * kGRec};
-        rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
-      } else if constexpr (TB == 2) {
-        const CamRc cam = cam_rc(rec, c);
-        rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
-      } else if constexpr (LAZY) {   // table entries read from LDS at use (fewer registers)
-        const CamLdsLazy cam{tbl + c * kTblRec, ktb + c * 9};
-        rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
-      } else {
-        const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
-        rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
-      }
+      const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
+      const double rho = lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, out, fin);
       acc[0] += 0.5 * rho;
       acc[1] += fin ? 0.0 : 1.0;
       // k_point_assemble's accumulation of the JB record (Jp rows, r)
@@ -2536,7 +2429,8 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
   }
 }
 
-// k_lin_point<.., TB 2> with the compact camera records gathered by LDS-DMA
+// k_lin_point beyond kLinLdsCams cameras: the compact camera records
+// (k_cam_compact; the dual Rodrigues per observation) gathered by LDS-DMA
 // (8 lanes per 128-B record, a wave-instruction touching 8 records instead of
 // 64; pieces XOR-swizzled through the source address as in k_schur_pairs_cd)
 // one observation round ahead — across point boundaries too: the last round
@@ -2544,7 +2438,7 @@ __global__ __launch_bounds__(NT) void k_lin_point(DevProblem P, const double* __
 // needs every lane of the wave, so the point and observation loops run in
 // wave-uniform rounds (a lane past its point's observations, or past the
 // points, computes nothing).  Per lane the same lin_obs on the same record
-// values and the same accumulation order: bitwise k_lin_point<.., 2>.
+// values and the same accumulation order as per-lane register gathers.
 template <int NT, int LANES>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_lin_point_d(DevProblem P, const double* __restrict__ crec,
                                                     const double* __restrict__ pts, double* __restrict__ Hpp,
@@ -2787,9 +2681,9 @@ __global__ __launch_bounds__(NT) void k_cam_assemble_rc(DevProblem P, const doub
 // f are exact zeros there), then Z: 16 values, one 128-B line (fp64) instead
 // of 144 B, with no per-camera constants to gather (k_pcg_point_seg<.., PC>)
 constexpr int kObsWRcWaves = 6;   // table + K + scales + 6 staging slots fit the 160 KB LDS
-// TB (nc > kLinLdsCams, k_lin_point's camera sources): rec is the global
-// table gtbl (1) or the compact records crec (2); the camera scalings are
-// read from scale_c
+// TB: 0 the LDS copy of the camera table, 3 (nc > kLinLdsCams) rec is the
+// compact records crec, gathered by LDS-DMA (below); the camera scalings are
+// then read from scale_c
 // WAVES: waves per workgroup.  The LDS-table form (TB 0) holds one 148-KB
 // workgroup per CU: 6.  The global-source forms need ~230 VGPRs (two waves per
 // SIMD): a 6-wave workgroup then leaves a CU at one workgroup, 6 waves, where
@@ -2829,7 +2723,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_obs_w_rc(DevProblem P, const dou
   int oc = min(base + lane, P.no - 1);
   int c = P.obs_cam[oc], p = P.obs_pt[oc];
   float2 uv = P.uv[oc];
-  // TB 3: the compact records (TB 2) gathered by LDS-DMA into the wave's
+  // TB 3: the compact records gathered by LDS-DMA into the wave's
   // staging slot, 8 lanes per 128-B record (pieces XOR-swizzled through the
   // source address, as k_schur_pairs_cd): a wave-instruction touches 8
   // records instead of 64.  The next chunk's records are requested after
@@ -2877,15 +2771,10 @@ __global__ __launch_bounds__(64 * WAVES) void k_obs_w_rc(DevProblem P, const dou
     bool fin;
     double prf[3];
     double sc[6];
-    if constexpr (TB) {
-      if constexpr (TB == 1) {
-        const CamG cam{rec + (size_t)c * kGRec};
-        (void)lin_obs(P, cam, v >= 0, pv, X0, X1, X2, uv, j, fin, prf);
-      } else if constexpr (TB == 3) {
+    static_assert(TB == 0 || TB == 3, "camera source: LDS table or DMA-gathered compact records");
+    if constexpr (TB == 3) {
+      {
         const CamRc cam = cam_make(CamRcOf{rec, nullptr}, crp);
-        (void)lin_obs(P, cam, v >= 0, pv, X0, X1, X2, uv, j, fin, prf);
-      } else {
-        const CamRc cam = cam_rc(rec, c);
         (void)lin_obs(P, cam, v >= 0, pv, X0, X1, X2, uv, j, fin, prf);
       }
       // (v < 0: the record is zero, !live).  Three 16-B gathers, not six
@@ -2975,94 +2864,6 @@ __global__ __launch_bounds__(64 * WAVES) void k_obs_w_rc(DevProblem P, const dou
   }
 }
 
-// Camera-major W (ITERATIVE_SCHUR, W.wcm): the same W_o as k_obs_w_rc, row
-// i of the cam_op order, so that the camera-side passes (the diagonal Schur
-// blocks and every CG iteration's camera pass) stream it instead of
-// gathering point-major records (random 72 / 144-B gathers from an array
-// past the Infinity Cache at C5).  One workgroup per camera slice, the
-// camera's table row in registers (k_cam_assemble_rc), the point's record
-// (k_point_elim's prec: one 128-B line) and pixel gathered per observation;
-// J by the same lin_obs on the same table values: bitwise k_obs_w_rc's W.
-template <int NT, typename WT, int TB = 0>
-__global__ __launch_bounds__(NT) void k_obs_w_cam(DevProblem P, const double* __restrict__ rec,
-                                                  const double* __restrict__ prec,
-                                                  const double* __restrict__ scale_c, WT* __restrict__ Wcm) {
-  const int v = blockIdx.x;
-  const int c = P.cam_of_vc[v];
-  typename std::conditional<TB == 2, CamRcR, CamRegs>::type cam;
-  if constexpr (TB == 2) {
-    cam.make(cam_rc(rec, c));
-  } else {
-    const double2* s2 = reinterpret_cast<const double2*>(rec + (size_t)c * kCamRec + kRecL);
-#pragma unroll
-    for (int k = 0; k < kLin / 2; ++k) { const double2 q = s2[k]; cam.t[2 * k] = q.x; cam.t[2 * k + 1] = q.y; }
-#pragma unroll
-    for (int k = 0; k < 9; ++k) cam.k[k] = (double)P.K[9 * c + k];   // float-valued (Matrix3f)
-  }
-  double sc[6];
-#pragma unroll
-  for (int a = 0; a < 6; ++a) sc[a] = scale_c[(size_t)v * 6 + a];
-  int i0, i1;
-  cam_slice(P, v, i0, i1);
-  using V2 = typename std::conditional<sizeof(WT) == 8, double2, float2>::type;
-  // each wave writes 64 consecutive rows through its LDS slot as contiguous
-  // wave stores (k_obs_w_rc's staging; a row-per-lane store of 72 / 144 B
-  // leaves every store instruction partial lines)
-  __shared__ double stage[(NT / 64) * 64 * kStageLd];
-  const int lane = threadIdx.x & 63, wv_ = threadIdx.x >> 6;
-  double* st = stage + wv_ * (64 * kStageLd);
-  for (int base = i0 + 64 * wv_; base < i1; base += NT) {   // (uniform per wave)
-    const int i = min(base + lane, i1 - 1);
-    const bool live = base + lane < i1;
-    const int2 op = P.cam_op[i];
-    double r[kPRec];
-    {
-      const double2* q = reinterpret_cast<const double2*>(prec + (size_t)op.y * kPRec);
-#pragma unroll
-      for (int k = 0; k < 7; ++k) { const double2 t = q[k]; r[2 * k] = t.x; r[2 * k + 1] = t.y; }
-    }
-    const bool pv = r[3] != 0.0;
-    double j[kJR];
-    bool fin;
-    (void)lin_obs(P, cam, true, pv, r[0], r[1], r[2], P.uv_cm[i], j, fin);
-    const double s0 = r[4], s1 = r[5], s2 = r[6];
-    const double i00 = r[7], i10 = r[8], i11 = r[9], i20 = r[10], i21 = r[11], i22 = r[12];
-    const double jp0[3] = {j[12] * s0, j[13] * s1, j[14] * s2};
-    const double jp1[3] = {j[15] * s0, j[16] * s1, j[17] * s2};
-    double wv[kWRec];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {   // k_obs_w_rc's arithmetic
-      const double c0 = j[a] * sc[a], c1 = j[6 + a] * sc[a];
-      const double e0 = c0 * jp0[0] + c1 * jp1[0];
-      const double e1 = c0 * jp0[1] + c1 * jp1[1];
-      const double e2 = c0 * jp0[2] + c1 * jp1[2];
-      wv[a * 3 + 0] = pv ? e0 * i00 : 0.0;
-      wv[a * 3 + 1] = pv ? e0 * i10 + e1 * i11 : 0.0;
-      wv[a * 3 + 2] = pv ? e0 * i20 + e1 * i21 + e2 * i22 : 0.0;
-    }
-#pragma unroll
-    for (int k = 0; k < kWRec; ++k) st[lane * kStageLd + k] = live ? wv[k] : 0.0;
-    wave_lds_sync();
-    constexpr int NIT = kWRec / 2;
-    V2 ov[NIT];
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int e = it * 64 + lane;
-      const int r = e / NIT, f = 2 * (e - r * NIT);
-      ov[it].x = (WT)st[r * kStageLd + f];
-      ov[it].y = (WT)st[r * kStageLd + f + 1];
-    }
-    wave_lds_sync();
-    V2* dst = reinterpret_cast<V2*>(Wcm + (size_t)base * kWRec);
-    const int nrec = min(64, i1 - base);
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int e = it * 64 + lane;
-      if (e / NIT < nrec) dst[e] = ov[it];
-    }
-  }
-}
-
 // The diagonal Schur blocks and the reduced rhs per camera, J-free
 // (k_cam_schur_diag without W): the camera's table row (or its compact
 // record's dual Rodrigues) in registers, per observation the point's
@@ -3143,208 +2944,17 @@ __global__ __launch_bounds__(NT) void k_cam_schur_diag_rc(DevProblem P, const do
   cam_slice_store(tot, cpart, v, P.nvc);
 }
 
-// k_cam_schur_diag on compact records:
-//   W W^T = c^T (Z Z^T) c,  W u = c^T (Z u)
-// NT threads per workgroup (W.cam_split workgroups per camera).  PREF: the
-// next observation's record and u one step ahead.  At 256 threads a thread
-// has ~2.5 observations at C3 and the 27-value workgroup reduction (DS
-// permutes) is a third of the kernel's instructions (SQ counters,
-// profiles/r03_v12_pmc_sq.txt); one wave per workgroup has ~10.
-template <int NT, bool PREF>
-__global__ __launch_bounds__(NT) void k_cam_schur_diag_c(DevProblem P, const double* __restrict__ Wc,
-                                                         const double* __restrict__ scale_c,
-                                                         const double* __restrict__ u, double* __restrict__ cpart) {
-  __shared__ double lds[27 * 16];
-  const int v = blockIdx.x;
-  WcCam m;
-  m.load(P, scale_c, v);
-  double acc[27];
-#pragma unroll
-  for (int k = 0; k < 27; ++k) acc[k] = 0.0;
-  int i0, i1;
-  cam_slice(P, v, i0, i1);
-  auto add = [&](const WcRaw& w, double2 u01, double u2) {
-    double c0[6], c1[6];
-    wc_rows(w, m, c0, c1);
-    const double* z0 = w.r + 9;
-    const double* z1 = w.r + 12;
-    const double m00 = z0[0] * z0[0] + z0[1] * z0[1] + z0[2] * z0[2];
-    const double m01 = z0[0] * z1[0] + z0[1] * z1[1] + z0[2] * z1[2];
-    const double m11 = z1[0] * z1[0] + z1[1] * z1[1] + z1[2] * z1[2];
-    const double zu0 = z0[0] * u01.x + z0[1] * u01.y + z0[2] * u2;
-    const double zu1 = z1[0] * u01.x + z1[1] * u01.y + z1[2] * u2;
-    double n0[6], n1[6];
-#pragma unroll
-    for (int b = 0; b < 6; ++b) {
-      n0[b] = m00 * c0[b] + m01 * c1[b];
-      n1[b] = m01 * c0[b] + m11 * c1[b];
-    }
-    int t = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-#pragma unroll
-      for (int b = 0; b <= a; ++b) acc[t++] += c0[a] * n0[b] + c1[a] * n1[b];
-    }
-#pragma unroll
-    for (int a = 0; a < 6; ++a) acc[21 + a] += c0[a] * zu0 + c1[a] * zu1;
-  };
-  if constexpr (PREF) {
-    int i = i0 + threadIdx.x;
-    WcRaw nw;
-    double2 nu01 = make_double2(0.0, 0.0);
-    double nu2 = 0.0;
-    if (i < i1) {
-      const int2 op = P.cam_op[i];
-      nw = wc_fetch(Wc, op.x);
-      nu01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
-      nu2 = u[4 * (size_t)op.y + 2];
-    }
-    for (; i < i1; i += NT) {
-      const WcRaw w = nw;
-      const double2 u01 = nu01;
-      const double u2 = nu2;
-      if (i + NT < i1) {
-        const int2 op = P.cam_op[i + NT];
-        nw = wc_fetch(Wc, op.x);
-        nu01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
-        nu2 = u[4 * (size_t)op.y + 2];
-      }
-      add(w, u01, u2);
-    }
-  } else {
-    for (int i = i0 + threadIdx.x; i < i1; i += NT) {
-      const int2 op = P.cam_op[i];
-      const WcRaw w = wc_fetch(Wc, op.x);
-      const double2 u01 = *reinterpret_cast<const double2*>(u + 4 * (size_t)op.y);
-      add(w, u01, u[4 * (size_t)op.y + 2]);
-    }
-  }
-  double tot[27];
-  block_sum<27>(acc, lds, tot);
-  cam_slice_store(tot, cpart, v, P.nvc);
-}
-
-// k_cam_schur_diag_c with the compact records and u gathered into LDS by
-// LDS-DMA (as k_schur_pairs_cd: 8 lanes per 128-B record, 2 per 32-B u
-// record, pieces XOR-swizzled through the source address), one wave per
-// workgroup.  The next round's observation indices are loaded one round
-// ahead, its DMA issued right after this round's records are read out of
-// LDS.  The same adds per lane in the same order: bitwise k_cam_schur_diag_c.
-
-// model cost change + candidate cost with J recomputed at x (the lin table of
-// the linearisation point) beside the value-only candidate table
-// TB (nc > kLinLdsCams, k_lin_point's camera sources): rec is gtbl (1) or
-// crec (2), rec_c the global candidate table ctbl (k_cand_table), K from
-// gtbl / P.K
-template <int NT, int TB = 0>
-__global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double* __restrict__ rec,
-                                                     const double* __restrict__ pts,
-                                                     const double* __restrict__ delta_c,
-                                                     const double* __restrict__ delta_p,
-                                                     const double* __restrict__ rec_c,
-                                                     const double* __restrict__ pts_c, double* __restrict__ part) {
-  __shared__ double lds[3 * 16];
-  __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
-  __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
-  __shared__ double ctb_s[TB ? 1 : kLinLdsCams * kCandRec];
-  if constexpr (!TB) {
-    fill_lin_table<NT>(P, rec, tbl, ktb);
-    const int n = P.nc * kCandRec;
-    for (int e = threadIdx.x; e < n; e += NT) ctb_s[e] = cand_entry(P, rec_c, delta_c, e);
-    __syncthreads();
-  }
-  const double* ctb = TB ? rec_c : ctb_s;
-  double acc[3] = {0.0, 0.0, 0.0};  // mneg, ccost, cand_bad
-  // the next observation's indices, pixel and point data are loaded one step
-  // ahead (clamped, unconditional)
-  struct ObsIn {
-    int c, p;
-    float2 uv;
-    bool pv;
-    double X[3], Xc[3], dp[3];
-  };
-  const int lasto = max(P.no - 1, 0);
-  auto load_in = [&](int o, ObsIn& q) {
-    const int oc = min(o, lasto);
-    q.c = P.obs_cam[oc];
-    q.p = P.obs_pt[oc];
-    q.uv = P.uv[oc];
-    q.pv = P.pt_var[q.p] != 0;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      q.X[k] = pts[3 * q.p + k];
-      q.Xc[k] = pts_c[3 * q.p + k];
-      q.dp[k] = delta_p[3 * q.p + k];
-    }
-  };
-  const int ostep = gridDim.x * NT;
-  int o = P.no > 0 ? blockIdx.x * NT + threadIdx.x : P.no;
-  ObsIn cur;
-  if (P.no > 0) load_in(o, cur);
-  for (; o < P.no; o += ostep) {
-    ObsIn nxt;
-    load_in(o + ostep, nxt);
-    const int c = cur.c;
-    const float2 uv = cur.uv;
-    double j[kJR];
-    bool fin;
-    const float* Kc;
-    if constexpr (TB == 1) {
-      const CamG cam{rec + (size_t)c * kGRec};
-      (void)lin_obs(P, cam, cam.var(), cur.pv, cur.X[0], cur.X[1], cur.X[2], uv, j, fin);
-      Kc = cam.Kf();
-    } else if constexpr (TB == 2) {
-      const CamRc cam = cam_rc(rec, c);
-      (void)lin_obs(P, cam, cam.var(), cur.pv, cur.X[0], cur.X[1], cur.X[2], uv, j, fin);
-      Kc = P.K + 9 * c;
-    } else {
-      const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
-      (void)lin_obs(P, cam, cam.var(), cur.pv, cur.X[0], cur.X[1], cur.X[2], uv, j, fin);
-      Kc = ktb + c * 9;
-    }
-    const double dp0 = cur.dp[0], dp1 = cur.dp[1], dp2 = cur.dp[2];
-    const double X0 = cur.Xc[0], X1 = cur.Xc[1], X2 = cur.Xc[2];
-    const bool cfix = P.cam_fixed && P.cam_fixed[c];
-    const double* cr = ctb + (size_t)c * kCandRec;
-    // k_candidate_lds' arithmetic on the same values
-    double jd0 = 0.0, jd1 = 0.0;
-#pragma unroll
-    for (int a2 = 0; a2 < 6; ++a2) { jd0 += j[a2] * cr[16 + a2]; jd1 += j[6 + a2] * cr[16 + a2]; }
-    jd0 += j[12] * dp0 + j[13] * dp1 + j[14] * dp2;
-    jd1 += j[15] * dp0 + j[16] * dp1 + j[17] * dp2;
-    const double mneg = jd0 * (j[18] + jd0 / 2.0) + jd1 * (j[19] + jd1 / 2.0);
-    double pc[3];
-    if (!cfix) {
-#pragma unroll
-      for (int i = 0; i < 3; ++i) pc[i] = cr[i] * X0 + cr[3 + i] * X1 + cr[6 + i] * X2 + cr[9 + i];
-    } else {
-      double ph[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ph[i] = X0 * cr[i] + X1 * cr[4 + i] + X2 * cr[8 + i] + cr[12 + i];
-      pc[0] = ph[0] / ph[3]; pc[1] = ph[1] / ph[3]; pc[2] = ph[2] / ph[3];
-    }
-    double q[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) q[i] = pc[0] * (double)Kc[i] + pc[1] * (double)Kc[3 + i] + pc[2] * (double)Kc[6 + i];
-    const double rc0 = q[0] / q[2] - (double)uv.x, rc1 = q[1] / q[2] - (double)uv.y;
-    double sc;
-    const double rho = huber(rc0 * rc0 + rc1 * rc1, P.huber_a, P.huber_b, &sc);
-    acc[0] += mneg;
-    acc[1] += 0.5 * rho;
-    if (!isfinite(rc0) || !isfinite(rc1)) acc[2] += 1.0;
-    cur = nxt;
-  }
-  double out[3];
-  block_sum<3>(acc, lds, out);
-  if (threadIdx.x == 0) {
-    part_of(part, SL_MCC_NEG)[blockIdx.x] = out[0];
-    part_of(part, SL_CCOST)[blockIdx.x] = out[1];
-    part_of(part, SL_CAND_BAD)[blockIdx.x] = out[2];
-  }
-}
+// k_cam_schur_diag on compact records (W W^T = c^T (Z Z^T) c, W u = c^T (Z u)),
+// the records and u gathered into LDS by LDS-DMA (as k_schur_pairs_cd: 8
+// lanes per 128-B record, 2 per 32-B u record, pieces XOR-swizzled through
+// the source address), one wave per workgroup (a thread has ~10
+// observations at C3; at 256 threads ~2.5 and the 27-value reduction was a
+// third of the instructions, profiles/r03_v12_pmc_sq.txt).  The next round's
+// observation indices are loaded one round ahead, its DMA issued right after
+// this round's records are read out of LDS.
 
 // Back substitution of the points fused with the model cost change and the
-// candidate cost (J-free; replaces k_backsub + k_candidate_rc).  Per point,
+// candidate cost (J-free; replaces k_backsub + a candidate pass).  Per point,
 // LANES lanes (k_lin_point's layout):
 //   pass 1  v = sum_o Jp_o^T (Jc_o dc_o) over the point's observations (J
 //           recomputed at x), folded in the group; then
@@ -3354,9 +2964,9 @@ __global__ __launch_bounds__(NT) void k_candidate_rc(DevProblem P, const double*
 //   pass 2  J d . (r + J d / 2) (Jc dc, Jp and r kept from pass 1 for the
 //           lane's first KC observations, J again past them) and the
 //           candidate residual at (camera', x'_p) per observation.
-// TB (nc > kLinLdsCams, k_lin_point's camera sources): rec is gtbl (1) or
-// crec (2), rec_c the global candidate table ctbl (k_cand_table)
-template <int NT, int LANES, bool LAZY, int KC = 3, int TB = 0>
+// TB 2 (nc > kLinLdsCams): rec is the compact records crec, rec_c the
+// global candidate table ctbl (k_cand_table)
+template <int NT, int LANES, int KC = 3, int TB = 0>
 __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double* __restrict__ rec,
                                                       const double* __restrict__ pts,
                                                       const double* __restrict__ delta_c,
@@ -3389,14 +2999,8 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
   const int lastp = max(P.np - 1, 0), lasto = max(P.no - 1, 0);
   auto lin = [&](int c, bool pv, double X0, double X1, double X2, float2 uv, double (&j)[kJR]) {
     bool fin;
-    if constexpr (TB == 1) {
-      const CamG cam{rec + (size_t)c * kGRec};
-      (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
-    } else if constexpr (TB == 2) {
+    if constexpr (TB == 2) {
       const CamRc cam = cam_rc(rec, c);
-      (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
-    } else if constexpr (LAZY) {
-      const CamLdsLazy cam{tbl + c * kTblRec, ktb + c * 9};
       (void)lin_obs(P, cam, cam.var(), pv, X0, X1, X2, uv, j, fin);
     } else {
       const CamLds cam{tbl + c * kTblRec, ktb + c * 9};
@@ -3550,7 +3154,7 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
               kq[4 * k + 3] = __builtin_bit_cast(float, (unsigned)(b >> 32));
             }
           }
-          const float* Kc = TB == 1 ? CamG{rec + (size_t)c * kGRec}.Kf() : (TB == 2 ? kq : ktb + c * 9);
+          const float* Kc = TB == 2 ? kq : ktb + c * 9;
           double q[3];
 #pragma unroll
           for (int i = 0; i < 3; ++i)
@@ -3606,30 +3210,20 @@ static int lds_grid(int n) {
   return g < 1 ? 1 : (g > n_cu ? n_cu : g);
 }
 
-// the J-free kernels read the LDS copy of the camera records' lin tables up
-// to kLinLdsCams cameras and the global table gtbl beyond
 // camera source of the J-free kernels: 0 the LDS copy of the records' lin
-// tables (nc <= kLinLdsCams), beyond: 1 the global table gtbl, 2 the compact
-// records crec (W.jtab)
-static int jr_tab(const DevProblem& P, const DevWork& W) { return W.jrfree && P.nc > kLinLdsCams ? W.jtab : 0; }
+// tables (nc <= kLinLdsCams), 2 beyond: the compact records crec (each
+// observation forms its camera's dual Rodrigues from them)
+static int jr_tab(const DevProblem& P, const DevWork& W) { return W.jrfree && P.nc > kLinLdsCams ? 2 : 0; }
 void launch_lin_prep(const DevProblem& P, const DevWork& W, hipStream_t s) {
-  const int tb = jr_tab(P, W);
-  if (tb == 2 || (P.nc > kLinLdsCams && !lin_legacy() && !W.jrfree)) {
+  if (P.nc > kLinLdsCams) {   // (the JR path's k_linearize_rc reads them too)
     hipLaunchKernelGGL(k_cam_compact, dim3((P.nc + 255) / 256), dim3(256), 0, s, P, W.cams, W.crec);
     return;
   }
   launch_cam_prep(P, W.cams, W.rec, true, s);
-  if (tb == 1)
-    hipLaunchKernelGGL(k_lin_gtbl, dim3((P.nc * kGRec + 255) / 256), dim3(256), 0, s, P, (const double*)W.rec, W.gtbl);
 }
-// the W writers that have a 16-value PCG record form (k_obs_w_rc<.., PC>):
-// the LDS camera table (TB 0) and the DMA-gathered compact records (TB 3)
-static bool crec_dma();
-bool obs_w_pc_ok(const DevProblem& P, const DevWork& W) {
-  if (!W.jrfree) return false;
-  const int tb = jr_tab(P, W);
-  return tb == 0 || (tb == 2 && crec_dma());
-}
+// the W writers have a 16-value PCG record form (k_obs_w_rc<.., PC>) for the
+// LDS camera table (TB 0) and the DMA-gathered compact records (TB 3)
+bool obs_w_pc_ok(const DevProblem&, const DevWork& W) { return W.jrfree; }
 void launch_linearize(const DevProblem& P, const DevWork& W, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   // t0 / t1 (optional): start / stop of the kernel's execution, stamped by
   // hipExtLaunchKernel itself (no separate event records around the launch)
@@ -3644,79 +3238,33 @@ void launch_linearize_jr(const DevProblem& P, const DevWork& W, hipStream_t s, h
     return;
   }
   // (J-free beyond kLinLdsCams cameras, ba_linearize's read-back: the
-  // global-record kernel below evaluates the same lin tables as gtbl holds,
-  // so the records are bitwise what the J-free consumers compute)
-  if (!lin_legacy() && (!W.jrfree || jr_tab(P, W) == 2)) {
-    hipExtLaunchKernelGGL(k_linearize_rc, dim3(grid_for(P.no)), dim3(kThreads), 0, s, t0, t1, 0, P,
-                          (const double*)W.crec, (const double*)W.pts, W.JR, W.part);
-    return;
-  }
-  if (t0) (void)hipEventRecord(t0, s);
-  hipLaunchKernelGGL(k_linearize, dim3(grid_for(P.no)), dim3(kThreads), 0, s, P, W.rec, W.pts, W.JR, W.part);
-  if (t1) (void)hipEventRecord(t1, s);
-}
-// compact camera records gathered by LDS-DMA in the point-major kernels
-// beyond 200 cameras; BA_CREC_DMA=0: per-lane register gathers (read per
-// launch: tests compare both forms in one process)
-static bool crec_dma() {
-  const char* e = getenv("BA_CREC_DMA");
-  return !(e && e[0] == '0');
-}
-// k_lin_point_d (with BA_CREC_DMA; BA_LP_DMA=0 alone turns it off): C5 shard
-// 386.5 -> 331.3 us, 3183 -> 3235 M-obs/s; C4 2883 -> 2896
-// (profiles/r04_v11_ab_lp_dma.txt)
-static bool lp_dma() {
-  const char* e = getenv("BA_LP_DMA");
-  return crec_dma() && !(e && e[0] == '0');
+  // compact-record kernel forms the camera terms in the order of the J-free
+  // consumers, so the records are bitwise what they compute)
+  hipExtLaunchKernelGGL(k_linearize_rc, dim3(grid_for(P.no)), dim3(kThreads), 0, s, t0, t1, 0, P,
+                        (const double*)W.crec, (const double*)W.pts, W.JR, W.part);
 }
 void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_scale, double min_diag,
                            double max_diag, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   if (W.jrfree) {   // r, J, cost and the point blocks in one pass (J never materialised)
-    // diagnostics: BA_LP_LANES (2 / 4 / 8 lanes per point), BA_LP_LAZY=1
-    // (camera-table entries read from LDS at use), BA_LP_NT (256 / 512)
-    static int lanes = -1, lazy = -1, nt = -1;
-    // 2 lanes per point: 30.7 us at C3 vs 32.4 at 4 and 38 at 512 threads;
-    // lazy table reads 42.5 (profiles/r03_v4_ab_lin_point.txt)
-    if (lanes < 0) { const char* e = getenv("BA_LP_LANES"); lanes = e ? atoi(e) : 2; }
-    if (lazy < 0) { const char* e = getenv("BA_LP_LAZY"); lazy = e ? atoi(e) : 0; }
-    if (nt < 0) { const char* e = getenv("BA_LP_NT"); nt = e ? atoi(e) : 256; }
-    const int L = lanes == 2 || lanes == 8 ? lanes : 4;
-    const int NT = nt == 512 ? 512 : 256;
-    // two 74-KB-LDS workgroups per CU at most: a grid of that size, grid-stride
-    // over the points (no second round of table fills); the global-table
-    // variant has no table to fill: up to kMaxBlocks (its partials' slots)
-    const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
-    const int tb = jr_tab(P, W);
-    const int g = std::max(1, std::min(want, tb ? kMaxBlocks : 2 * lds_grid(1 << 30)));
-    using KF = void (*)(DevProblem, const double*, const double*, double*, double*, double*, double*, int, double,
-                        double, double*, double*);
-    KF kern;
-    if (tb) {
-      if (tb == 1)
-        kern = NT == 512 ? (L == 2 ? k_lin_point<512, 2, false, 1> : (L == 8 ? k_lin_point<512, 8, false, 1> : k_lin_point<512, 4, false, 1>))
-                         : (L == 2 ? k_lin_point<256, 2, false, 1> : (L == 8 ? k_lin_point<256, 8, false, 1> : k_lin_point<256, 4, false, 1>));
-      else if (lp_dma())   // (LDS-DMA camera records: 2 lanes per point, 256 threads)
-        kern = k_lin_point_d<256, 2>;
-      else
-        kern = NT == 512 ? (L == 2 ? k_lin_point<512, 2, false, 2> : (L == 8 ? k_lin_point<512, 8, false, 2> : k_lin_point<512, 4, false, 2>))
-                         : (L == 2 ? k_lin_point<256, 2, false, 2> : (L == 8 ? k_lin_point<256, 8, false, 2> : k_lin_point<256, 4, false, 2>));
-      const bool dma = tb == 2 && lp_dma();
-      const int nt_l = dma ? 256 : NT;
-      const int g_l = dma ? std::max(1, std::min((int)std::min<long long>(((long long)P.np * 2 + 255) / 256, 1LL << 30), kMaxBlocks)) : g;
-      hipExtLaunchKernelGGL(kern, dim3(g_l), dim3(nt_l), 0, s, t0, t1, 0, P, (const double*)(tb == 1 ? W.gtbl : W.crec),
+    // 2 lanes per point, 256 threads: 30.7 us at C3 vs 32.4 at 4 lanes and 38
+    // at 512 threads; lazy table reads 42.5 (profiles/r03_v4_ab_lin_point.txt).
+    // Two 74-KB-LDS workgroups per CU at most: a grid of that size,
+    // grid-stride over the points (no second round of table fills)
+    const int want = (int)std::min<long long>(((long long)P.np * 2 + 255) / 256, 1LL << 30);
+    if (jr_tab(P, W)) {
+      // beyond 200 cameras the compact camera records by LDS-DMA (wave-uniform
+      // point rounds): C5 shard 386.5 -> 331.3 us against per-lane register
+      // gathers, C4 2883 -> 2896 M-obs/s (profiles/r04_v11_ab_lp_dma.txt)
+      const int g = std::max(1, std::min(want, kMaxBlocks));
+      hipExtLaunchKernelGGL((k_lin_point_d<256, 2>), dim3(g), dim3(256), 0, s, t0, t1, 0, P, (const double*)W.crec,
                             (const double*)W.pts, W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag,
                             max_diag, W.part, W.pxv);
       return;
     }
-    if (NT == 256) {
-      if (lazy) kern = L == 2 ? k_lin_point<256, 2, true> : (L == 8 ? k_lin_point<256, 8, true> : k_lin_point<256, 4, true>);
-      else kern = L == 2 ? k_lin_point<256, 2> : (L == 8 ? k_lin_point<256, 8> : k_lin_point<256, 4>);
-    } else {
-      if (lazy) kern = L == 2 ? k_lin_point<512, 2, true> : (L == 8 ? k_lin_point<512, 8, true> : k_lin_point<512, 4, true>);
-      else kern = L == 2 ? k_lin_point<512, 2> : (L == 8 ? k_lin_point<512, 8> : k_lin_point<512, 4>);
-    }
-    hipExtLaunchKernelGGL(kern, dim3(g), dim3(NT), 0, s, t0, t1, 0, P, (const double*)W.rec, (const double*)W.pts,
-                          W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag, max_diag, W.part, W.pxv);
+    const int g = std::max(1, std::min(want, 2 * lds_grid(1 << 30)));
+    hipExtLaunchKernelGGL((k_lin_point<256, 2>), dim3(g), dim3(256), 0, s, t0, t1, 0, P, (const double*)W.rec,
+                          (const double*)W.pts, W.Hpp, W.gp, W.scale_p, W.diag_p, compute_scale ? 1 : 0, min_diag,
+                          max_diag, W.part, W.pxv);
     return;
   }
   const bool many = P.nc > kLinLdsCams;
@@ -3728,15 +3276,9 @@ void launch_point_assemble(const DevProblem& P, const DevWork& W, bool compute_s
 void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
   if (W.jrfree) {
-    // diagnostics: BA_CA_NT (128 / 256 / 512 threads), BA_CA_SPLIT (workgroups
-    // per camera, <= W.cam_split; > 1 adds the ordered slice fold).  One
-    // 512-thread workgroup per camera measured best: 30.6 us vs 37 / 49 us at
-    // 2 / 4 slices, 32.5 us at 256 threads x 2 (profiles/r03_v13_ab_pairs_ca.txt)
-    static int nt = -1, sp = -1;
-    if (nt < 0) { const char* e = getenv("BA_CA_NT"); nt = e ? atoi(e) : 512; }
-    if (sp < 0) { const char* e = getenv("BA_CA_SPLIT"); sp = e ? atoi(e) : 1; }
-    const int sl = std::max(1, std::min(sp, W.cam_split));
-    const dim3 g(P.nvc, sl);
+    // one 512-thread workgroup per camera: 30.6 us vs 37 / 49 us at 2 / 4
+    // slices, 32.5 us at 256 threads x 2 (profiles/r03_v13_ab_pairs_ca.txt)
+    const dim3 g(P.nvc);
     if (jr_tab(P, W) == 2) {
       // (the compact records: the camera's dual Rodrigues once per
       // workgroup).  Threads per camera by its observations (~8 per thread):
@@ -3754,42 +3296,18 @@ void launch_cam_assemble(const DevProblem& P, const DevWork& W, hipStream_t s) {
         hipLaunchKernelGGL((k_cam_assemble_rc<128, 2>), g, dim3(128), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
       else
         hipLaunchKernelGGL((k_cam_assemble_rc<64, 2>), g, dim3(64), 0, s, P, cr, (const double*)W.pxv, W.cpart, W.Hcc, W.gc);
-    } else if (nt == 128)
-      hipLaunchKernelGGL(k_cam_assemble_rc<128>, g, dim3(128), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
-                         W.cpart, W.Hcc, W.gc);
-    else if (nt == 256)
-      hipLaunchKernelGGL(k_cam_assemble_rc<256>, g, dim3(256), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
-                         W.cpart, W.Hcc, W.gc);
-    else
+    } else {
       hipLaunchKernelGGL(k_cam_assemble_rc<512>, g, dim3(512), 0, s, P, (const double*)W.rec, (const double*)W.pxv,
                          W.cpart, W.Hcc, W.gc);
-    if (sl > 1)
-      hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
-                         nullptr);
+    }
     return;
   }
   const bool many = P.nc > kLinLdsCams;   // JR layout (jr_ja)
-  // one workgroup per camera: measured faster than slicing at C3 (57 vs
-  // 66 us at 8 slices) and at C5 (where 2048 / nvc < 1 anyway);
-  // BA_ASM_SPLIT (diagnostics) overrides
-  static int split = -1;
-  if (split < 0) { const char* e = getenv("BA_ASM_SPLIT"); split = e ? atoi(e) : 0; }
-  const int sl = split > 0 ? std::min(split, kCamSplit) : 1;
-  static int nt = -1;   // diagnostics: BA_ASM_THREADS (256 / 512 / 1024)
-  if (nt < 0) { const char* e = getenv("BA_ASM_THREADS"); nt = e ? atoi(e) : 0; }
-  const int th = nt == 256 || nt == 512 || nt == 1024 ? nt : 512;   // C3: 54 us at 512, 57 at 256 / 1024
-  if (th == 1024)
-    hipLaunchKernelGGL((many ? k_cam_assemble<1024, jr_ja(true)> : k_cam_assemble<1024, jr_ja(false)>), dim3(P.nvc, sl),
-                       dim3(1024), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
-  else if (th == 512)
-    hipLaunchKernelGGL((many ? k_cam_assemble<512, jr_ja(true)> : k_cam_assemble<512, jr_ja(false)>), dim3(P.nvc, sl),
-                       dim3(512), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
-  else
-    hipLaunchKernelGGL((many ? k_cam_assemble<256, jr_ja(true)> : k_cam_assemble<256, jr_ja(false)>), dim3(P.nvc, sl),
-                       dim3(256), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
-  if (sl > 1)
-    hipLaunchKernelGGL(k_cam_fold, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart, sl, 0, W.Hcc, W.gc,
-                       nullptr);
+  // one 512-thread workgroup per camera: measured faster than slicing at C3
+  // (57 vs 66 us at 8 slices) and at C5 (where 2048 / nvc < 1 anyway); 54 us
+  // at 512 threads, 57 at 256 / 1024
+  hipLaunchKernelGGL((many ? k_cam_assemble<512, jr_ja(true)> : k_cam_assemble<512, jr_ja(false)>), dim3(P.nvc),
+                     dim3(512), 0, s, P, W.JR, W.cpart, W.Hcc, W.gc);
 }
 NormsFold norms_fold(const DevWork& W, bool compute_scale, double min_diag, double max_diag) {
   return NormsFold{W.cams, W.Hcc, W.gc, W.scale_c, W.diag_c, compute_scale ? 1 : 0, min_diag, max_diag};
@@ -3800,8 +3318,7 @@ void launch_cam_norms(const DevProblem& P, const DevWork& W, bool compute_scale,
                      W.diag_c, compute_scale ? 1 : 0, min_diag, max_diag, W.part);
 }
 void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hipStream_t s, const NormsFold* nf) {
-  const bool cm = W.wcm && W.jrfree;
-  double* prec = cm || W.jdiag ? W.prec : nullptr;
+  double* prec = W.jdiag ? W.prec : nullptr;
   if (nf) {
     const int nbp = grid_for(P.np);
     hipLaunchKernelGGL(k_point_elim_norms, dim3(nbp + grid_for(P.nvc)), dim3(kThreads), 0, s, P, W.Hpp, W.gp,
@@ -3811,75 +3328,31 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
                        radius, W.Linv, W.u, W.part, (const double*)W.pts, prec);
   }
   if (P.no == 0) return;
-  const int tb = jr_tab(P, W);
-  if (cm && P.nvc > 0) {   // the camera-major copy (the point-major W below stays: the point passes read it)
-    const dim3 g(P.nvc, W.cam_split);
-    if (tb == 2) {
-      // threads per camera slice by its observations (~8 per thread, as
-      // k_cam_assemble_rc)
-      const int per = (int)std::max<long long>(1, (long long)P.no / std::max(P.nvc * W.cam_split, 1));
-      const int t = per >= 8 * 256 ? 256 : (per >= 8 * 128 ? 128 : 64);
-      const double* cr = W.crec;
-      const double* pr = W.prec;
-      if (W.w32) {
-        if (t == 256) hipLaunchKernelGGL((k_obs_w_cam<256, float, 2>), g, dim3(256), 0, s, P, cr, pr, W.scale_c, W.Wcmf);
-        else if (t == 128) hipLaunchKernelGGL((k_obs_w_cam<128, float, 2>), g, dim3(128), 0, s, P, cr, pr, W.scale_c, W.Wcmf);
-        else hipLaunchKernelGGL((k_obs_w_cam<64, float, 2>), g, dim3(64), 0, s, P, cr, pr, W.scale_c, W.Wcmf);
-      } else {
-        if (t == 256) hipLaunchKernelGGL((k_obs_w_cam<256, double, 2>), g, dim3(256), 0, s, P, cr, pr, W.scale_c, W.Wcm);
-        else if (t == 128) hipLaunchKernelGGL((k_obs_w_cam<128, double, 2>), g, dim3(128), 0, s, P, cr, pr, W.scale_c, W.Wcm);
-        else hipLaunchKernelGGL((k_obs_w_cam<64, double, 2>), g, dim3(64), 0, s, P, cr, pr, W.scale_c, W.Wcm);
-      }
-    } else {
-      if (W.w32)
-        hipLaunchKernelGGL((k_obs_w_cam<256, float>), g, dim3(256), 0, s, P, (const double*)W.rec,
-                           (const double*)W.prec, W.scale_c, W.Wcmf);
-      else
-        hipLaunchKernelGGL((k_obs_w_cam<256, double>), g, dim3(256), 0, s, P, (const double*)W.rec,
-                           (const double*)W.prec, W.scale_c, W.Wcm);
-    }
-  }
-  if (tb) {   // global camera source: 64.5 KB of staging LDS, two workgroups per CU
-    // (BA_OBSW_WAVES=6, diagnostics, read per launch: the 6-wave form of
-    // the default DMA-gathered kernels)
-    const char* we = getenv("BA_OBSW_WAVES");
-    const bool w6 = we && atoi(we) == 6 && tb == 2 && crec_dma();
+  if (jr_tab(P, W)) {
+    // the compact camera records gathered by LDS-DMA through the W staging
+    // slot (C5 shard 707 -> 568 us against register gathers), 64.5 KB of
+    // staging LDS: two 4-wave workgroups per CU at ~230 VGPRs (C5 shard
+    // 3346-3349 vs 3315-3320 M-obs/s for one 6-wave workgroup,
+    // profiles/r04_v18_obsw_waves_ab.txt)
     constexpr int WG = kObsWRcWavesG;
-    const int wv = w6 ? kObsWRcWaves : WG;
-    const int g = std::min(2 * lds_grid(1 << 30), std::max(1, (P.no + 64 * wv - 1) / (64 * wv)));
-    const double* src = tb == 1 ? W.gtbl : W.crec;
-    // compact records by LDS-DMA (TB 3) unless BA_CREC_DMA=0
-    const bool dma = tb == 2 && crec_dma();
-    const dim3 b(64 * wv);
-    if (W.pcgc && dma) {   // (the host enables the PCG records only with the DMA gathers)
-      if (W.w32)
-        hipLaunchKernelGGL((w6 ? k_obs_w_rc<float, false, 3, true, kObsWRcWaves> : k_obs_w_rc<float, false, 3, true, WG>),
-                           dim3(g), b, 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
-      else
-        hipLaunchKernelGGL((w6 ? k_obs_w_rc<double, false, 3, true, kObsWRcWaves> : k_obs_w_rc<double, false, 3, true, WG>),
-                           dim3(g), b, 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
-    } else if (w6) {
-      if (W.w32)
-        hipLaunchKernelGGL((k_obs_w_rc<float, false, 3, false, kObsWRcWaves>), dim3(g), b, 0, s, P, src,
-                           (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
-      else if (W.wcompact)
-        hipLaunchKernelGGL((k_obs_w_rc<double, true, 3, false, kObsWRcWaves>), dim3(g), b, 0, s, P, src,
-                           (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
-      else
-        hipLaunchKernelGGL((k_obs_w_rc<double, false, 3, false, kObsWRcWaves>), dim3(g), b, 0, s, P, src,
-                           (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
-    } else if (W.w32)
-      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<float, false, 1, false, WG>
-                                  : dma ? k_obs_w_rc<float, false, 3, false, WG> : k_obs_w_rc<float, false, 2, false, WG>),
-                         dim3(g), b, 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.Wf);
+    const int g = std::min(2 * lds_grid(1 << 30), std::max(1, (P.no + 64 * WG - 1) / (64 * WG)));
+    const double* src = W.crec;
+    const dim3 b(64 * WG);
+    if (W.pcgc && W.w32)
+      hipLaunchKernelGGL((k_obs_w_rc<float, false, 3, true, WG>), dim3(g), b, 0, s, P, src, (const double*)W.pxv,
+                         W.scale_c, W.scale_p, W.Linv, W.Wf);
+    else if (W.pcgc)
+      hipLaunchKernelGGL((k_obs_w_rc<double, false, 3, true, WG>), dim3(g), b, 0, s, P, src, (const double*)W.pxv,
+                         W.scale_c, W.scale_p, W.Linv, W.W);
+    else if (W.w32)
+      hipLaunchKernelGGL((k_obs_w_rc<float, false, 3, false, WG>), dim3(g), b, 0, s, P, src, (const double*)W.pxv,
+                         W.scale_c, W.scale_p, W.Linv, W.Wf);
     else if (W.wcompact)   // (DENSE_SCHUR up to kWcCams variable cameras: the compact records)
-      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, true, 1, false, WG>
-                                  : dma ? k_obs_w_rc<double, true, 3, false, WG> : k_obs_w_rc<double, true, 2, false, WG>),
-                         dim3(g), b, 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
+      hipLaunchKernelGGL((k_obs_w_rc<double, true, 3, false, WG>), dim3(g), b, 0, s, P, src, (const double*)W.pxv,
+                         W.scale_c, W.scale_p, W.Linv, W.W);
     else
-      hipLaunchKernelGGL((tb == 1 ? k_obs_w_rc<double, false, 1, false, WG>
-                                  : dma ? k_obs_w_rc<double, false, 3, false, WG> : k_obs_w_rc<double, false, 2, false, WG>),
-                         dim3(g), b, 0, s, P, src, (const double*)W.pxv, W.scale_c, W.scale_p, W.Linv, W.W);
+      hipLaunchKernelGGL((k_obs_w_rc<double, false, 3, false, WG>), dim3(g), b, 0, s, P, src, (const double*)W.pxv,
+                         W.scale_c, W.scale_p, W.Linv, W.W);
     return;
   }
   if (W.jrfree) {   // one 148-KB-LDS workgroup per CU
@@ -3914,12 +3387,8 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
       hipLaunchKernelGGL((k_obs_w<false, double>), dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.W);
   }
 }
-// camera slices of the diagonal pass (BA_DIAG_SPLIT: diagnostics)
-int cam_split_count(const DevWork& W) {
-  static int dsplit = -1;
-  if (dsplit < 0) { const char* e = getenv("BA_DIAG_SPLIT"); dsplit = e ? atoi(e) : 0; }
-  return dsplit > 0 ? std::min(dsplit, kCamSplit) : W.cam_split;
-}
+// camera slices of the diagonal pass
+int cam_split_count(const DevWork& W) { return W.cam_split; }
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact, double radius,
                            bool skip_fold) {
   if (P.nvc == 0) return;
@@ -3943,43 +3412,16 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
       else { if (W.w32) BA_DIAG_RC(256, 0, true); else BA_DIAG_RC(256, 0, false); }
     }
 #undef BA_DIAG_RC
-  } else if (W.wcm && W.jrfree) {
-    const dim3 g(P.nvc, sl);
-    if (W.w32) {
-      if (t128) hipLaunchKernelGGL((k_cam_schur_diag<float, true, 128>), g, dim3(128), 0, s, P, W.Wcmf, W.u, W.S, W.cpart);
-      else hipLaunchKernelGGL((k_cam_schur_diag<float, true>), g, dim3(kThreads), 0, s, P, W.Wcmf, W.u, W.S, W.cpart);
-    } else {
-      if (t128) hipLaunchKernelGGL((k_cam_schur_diag<double, true, 128>), g, dim3(128), 0, s, P, W.Wcm, W.u, W.S, W.cpart);
-      else hipLaunchKernelGGL((k_cam_schur_diag<double, true>), g, dim3(kThreads), 0, s, P, W.Wcm, W.u, W.S, W.cpart);
-    }
   } else if (W.w32 && t128)
-    hipLaunchKernelGGL((k_cam_schur_diag<float, false, 128>), dim3(P.nvc, sl), dim3(128), 0, s, P, W.Wf, W.u, W.S, W.cpart);
+    hipLaunchKernelGGL((k_cam_schur_diag<float, 128>), dim3(P.nvc, sl), dim3(128), 0, s, P, W.Wf, W.u, W.S, W.cpart);
   else if (W.w32)
     hipLaunchKernelGGL(k_cam_schur_diag<float>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.Wf, W.u, W.S, W.cpart);
   else if (W.wcompact) {
-    // diagnostics: BA_DIAG_NT (64 / 128 / 256 threads), BA_DIAG_PREF (0 / 1)
-    // (the observation index alone one step ahead measured 50.7 vs 49 us,
-    // profiles/r03_v15_ab_scal_spin.txt)
-    static int nt = -1, pref = -1;
-    // 64: 49 vs 65.5 us at C3, 1355-1369 vs 1331-1338 M-obs/s
-    // (profiles/r03_v13_ab_diag_nt.txt); the one-ahead prefetch measured 52 us
-    if (nt < 0) { const char* e = getenv("BA_DIAG_NT"); nt = e ? atoi(e) : 64; }
-    if (pref < 0) { const char* e = getenv("BA_DIAG_PREF"); pref = e ? atoi(e) : 0; }
-    const dim3 g(P.nvc, sl);
-    // BA_DIAG_DMA=0: the register-gather form (read per launch: A/B in one process)
-    const char* de = getenv("BA_DIAG_DMA");
-    const bool dma = !(de && de[0] == '0');
-    if (nt == 64 && dma && !pref)
-      hipLaunchKernelGGL(k_cam_schur_diag_cd, g, dim3(64), 0, s, P, W.W, W.scale_c, W.u, W.cpart);
-    else if (nt == 64)
-      hipLaunchKernelGGL((pref ? k_cam_schur_diag_c<64, true> : k_cam_schur_diag_c<64, false>), g, dim3(64), 0, s, P,
-                         W.W, W.scale_c, W.u, W.cpart);
-    else if (nt == 128)
-      hipLaunchKernelGGL((pref ? k_cam_schur_diag_c<128, true> : k_cam_schur_diag_c<128, false>), g, dim3(128), 0, s, P,
-                         W.W, W.scale_c, W.u, W.cpart);
-    else
-      hipLaunchKernelGGL((pref ? k_cam_schur_diag_c<256, true> : k_cam_schur_diag_c<256, false>), g, dim3(256), 0, s, P,
-                         W.W, W.scale_c, W.u, W.cpart);
+    // compact records + 32-B u records gathered by LDS-DMA, two lanes each,
+    // 64-thread workgroups: 46.6 -> 37.9 us against the register gathers at
+    // C3 (profiles/r04_v8_ab_diag_dma.txt; 64 threads: 49 vs 65.5 us at 256,
+    // profiles/r03_v13_ab_diag_nt.txt)
+    hipLaunchKernelGGL(k_cam_schur_diag_cd, dim3(P.nvc, sl), dim3(64), 0, s, P, W.W, W.scale_c, W.u, W.cpart);
   }
   else
     hipLaunchKernelGGL(k_cam_schur_diag<double>, dim3(P.nvc, sl), dim3(kThreads), 0, s, P, W.W, W.u, W.S, W.cpart);
@@ -3994,35 +3436,26 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
                      W.gc, compact ? compact : W.S);
 }
 // the diagonal fold (k_cam_fold_diag) can ride in the pair pass's launch
+// (one launch fewer: C3 1517-1556 vs 1494-1512 M-obs/s,
+// profiles/r04_v14_ab_fusions_psdma.txt)
 bool pairs_take_fold(const DevProblem& P, const DevWork& W) {
-  const char* dma_env = getenv("BA_PAIRS_DMA");
-  const int dma = dma_env ? atoi(dma_env) : 1;
-  const char* fe = getenv("BA_FOLD_IN_PAIRS");
-  return W.nblocks > 0 && W.wcompact && dma && kPairsDmaLds + sizeof(WcCam) * (size_t)P.nvc <= 80 * 1024 &&
-         !(fe && fe[0] == '0');
+  return W.nblocks > 0 && W.wcompact && kPairsDmaLds + sizeof(WcCam) * (size_t)P.nvc <= 80 * 1024;
 }
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius) {
   if (W.nblocks == 0) return;
-  static int grid_cap = 0;
-  if (grid_cap == 0) {
-    const char* e = getenv("BA_PAIRS_GRID");   // diagnostics: workgroups (multiple of 8)
-    grid_cap = e ? atoi(e) : 2048;
-    if (grid_cap < 8) grid_cap = 8;
-  }
-  // 16 blocks per workgroup (4 waves of 4) over the largest XCD range
+  // 16 blocks per workgroup (4 waves of 4) over the largest XCD range, at
+  // most 2048 workgroups (256 sweeping the ranges in rounds ties it:
+  // profiles/r02_v7_ab_pairs_grid_np.txt)
   const int* xoff = W.xoff;
   int grid = 8 * ((W.xmax + 15) / 16);
   if (grid == 0) return;
-  if (grid > grid_cap) grid = grid_cap;
+  if (grid > 2048) grid = 2048;
   grid = (grid + 7) / 8 * 8;   // k_schur_pairs' XCD ranges need a multiple of 8
   // the LDS-DMA gather form while its 64 KB + the camera constants fit half
   // the LDS (two workgroups per CU): C3 159 -> 121 us, 1409-1424 -> 1487-1503
-  // M-obs/s (profiles/r04_v7_ab_pairs_dma.txt).  BA_PAIRS_DMA=0: the register
-  // form (read per launch: tests compare both forms in one process)
-  const char* dma_env = getenv("BA_PAIRS_DMA");
-  const int dma = dma_env ? atoi(dma_env) : 1;
+  // M-obs/s (profiles/r04_v7_ab_pairs_dma.txt); beyond, the register form
   const size_t ctab_bytes = sizeof(WcCam) * (size_t)P.nvc;
-  if (W.wcompact && dma && kPairsDmaLds + ctab_bytes <= 80 * 1024) {
+  if (W.wcompact && kPairsDmaLds + ctab_bytes <= 80 * 1024) {
     FoldArgs fa{W.cpart, 0, W.Hcc, W.gc, W.diag_c, fold_radius, W.scal};
     int fgrid = 0;
     if (fold_radius > 0.0) {   // the diagonal fold rides in this launch
@@ -4083,66 +3516,32 @@ void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) 
   hipLaunchKernelGGL(k_cam_candidate, dim3(P.nc < kMaxBlocks ? P.nc : kMaxBlocks), dim3(64), 0, s, P, W.cams, W.y,
                      W.scale_c, W.cams_c, W.delta_c, W.rec_c, W.part);
 }
-// back substitution + candidate in one point-major pass (diagnostics:
-// BA_PSTEP=0 runs k_backsub + k_candidate_rc instead), read once per process
-bool point_step_fused() {
-  static int fused = -1;
-  if (fused < 0) { const char* e = getenv("BA_PSTEP"); fused = e ? atoi(e) : 1; }
-  return fused != 0;
-}
+// J-free: back substitution + model cost change + candidate cost in one
+// point-major pass (k_point_step_rc; separate back substitution and
+// candidate kernels measured 1126 vs 1151 M-obs/s at C3, r03_v5_ab.txt)
 void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
-  if (const int tb = jr_tab(P, W)) {
-    // global camera source: the candidate table (value-only records + the
-    // camera step) from k_cam_candidate's records, then the same kernels as
-    // below
+  if (jr_tab(P, W)) {
+    // compact camera records: the candidate table (value-only records + the
+    // camera step) from k_cam_candidate's records first
     hipLaunchKernelGGL(k_cand_table, dim3((P.nc * kCandRec + 255) / 256), dim3(256), 0, s, P, W.rec_c, W.delta_c,
                        W.ctbl);
-    if (point_step_fused()) {
-      constexpr int NT = 512, L = 4;
-      const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
-      const int g = std::max(1, std::min(want, kMaxBlocks));
-      hipLaunchKernelGGL((tb == 1 ? k_point_step_rc<NT, L, false, 3, 1> : k_point_step_rc<NT, L, false, 3, 2>), dim3(g),
-                         dim3(NT), 0, s, P, (const double*)(tb == 1 ? W.gtbl : W.crec), (const double*)W.pts,
-                         W.delta_c, (const double*)W.ctbl, W.u, W.Linv, W.scale_p, W.pts_c, W.delta_p, W.part);
-      return;
-    }
-    if (W.w32)
-      hipLaunchKernelGGL(k_backsub<float>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c,
-                         W.delta_p, W.Wf, W.u, W.Linv, W.y, W.scale_p, W.part);
-    else
-      hipLaunchKernelGGL(k_backsub<double>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c,
-                         W.delta_p, W.W, W.u, W.Linv, W.y, W.scale_p, W.part);
-    const int g = std::max(1, std::min(kMaxBlocks, (P.no + 511) / 512));
-    hipLaunchKernelGGL((tb == 1 ? k_candidate_rc<512, 1> : k_candidate_rc<512, 2>), dim3(g), dim3(512), 0, s, P,
-                       (const double*)(tb == 1 ? W.gtbl : W.crec), (const double*)W.pts, W.delta_c, W.delta_p,
-                       (const double*)W.ctbl, W.pts_c, W.part);
+    constexpr int NT = 512, L = 4;
+    const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
+    const int g = std::max(1, std::min(want, kMaxBlocks));
+    hipLaunchKernelGGL((k_point_step_rc<NT, L, 3, 2>), dim3(g), dim3(NT), 0, s, P, (const double*)W.crec,
+                       (const double*)W.pts, W.delta_c, (const double*)W.ctbl, W.u, W.Linv, W.scale_p, W.pts_c,
+                       W.delta_p, W.part);
     return;
   }
   if (W.jrfree) {
-    // (BA_PSTEP_LAZY=1: lazy camera-table reads, diagnostics)
-    static int lazy = -1;
-    const bool fused = point_step_fused();
-    if (lazy < 0) { const char* e = getenv("BA_PSTEP_LAZY"); lazy = e ? atoi(e) : 0; }
     // (fp32 W storage too: the back substitution is exact in fp64 from J,
     // as the oracle's fp32-W mode restates it; only the matvec, the rhs and
     // the preconditioner see the fp32 blocks)
-    if (fused) {
-      constexpr int NT = 512, L = 4;
-      const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
-      const int g = std::max(1, std::min(want, lds_grid(1 << 30)));   // one 110-KB-LDS workgroup per CU
-      hipLaunchKernelGGL((lazy ? k_point_step_rc<NT, L, true> : k_point_step_rc<NT, L, false>), dim3(g), dim3(NT), 0,
-                         s, P, (const double*)W.rec, (const double*)W.pts, W.delta_c, W.rec_c, W.u, W.Linv,
-                         W.scale_p, W.pts_c, W.delta_p, W.part);
-      return;
-    }
-    if (W.w32)
-      hipLaunchKernelGGL(k_backsub<float>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c,
-                         W.delta_p, W.Wf, W.u, W.Linv, W.y, W.scale_p, W.part);
-    else
-      hipLaunchKernelGGL(k_backsub<double>, dim3(pt_group_grid(P.np)), dim3(kThreads), 0, s, P, W.pts, W.pts_c,
-                         W.delta_p, W.W, W.u, W.Linv, W.y, W.scale_p, W.part);
-    hipLaunchKernelGGL(k_candidate_rc<512>, dim3(lds_grid(P.no)), dim3(512), 0, s, P, (const double*)W.rec,
-                       (const double*)W.pts, W.delta_c, W.delta_p, W.rec_c, W.pts_c, W.part);
+    constexpr int NT = 512, L = 4;
+    const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
+    const int g = std::max(1, std::min(want, lds_grid(1 << 30)));   // one 110-KB-LDS workgroup per CU
+    hipLaunchKernelGGL((k_point_step_rc<NT, L>), dim3(g), dim3(NT), 0, s, P, (const double*)W.rec,
+                       (const double*)W.pts, W.delta_c, W.rec_c, W.u, W.Linv, W.scale_p, W.pts_c, W.delta_p, W.part);
     return;
   }
   if (W.w32)

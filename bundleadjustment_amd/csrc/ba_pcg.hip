@@ -265,9 +265,7 @@ __global__ __launch_bounds__(256) void k_pcg_point(DevProblem P, const WT* __res
 // ---------------------------------------------------------------------------
 // matvec, camera pass: slice g of camera v: sum_{o in slice} W_o v_{p(o)}
 // ---------------------------------------------------------------------------
-// CM: Wm is the camera-major copy (row i of cam_op, ba_kernels.hip
-// k_obs_w_cam), streamed; the same products in the same order
-template <typename WT, bool CM = false>
+template <typename WT>
 __global__ __launch_bounds__(256) void k_pcg_cam(DevProblem P, const WT* __restrict__ Wm,
                                                  const double* __restrict__ vpt, double* __restrict__ tpart,
                                                  const double* __restrict__ st) {
@@ -282,7 +280,7 @@ __global__ __launch_bounds__(256) void k_pcg_cam(DevProblem P, const WT* __restr
     const int2 op = P.cam_op[i];   // fixed points: W_o = 0, v_p = 0
     const int o = op.x, p = op.y;
     double wv[18];
-    load_w18(Wm, CM ? (size_t)i : (size_t)o, wv);
+    load_w18(Wm, (size_t)o, wv);
     const double u0 = vpt[3 * (size_t)p], u1 = vpt[3 * (size_t)p + 1], u2 = vpt[3 * (size_t)p + 2];
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[a] += wv[a * 3] * u0 + wv[a * 3 + 1] * u1 + wv[a * 3 + 2] * u2;
@@ -417,9 +415,6 @@ __global__ __launch_bounds__(256) void k_pcg_cam_td(DevProblem P, const double* 
 // from the run's last lane) and forms t_o = W_o v_p, stored as contiguous
 // wave stores.  (k_pcg_point_t's value-pair loop issued ~4 loads per 8-16 B
 // of W and re-read every record for t_o: 3.4 TB/s at C4.)
-// SCAT (with TOUT): t_o is stored at its camera-order position cam_pos[o]
-// instead (one 48-B scattered store per observation), so that the camera
-// pass streams the products (k_pcg_cam_s) instead of gathering them.
 // PC: the 16-value rank-2 records of k_obs_w_rc<.., PC> (W_o = c^T Z: c's
 // scaled rotation columns, its four nonzero translation entries, Z):
 // W_o^T x = Z^T (c x), W_o v = c^T (Z v).  A record is 8 units (8 units of
@@ -427,11 +422,10 @@ __global__ __launch_bounds__(256) void k_pcg_cam_td(DevProblem P, const double* 
 // would conflict, so the units of record r sit XOR-swizzled in the slot
 // (unit k at k ^ ((r >> SH) & 7), SH = 1 fp64 / 2 fp32: the records of one
 // LDS row pass then cover distinct banks).
-template <typename WT, bool TOUT, bool SCAT = false, bool PC = false>
+template <typename WT, bool TOUT, bool PC = false>
 __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2* __restrict__ chunks, int nchunks,
                                                        const WT* __restrict__ Wm, const double* __restrict__ xv,
                                                        double* __restrict__ vpt, double* __restrict__ tobs,
-                                                       const int* __restrict__ cam_pos,
                                                        const double* __restrict__ st) {
   static_assert(!PC || TOUT, "rank-2 records: the products");
   if (st[PS_DONE] != 0.0) return;
@@ -550,27 +544,7 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
 #pragma unroll
       for (int k = 0; k < 3; ++k) vpt[3 * (size_t)pt + k] = v[k];
     }
-    if constexpr (TOUT && SCAT) {
-      double vp[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) vp[k] = __shfl(v[k], last, 64);
-      const int q = live ? cam_pos[o] : -1;   // (-1: a fixed camera, no camera-side entry)
-      if (q >= 0) {
-        double2* d = reinterpret_cast<double2*>(tobs + 6 * (size_t)q);
-        if constexpr (PC) {   // q = Z v_p, t_o = c^T q (as the point-order form)
-          const double q0 = wr[10] * vp[0] + wr[11] * vp[1] + wr[12] * vp[2];
-          const double q1 = wr[13] * vp[0] + wr[14] * vp[1] + wr[15] * vp[2];
-          d[0] = make_double2(wr[0] * q0 + wr[3] * q1, wr[1] * q0 + wr[4] * q1);
-          d[1] = make_double2(wr[2] * q0 + wr[5] * q1, wr[6] * q0);
-          d[2] = make_double2(wr[8] * q1, wr[7] * q0 + wr[9] * q1);
-        } else {
-#pragma unroll
-          for (int a = 0; a < 6; a += 2)
-            d[a / 2] = make_double2(wr[a * 3] * vp[0] + wr[a * 3 + 1] * vp[1] + wr[a * 3 + 2] * vp[2],
-                                    wr[a * 3 + 3] * vp[0] + wr[a * 3 + 4] * vp[1] + wr[a * 3 + 5] * vp[2]);
-        }
-      }
-    } else if constexpr (TOUT) {
+    if constexpr (TOUT) {
       double vp[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) vp[k] = __shfl(v[k], last, 64);
@@ -602,31 +576,6 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
       }
     }
     wave_lds_sync_pcg();   // (the slots are rewritten by the next chunk)
-  }
-}
-
-// camera pass over products stored in camera order (k_pcg_point_seg<.., SCAT>):
-// the same sums as k_pcg_cam_t in the same order, the reads contiguous
-__global__ __launch_bounds__(256) void k_pcg_cam_s(DevProblem P, const double* __restrict__ tcm,
-                                                   double* __restrict__ tpart, const double* __restrict__ st) {
-  if (st[PS_DONE] != 0.0) return;
-  __shared__ double lds[6 * 16];
-  const int v = blockIdx.x, g = blockIdx.y, G = gridDim.y;
-  const int a0 = P.cam_off[v], a1 = P.cam_off[v + 1];
-  const int len = (a1 - a0 + G - 1) / G;
-  const int i0 = min(a1, a0 + g * len), i1 = min(a1, i0 + len);
-  double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const double2* t = reinterpret_cast<const double2*>(tcm + 6 * (size_t)i);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { const double2 x = t[k]; acc[2 * k] += x.x; acc[2 * k + 1] += x.y; }
-  }
-  double tot[6];
-  block_sum<6>(acc, lds, tot);
-  if (threadIdx.x == 0) {
-    double* dst = tpart + ((size_t)g * P.nvc + v) * 6;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) dst[a] = tot[a];
   }
 }
 
@@ -912,59 +861,31 @@ void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec,
   const double* st = W.scal + kNumSlots;
   if (W.npchunks > 0) {   // point-aligned chunks of <= 64 observations (k_pcg_point_seg)
     const int g = std::max(1, std::min((W.npchunks + 3) / 4, 16384));
-    if (W.tobs && W.tscat) {   // products scattered to camera order, streamed by the camera pass
-      if (W.pcgc && W.w32)
-        hipLaunchKernelGGL((k_pcg_point_seg<float, true, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks,
-                           W.npchunks, W.Wf, vec, W.vpt, W.tobs, W.cam_pos, st);
-      else if (W.pcgc)
-        hipLaunchKernelGGL((k_pcg_point_seg<double, true, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks,
-                           W.npchunks, W.W, vec, W.vpt, W.tobs, W.cam_pos, st);
-      else if (W.w32)
-        hipLaunchKernelGGL((k_pcg_point_seg<float, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks,
-                           W.Wf, vec, W.vpt, W.tobs, W.cam_pos, st);
-      else
-        hipLaunchKernelGGL((k_pcg_point_seg<double, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks,
-                           W.W, vec, W.vpt, W.tobs, W.cam_pos, st);
-      hipLaunchKernelGGL(k_pcg_cam_s, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
-      return;
-    }
     if (W.tobs) {
       if (W.pcgc && W.w32)   // (the 16-value rank-2 records)
-        hipLaunchKernelGGL((k_pcg_point_seg<float, true, false, true>), dim3(g), dim3(256), 0, s, P, W.pchunks,
-                           W.npchunks, W.Wf, vec, W.vpt, W.tobs, nullptr, st);
+        hipLaunchKernelGGL((k_pcg_point_seg<float, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks,
+                           W.Wf, vec, W.vpt, W.tobs, st);
       else if (W.pcgc)
-        hipLaunchKernelGGL((k_pcg_point_seg<double, true, false, true>), dim3(g), dim3(256), 0, s, P, W.pchunks,
-                           W.npchunks, W.W, vec, W.vpt, W.tobs, nullptr, st);
+        hipLaunchKernelGGL((k_pcg_point_seg<double, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks,
+                           W.W, vec, W.vpt, W.tobs, st);
       else if (W.w32)
         hipLaunchKernelGGL((k_pcg_point_seg<float, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks, W.Wf,
-                           vec, W.vpt, W.tobs, nullptr, st);
+                           vec, W.vpt, W.tobs, st);
       else
         hipLaunchKernelGGL((k_pcg_point_seg<double, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks, W.W,
-                           vec, W.vpt, W.tobs, nullptr, st);
-      // BA_CAMT_DMA=0: the register-gather camera pass (read per launch)
-      const char* ce = getenv("BA_CAMT_DMA");
-      if (ce && ce[0] == '0')
-        hipLaunchKernelGGL(k_pcg_cam_t, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
-      else
-        hipLaunchKernelGGL(k_pcg_cam_td, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
+                           vec, W.vpt, W.tobs, st);
+      // the products gathered into LDS by LDS-DMA: 152 -> 149 us at C4
+      hipLaunchKernelGGL(k_pcg_cam_td, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
       return;
     }
-    const bool cm = W.wcm && W.jrfree;
     if (W.w32) {
       hipLaunchKernelGGL((k_pcg_point_seg<float, false>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks, W.Wf,
-                         vec, W.vpt, nullptr, nullptr, st);
-      if (cm)
-        hipLaunchKernelGGL((k_pcg_cam<float, true>), dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wcmf, W.vpt, W.tpart, st);
-      else
-        hipLaunchKernelGGL(k_pcg_cam<float>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wf, W.vpt, W.tpart, st);
+                         vec, W.vpt, nullptr, st);
+      hipLaunchKernelGGL(k_pcg_cam<float>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wf, W.vpt, W.tpart, st);
     } else {
       hipLaunchKernelGGL((k_pcg_point_seg<double, false>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks, W.W,
-                         vec, W.vpt, nullptr, nullptr, st);
-      if (cm)
-        hipLaunchKernelGGL((k_pcg_cam<double, true>), dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wcm, W.vpt, W.tpart,
-                           st);
-      else
-        hipLaunchKernelGGL(k_pcg_cam<double>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.W, W.vpt, W.tpart, st);
+                         vec, W.vpt, nullptr, st);
+      hipLaunchKernelGGL(k_pcg_cam<double>, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.W, W.vpt, W.tpart, st);
     }
     return;
   }
@@ -974,18 +895,6 @@ void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec,
     else
       hipLaunchKernelGGL(k_pcg_point_t<double>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.W, vec, W.tobs, st);
     hipLaunchKernelGGL(k_pcg_cam_t, dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.tobs, W.tpart, st);
-    return;
-  }
-  if (W.wcm && W.jrfree) {   // camera pass over the camera-major copy
-    if (W.w32) {
-      hipLaunchKernelGGL(k_pcg_point<float>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.Wf, vec, W.vpt, st);
-      hipLaunchKernelGGL((k_pcg_cam<float, true>), dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wcmf, W.vpt, W.tpart,
-                         st);
-    } else {
-      hipLaunchKernelGGL(k_pcg_point<double>, dim3(pt_group_grid(P.np)), dim3(256), 0, s, P, W.W, vec, W.vpt, st);
-      hipLaunchKernelGGL((k_pcg_cam<double, true>), dim3(P.nvc, W.pcg_G), dim3(256), 0, s, P, W.Wcm, W.vpt, W.tpart,
-                         st);
-    }
     return;
   }
   if (W.w32) {

@@ -130,7 +130,6 @@ struct ba_ctx {
   size_t pcg_ndup = 0;     // ITERATIVE_SCHUR duplicate (camera, point) pairs (ensure_pcg)
   double* tobs_buf = nullptr;   // [no][6] ITERATIVE_SCHUR per-observation products (allocated on first use)
   int max_no = 0;               // largest observation count over the ranks (collective matvec-path choice)
-  int ncamobs = 0;              // observations of variable cameras (the cam_op list)
 
   // solver state
   std::vector<ba_iteration> log;
@@ -243,9 +242,7 @@ struct ba_ctx {
     }
     // scalars still to be folded (pend_*: the step's and the deferred
     // linearisation's, single rank): one launch folds and publishes them
-    // (BA_REDUCE_PUB=0: a separate fold launch before the publish, A/B)
-    static const bool fused = [] { const char* e = std::getenv("BA_REDUCE_PUB"); return !(e && e[0] == '0'); }();
-    if ((pend_sum | pend_max) && d_ticket && fused) {
+    if ((pend_sum | pend_max) && d_ticket) {
       bahip::launch_reduce_publish(W, pend_sum, pend_max, d_hscal, (int)cnt, d_hseq, ++scal_seq, d_ticket, stream);
       pend_sum = pend_max = 0;
     } else {
@@ -358,7 +355,6 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   for (int s = 0; s < no; ++s) if (vc[obs_cam[s]] >= 0) cam_off[vc[obs_cam[s]] + 1]++;
   for (int v = 0; v < nvc; ++v) cam_off[v + 1] += cam_off[v];
   std::vector<int> cam_obs(cam_off[nvc]);
-  ctx->ncamobs = cam_off[nvc];
   {
     std::vector<int> fill(cam_off.begin(), cam_off.end() - 1);
     for (int s = 0; s < no; ++s) if (vc[obs_cam[s]] >= 0) cam_obs[fill[vc[obs_cam[s]]]++] = s;
@@ -415,21 +411,14 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   W.crec = ctx->dalloc<double>((size_t)16 * nc);
   W.ctbl = ctx->dalloc<double>((size_t)22 * nc);
   // J-free iteration: r and J are recomputed by every consumer and never
-  // stored (camera tables in LDS up to 200 cameras, the L2-resident global
-  // table gtbl beyond); BA_JR=1 forces the JR-materialising kernels (A/B,
+  // stored (camera tables in LDS up to 200 cameras, the compact 128-B camera
+  // records beyond: each observation forms its camera's dual Rodrigues from
+  // them); BA_JR=1 forces the JR-materialising kernels (A/B,
   // diagnostics).  JR is then allocated only for ba_linearize's read-back.
   {
     const char* e = std::getenv("BA_JR");
     W.jrfree = nc > 0 && !(e && e[0] == '1');
   }
-  {
-    // beyond 200 cameras the J-free kernels gather the camera per
-    // observation: the compact 128-B records (2, default; the dual Rodrigues
-    // per observation) or the 384-B lin-table rows (1, BA_JTAB=1)
-    const char* e = std::getenv("BA_JTAB");
-    W.jtab = e && atoi(e) == 1 ? 1 : 2;
-  }
-  W.gtbl = W.jrfree && nc > bahip::kLinLdsCamsHost && W.jtab == 1 ? ctx->dalloc<double>((size_t)48 * nc) : nullptr;
   W.JR = W.jrfree ? nullptr : ctx->dalloc<double>((size_t)(bahip::jr_ja_host(nc) + 8) * no);   // JA [no][jr_ja] + JB [no][8] (ba_kernels.hip)
   W.delta_p = ctx->dalloc<double>(3 * (size_t)np);
   W.pxv = ctx->dalloc<double>(4 * (size_t)np);
@@ -646,18 +635,6 @@ void ensure_pcg(ba_ctx* ctx) {
     W.npchunks = ok ? (int)ch.size() : 0;
     W.pchunks = ok && !ch.empty() ? ctx->upload(ch) : nullptr;
     if (!W.pchunks) W.npchunks = 0;
-    // camera-order positions for the scattered products
-    std::vector<int> pos(std::max(ctx->no, 1), -1);
-    {
-      std::vector<int> fill(nvc + 1, 0);
-      // (cam_op is the observations of each variable camera in increasing
-      // sorted index: rebuild the same order)
-      std::vector<int> cnt(nvc + 1, 0);
-      for (int o = 0; o < ctx->no; ++o) { const int v = ctx->h_vc[ctx->h_obs_cam[o]]; if (v >= 0) cnt[v + 1]++; }
-      for (int v = 0; v < nvc; ++v) cnt[v + 1] += cnt[v];
-      for (int o = 0; o < ctx->no; ++o) { const int v = ctx->h_vc[ctx->h_obs_cam[o]]; if (v >= 0) pos[o] = cnt[v]++; }
-    }
-    W.cam_pos = ctx->upload(pos);
   }
   HIP_OK(hipStreamSynchronize(ctx->stream));
   ctx->have_pcg = true;
@@ -806,18 +783,10 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
     const int force = fe ? atoi(fe) : -1;
     // (decided from the largest rank's shard: every rank runs the same path)
     const bool big = 144.0 * (double)ctx->max_no > 256.0 * 1024 * 1024;
-    const bool use_t = !W.wcm && (force >= 0 ? force != 0 : W.npchunks > 0 || (big && !W.w32));
+    const bool use_t = force >= 0 ? force != 0 : W.npchunks > 0 || (big && !W.w32);
     if (use_t && !ctx->tobs_buf) ctx->tobs_buf = ctx->dalloc<double>(6 * (size_t)std::max(ctx->no, 1));
     if (!use_t && ctx->tobs_buf) { ctx->dfree(ctx->tobs_buf); ctx->tobs_buf = nullptr; }   // 48 B/obs back
     W.tobs = use_t ? ctx->tobs_buf : nullptr;
-    // the products in camera order (streamed camera pass, BA_TSCAT=1): off
-    // by default.  fp32 W: the 48-B scattered stores cost more than the
-    // gathers they save (C5 shard 4.41 vs 4.20 ms,
-    // profiles/r04_v4_jdiag_tscat_ab.txt); fp64 W: within the spread between
-    // boxes (C4 3.53 vs 3.56 ms on one box, 3.76 vs 3.60 ms on another,
-    // profiles/r04_v6_tscat_ab.txt)
-    const char* se = getenv("BA_TSCAT");
-    W.tscat = use_t && W.npchunks > 0 && se && atoi(se) != 0;
   }
   PcgOpts po{o.eta, o.min_linear_solver_iterations, std::max(1, o.max_linear_solver_iterations),
              o.preconditioner_type == BA_SCHUR_JACOBI ? 1 : 0};
@@ -874,42 +843,28 @@ void step_w_storage(ba_ctx* ctx, const ba_options& o) {
     // BA_WCOMPACT=0 (diagnostics, read per solve) keeps the 18-double blocks
     const char* e = getenv("BA_WCOMPACT");
     W.wcompact = W.jrfree && ctx->nvc <= bahip::kWcCamsHost && !W.w32 && o.linear_solver == BA_DENSE_SCHUR &&
-                 !(e && e[0] == '0') && point_step_fused();
+                 !(e && e[0] == '0');
   }
   {
-    // ITERATIVE_SCHUR, J-free: a camera-major copy of W written beside the
-    // point-major one (k_obs_w_cam), streamed by the diagonal Schur blocks and
-    // by every CG iteration's camera pass.  Measured: the extra pass costs
-    // what the streamed camera passes save (C4 3.84 vs 4.51 ms, C5 shard
-    // 5.08 vs 5.17 ms without / with it: profiles/r04_v2_*), so off unless
-    // BA_WCM=1 (read per solve)
-    const char* e = getenv("BA_WCM");
-    const int force = e ? atoi(e) : -1;
-    W.wcm = W.jrfree && o.linear_solver == BA_ITERATIVE_SCHUR && (force >= 0 ? force != 0 : false);
     // the diagonal Schur blocks J-free (k_cam_schur_diag_rc) where they would
     // gather the 18-value W (ITERATIVE_SCHUR, or DENSE_SCHUR without compact
-    // records); BA_JDIAG=0 (read per solve) gathers W
-    const char* de = getenv("BA_JDIAG");
-    W.jdiag = W.jrfree && !W.wcm && !W.wcompact && !(de && de[0] == '0');
-    if ((W.wcm || W.jdiag) && !W.prec) W.prec = ctx->dalloc<double>(16 * (size_t)std::max(ctx->np, 1));
+    // records): C4 3.53 vs 3.74 ms with the W-reading pass
+    // (profiles/r04_v4_jdiag_tscat_ab.txt)
+    W.jdiag = W.jrfree && !W.wcompact;
+    if (W.jdiag && !W.prec) W.prec = ctx->dalloc<double>(16 * (size_t)std::max(ctx->np, 1));
     // the PCG point pass over the 16-value rank-2 records (k_obs_w_rc<.., PC>:
     // 128 B per observation fp64, 64 B fp32): only where nothing else reads
-    // W — the diagonal blocks J-free, the fused point step, the products t_o
-    // (point order, or scattered to camera order with BA_TSCAT=1), no
-    // duplicate (camera, point) pairs, every point in the point-aligned
+    // W — the diagonal blocks J-free, the fused point step, the products t_o,
+    // no duplicate (camera, point) pairs, every point in the point-aligned
     // chunks — and K without skew.  BA_PCG_PC=0
     // (read per solve) keeps the 18-value records
     W.pcgc = false;
     const char* pe = getenv("BA_PCG_PC");
     const char* te = getenv("BA_PCG_T");
     if (!(pe && pe[0] == '0') && o.linear_solver == BA_ITERATIVE_SCHUR && W.jdiag && ctx->k_plain &&
-        point_step_fused() && obs_w_pc_ok(ctx->P, W) && !(te && te[0] == '0')) {
+        obs_w_pc_ok(ctx->P, W) && !(te && te[0] == '0')) {
       ensure_pcg(ctx);
       W.pcgc = W.npchunks > 0 && ctx->pcg_ndup == 0;
-    }
-    if (W.wcm) {
-      if (W.w32 && !W.Wcmf) W.Wcmf = ctx->dalloc<float>(18 * (size_t)std::max(ctx->ncamobs, 1));
-      if (!W.w32 && !W.Wcm) W.Wcm = ctx->dalloc<double>(18 * (size_t)std::max(ctx->ncamobs, 1));
     }
   }
 }

@@ -683,7 +683,7 @@ struct Options {
   int preconditioner_type;            // 0 JACOBI (ceres default), 1 SCHUR_JACOBI
   int max_linear_solver_iterations;   // 500
   int min_linear_solver_iterations;   // 0
-  int precision;                      // 0 fp64; 1 MIXED_FP32: the Schur blocks W stored in float
+  int precision;                      // 0 fp64; 1 MIXED_FP32: the Schur blocks W stored in float; 3: c, Z of W = c'Z in float (matvec)
                                       // (iterative_schur_solve_w below); 2 the W form in fp64 (test hook)
   double eta;                         // 1e-1 (LM forcing sequence -> CG q_tolerance)
 };
@@ -1004,6 +1004,11 @@ static bool iterative_schur_solve(const Problem& P, const Schur& S, const std::v
 // substitution uses the unrounded W_o (the device recomputes it from J in
 // fp64: k_point_step_rc); all sums, the CG vectors and everything else stay
 // fp64.
+// precision 3 (MIXED_FP32 with the rank-2 records of the PCG point pass,
+// include/ba_hip.h BA_MIXED_FP32): W_o = c_o' Z_o with c_o = F_o (scaled,
+// 2x6) and Z_o = E_o L_p^-T (2x3); the matvec uses c_o and Z_o each rounded
+// to float, associated as W_o' x = Z_o' (c_o x) and W_o v = c_o' (Z_o v);
+// the rhs and the SCHUR_JACOBI blocks use the rounded W_o entries (mode 1).
 // The CG (termination rules, preconditioner inversion) is the one above.
 // ----------------------------------------------------------------------------
 static bool iterative_schur_solve_w(const Problem& P, const Schur& S, const std::vector<Lin>& L,
@@ -1012,7 +1017,8 @@ static bool iterative_schur_solve_w(const Problem& P, const Schur& S, const std:
   const int nf = S.nf, n = 6 * nf, npv = (int)P.var_pts.size();
   y.assign(P.ncols, 0.0);
   *cg_iterations = 0;
-  auto rnd = [&](double v) { return opt.precision == 1 ? (double)(float)v : v; };
+  auto rnd = [&](double v) { return opt.precision == 1 || opt.precision == 3 ? (double)(float)v : v; };
+  const bool rank2 = opt.precision == 3;
   auto scJc = [&](int o, double* Jc) {
     const int cc = P.cam_col[P.obs_cam[o]];
     for (int i = 0; i < 2; ++i) for (int k = 0; k < 6; ++k) Jc[i * 6 + k] = L[o].Jc[i * 6 + k] * s[cc + k];
@@ -1057,6 +1063,8 @@ static bool iterative_schur_solve_w(const Problem& P, const Schur& S, const std:
   }
   // W_o (stored rounded) for residuals with a variable camera and point
   std::vector<double> W((size_t)P.no * 18, 0.0), W64((size_t)P.no * 18, 0.0);   // (W64: unrounded)
+  // precision 3: the float-rounded factors c_o (2x6) and Z_o (2x3)
+  std::vector<double> Cr(rank2 ? (size_t)P.no * 12 : 0, 0.0), Zr(rank2 ? (size_t)P.no * 6 : 0, 0.0);
   for (int o = 0; o < P.no; ++o) {
     if (P.type[o] != RB_ANGLE) continue;
     const int ip = vp[P.obs_pt[o]];
@@ -1064,6 +1072,13 @@ static bool iterative_schur_solve_w(const Problem& P, const Schur& S, const std:
     scJc(o, Jc);
     scJp(o, Jp);
     const double* M = &Linv[(size_t)ip * 9];
+    if (rank2) {
+      for (int k = 0; k < 12; ++k) Cr[(size_t)o * 12 + k] = (double)(float)Jc[k];
+      for (int i = 0; i < 2; ++i)
+        for (int k = 0; k < 3; ++k)   // (Jp_i L^-T)_k = sum_t Jp_it M[k][t]
+          Zr[(size_t)o * 6 + i * 3 + k] =
+              (double)(float)(Jp[i * 3] * M[k * 3] + Jp[i * 3 + 1] * M[k * 3 + 1] + Jp[i * 3 + 2] * M[k * 3 + 2]);
+    }
     for (int a = 0; a < 6; ++a) {
       const double e[3] = {Jc[a] * Jp[0] + Jc[6 + a] * Jp[3], Jc[a] * Jp[1] + Jc[6 + a] * Jp[4],
                            Jc[a] * Jp[2] + Jc[6 + a] * Jp[5]};
@@ -1102,9 +1117,18 @@ static bool iterative_schur_solve_w(const Problem& P, const Schur& S, const std:
     std::vector<double> v((size_t)npv * 3, 0.0);
     for (int o = 0; o < P.no; ++o) {
       if (P.type[o] != RB_ANGLE) continue;
-      const double* w = &W[(size_t)o * 18];
       const double* xc = &x[6 * S.fidx[P.obs_cam[o]]];
       double* vv = &v[(size_t)vp[P.obs_pt[o]] * 3];
+      if (rank2) {   // Z' (c x)
+        const double* c = &Cr[(size_t)o * 12];
+        const double* z = &Zr[(size_t)o * 6];
+        double y[2] = {0.0, 0.0};
+        for (int i = 0; i < 2; ++i)
+          for (int a = 0; a < 6; ++a) y[i] += c[i * 6 + a] * xc[a];
+        for (int k = 0; k < 3; ++k) vv[k] += z[k] * y[0] + z[3 + k] * y[1];
+        continue;
+      }
+      const double* w = &W[(size_t)o * 18];
       for (int k = 0; k < 3; ++k)
         for (int a = 0; a < 6; ++a) vv[k] += w[a * 3 + k] * xc[a];
     }
@@ -1117,9 +1141,17 @@ static bool iterative_schur_solve_w(const Problem& P, const Schur& S, const std:
       }
     for (int o = 0; o < P.no; ++o) {
       if (P.type[o] != RB_ANGLE) continue;
-      const double* w = &W[(size_t)o * 18];
       const double* vv = &v[(size_t)vp[P.obs_pt[o]] * 3];
       double* oc = &out[6 * S.fidx[P.obs_cam[o]]];
+      if (rank2) {   // c' (Z v)
+        const double* c = &Cr[(size_t)o * 12];
+        const double* z = &Zr[(size_t)o * 6];
+        const double q0 = z[0] * vv[0] + z[1] * vv[1] + z[2] * vv[2];
+        const double q1 = z[3] * vv[0] + z[4] * vv[1] + z[5] * vv[2];
+        for (int a = 0; a < 6; ++a) oc[a] -= c[a] * q0 + c[6 + a] * q1;
+        continue;
+      }
+      const double* w = &W[(size_t)o * 18];
       for (int a = 0; a < 6; ++a) oc[a] -= w[a * 3] * vv[0] + w[a * 3 + 1] * vv[1] + w[a * 3 + 2] * vv[2];
     }
   };
@@ -1180,8 +1212,9 @@ static bool linear_solve(const Problem& P, const Schur& S, const std::vector<Lin
   *ls_iters = 1;
   if (opt.linear_solver == LS_ITERATIVE_SCHUR) {
     // precision 1: MIXED_FP32 (W in float); 2: the same W form in fp64 (test
-    // hook: checks the W-form restatement against the F/E form above)
-    if (opt.precision == 1 || opt.precision == 2) return iterative_schur_solve_w(P, S, L, s, D, opt, y, ls_iters);
+    // hook: checks the W-form restatement against the F/E form above); 3:
+    // MIXED_FP32 with the rank-2 records (c, Z in float) in the matvec
+    if (opt.precision >= 1 && opt.precision <= 3) return iterative_schur_solve_w(P, S, L, s, D, opt, y, ls_iters);
     return iterative_schur_solve(P, S, L, s, D, opt, y, ls_iters);
   }
   return dense_schur_solve(P, S, L, s, D, y);

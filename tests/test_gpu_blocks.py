@@ -85,26 +85,3 @@ def test_jfree_blocks_and_reduced_system_match_oracle(oracle_lib, cfg, scale):
     assert np.allclose(got["S"][d, d], lhs[d, d], rtol=1e-11, atol=0), "S diagonal"
     close_to_scale(got["rhs"], rhs, 1e-10, "rhs")
 
-
-@pytest.mark.timeout(600)
-@pytest.mark.parametrize("switch,cfg", [("BA_PAIRS_DMA", "c3"), ("BA_DIAG_DMA", "c3"), ("BA_CREC_DMA", "c4"),
-                                        ("BA_FOLD_IN_PAIRS", "c3")])
-def test_dma_gathers_are_bitwise_the_register_gathers(monkeypatch, switch, cfg):
-    """k_schur_pairs_cd / k_cam_schur_diag_cd (compact records gathered into
-    LDS by LDS-DMA, the defaults) form the same products in the same order as
-    k_schur_pairs_c / k_cam_schur_diag_c (register gathers, switch=0): S and
-    the rhs must agree bitwise (C3 camera count: the LDS form's size limit).
-    BA_CREC_DMA: the compact W records of the C4 shard from camera records
-    gathered by LDS-DMA (k_obs_w_rc TB 3) or per lane (TB 2).
-    BA_FOLD_IN_PAIRS: the diagonal fold as extra workgroups of the pair
-    pass's launch or as a launch of its own."""
-    p = make_config(cfg, scale=0.2 if cfg == "c3" else 0.02)
-    out = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv(switch, mode)
-        with Solver(0) as s:
-            s.set_problem(p)
-            out[mode] = s.debug_blocks(1e4)
-    assert np.array_equal(out["0"]["S"], out["1"]["S"])
-    assert np.array_equal(out["0"]["rhs"], out["1"]["rhs"])
-

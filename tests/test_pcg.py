@@ -93,10 +93,11 @@ def test_oracle_w_form_and_mixed_precision(oracle_lib, pc):
     """precision 2 (oracle test hook): the per-observation W-block form of the
     implicit reduced system, the form MIXED_FP32 rounds, restates Ceres' F/E
     form — identical CG counts, costs to 1e-12.  precision 1 (MIXED_FP32, W
-    rounded to fp32): final cost within 1e-6 of fp64."""
+    rounded to fp32) and 3 (MIXED_FP32 with W = c'Z, c and Z rounded to fp32
+    in the matvec): final cost within 1e-6 of fp64."""
     p = gauge_fixed("c2", 0.5)
     runs = {}
-    for prec in (0, 2, 1):
+    for prec in (0, 2, 1, 3):
         _, _, s, log = oracle_lib.solve(p, oracle_opts(oracle_lib, pc, max_num_iterations=12, precision=prec))
         runs[prec] = (s, log)
     s0, l0 = runs[0]
@@ -104,10 +105,12 @@ def test_oracle_w_form_and_mixed_precision(oracle_lib, pc):
     assert [r["linear_solver_iterations"] for r in l2] == [r["linear_solver_iterations"] for r in l0]
     for a, b in zip(l2, l0):
         assert a["cost"] == pytest.approx(b["cost"], rel=1e-12)
-    s1, l1 = runs[1]
-    assert s1["termination_type"] != "FAILURE"
-    assert s1["final_cost"] == pytest.approx(s0["final_cost"], rel=1e-6)
-    assert s1["final_cost"] != s0["final_cost"]   # the rounding is really applied
+    for prec in (1, 3):
+        s1, l1 = runs[prec]
+        assert s1["termination_type"] != "FAILURE"
+        assert s1["final_cost"] == pytest.approx(s0["final_cost"], rel=1e-6)
+        assert s1["final_cost"] != s0["final_cost"]   # the rounding is really applied
+    assert runs[3][0]["final_cost"] != runs[1][0]["final_cost"]   # another rounding
 
 
 # ---------------------------------------------------------------------------
@@ -140,70 +143,26 @@ def compare(glog, olog, n, rtol=1e-9):
 
 
 # matvec forms of the implicit Schur complement: "auto" the solver's choice
-# by size; "gather" the point-major W gathered in camera order (BA_PCG_T=0);
-# "t" the per-observation products t_o = W_o v_p scattered to camera order
-# and streamed by the camera pass (BA_PCG_T=1, BA_TSCAT=1); "t_gather" the
-# products in point order, gathered into LDS by LDS-DMA (BA_TSCAT=0, the
-# default); "t_gather_reg" the same with register gathers (BA_CAMT_DMA=0);
-# "pairs" the value-pair point passes k_pcg_point / k_pcg_point_t instead of
-# the point-aligned chunks (BA_PCG_SEG=0, BA_PCG_T=1); "wcm" the camera-major
-# copy of W (k_obs_w_cam, BA_WCM=1: the camera passes stream it); "w18" the
-# point-aligned chunks over the 18-value W records instead of the 16-value
-# rank-2 ones the default picks (BA_PCG_PC=0)
-MATVECS = ["auto", "gather", "t", "t_gather", "t_gather_reg", "pairs", "wcm", "w18"]
+# by size (point-aligned chunks over the 16-value rank-2 records W_o = c'Z
+# with the per-observation products t_o = W_o v_p); "gather" the point-major
+# 18-value W gathered in camera order (BA_PCG_T=0); "t_gather" the products
+# forced on (BA_PCG_T=1); "pairs" the value-pair point passes k_pcg_point /
+# k_pcg_point_t instead of the point-aligned chunks (BA_PCG_SEG=0,
+# BA_PCG_T=1); "w18" the point-aligned chunks over the 18-value W records
+# (BA_PCG_PC=0)
+MATVECS = ["auto", "gather", "t_gather", "pairs", "w18"]
+# the matvec forms that run on the rank-2 records (oracle precision 3 with
+# fp32 W; the others round the 18 W entries: precision 1)
+RANK2 = {"auto", "t_gather"}
 
 
 def set_matvec(monkeypatch, mode):
-    if mode == "wcm":
-        monkeypatch.setenv("BA_WCM", "1")
-    elif mode == "w18":
+    if mode == "w18":
         monkeypatch.setenv("BA_PCG_PC", "0")
     elif mode != "auto":
-        monkeypatch.setenv("BA_WCM", "0")
         monkeypatch.setenv("BA_PCG_T", "0" if mode == "gather" else "1")
-        monkeypatch.setenv("BA_TSCAT", "1" if mode == "t" else "0")
-        if mode == "t_gather_reg":
-            monkeypatch.setenv("BA_CAMT_DMA", "0")
         if mode == "pairs":
             monkeypatch.setenv("BA_PCG_SEG", "0")
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
-@pytest.mark.parametrize("switch,on,off", [("BA_CREC_DMA", "1", "0"), ("BA_LP_DMA", "1", "0")])
-def test_gpu_camera_record_dma_is_bitwise_the_register_gather(solver, precision, switch, on, off, monkeypatch):
-    """The point-major kernels beyond 200 cameras with the compact camera
-    records gathered by LDS-DMA (k_obs_w_rc TB 3: BA_CREC_DMA; k_lin_point_d:
-    BA_LP_DMA) run the same lin_obs on the same record values as the per-lane
-    register gathers: the same trajectory bitwise.  (The 18-value PCG
-    records in both runs: the register-gather W kernel has no 16-value form.)"""
-    p = make_config("c4", scale=0.01)
-    kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=6, precision=precision)
-    monkeypatch.setenv("BA_PCG_PC", "0")
-    monkeypatch.setenv(switch, on)
-    ca, xa, sa, la = gpu_solve(solver, p, **kw)
-    monkeypatch.setenv(switch, off)
-    cb, xb, sb, lb = gpu_solve(solver, p, **kw)
-    assert [it["cost"] for it in la] == [it["cost"] for it in lb]
-    assert sa.final_cost == sb.final_cost
-    assert np.array_equal(ca, cb) and np.array_equal(xa, xb)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
-def test_gpu_camera_pass_dma_gather_is_bitwise_the_register_gather(solver, precision, monkeypatch):
-    """k_pcg_cam_td (the products gathered into LDS by LDS-DMA) sums the same
-    values per thread in the same order as k_pcg_cam_t: the same trajectory
-    bitwise (C4 camera count, the compact camera records)."""
-    p = make_config("c4", scale=0.01)
-    kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=6, precision=precision)
-    set_matvec(monkeypatch, "t_gather")
-    ca, xa, sa, la = gpu_solve(solver, p, **kw)
-    monkeypatch.setenv("BA_CAMT_DMA", "0")
-    cb, xb, sb, lb = gpu_solve(solver, p, **kw)
-    assert [it["cost"] for it in la] == [it["cost"] for it in lb]
-    assert sa.final_cost == sb.final_cost
-    assert np.array_equal(ca, cb) and np.array_equal(xa, xb)
 
 
 @pytest.mark.gpu
@@ -369,14 +328,18 @@ def test_gpu_mixed_fp32_matches_fp64(solver, pc):
 @pytest.mark.parametrize("cfg,scale", [("c2", 0.2), ("c3", 0.01)])
 @pytest.mark.parametrize("mv", MATVECS)
 def test_gpu_mixed_fp32_matches_oracle_mixed(solver, oracle_lib, cfg, scale, pc, mv, monkeypatch):
-    """BA_MIXED_FP32 against the oracle's independent fp32-W restatement
-    (oracle precision 1): the same W entries rounded to float in the matvec,
-    the rhs and the preconditioner, the back substitution in fp64, so the
-    iterations match like the fp64 ones — cost 1e-9, identical decisions and
-    CG counts — on every matvec form (mv "t" runs k_pcg_point_t<float>)."""
+    """BA_MIXED_FP32 against the oracle's independent fp32 restatement: the
+    18 W entries rounded to float in the matvec (oracle precision 1), or for
+    the forms on the 16-value rank-2 records c and Z rounded to float and
+    associated as Z'(c x), c'(Z v) (precision 3); the rhs and the
+    preconditioner from the rounded W entries, the back substitution in fp64.
+    The iterations match like the fp64 ones — cost 1e-9, identical decisions
+    and CG counts — on every matvec form (mv "pairs" runs
+    k_pcg_point_t<float>)."""
     set_matvec(monkeypatch, mv)
     p = make_config(cfg, scale=scale)
-    _, _, so, olog = oracle_lib.solve(p, oracle_opts(oracle_lib, pc, max_num_iterations=8, precision=1))
+    prec = 3 if mv in RANK2 else 1
+    _, _, so, olog = oracle_lib.solve(p, oracle_opts(oracle_lib, pc, max_num_iterations=8, precision=prec))
     _, _, sg, glog = gpu_solve(solver, p, preconditioner_type=pc, max_num_iterations=8, precision="MIXED_FP32")
     compare(glog, olog, min(len(glog), len(olog), 6))
     assert sg.final_cost == pytest.approx(so["final_cost"], rel=1e-8)
@@ -397,28 +360,6 @@ def test_gpu_pcg_t_auto_threshold(solver, monkeypatch):
     _, _, sb, lb = gpu_solve(solver, p, **kw)
     compare(la, lb, len(lb), rtol=1e-10)
     assert sa.final_cost == pytest.approx(sb.final_cost, rel=1e-10)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
-@pytest.mark.parametrize("cfg,scale", [("c2", 0.2), ("c4", 0.01)])
-def test_gpu_camera_major_w_matches_the_gather(solver, cfg, scale, precision, monkeypatch):
-    """The camera-major copy of W (k_obs_w_cam) holds the point-major records
-    (the same lin_obs on the same table values; the compiler's fma
-    contraction may differ between the two kernels, so not bitwise: a 1-ulp
-    candidate cost was measured) and the camera passes read them in the same
-    order: the same trajectory to 1e-12 (also beyond 200 cameras: c4, the
-    compact camera records)."""
-    p = make_config(cfg, scale=scale)
-    kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=6, precision=precision)
-    monkeypatch.setenv("BA_WCM", "1")
-    ca, xa, sa, la = gpu_solve(solver, p, **kw)
-    monkeypatch.setenv("BA_WCM", "0")
-    monkeypatch.setenv("BA_PCG_T", "0")
-    cb, xb, sb, lb = gpu_solve(solver, p, **kw)
-    compare(la, lb, len(lb), rtol=1e-12)
-    assert sa.final_cost == pytest.approx(sb.final_cost, rel=1e-12)
-    assert np.allclose(ca, cb, rtol=1e-10, atol=1e-12) and np.allclose(xa, xb, rtol=1e-10, atol=1e-12)
 
 
 @pytest.mark.gpu

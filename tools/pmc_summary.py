@@ -27,10 +27,19 @@ def per_kernel(d: Path, counter: str):
 
 
 def main():
-    fdir, wdir, out = Path(sys.argv[1]), Path(sys.argv[2]), Path(sys.argv[3])
-    algo = float(sys.argv[4]) if len(sys.argv) > 4 else None
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("out")
+    ap.add_argument("algo", nargs="?", type=float, default=None)
+    ap.add_argument("--sq", default=None, help="SQ pass dir: SQ_INSTS_VALU per launch joins the record")
+    ap.add_argument("--n-obs", type=int, default=None, help="observations of the profiled problem (per rank)")
+    a = ap.parse_args()
+    fdir, wdir, out, algo = Path(a.fetch_dir), Path(a.write_dir), Path(a.out), a.algo
     fetch, nf = per_kernel(fdir, "FETCH_SIZE")
     write, nw = per_kernel(wdir, "WRITE_SIZE")
+    valu = per_kernel(Path(a.sq), "SQ_INSTS_VALU")[0] if a.sq else {}
     res = {}
     for k in sorted(set(fetch) | set(write)):
         short = k.split("(")[0].replace("bahip::", "").replace("void ", "").split("<")[0].strip()
@@ -40,8 +49,12 @@ def main():
         wb = write.get(k, 0.0)
         res[short] = {"fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                       "hbm_bytes_per_launch": fb + wb, "dispatches": [nf.get(k, 0), nw.get(k, 0)]}
+        if k in valu:   # (per_kernel scales by 1024 for the KiB counters: undo)
+            res[short]["valu_insts_per_launch"] = valu[k] / 1024.0
     res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes of `bench.py --steps 3`; "
                     "FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md); KiB -> bytes")
+    if a.n_obs:
+        res["_problem"] = {"n_obs": a.n_obs}
     if algo and "k_linearize" in res:
         res["k_linearize"]["algorithmic_bytes"] = algo
         res["k_linearize"]["traffic_over_algorithmic"] = res["k_linearize"]["hbm_bytes_per_launch"] / algo
