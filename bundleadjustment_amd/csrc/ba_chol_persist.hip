@@ -71,6 +71,8 @@ __device__ unsigned long long g_wstamps[64][6];   // worker (J+1, J), its last u
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 constexpr unsigned kPersistSpin = 1u << 17;   // ~0.2 s of polls: far beyond any real wait (~20 us)
+// (BA_CHOL_SPIN_MAX, diagnostics: a smaller bound, e.g. 1, so that the
+// spin-fallback path of ba_solve runs; tests/test_gpu_parity.py)
 constexpr int kAuxSc1 = 16;                    // buffer-instruction cache policy: sc1
 
 __device__ __forceinline__ Rsrc make_rsrc(const void* base, size_t bytes) {
@@ -130,12 +132,12 @@ __device__ __forceinline__ void lds_barrier() {
 // lane 0 polls (relaxed, bounded), the barrier releases the workgroup.
 // Returns false in thread 0 if the bound was hit (the failure is reported by
 // thread 0 alone; other threads return true)
-__device__ __forceinline__ bool wait_flag(const unsigned* flag, unsigned epoch) {
+__device__ __forceinline__ bool wait_flag(const unsigned* flag, unsigned epoch, unsigned spin_max) {
   bool ok = true;
   if (threadIdx.x == 0) {
     unsigned it = 0;
     while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-      if (++it >= kPersistSpin) { ok = false; break; }
+      if (++it >= spin_max) { ok = false; break; }
       __builtin_amdgcn_s_sleep(1);
     }
   }
@@ -151,6 +153,7 @@ struct PersistArgs {
   unsigned* flags;   // [T] V_c published | [TR][T] tile (I, J) published
   int ld, n, T, TR;
   unsigned epoch;
+  unsigned spin_max;   // polls per hand-off before SL_CHOL_SPIN (kPersistSpin)
 };
 
 // worker w (>= 1) -> its tile (I, J): tiles with J >= 1 and I >= J, in
@@ -351,13 +354,13 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         // it lands behind the panel GEMM
         const bool have_pref = pref_ok[0] == 1 && pref_ok[1] == 1;   // (read after the factor's last barrier)
         if (!have_pref) {
-          if (k >= 1) spin |= !wait_flag(&tflag[c * T + k], a.epoch);
+          if (k >= 1) spin |= !wait_flag(&tflag[c * T + k], a.epoch, a.spin_max);
           const TileRegs tP = tile_fetch_sc1(rA, ld, s, kc, nrows, kc + kb);   // A_{c,k}
           tile_put(S3, tP);
         }
         // (its barrier also covers S3; the plain form is an LDS-only
         // barrier, so the diagonal tile's loads stay in flight across it)
-        if (c >= 2 && !have_diag) spin |= !wait_flag(&tflag[c * T + c], a.epoch);
+        if (c >= 2 && !have_diag) spin |= !wait_flag(&tflag[c * T + c], a.epoch, a.spin_max);
         else lds_barrier();
         if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
         PSTAMP(c, 1);
@@ -438,8 +441,8 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   auto stage_panels = [&](int k) {
     const int kc = k * CB, kb = min(CB, n - kc);
     if (k >= 1) {
-      spin |= !wait_flag(&tflag[I * T + k], a.epoch);
-      if (!diag) spin |= !wait_flag(&tflag[J * T + k], a.epoch);
+      spin |= !wait_flag(&tflag[I * T + k], a.epoch, a.spin_max);
+      if (!diag) spin |= !wait_flag(&tflag[J * T + k], a.epoch, a.spin_max);
     }
     const TileRegs tI = tile_fetch_sc1(rA, ld, r0, kc, nrows, kc + kb);        // A_{I,k}
     TileRegs tJ;
@@ -449,7 +452,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   };
   if (kmax >= 0) stage_panels(0);
   for (int k = 0; k <= kmax; ++k) {
-    spin |= !wait_flag(&vflag[k], a.epoch);
+    spin |= !wait_flag(&vflag[k], a.epoch, a.spin_max);
     if (stamp && k == kmax) WSTAMP(J, 0);
     tile_put(S2, tile_fetch_sc1(rV, CB, k * CB, 0, (k + 1) * CB, CB));          // V_k (stored cleaned)
     __syncthreads();
@@ -547,6 +550,8 @@ void launch_chol_persist(double* A, double* L, int ld, int n, double* Vbuf, doub
   a.T = (n + CB - 1) / CB;
   a.TR = (n + 1 + CB - 1) / CB;
   a.epoch = epoch;
+  const char* e = getenv("BA_CHOL_SPIN_MAX");   // (read per launch: tests switch it)
+  a.spin_max = e && atoi(e) > 0 ? (unsigned)atoi(e) : kPersistSpin;
   hipLaunchKernelGGL(k_chol_persist, dim3(chol_persist_grid(n)), dim3(256), 0, s, a);
 }
 

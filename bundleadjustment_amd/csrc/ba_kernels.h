@@ -25,10 +25,12 @@ enum Slot {
   SL_STEP2_P,       // sum (x - x')^2 over point params
   SL_CAND_BAD,      // non-finite candidate residual count
   SL_STEP_BAD,      // non-finite step component count (linear solver failure)
+  SL_CHOL_SPIN,     // a hand-off spin bound of the dataflow Cholesky / back substitution was hit (not a pivot failure)
+  // (MCC_NEG..CHOL_SPIN are contiguous: one all-reduce per step under
+  // collectives, so every rank sees every rank's spin and they decide alike)
   SL_ELIM_BAD,      // failed 3x3 point-block Cholesky count
   SL_GMAX_C, SL_GN2_C, SL_XN2_C, SL_STEP2_C,
   SL_CHOL_BAD,      // non-positive pivot in the reduced camera system
-  SL_CHOL_SPIN,     // a hand-off spin bound of the dataflow Cholesky / back substitution was hit (not a pivot failure)
   kNumSlots
 };
 

@@ -235,6 +235,7 @@ __global__ __launch_bounds__(64) void k_pcg_setup_fin(const double* __restrict__
     st[PS_RHO] = st[PS_RHO1] = 1.0; st[PS_Q0] = st[PS_Q01] = -0.0; st[PS_ALPHA] = 0.0; st[PS_NORM_B] = sqrt(bb);
     st[PS_ITER] = 0.0; st[PS_DONE] = 0.0; st[PS_TERM] = PCG_NO_CONVERGENCE;
     scal[SL_CHOL_BAD] = 0.0;   // linear-solver failure flag of this step
+    scal[SL_CHOL_SPIN] = 0.0;  // (a dense step's spin on this context must not fail this one)
   }
   if (sqrt(bb) == 0.0) { pcg_stop(st, scal, PCG_SUCCESS, 0); return; }   // x = 0
   // iteration 1 starts: rho = r.z (an indefinite / singular preconditioner

@@ -781,7 +781,11 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
     // ~0.7 %).  BA_PCG_T=0 / 1 (diagnostics) forces it off / on.
     const char* fe = getenv("BA_PCG_T");   // (read per solve: tests switch it)
     const int force = fe ? atoi(fe) : -1;
-    // (decided from the largest rank's shard: every rank runs the same path)
+    // (the Infinity-Cache test uses the largest rank's shard; the chunk and
+    // duplicate-pair tests below are per rank, so ranks may run different
+    // matvec forms: that changes only the rounding of each rank's own
+    // contribution, which is all-reduced before anything is decided, so the
+    // ranks' decisions stay identical)
     const bool big = 144.0 * (double)ctx->max_no > 256.0 * 1024 * 1024;
     const bool use_t = force >= 0 ? force != 0 : W.npchunks > 0 || (big && !W.w32);
     if (use_t && !ctx->tobs_buf) ctx->tobs_buf = ctx->dalloc<double>(6 * (size_t)std::max(ctx->no, 1));
@@ -793,16 +797,16 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
   launch_point_elim(P, W, radius, s, ctx->take_norms());
   launch_cam_schur_diag(P, W, s, W.Sd);
   if (po.schur_jacobi && ctx->pcg_ndup > 0) launch_pcg_dup(P, W, s);   // (this rank's duplicate pairs)
-  if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
   // exchange path: one 6 nvc vector per matvec crosses the ranks (the
   // camera slices are folded first, in the order the single-rank update
-  // folds them, so both paths round identically)
+  // folds them, so both paths round identically).  The point-elimination
+  // failure count is folded and all-reduced with the step's scalars at its
+  // end (step_enqueue): a failed elimination on any rank makes the all-reduced
+  // products non-finite, so every rank's CG stops alike and the step is
+  // rejected on every rank (one collective fewer per LM iteration)
   const size_t tcount = (size_t)6 * ctx->nvc;
   W.pcg_folded = ctx->coll();
-  if (ctx->coll()) {
-    ctx->allreduce(W.Sd, 27 * (size_t)ctx->nvc);
-    ctx->allreduce(W.scal + SL_ELIM_BAD, 1);
-  }
+  if (ctx->coll()) ctx->allreduce(W.Sd, 27 * (size_t)ctx->nvc);
   if (ctx->nvc == 0) return 0;
   launch_pcg_setup(P, W, radius, po, s);
   int it = 0, batch = 4;
@@ -880,8 +884,11 @@ int step_enqueue(ba_ctx* ctx, double radius, const ba_options& o) {
   else reduced_solve_dense(ctx, radius);
   launch_cam_candidate(P, W, s);
   launch_backsub_candidate(P, W, s);
+  // (DENSE_SCHUR under collectives: the elimination failures already
+  // crossed the ranks with the packed S)
+  const bool pcg = o.linear_solver == BA_ITERATIVE_SCHUR;
   const uint32_t step_sum = bit(SL_MCC_NEG) | bit(SL_CCOST) | bit(SL_STEP2_P) | bit(SL_CAND_BAD) | bit(SL_STEP_BAD) |
-                            bit(SL_STEP2_C) | (ctx->coll() ? 0u : bit(SL_ELIM_BAD));
+                            bit(SL_STEP2_C) | (ctx->coll() && !pcg ? 0u : bit(SL_ELIM_BAD));
   if (!ctx->coll()) {
     // folded by the scalar record's publish that follows every step
     // (ba_ctx::publish_scalars: one launch for the fold and the record)
@@ -891,7 +898,8 @@ int step_enqueue(ba_ctx* ctx, double radius, const ba_options& o) {
   launch_reduce(W, step_sum | ctx->pend_sum, ctx->pend_max, s);
   ctx->pend_sum = ctx->pend_max = 0;
   if (ctx->coll()) {
-    ctx->allreduce(W.scal + SL_MCC_NEG, 5);  // MCC_NEG, CCOST, STEP2_P, CAND_BAD, STEP_BAD
+    // MCC_NEG, CCOST, STEP2_P, CAND_BAD, STEP_BAD, CHOL_SPIN (+ ELIM_BAD: ITERATIVE_SCHUR)
+    ctx->allreduce(W.scal + SL_MCC_NEG, pcg ? 7 : 6);
   }
   return ls_iters;
 }
@@ -1028,11 +1036,11 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
       // a hand-off of the persistent factorisation never came (its grid
       // could not be fully resident, e.g. beside another process's kernels):
       // not a pivot failure.  Redo the step with the per-step launches (and
-      // keep them for this context); the back substitution's own spins have
-      // no fallback.
-      // (with collectives the ranks could not agree on a redo: one process
-      // per GPU there, where the grid fits by construction)
-      if (!ctx->W.chol_persist || ctx->coll())
+      // keep them for this context).  A spin of the per-step form's back
+      // substitution (k_back_flow) has no fallback: BA_ERR_DEVICE.  Under
+      // collectives the spin slot is all-reduced with the step's scalars, so
+      // every rank redoes (or throws) together.
+      if (!ctx->W.chol_persist)
         throw BaError{BA_ERR_DEVICE, "dense Cholesky: a hand-off spin bound was hit"};
       ctx->W.chol_persist = false;
       if (ctx->lin_at_cand) linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, false, true);

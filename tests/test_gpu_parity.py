@@ -302,6 +302,31 @@ def test_persistent_cholesky_is_bitwise_the_per_step_form(monkeypatch, cfg, scal
     assert [r["step_is_successful"] for r in a[3]] == [r["step_is_successful"] for r in b[3]]
 
 
+@pytest.mark.parametrize("spec", ["0", "1"])
+def test_persistent_cholesky_spin_fallback_redoes_the_step(monkeypatch, spec):
+    """A hand-off spin bound hit by the persistent factorisation (forced here:
+    BA_CHOL_SPIN_MAX=1 gives up at the first flag that is not up yet) is not
+    a pivot failure: ba_solve re-linearises if the speculative linearisation
+    ran, redoes the step with the per-step launches and keeps them for the
+    context.  The trajectory must be bitwise the per-step one
+    (BA_CHOL_PERSIST=0), with the speculative linearisation on and off."""
+    p = bp.fix_camera(make_config("c3", scale=0.05), 1)
+    opts = Options(max_num_iterations=6)
+    monkeypatch.setenv("BA_SPEC_LIN", spec)
+    monkeypatch.setenv("BA_CHOL_PERSIST", "0")
+    with Solver(0) as s:
+        ref = run_gpu(s, p, opts)
+    monkeypatch.setenv("BA_CHOL_PERSIST", "1")
+    monkeypatch.setenv("BA_CHOL_SPIN_MAX", "1")
+    with Solver(0) as s:
+        got = run_gpu(s, p, opts)
+        again = run_gpu(s, p, opts)   # (a new problem on the context: the fallback again)
+    for r in (got, again):
+        assert np.array_equal(ref[0], r[0]) and np.array_equal(ref[1], r[1])
+        assert [x["cost"] for x in ref[3]] == [x["cost"] for x in r[3]]
+        assert [x["step_is_successful"] for x in ref[3]] == [x["step_is_successful"] for x in r[3]]
+
+
 # ---------------------------------------------------------------------------
 # speculative linearisation (BA_SPEC_LIN: the linearisation at a step's
 # candidate is enqueued behind the step's scalar record; a rejected or invalid
