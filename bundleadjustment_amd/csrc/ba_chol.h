@@ -16,8 +16,6 @@
 // so the serial chain per 64 columns is one panel GEMM, one tile update and
 // the 64-column factor + inverse of the critical workgroup.  Back
 // substitution L^T y = z then uses the explicit V_K (no triangular solves).
-#include <utility>
-
 #include "ba_kernels.h"
 
 namespace bahip {
@@ -256,12 +254,6 @@ struct CholLds {
   double2 colp[2][CB];     // column-pair broadcast of the sub-panel sweep
   double rsv[CB];          // 1/sqrt(pivot) broadcast for the final scaling
   int bad;
-  // hand-offs between the waves of the 64-column register sweep
-  // (factor_invert_sweep64), LDS counters reset at its start:
-  int prog;                // columns of L (scaled, in T) and their rsv final (even)
-  int fl[3];               // row blocks 0..2 of X = L^-1 final
-  int rest;                // waves that stored their C = A - P P^T products
-  int loaded;              // the sweeping wave holds its rows (T may be overwritten)
 };
 
 // 1/d to ~1 ulp: hardware reciprocal + two Newton steps
@@ -535,292 +527,6 @@ __device__ __forceinline__ void inverse_rowblock(const double (*T)[LDP], const d
   }
 }
 
-// ---------------------------------------------------------------------------
-// The full 64 x 64 diagonal block (b = m = CB) as ONE register sweep.
-//
-// Wave 0 holds row r of the block in lane r (64 doubles) and eliminates the
-// 32 column pairs in order (2 x 2 pivot blocks, division-free, as
-// panel_sweep does for 16 columns): per pair the chain is the next pair's two
-// columns, its pivot block by readlane and its multipliers; the other columns
-// of every row take their rank-2 update with the pivot columns broadcast
-// through LDS (one 16-B write per lane, broadcast reads), FS_CHUNK columns at
-// a time with the next chunk's reads in flight.  No sub-panels: no barriers,
-// no MFMA trailing updates, no row reloads or scaled restores between them
-// (those were ~55 % of the four-sub-panel factor's 29k critical cycles,
-// profiles/r04_final_chol_bench_1194_stamped.txt).  As each pair completes its
-// two L columns are scaled into T and W.prog advances; waves 1..3 form X =
-// L^-1 behind it (diag_inverse16_stream: each column as it arrives; the
-// off-diagonal blocks once their row blocks are final), so only the last
-// blocks' products follow the sweep.
-// Pc != nullptr: T is final in its column-0 tiles only; waves 1..3 form the
-// other six lower tiles of Pc Pc^T and store them over T once wave 0 holds
-// its rows (W.loaded), and wave 0 subtracts them from its registers before
-// pair 14's chain needs column 16 (W.rest == 3).  (The sums round
-// differently from C = A - P P^T before the sweep; every caller uses this
-// form, so the persistent and per-step factorisations stay bitwise equal.)
-// ---------------------------------------------------------------------------
-#ifndef FS_CHUNK
-#define FS_CHUNK 8
-#endif
-// reads stay in their chunk: a compiler memory fence (the selection DAG
-// otherwise hoists every LDS read of the unrolled sweep: 512 VGPRs and
-// spills) plus a scheduling barrier for the machine scheduler
-__device__ __forceinline__ void fs_fence() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-// LDS counters between the waves of one workgroup (LDS operations of one
-// wave complete in order, so a counter seen up covers the wave's earlier
-// stores)
-__device__ __forceinline__ int lds_poll(int* p) {
-  return __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile int*>(p));
-}
-__device__ __forceinline__ void wait_lds(int* p, int v) {
-  while (lds_poll(p) < v) __builtin_amdgcn_s_sleep(1);
-  asm volatile("" ::: "memory");
-}
-__device__ __forceinline__ void set_lds(int* p, int v) {
-  asm volatile("" ::: "memory");
-  if ((ctid() & 63) == 0) *reinterpret_cast<volatile int*>(p) = v;
-}
-struct FsState {
-  double a[64];        // row r of the block (lane r)
-  double2 c2, c3;      // this pair's chain operands: columns JJ+2, JJ+3 of its pivot rows
-  double f0, f1;       // this lane's multipliers of this pair
-  double d0, e, d1;    // this pair's pivot block
-};
-// pair JJ (pivot columns JJ, JJ+1; f0, f1 formed in pair JJ-2):
-//   A  the next pair's two columns (the chain), its pivot block by readlane,
-//      those columns published, the next pair's chain operands read
-//   B  the next pair's reciprocal and multipliers (under this pair's bulk)
-//   C  the remaining columns, FS_CHUNK at a time, reads one chunk ahead
-template <int JJ>
-__device__ __forceinline__ void fs_pair(FsState& s, double (*T)[LDP], CholLds& W, double2 (*colp)[CB], int r,
-                                        bool& bad, bool merge) {
-  constexpr int buf = (JJ >> 1) & 1;
-  constexpr int NB = (64 - (JJ + 4) + FS_CHUNK - 1) / FS_CHUNK;   // bulk chunks (0 on the last two pairs)
-  if constexpr (JJ == 14) {
-    if (merge) {   // the rest of C = A - P P^T (waves 1..3: stored over T's tiles)
-      wait_lds(&W.rest, 3);
-      const double2* q = reinterpret_cast<const double2*>(&T[r][16]);
-#pragma unroll
-      for (int k = 0; k < 24; ++k) {
-        const double2 v = q[k];
-        s.a[16 + 2 * k] -= v.x;
-        s.a[17 + 2 * k] -= v.y;
-      }
-      fs_fence();
-    }
-  }
-  const double f0 = s.f0, f1 = s.f1, u0 = s.a[JJ];
-  const double d0j = s.d0, ej = s.e;
-  double2 ct[2][FS_CHUNK];
-  if constexpr (JJ + 2 < 64) {
-    s.a[JJ + 2] = fma(-f1, s.c2.y, fma(-f0, s.c2.x, s.a[JJ + 2]));
-    s.a[JJ + 3] = fma(-f1, s.c3.y, fma(-f0, s.c3.x, s.a[JJ + 3]));
-    s.d0 = readlane_f64(s.a[JJ + 2], JJ + 2);
-    s.e = readlane_f64(s.a[JJ + 2], JJ + 3);
-    s.d1 = readlane_f64(s.a[JJ + 3], JJ + 3);
-    W.colp[buf ^ 1][r] = make_double2(s.a[JJ + 2], s.a[JJ + 3]);
-    __builtin_amdgcn_wave_barrier();
-    if constexpr (JJ + 4 < 64) {
-      s.c2 = colp[buf ^ 1][JJ + 4];
-      s.c3 = colp[buf ^ 1][JJ + 5];
-    }
-    if constexpr (NB > 0) {
-#pragma unroll
-      for (int q = 0; q < FS_CHUNK; ++q)
-        if (JJ + 4 + q < 64) ct[0][q] = colp[buf][JJ + 4 + q];
-    }
-    fs_fence();
-    {   // B
-      const double rdet = recip(s.d0 * s.d1 - s.e * s.e);
-      const double un0 = s.a[JJ + 2], un1 = s.a[JJ + 3];
-      s.f0 = fma(un0, s.d1, -un1 * s.e) * rdet;
-      s.f1 = fma(un1, s.d0, -un0 * s.e) * rdet;
-    }
-#pragma unroll
-    for (int k = 0; k < NB; ++k) {   // C
-      const int t0 = JJ + 4 + k * FS_CHUNK;
-      if (k + 1 < NB) {
-#pragma unroll
-        for (int q = 0; q < FS_CHUNK; ++q)
-          if (t0 + FS_CHUNK + q < 64) ct[(k + 1) & 1][q] = colp[buf][t0 + FS_CHUNK + q];
-      }
-#pragma unroll
-      for (int q = 0; q < FS_CHUNK; ++q)
-        if (t0 + q < 64) {
-          s.a[t0 + q] = fma(-f1, ct[k & 1][q].y, fma(-f0, ct[k & 1][q].x, s.a[t0 + q]));
-          asm volatile("" : "+v"(s.a[t0 + q]));   // (pins the update into this chunk)
-        }
-      fs_fence();
-    }
-  }
-  // column JJ+1 to its 1 x 1 form: its pivot d1 - e^2 / d0 on the diagonal
-  s.a[JJ + 1] -= u0 * (ej * recip(d0j));
-  // columns JJ, JJ+1 are final: scaled into T, then the progress counter
-  const double dn = readlane_f64(s.a[JJ + 1], JJ + 1);
-  bad |= !(d0j > 0.0 && isfinite(d0j)) || !(dn > 0.0 && isfinite(dn));
-  const double rs0 = rsqrt_nr(d0j), rs1 = rsqrt_nr(dn);   // (t == r: sqrt(d_t) = d_t / sqrt(d_t))
-  *reinterpret_cast<double2*>(&T[r][JJ]) =
-      make_double2(JJ <= r ? s.a[JJ] * rs0 : 0.0, JJ + 1 <= r ? s.a[JJ + 1] * rs1 : 0.0);
-  if (r == 0) {
-    *reinterpret_cast<double2*>(&W.rsv[JJ]) = make_double2(rs0, rs1);
-    *reinterpret_cast<volatile int*>(&W.prog) = JJ + 2;
-  }
-}
-template <int... P>
-__device__ __forceinline__ void fs_pairs(FsState& s, double (*T)[LDP], CholLds& W, double2 (*colp)[CB], int r,
-                                         bool& bad, bool merge, std::integer_sequence<int, P...>) {
-  (fs_pair<2 * P>(s, T, W, colp, r, bad, merge), ...);
-}
-__device__ __forceinline__ void full_sweep64(double (*T)[LDP], CholLds& W, bool merge) {
-  const int r = ctid() & 63;
-  int zo = 0;   // (an opaque base: see panel_sweep)
-  asm volatile("" : "+v"(zo));
-  double2 (*colp)[CB] = reinterpret_cast<double2 (*)[CB]>(&W.colp[0][zo]);
-  FsState s;
-  {
-    const double2* src = reinterpret_cast<const double2*>(&T[r][0]);
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const double2 v = src[k];
-      s.a[2 * k] = v.x;
-      s.a[2 * k + 1] = v.y;
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  set_lds(&W.loaded, 1);   // (the rows are in registers: waves 1..3 may store over T)
-  W.colp[0][r] = make_double2(s.a[0], s.a[1]);
-  __builtin_amdgcn_wave_barrier();
-  s.c2 = colp[0][2];
-  s.c3 = colp[0][3];
-  s.d0 = readlane_f64(s.a[0], 0);
-  s.e = readlane_f64(s.a[0], 1);
-  s.d1 = readlane_f64(s.a[1], 1);
-  {
-    const double rdet = recip(s.d0 * s.d1 - s.e * s.e);
-    s.f0 = fma(s.a[0], s.d1, -s.a[1] * s.e) * rdet;
-    s.f1 = fma(s.a[1], s.d0, -s.a[0] * s.e) * rdet;
-  }
-  bool bad = false;
-  fs_pairs(s, T, W, colp, r, bad, merge, std::make_integer_sequence<int, 32>{});
-  if (bad && r == 0) W.bad = 1;
-}
-// diag_inverse16 of a block whose L columns arrive while it runs: column
-// c0 + k (and 1 / L_kk) is read once W.prog covers it.  The same arithmetic
-// in the same order; every lane runs (lanes c >= 16 store nothing)
-__device__ __forceinline__ void diag_inverse16_stream(const double (*T)[LDP], const double* rinv, double (*X)[LDP],
-                                                      int p, int* prog) {
-  const int c = ctid() & 63;
-  const int c0 = 16 * p;
-  int zo = 0;
-  asm volatile("" : "+v"(zo));
-  T = reinterpret_cast<const double (*)[LDP]>(&T[0][zo]);
-  double acc[16], col[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = (i == c) ? 1.0 : 0.0;
-  wait_lds(prog, c0 + 2);
-#pragma unroll
-  for (int i = 1; i < 16; ++i) col[i] = T[c0 + i][c0];
-  double rk = rinv[c0];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    double nxt[16], rn = 0.0;
-    if (k + 1 < 16) {
-      if (k & 1) wait_lds(prog, c0 + k + 3);   // (column c0 + k + 1 opens the next pair)
-#pragma unroll
-      for (int i = k + 2; i < 16; ++i) nxt[i] = T[c0 + i][c0 + k + 1];
-      rn = rinv[c0 + k + 1];
-    }
-    const double xk = acc[k] * rk;
-    acc[k] = xk;
-#pragma unroll
-    for (int i = k + 1; i < 16; ++i) acc[i] = fma(-col[i], xk, acc[i]);
-#pragma unroll
-    for (int i = k + 2; i < 16; ++i) col[i] = nxt[i];
-    rk = rn;
-  }
-  if (c < 16) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) X[c0 + i][c0 + c] = acc[i];
-  }
-}
-// waves 1..3: one lower tile (ti, tj) of Pc Pc^T stored over T (after wave 0
-// holds its rows)
-__device__ __forceinline__ d4 fs_rest_tile(const double (*Pc)[LDP], int ti, int tj) {
-  const int lane = ctid() & 63, li = lane & 15, lk = lane >> 4;
-  d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-  for (int k0 = 0; k0 < CB; k0 += 4)
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Pc[16 * ti + li][k0 + lk], Pc[16 * tj + li][k0 + lk], acc, 0, 0, 0);
-  return acc;
-}
-template <int ZLD, class Hook>
-__device__ __forceinline__ void factor_invert_sweep64(double (*T)[LDP], double (*X)[LDP], double (*Z)[ZLD],
-                                                      CholLds& W, const double (*Pc)[LDP], const Hook& hook) {
-  const int w = cwave();
-  if (threadIdx.x == 0) { W.prog = 0; W.fl[0] = W.fl[1] = W.fl[2] = 0; W.rest = 0; W.loaded = 0; }
-  __syncthreads();
-  CHOL_STAMP(2);
-  if (w == 0) {
-    full_sweep64(T, W, Pc != nullptr);
-    CHOL_STAMP(3);
-  } else {
-    if (Pc != nullptr) {
-      constexpr int TL[6][2] = {{1, 1}, {2, 1}, {2, 2}, {3, 1}, {3, 2}, {3, 3}};
-      const int lane = ctid() & 63, li = lane & 15, lk = lane >> 4;
-      const d4 q0 = fs_rest_tile(Pc, TL[2 * (w - 1)][0], TL[2 * (w - 1)][1]);
-      const d4 q1 = fs_rest_tile(Pc, TL[2 * (w - 1) + 1][0], TL[2 * (w - 1) + 1][1]);
-      wait_lds(&W.loaded, 1);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        T[16 * TL[2 * (w - 1)][0] + lk + 4 * g][16 * TL[2 * (w - 1)][1] + li] = q0[g];
-        T[16 * TL[2 * (w - 1) + 1][0] + lk + 4 * g][16 * TL[2 * (w - 1) + 1][1] + li] = q1[g];
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if ((ctid() & 63) == 0) atomicAdd(&W.rest, 1);
-    }
-    if (w >= 2) hook(1);
-    if (w == 1) {
-      // row blocks 0 and 1, then the diagonal block of row block 3
-      diag_inverse16_stream(T, W.rsv, X, 0, &W.prog);
-      set_lds(&W.fl[0], 1);
-      diag_inverse16_stream(T, W.rsv, X, 1, &W.prog);
-      inv_offdiag_sum(T, X, Z, 1, 0, 0);
-      inv_offdiag_fin(X, Z, 1, 0, 0);
-      set_lds(&W.fl[1], 1);
-      diag_inverse16_stream(T, W.rsv, X, 3, &W.prog);
-    } else if (w == 2) {
-      // row block 2
-      diag_inverse16_stream(T, W.rsv, X, 2, &W.prog);
-      hook(2);
-      wait_lds(&W.fl[1], 1);
-      inv_offdiag_sum(T, X, Z, 2, 0, 16);
-      inv_offdiag_fin(X, Z, 2, 0, 16);
-      inv_offdiag_sum(T, X, Z, 2, 1, 16);
-      inv_offdiag_fin(X, Z, 2, 1, 16);
-      set_lds(&W.fl[2], 1);
-      hook(3);
-    } else {
-      // row block 3's off-diagonal sums (L_3k final at 48 columns)
-      wait_lds(&W.prog, 48);
-      hook(2);
-      wait_lds(&W.fl[2], 1);
-      hook(3);
-#pragma unroll
-      for (int q = 0; q < 3; ++q) inv_offdiag_sum(T, X, Z, 3, q, 16 + 16 * q);
-    }
-  }
-  CHOL_STAMP(40);
-  __syncthreads();
-  CHOL_STAMP(41);
-  if (w >= 1) inv_offdiag_fin(X, Z, 3, w - 1, 16 * w);
-  if (w >= 2) hook.finish();
-  __syncthreads();
-  CHOL_STAMP(4);
-}
-
 // Factor the 64x64 block in four 16-column sub-panels (wave 0 sweeps, all
 // waves apply the trailing updates) and form X = L^-1 row block by row block:
 // row block p - 1 (wave 1) overlaps the sweep of sub-panel p, so only the
@@ -844,16 +550,9 @@ struct NoFactorHook {
 // unrolled, so the sweeps' row predicates and LDS offsets are compile-time
 // (tools/sweep_probe.hip: a sweep with run-time c0 / b / m costs ~800 more
 // cycles of its ~3.5k).
-#ifndef BA_CHOL_SWEEP64
-#define BA_CHOL_SWEEP64 0   // 1: the 64-column register sweep for full blocks (A/B builds until validated)
-#endif
 template <bool FULL, int ZLD, class Hook>
 __device__ __forceinline__ void factor_invert_impl(double (*T)[LDP], double (*X)[LDP], double (*Z)[ZLD], CholLds& W,
                                                    int b, int m, const double (*Pc)[LDP], const Hook& hook) {
-  if constexpr (FULL && BA_CHOL_SWEEP64) {
-    factor_invert_sweep64(T, X, Z, W, Pc, hook);
-    return;
-  }
   if constexpr (FULL) { b = CB; m = CB; }
   const int w = cwave();
   __syncthreads();
