@@ -147,26 +147,38 @@ def strong_shard(cfg: str, rank: int, world: int, scale: float = 1.0):
     return p.normalized()
 
 
-def cpu_baseline_leg(problem, cfg: str, target_s: float):
-    """The oracle (C++ restatement of Ceres LM + DENSE_SCHUR, not Ceres) on the
-    host cores: at the reference's num_threads = 4 (Optimizer.cpp:88) and at
-    every thread this process may use (OMP_NUM_THREADS, else os.cpu_count())."""
+def cpu_baseline_leg(problem, cfg: str, target_s: float, precision: str = "FP64"):
+    """The oracle (C++ restatement of Ceres LM, not Ceres) on the host cores:
+    at the reference's num_threads = 4 (Optimizer.cpp:88) and at every thread
+    this process may use (OMP_NUM_THREADS, else os.cpu_count()).  DENSE_SCHUR
+    (the reference's solver) up to 2000 cameras; beyond, where a dense 6C x 6C
+    system is infeasible (C5: 60000^2), its ITERATIVE_SCHUR restatement, timed
+    as one-iteration solves (initial linearisation + one LM step)."""
     import oracle
     oracle.build()
     nproc = os.cpu_count() or 1
     allowed = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or nproc
+    iterative = problem.n_cams > 2000
 
     def leg(threads):
         oracle.set_threads(threads)
+        if iterative:
+            o = oracle.default_options(max_num_iterations=1, linear_solver=1, preconditioner_type=1,
+                                       precision=1 if precision == "MIXED_FP32" else 0)
+            t0 = time.perf_counter()
+            oracle.solve(problem, o)
+            return time.perf_counter() - t0, 1
         first = oracle.bench_seconds_per_iteration(problem, 1)
         iters = max(1, min(30, int(target_s / max(first, 1e-3))))
         return oracle.bench_seconds_per_iteration(problem, iters), iters
 
     spi4, it4 = leg(min(4, allowed))
     spia, ita = leg(allowed) if allowed != min(4, allowed) else (spi4, it4)
+    solver = ("ITERATIVE_SCHUR (SCHUR_JACOBI" + (", fp32 W" if precision == "MIXED_FP32" else "") +
+              "; one-iteration solves: initial linearisation + one LM step)") if iterative else "DENSE_SCHUR"
     return {"value": round(problem.n_obs / spia / 1e6, 3), "unit": "M-obs/s", "cores": allowed, "kind": "port",
-            "sample": f"full {cfg} problem ({problem.n_obs} obs), {ita} LM iterations of the C++ CPU restatement of "
-                      f"Ceres LM+DENSE_SCHUR (oracle/), not Ceres; {spia:.3f} s/iteration at {allowed} threads "
+            "sample": f"full {cfg} problem ({problem.n_obs} obs), {ita} LM iteration(s) of the C++ CPU restatement "
+                      f"of Ceres LM + {solver} (oracle/), not Ceres; {spia:.3f} s/iteration at {allowed} threads "
                       f"(host nproc {nproc})",
             "nproc": nproc,
             "reference_threads": {"threads": min(4, allowed), "value": round(problem.n_obs / spi4 / 1e6, 3),
@@ -378,12 +390,16 @@ def main():
         # would have ended the solve
         stop = next((i + 1 for i, r in enumerate(tlog) if r["step_is_successful"]
                      and abs(r["cost_change"]) <= 1e-6 * (r["cost"] + r["cost_change"])), None)
+        productive = float(np.mean(it_ms[:stop])) if stop else None
         trajectory = {"lm_iterations": summ.num_iterations, "successful_steps": summ.num_successful_steps,
                       "unsuccessful_steps": summ.num_unsuccessful_steps,
                       "initial_cost": summ.initial_cost, "final_cost": summ.final_cost,
                       "linear_solver_iterations": cg,
                       "iteration_ms": [round(float(x), 4) for x in it_ms],
                       "ceres_default_function_tolerance_stop": stop,
+                      "ms_per_iteration_to_that_stop": round(productive, 4) if productive else None,
+                      "linear_solver_iterations_to_that_stop": (round(float(np.mean(cg[:stop])), 2) if stop
+                                                                 else None),
                       "note": "one ba_solve from x0 (termination tests off, Ceres' radius schedule); ms_per_step "
                               "= the solve's wall time / its LM iterations, initial linearisation included"}
         steps_done = summ.num_iterations
@@ -471,6 +487,7 @@ def main():
         if pmc.get("valu_insts_per_launch"):
             # fp64 VALU issue: a wave64 fp64 instruction holds its SIMD's 16
             # fp64 lanes 4 cycles; 4 SIMDs x 256 CUs at the 2.4 GHz peak clock
+            # (4 cycles per wave64 VALU instruction on a 16-lane SIMD)
             busy = pmc["valu_insts_per_launch"] * 4.0 / (ms_rj * 1e-3 * 2.4e9 * 1024.0)
             roofline["real"]["valu_insts_per_launch"] = pmc["valu_insts_per_launch"]
             roofline["real"]["valu_busy_frac_est"] = round(busy, 4)
@@ -497,7 +514,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if problem.n_obs <= 20_000_000:
-            cpu = cpu_baseline_leg(problem, cfg, args.cpu_seconds)
+            cpu = cpu_baseline_leg(problem, cfg, args.cpu_seconds, precision)
         else:   # one CPU LM iteration alone would take minutes: no bounded sample
             log(f"cpu baseline skipped: {problem.n_obs} observations")
 
