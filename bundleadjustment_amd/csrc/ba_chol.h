@@ -541,11 +541,22 @@ __device__ __forceinline__ void inverse_rowblock(const double (*T)[LDP], const d
 // Hook: work for waves 2 and 3 while wave 0 sweeps sub-panel p = 1, 2, 3 and
 // wave 1 inverts row block p - 1 (the persistent factorisation prefetches its
 // next panel tile there); the per-step kernels pass none.
-// hook.finish(): waves 2 and 3 again, at the end of the inverse tail.
+// hook.land(): waves 2 and 3 again, in the inverse tail beside wave 0's last
+// diagonal inverse; hook.finish(): waves 2 and 3 at the end of the tail.
 struct NoFactorHook {
   __device__ void operator()(int) const {}
+  __device__ void land() const {}
   __device__ void finish() const {}
 };
+// A workgroup barrier for LDS only: every hand-off inside the factor goes
+// through LDS, and __syncthreads' release fence would also drain every global
+// load and store in flight (the persistent factorisation's next-panel
+// prefetch, V's row blocks stored as they complete)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 // FULL: b = m = CB (every block but the last): the sub-panel loop is
 // unrolled, so the sweeps' row predicates and LDS offsets are compile-time
 // (tools/sweep_probe.hip: a sweep with run-time c0 / b / m costs ~800 more
@@ -555,7 +566,7 @@ __device__ __forceinline__ void factor_invert_impl(double (*T)[LDP], double (*X)
                                                    int b, int m, const double (*Pc)[LDP], const Hook& hook) {
   if constexpr (FULL) { b = CB; m = CB; }
   const int w = cwave();
-  __syncthreads();
+  lds_barrier();
   CHOL_STAMP(2);
   int last = 0;
   // one trailing-update tile (ti, ts) -= (sub-panel c0 columns) products
@@ -581,13 +592,13 @@ __device__ __forceinline__ void factor_invert_impl(double (*T)[LDP], double (*X)
       hook(p);
     }
     CHOL_STAMP(10 + 2 * p);
-    __syncthreads();
+    lds_barrier();
     if constexpr (FULL) {
       if (p == 0) {   // the tiles the next sweeps read first: one round
         const int ti = w == 0 ? 1 : (w == 1 ? 2 : (w == 2 ? 2 : 3));
         const int ts = w == 2 ? 2 : 1;
         upd_tile(ti, ts, c0);
-        __syncthreads();
+        lds_barrier();
         CHOL_STAMP(11 + 2 * p);
         return;
       }
@@ -606,7 +617,7 @@ __device__ __forceinline__ void factor_invert_impl(double (*T)[LDP], double (*X)
         tile_store(T, 16 * ti, 16 * ts, acc);
       }
     }
-    __syncthreads();
+    lds_barrier();
     CHOL_STAMP(11 + 2 * p);
   };
   if constexpr (FULL) {
@@ -618,14 +629,16 @@ __device__ __forceinline__ void factor_invert_impl(double (*T)[LDP], double (*X)
   }
   CHOL_STAMP(3);
   // last row block: diagonal inverse (wave 0) beside the sums Z_q (wave q + 1)
+  // and the landing of the hook's loads (waves 2, 3: under wave 0's chain)
   if (w == 0) diag_inverse16(T, W.rsv, X, last, b);
   else if (w - 1 < last) inv_offdiag_sum(T, X, Z, last, w - 1, 16 * w);
+  if (w >= 2) hook.land();
   CHOL_STAMP(40);
-  __syncthreads();
+  lds_barrier();
   CHOL_STAMP(41);
   if (w >= 1 && w - 1 < last) inv_offdiag_fin(X, Z, last, w - 1, 16 * w);
   if (w >= 2) hook.finish();
-  __syncthreads();
+  lds_barrier();
   CHOL_STAMP(4);
 }
 // KIND: 1 = the caller guarantees b = m = CB, 0 = the general form, -1 =

@@ -45,6 +45,7 @@ namespace bahip {
 __device__ unsigned long long g_pstamps[64][8];
 __device__ unsigned long long g_prt[64][8];       // the same stamps in s_memrealtime (100 MHz, chip-wide)
 __device__ unsigned long long g_wstamps[64][6];   // worker (J+1, J), its last update (s_memrealtime)
+__device__ unsigned long long g_estamps[64][2];   // end_step: entered, V stores issued (s_memtime)
 #define WSTAMP(j, i)                                                                          \
   do {                                                                                        \
     __builtin_amdgcn_sched_barrier(0);                                                        \
@@ -107,6 +108,41 @@ __device__ inline TileRegs tile_fetch_sc1(Rsrc r, size_t ld, int r0, int c0, int
   return t;
 }
 
+// the same tile as tile_fetch_sc1 in two halves: the raw 16-B loads (clamped
+// addresses) now, the zeroing when the tile goes to LDS.  The masks read the
+// loaded registers, so formed at the fetch they made the compiler wait for
+// the loads right there (the diagonal tile's ~2k-cycle round trip on the
+// chain, before the panel GEMM it was meant to hide under)
+template <bool LOWER = false>
+__device__ inline TileRegs tile_issue_sc1(Rsrc r, size_t ld, int r0, int c0, int rmax, int cmax) {
+  TileRegs t;
+  const int tid = ctid();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int e = tid + 256 * it;
+    const int i = e >> 5, j = (e & 31) * 2;
+    const bool up = LOWER && j > i;
+    const int ri = r0 + i, cj = c0 + (up ? (i & ~1) : j);
+    const int ric = min(ri, rmax - 1), cjc = min(cj, cmax - 2) & ~1;
+    t.v[it] = ld_sc1(r, ((size_t)ric * ld + cjc) * sizeof(double));
+  }
+  return t;
+}
+template <bool LOWER = false>
+__device__ inline void tile_put_masked(double (*D)[LDP], const TileRegs& t, int r0, int c0, int rmax, int cmax) {
+  const int tid = ctid();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int e = tid + 256 * it;
+    const int i = e >> 5, j = (e & 31) * 2;
+    const bool up = LOWER && j > i;
+    const int ri = r0 + i, cj = c0 + (up ? (i & ~1) : j);
+    const bool rok = ri < rmax && !up;
+    D[i][j] = (rok && cj < cmax) ? t.v[it].x : 0.0;
+    D[i][j + 1] = (rok && cj + 1 < cmax) ? t.v[it].y : 0.0;
+  }
+}
+
 // drain this wave's stores, join the workgroup, one lane raises the flag
 __device__ __forceinline__ void publish(unsigned* flag, unsigned epoch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave
@@ -121,13 +157,6 @@ __device__ __forceinline__ void publish_before_loads(unsigned* flag, unsigned ep
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// a workgroup barrier for LDS only: __syncthreads' release fence would also
-// drain every outstanding global store and load of the waves
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
 }
 // lane 0 polls (relaxed, bounded), the barrier releases the workgroup.
 // Returns false in thread 0 if the bound was hit (the failure is reported by
@@ -170,6 +199,22 @@ __device__ inline bool worker_tile(int w, int T, int TR, int& I, int& J) {
   return false;
 }
 
+// V_c's lower 16x16 blocks [blk0, blk0 + nblk) in row-block order ((0,0),
+// (1,0), (1,1), (2,0), ...) from LDS to Vbuf (write-through, 16-B pieces,
+// row-contiguous), by the nthr threads with index t
+__device__ __forceinline__ void store_v_blocks(Rsrc rV, size_t vbase, const double (*X)[LDP], int blk0, int nblk,
+                                               int t, int nthr) {
+  for (int e = t; e < nblk * 16 * 8; e += nthr) {
+    const int blk = blk0 + (e >> 7), rr = (e >> 3) & 15, cc = (e & 7) * 2;
+    const int bi = blk < 1 ? 0 : (blk < 3 ? 1 : (blk < 6 ? 2 : 3));
+    const int bj = blk - bi * (bi + 1) / 2;
+    const int i = 16 * bi + rr, j = 16 * bj + cc;
+#ifndef BA_CHOL_NO_VSTORE
+    st_sc1(rV, vbase + ((size_t)i * CB + j) * sizeof(double), make_double2(X[i][j], X[i][j + 1]));
+#endif
+  }
+}
+
 // The next panel tile A_{c+1,c} into S3 by waves 2 and 3 (each wave one half,
 // 32 rows), spread over the factor so that no global round trip lands on a
 // sub-panel barrier: p = 1 polls the worker's flag (one relaxed load, no
@@ -191,7 +236,16 @@ struct PanelPrefetch {
   int c;                  // diagnostics (BA_CHOL_STAMPS): the step, for the fetch-phase record
   const unsigned* dflag;  // the next diagonal tile's flag (nullptr: no worker, ready)
   int* dready;            // finish(): that flag seen up (polled once by wave 2)
-  mutable double2 v[16];  // loads in flight between p = 3 and finish()
+  // V_c's row blocks 0..2, final before the last sub-panel's sweep ends
+  // (row block q by wave 1 beside sweep q + 1): stored here, under wave 0's
+  // chain — row blocks 0, 1 in sub-panel 3, row block 2 in the inverse tail
+  // — so that the end of the step stores only row block 3 (4 of the 10 lower
+  // blocks; the stores and the diagonal tile's loads behind them were ~3.5k
+  // cycles of the step's chain, tools/chol_bench.hip)
+  Rsrc rV;
+  size_t vbase;           // byte offset of V_c in Vbuf
+  const double (*X)[LDP];
+  mutable double2 v[16];  // loads in flight between p = 3 and land()
   mutable bool pending = false;
   __device__ bool poll() const {
     if (!flag) return true;
@@ -228,6 +282,7 @@ struct PanelPrefetch {
   }
   __device__ void operator()(int p) const {
     const int w = cwave(), lane = ctid() & 63;   // w = 2 or 3
+    if (p == 3) store_v_blocks(rV, vbase, X, 0, 3, ctid() - 128, 128);
     const int st = __builtin_amdgcn_readfirstlane(ok[w - 2]);   // 0 at p = 1 (reset at the step start)
     if (st == 1) return;
     if (st == 0) {
@@ -240,6 +295,11 @@ struct PanelPrefetch {
     issue();
     if (p == 2) land(p);
     else pending = true;
+  }
+  __device__ void land() const {
+    if (pending) land(3);
+    pending = false;
+    store_v_blocks(rV, vbase, X, 3, 3, ctid() - 128, 128);
   }
   __device__ void finish() const {
     if (pending) land(3);
@@ -288,20 +348,35 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
     // never live across the loop's back edge.
     auto end_step = [&](int cp) {
       const int sp = cp * CB, bp = min(CB, n - sp), mp = min(CB, nrows - sp);
+#ifdef BA_CHOL_STAMPS
+      {
+        __builtin_amdgcn_sched_barrier(0);
+        unsigned long long t_;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (threadIdx.x == 0 && cp < 64) g_estamps[cp][0] = t_;
+      }
+#endif
       if (bp == CB) {
         // a full block: only the lower block triangle (10 of 16 blocks) is
         // read again — the panel products skip the upper blocks, k_back_flow
         // masks them — and the diagonal blocks already hold exact zeros
         // above the diagonal (diag_inverse16): no clean-up pass, 5 / 8 of
-        // the stores (the upper blocks' Vbuf entries stay stale, unread)
-        for (int e = ctid(); e < 10 * 16 * 8; e += 256) {
-          const int blk = e >> 7, rr = (e >> 3) & 15, cc = (e & 7) * 2;
-          const int bi = blk < 1 ? 0 : (blk < 3 ? 1 : (blk < 6 ? 2 : 3));
-          const int bj = blk - bi * (bi + 1) / 2;
-          const int i = 16 * bi + rr, j = 16 * bj + cc;
-          st_sc1(rV, ((size_t)cp * CB * CB + (size_t)i * CB + j) * sizeof(double), make_double2(S2[i][j], S2[i][j + 1]));
-        }
+        // the stores; row blocks 0..2 went out during the factor (the
+        // prefetch hook) unless this was the last block column
+        // (the upper blocks' Vbuf entries stay stale, unread)
+        const bool hooked = cp + 1 < T;
+        store_v_blocks(rV, (size_t)cp * CB * CB * sizeof(double), S2, hooked ? 6 : 0, hooked ? 4 : 10, ctid(), 256);
         bad |= cw.bad != 0;
+#ifdef BA_CHOL_STAMPS
+        {
+          __builtin_amdgcn_sched_barrier(0);
+          unsigned long long t_;
+          asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+          __builtin_amdgcn_sched_barrier(0);
+          if (threadIdx.x == 0 && cp < 64) g_estamps[cp][1] = t_;
+        }
+#endif
         return;
       }
       for (int e2 = ctid(); e2 < CB * CB / 2; e2 += 256) {
@@ -332,7 +407,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         have_diag = dready[0] != 0;
         if (have_diag) {
           asm volatile("" ::: "memory");   // (the loads after the V stores)
-          tD = tile_fetch_sc1<true>(rA, ld, s, s, nrows, s + b);
+          tD = tile_issue_sc1<true>(rA, ld, s, s, nrows, s + b);
         }
         PSTAMP(c - 1, 6);
         if (have_diag) publish_before_loads(&vflag[c - 1], a.epoch);
@@ -364,12 +439,12 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         else lds_barrier();
         if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
         PSTAMP(c, 1);
-        if (!have_diag) tD = tile_fetch_sc1<true>(rA, ld, s, s, nrows, s + b);   // A_{c,c} (+ rhs row), in flight
+        if (!have_diag) tD = tile_issue_sc1<true>(rA, ld, s, s, nrows, s + b);   // A_{c,c} (+ rhs row), in flight
         PSTAMP(c, 2);
         d4 acc[4];
         mfma_xVT_strip(S3, S2, acc);            // P = A_{c,k} V_k^T (V_k: S2, from the last iteration)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the diagonal tile has landed
-        tile_put(S0, tD);
+        tile_put_masked<true>(S0, tD, s, s, nrows, s + b);
         // P = L_{c,k} to the factor: here only without a worker (c+1, c),
         // which otherwise stores the same product (its P_J) off this chain
         const bool store_l = c + 1 >= a.TR;
@@ -395,7 +470,8 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         // it (column 0: from before the launch)
         const PanelPrefetch pf{rA, ld, c >= 1 ? &tflag[(c + 1) * T + c] : nullptr, a.epoch, S3, pref_ok,
                                (c + 1) * CB, c * CB, nrows, c * CB + min(CB, n - c * CB), c,
-                               c + 1 >= 2 ? &tflag[(c + 1) * T + c + 1] : nullptr, dready};
+                               c + 1 >= 2 ? &tflag[(c + 1) * T + c + 1] : nullptr, dready,
+                               rV, (size_t)c * CB * CB * sizeof(double), S2};
         factor_invert_blk<1>(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr, pf);   // b = m = CB before the last block
       } else {
         factor_invert_blk<0>(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr);

@@ -191,7 +191,7 @@ bool obs_w_pc_ok(const DevProblem& P, const DevWork& W);   // k_obs_w_rc has the
 bool chol_persist_fits(int device, int n);   // every workgroup of k_chol_persist resident at once
 int chol_split_blocks();                     // block columns from which the split step form is used   // resident k_back_flow workgroups (-1: query failed)
 constexpr int kLinLdsCamsHost = 200;   // = kLinLdsCams (ba_kernels.hip): cameras the LDS camera table holds
-constexpr int kWcCamsHost = 1024;      // = kWcCams: variable cameras of the compact-W DENSE_SCHUR pair pass
+constexpr int kWcCamsHost = 1024;      // variable cameras of the compact-W DENSE_SCHUR pair pass
 int jr_ja_host(int nc);   // JA stride of the JR records for nc cameras (12 or 14)
 void launch_stream_copy(const double* a, double* b, size_t n2, hipStream_t s);
 // the scalar record into pinned host memory, then its sequence number

@@ -1573,7 +1573,6 @@ __global__ __launch_bounds__(NT) void k_candidate_lds(DevProblem P, const double
 
 // compact W records (k_obs_w_rc<double, true>, described there): 16 doubles
 constexpr int kWcRec = 16;
-constexpr int kWcCams = kWcCamsHost;   // variable cameras k_schur_pairs_c's LDS table holds (72 KB)
 // the camera constants of the compact records: Jc's scaled translation
 // columns are f (A_row,k - pr_row B_k), A_row,k = s_{3+k} K_{3k+row},
 // B_k = s_{3+k} K_{3k+2}
@@ -3347,7 +3346,7 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
     else if (W.w32)
       hipLaunchKernelGGL((k_obs_w_rc<float, false, 3, false, WG>), dim3(g), b, 0, s, P, src, (const double*)W.pxv,
                          W.scale_c, W.scale_p, W.Linv, W.Wf);
-    else if (W.wcompact)   // (DENSE_SCHUR up to kWcCams variable cameras: the compact records)
+    else if (W.wcompact)   // (DENSE_SCHUR up to kWcCamsHost variable cameras: the compact records)
       hipLaunchKernelGGL((k_obs_w_rc<double, true, 3, false, WG>), dim3(g), b, 0, s, P, src, (const double*)W.pxv,
                          W.scale_c, W.scale_p, W.Linv, W.W);
     else

@@ -166,6 +166,20 @@ int main(int argc, char** argv) {
                  " LDS %.0f  strips %.0f  GEMM %.0f  published %.0f | critical: factor starts %.0f, ends %.0f\n",
                  nn, av[0] / nn, av[1] / nn, av[2] / nn, av[3] / nn, av[4] / nn, sp1 / nn, st / nn);
       }
+      {
+        unsigned long long es[64][2];
+        CK(hipMemcpyFromSymbol(es, HIP_SYMBOL(g_estamps), sizeof(es)));
+        double a0 = 0, a1 = 0, a2 = 0;
+        int ne = 0;
+        for (int c = 1; c + 2 < T && c < 63; ++c, ++ne) {
+          a0 += (double)(es[c][0] - ps[c][5]);
+          a1 += (double)(es[c][1] - es[c][0]);
+          a2 += (double)(ps[c][6] - es[c][1]);
+        }
+        if (ne)
+          printf("    V clean+store split (avg of %d): to end_step %.0f  V stores issued %.0f  diag fetch issue %.0f\n", ne,
+                 a0 / ne, a1 / ne, a2 / ne);
+      }
       int ph[4] = {0, 0, 0, 0};
       for (int c = 0; c + 1 < T && c < 64; ++c) ph[ps[c][7] & 3]++;
       printf("    next panel tile prefetched in sub-panel 1/2/3: %d/%d/%d, at the next step's start: %d\n", ph[1], ph[2],
