@@ -114,4 +114,50 @@ __host__ __device__ inline double huber(double s, double a, double b, double* sc
   return s;
 }
 
+
+// The 16-value rank-2 PCG record of one observation (ITERATIVE_SCHUR, K
+// without skew): W_o = c^T Z with c = Jc s_c (its scaled rotation columns
+// [0..5], the four nonzero translation entries c0[3], c0[5], c1[4], c1[5]
+// [6..9]) and Z = Jp s_p L_p^-T [10..15].  j: lin_obs's corrected row pair,
+// sc: s_c, s: s_p, li: L_p^-1 (lower, row-major 00 10 11 20 21 22).
+// The record's writer (k_obs_w_rc<.., PC>) and the J-free point pass
+// (k_pcg_point_jf) form it here, and the point passes take their products
+// through pc_v / pc_t, all without FMA contraction: each operation rounds on
+// its own, so the value does not depend on the code around the call and
+// both matvec forms are bitwise the same.
+__device__ __forceinline__ void pc_record(const double* j, const double (&sc)[6], const double (&s)[3],
+                                          const double (&li)[6], bool live, double (&wv)[16]) {
+#pragma clang fp contract(off)
+  const double jp0[3] = {j[12] * s[0], j[13] * s[1], j[14] * s[2]};
+  const double jp1[3] = {j[15] * s[0], j[16] * s[1], j[17] * s[2]};
+  const double z[6] = {jp0[0] * li[0], jp0[0] * li[1] + jp0[1] * li[2], jp0[0] * li[3] + jp0[1] * li[4] + jp0[2] * li[5],
+                       jp1[0] * li[0], jp1[0] * li[1] + jp1[1] * li[2], jp1[0] * li[3] + jp1[1] * li[4] + jp1[2] * li[5]};
+  for (int a = 0; a < 3; ++a) {
+    wv[a] = live ? j[a] * sc[a] : 0.0;
+    wv[3 + a] = live ? j[6 + a] * sc[a] : 0.0;
+  }
+  wv[6] = live ? j[3] * sc[3] : 0.0;
+  wv[7] = live ? j[5] * sc[5] : 0.0;
+  wv[8] = live ? j[10] * sc[4] : 0.0;
+  wv[9] = live ? j[11] * sc[5] : 0.0;
+  for (int k = 0; k < 6; ++k) wv[10 + k] = live ? z[k] : 0.0;
+}
+// v = Z^T (c x) of a record (zero unless on)
+__device__ __forceinline__ void pc_v(const double (&wr)[16], const double (&x)[6], bool on, double (&v)[3]) {
+#pragma clang fp contract(off)
+  const double y0 = wr[0] * x[0] + wr[1] * x[1] + wr[2] * x[2] + wr[6] * x[3] + wr[7] * x[5];
+  const double y1 = wr[3] * x[0] + wr[4] * x[1] + wr[5] * x[2] + wr[8] * x[4] + wr[9] * x[5];
+  for (int k = 0; k < 3; ++k) v[k] = on ? wr[10 + k] * y0 + wr[13 + k] * y1 : 0.0;
+}
+// t = c^T (Z v) of a record
+__device__ __forceinline__ void pc_t(const double (&wr)[16], const double (&vp)[3], double (&tv)[6]) {
+#pragma clang fp contract(off)
+  const double q0 = wr[10] * vp[0] + wr[11] * vp[1] + wr[12] * vp[2];
+  const double q1 = wr[13] * vp[0] + wr[14] * vp[1] + wr[15] * vp[2];
+  for (int a = 0; a < 3; ++a) tv[a] = wr[a] * q0 + wr[3 + a] * q1;
+  tv[3] = wr[6] * q0;
+  tv[4] = wr[8] * q1;
+  tv[5] = wr[7] * q0 + wr[9] * q1;
+}
+
 }  // namespace bahip

@@ -110,6 +110,9 @@ struct DevWork {
   // ITERATIVE_SCHUR point-pass records in the 16-value rank-2 form
   // (k_obs_w_rc<.., PC>, k_pcg_point_seg<.., PC>; step_w_storage decides)
   bool pcgc = false;
+  // the PCG point pass forms the rank-2 records itself from the compact camera
+  // records (k_pcg_point_jf): no W written or read (step_w_storage decides)
+  bool pcgjf = false;
   int npchunks;                      // 0: a point has more than 64 observations (value-pair point pass)
   bool pcg_folded;                   // exchange path: slices folded into slice 0 before the all-reduce
   const int* dup_off;                // [nvc+1] per variable camera: pairs of observations of one
@@ -175,6 +178,8 @@ void launch_pcg_setup(const DevProblem& P, const DevWork& W, double radius, cons
 void launch_pcg_dup(const DevProblem& P, const DevWork& W, hipStream_t s);   // Schur-Jacobi cross terms
 // one implicit matvec (point pass + camera pass) of vec into W.tpart
 void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s);
+// the J-free point pass of one implicit matvec (W.pcgjf): v_p into W.vpt, t_o into W.tobs
+void launch_pcg_point_jf(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s);
 // exchange path: fold the matvec's camera slices into slice 0 (one 6 nvc all-reduce)
 void launch_pcg_tfold(const DevProblem& P, const DevWork& W, hipStream_t s);
 // mode 0: full CG iteration; 1: up to the x update; 2: residual reset from W.tpart = matvec(x)

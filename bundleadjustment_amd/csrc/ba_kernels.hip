@@ -2793,19 +2793,7 @@ __global__ __launch_bounds__(64 * WAVES) void k_obs_w_rc(DevProblem P, const dou
     constexpr int REC = COMPACT || PC ? kWcRec : kWRec;
     double wv[REC];
     if constexpr (PC) {
-      const double z[6] = {jp0[0] * i00, jp0[0] * i10 + jp0[1] * i11, jp0[0] * i20 + jp0[1] * i21 + jp0[2] * i22,
-                           jp1[0] * i00, jp1[0] * i10 + jp1[1] * i11, jp1[0] * i20 + jp1[1] * i21 + jp1[2] * i22};
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        wv[a] = live ? j[a] * sc[a] : 0.0;
-        wv[3 + a] = live ? j[6 + a] * sc[a] : 0.0;
-      }
-      wv[6] = live ? j[3] * sc[3] : 0.0;
-      wv[7] = live ? j[5] * sc[5] : 0.0;
-      wv[8] = live ? j[10] * sc[4] : 0.0;
-      wv[9] = live ? j[11] * sc[5] : 0.0;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) wv[10 + k] = live ? z[k] : 0.0;
+      pc_record(j, sc, {s0, s1, s2}, {i00, i10, i11, i20, i21, i22}, live, wv);
     } else if constexpr (COMPACT) {
       const double z[6] = {jp0[0] * i00, jp0[0] * i10 + jp0[1] * i11, jp0[0] * i20 + jp0[1] * i21 + jp0[2] * i22,
                            jp1[0] * i00, jp1[0] * i10 + jp1[1] * i11, jp1[0] * i20 + jp1[1] * i21 + jp1[2] * i22};
@@ -2860,6 +2848,166 @@ __global__ __launch_bounds__(64 * WAVES) void k_obs_w_rc(DevProblem P, const dou
       }
     }
     c = cn; p = pn; uv = uvn;
+  }
+}
+
+// PCG point pass without W (ITERATIVE_SCHUR beyond kLinLdsCams cameras, the
+// rank-2 record conditions of k_obs_w_rc<.., PC> met): each lane forms its
+// observation's 16-value record c, Z from the compact camera record as
+// k_obs_w_rc<WT, false, 3, true> forms it (pc_record; rounded to WT, the
+// stored record's values), then runs k_pcg_point_seg<WT, true, true>'s
+// arithmetic on it (pc_v, the segmented per-point sum, pc_t) over the same
+// point-aligned chunks.  What it trades: per LM iteration k_obs_w_rc's 128-B
+// (fp64) record per observation, written once and read by every CG
+// iteration (C4: 1.28 GB written, 1.28 GB read per matvec), against lin_obs
+// once per matvec.  Per chunk two records per lane arrive by LDS-DMA, 8
+// lanes per record (a wave-instruction touching 8 records, not 64): the
+// compact camera record and the point record prec of k_point_elim (X, flag,
+// s_p, L_p^-1) — the camera record one chunk ahead, the point record
+// requested once its values are out of the slot (after lin_obs: holding them
+// across lin_obs spilled registers).  The products leave through a third
+// slot.  (Measured at C4: 520 us per working launch against 394 for
+// k_pcg_point_seg on the stored records; without its stores 456: it runs at
+// two waves per SIMD on lin_obs' ~250 VGPRs, latency-bound, not at the VALU
+// or HBM limit.)
+template <typename WT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_pcg_point_jf(
+    DevProblem P, const int2* __restrict__ chunks, int nchunks, const double* __restrict__ crec,
+    const double* __restrict__ prec, const double* __restrict__ scale_c, const double* __restrict__ xv,
+    double* __restrict__ vpt, double* __restrict__ tobs, const double* __restrict__ st) {
+  if (st[PS_DONE] != 0.0) return;
+  static_assert(kCRec == 16 && kPRec == 16, "16-double records");
+  __shared__ __attribute__((aligned(16))) double cbuf[4][64 * 16];
+  __shared__ __attribute__((aligned(16))) double pbuf[4][64 * 16];
+  __shared__ __attribute__((aligned(16))) double tbuf[4][64 * 6];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* cb = cbuf[w];
+  double* pb = pbuf[w];
+  double* tst = tbuf[w];
+  const int swr = (lane >> 1) & 7;
+  auto issue = [&](const double* base, int idx, double* slot) {   // record idx of this lane into slot
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int q = (lane >> 3) + 8 * k;
+      const int iq = __shfl(idx, q);
+      glds16(base + (size_t)iq * 16 + 2 * ((lane & 7) ^ ((q >> 1) & 7)), slot + k * 128);
+    }
+  };
+  auto piece = [&](const double* slot, int k) {   // piece k of this lane's record
+    return *reinterpret_cast<const double2*>(slot + lane * 16 + 2 * (k ^ swr));
+  };
+  const int cs = gridDim.x * 4;
+  int ch = blockIdx.x * 4 + w;
+  if (ch >= nchunks) return;   // (uniform per wave; no workgroup barrier below)
+  int2 cr = chunks[ch];
+  int2 crn = ch + cs < nchunks ? chunks[ch + cs] : cr;
+  int o = cr.x + min(lane, cr.y - cr.x - 1);
+  int c = P.obs_cam[o], p = P.obs_pt[o], vc = P.obs_vc[o];
+  float2 uv = P.uv[o];
+  issue(crec, c, cb);
+  issue(prec, p, pb);
+  for (;;) {
+    const int o0 = cr.x, n = cr.y - cr.x;
+    double sc[6], x[6];   // s_c, x_c (L2-resident gathers)
+    {
+      const double2* sv = reinterpret_cast<const double2*>(scale_c + (size_t)max(vc, 0) * 6);
+      const double2* xc = reinterpret_cast<const double2*>(xv + 6 * (size_t)max(vc, 0));
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const double2 u = sv[a], y = xc[a];
+        sc[2 * a] = u.x; sc[2 * a + 1] = u.y;
+        x[2 * a] = y.x; x[2 * a + 1] = y.y;
+      }
+    }
+    // the next chunk's indices
+    const bool more = ch + cs < nchunks;
+    const int on = crn.x + min(lane, crn.y - crn.x - 1);
+    const int cn = P.obs_cam[on], pn = P.obs_pt[on], vcn = P.obs_vc[on];
+    const float2 uvn = P.uv[on];
+    const int2 crnn = ch + 2 * cs < nchunks ? chunks[ch + 2 * cs] : crn;
+    CamRcPre crp;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this chunk's records have landed
+#pragma unroll
+    for (int k = 0; k < 8; ++k) crp.v[k] = piece(cb, k);
+    const double2 x01 = piece(pb, 0), x2v = piece(pb, 1);   // X, the variable flag
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the next request
+    if (more) issue(crec, cn, cb);
+    const bool inl = lane < n;
+    const bool pv = x2v.y != 0.0;
+    const bool live = inl && vc >= 0 && pv;
+    double j[kJR];
+    {
+      bool fin;
+      double prf[3];
+      const CamRc cam = cam_make(CamRcOf{crec, nullptr}, crp);
+      (void)lin_obs(P, cam, vc >= 0, pv, x01.x, x01.y, x2v.x, uv, j, fin, prf);
+    }
+    double sp[3], li[6];   // s_p, L_p^-1 (prec[4..12])
+    {
+      const double2 q2 = piece(pb, 2), q3 = piece(pb, 3), q4 = piece(pb, 4), q5 = piece(pb, 5), q6 = piece(pb, 6);
+      sp[0] = q2.x; sp[1] = q2.y; sp[2] = q3.x;
+      li[0] = q3.y; li[1] = q4.x; li[2] = q4.y; li[3] = q5.x; li[4] = q5.y; li[5] = q6.x;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (more) issue(prec, pn, pb);
+    // the record (k_obs_w_rc<.., PC>), rounded as stored
+    double wr[16];
+    {
+      double wv[16];
+      pc_record(j, sc, sp, li, live, wv);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) wr[k] = (double)(WT)wv[k];
+    }
+    // k_pcg_point_seg<WT, true, true> from here
+    double v[3];
+    pc_v(wr, x, inl, v);
+    const int pt = inl ? p : -1;
+    const int ptp = __shfl_up(pt, 1, 64);
+    const bool head = lane == 0 || pt != ptp;
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long upto = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1);
+    const int h0 = 63 - __clzll(heads & upto);   // this lane's run head
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      double y[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) y[k] = __shfl_up(v[k], off, 64);
+      if (lane - off >= h0) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) v[k] += y[k];
+      }
+    }
+    const unsigned long long after = heads & ~upto;
+    const int last = after ? __ffsll((long long)after) - 2 : n - 1;   // this run's last lane
+    if (inl && lane == last) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) vpt[3 * (size_t)pt + k] = v[k];
+    }
+    {
+      double vp[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) vp[k] = __shfl(v[k], last, 64);
+      double tv[6];
+      pc_t(wr, vp, tv);
+      double2* td = reinterpret_cast<double2*>(&tst[lane * 6]);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) td[a] = make_double2(tv[2 * a], tv[2 * a + 1]);
+    }
+    wave_lds_sync();
+    {
+      double2* dst = reinterpret_cast<double2*>(tobs + 6 * (size_t)o0);
+      const double2* tsrc = reinterpret_cast<const double2*>(tst);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int e = k * 64 + lane;
+        if (e < 3 * n) dst[e] = tsrc[e];
+      }
+    }
+    wave_lds_sync();   // (the product slot is rewritten by the next chunk)
+    if (!more) break;
+    ch += cs;
+    cr = crn; crn = crnn;
+    o = on; c = cn; p = pn; vc = vcn; uv = uvn;
   }
 }
 
@@ -3327,6 +3475,7 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
                        radius, W.Linv, W.u, W.part, (const double*)W.pts, prec);
   }
   if (P.no == 0) return;
+  if (W.pcgjf) return;   // (no W: the PCG point pass forms the records itself)
   if (jr_tab(P, W)) {
     // the compact camera records gathered by LDS-DMA through the W staging
     // slot (C5 shard 707 -> 568 us against register gathers), 64.5 KB of
@@ -3385,6 +3534,18 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
     else
       hipLaunchKernelGGL((k_obs_w<false, double>), dim3(g), dim3(512), 0, s, P, W.JR, W.scale_c, W.scale_p, W.Linv, W.W);
   }
+}
+void launch_pcg_point_jf(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s) {
+  const double* st = W.scal + kNumSlots;
+  // (two 4-wave workgroups per CU at ~250 VGPRs, 76 KB of LDS each: a grid of
+  // that size, chunk-stride)
+  const int g = std::max(1, std::min((W.npchunks + 3) / 4, 2 * lds_grid(1 << 30)));
+  if (W.w32)
+    hipLaunchKernelGGL(k_pcg_point_jf<float>, dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks,
+                       (const double*)W.crec, (const double*)W.prec, W.scale_c, vec, W.vpt, W.tobs, st);
+  else
+    hipLaunchKernelGGL(k_pcg_point_jf<double>, dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks,
+                       (const double*)W.crec, (const double*)W.prec, W.scale_c, vec, W.vpt, W.tobs, st);
 }
 // camera slices of the diagonal pass
 int cam_split_count(const DevWork& W) { return W.cam_split; }

@@ -510,10 +510,10 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
     double v[3];
     if constexpr (PC) {
       // y = c x (c0[4] = c1[3] = 0), v = Z^T y
-      const double y0 = wr[0] * x[0] + wr[1] * x[1] + wr[2] * x[2] + wr[6] * x[3] + wr[7] * x[5];
-      const double y1 = wr[3] * x[0] + wr[4] * x[1] + wr[5] * x[2] + wr[8] * x[4] + wr[9] * x[5];
+      double wp[16];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) v[k] = live ? wr[10 + k] * y0 + wr[13 + k] * y1 : 0.0;
+      for (int k = 0; k < 16; ++k) wp[k] = wr[k];
+      pc_v(wp, x, live, v);
     } else {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -552,13 +552,10 @@ __global__ __launch_bounds__(256) void k_pcg_point_seg(DevProblem P, const int2*
       {   // (three 16-B LDS stores at 3 slots' stride: conflict-free)
         double tv[6];
         if constexpr (PC) {   // q = Z v_p, t_o = c^T q
-          const double q0 = wr[10] * vp[0] + wr[11] * vp[1] + wr[12] * vp[2];
-          const double q1 = wr[13] * vp[0] + wr[14] * vp[1] + wr[15] * vp[2];
+          double wp[16];
 #pragma unroll
-          for (int a = 0; a < 3; ++a) tv[a] = wr[a] * q0 + wr[3 + a] * q1;
-          tv[3] = wr[6] * q0;
-          tv[4] = wr[8] * q1;
-          tv[5] = wr[7] * q0 + wr[9] * q1;
+          for (int k = 0; k < 16; ++k) wp[k] = wr[k];
+          pc_t(wp, vp, tv);
         } else {
 #pragma unroll
           for (int a = 0; a < 6; ++a) tv[a] = wr[a * 3] * vp[0] + wr[a * 3 + 1] * vp[1] + wr[a * 3 + 2] * vp[2];
@@ -863,7 +860,9 @@ void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec,
   if (W.npchunks > 0) {   // point-aligned chunks of <= 64 observations (k_pcg_point_seg)
     const int g = std::max(1, std::min((W.npchunks + 3) / 4, 16384));
     if (W.tobs) {
-      if (W.pcgc && W.w32)   // (the 16-value rank-2 records)
+      if (W.pcgjf)   // (the records formed in the pass itself, no W)
+        launch_pcg_point_jf(P, W, vec, s);
+      else if (W.pcgc && W.w32)   // (the 16-value rank-2 records)
         hipLaunchKernelGGL((k_pcg_point_seg<float, true, true>), dim3(g), dim3(256), 0, s, P, W.pchunks, W.npchunks,
                            W.Wf, vec, W.vpt, W.tobs, st);
       else if (W.pcgc)

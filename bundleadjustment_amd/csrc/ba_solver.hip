@@ -870,6 +870,16 @@ void step_w_storage(ba_ctx* ctx, const ba_options& o) {
       ensure_pcg(ctx);
       W.pcgc = W.npchunks > 0 && ctx->pcg_ndup == 0;
     }
+    // fp64 beyond the LDS camera table (compact camera records): the point
+    // pass forms those records itself instead of reading them
+    // (k_pcg_point_jf, no W): C4 fixed radius 2.82 vs 3.14 ms per LM
+    // iteration, along the trajectory 3.66 vs 3.89, C4 shard 0.50 vs 0.56;
+    // with fp32 W (64-B records) the stored records win (C5 shard 3.65 vs
+    // 3.81 ms: profiles/r05_v5_pcg_jfree_ab.txt).  BA_PCG_JF=0 / 1 (read per
+    // solve) forces it off / on
+    const char* je = getenv("BA_PCG_JF");
+    const bool jf_ok = W.pcgc && ctx->P.nc > bahip::kLinLdsCamsHost;
+    W.pcgjf = jf_ok && (je ? je[0] != '0' : !W.w32);
   }
 }
 int step_enqueue(ba_ctx* ctx, double radius, const ba_options& o) {

@@ -191,6 +191,35 @@ def test_gpu_rank2_pcg_records_track_the_full_records(solver, cfg, scale, precis
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
+@pytest.mark.parametrize("shape", ["c4", "many"])
+def test_gpu_jfree_pcg_point_pass_is_bitwise_the_record_pass(solver, shape, precision, monkeypatch):
+    """Beyond the LDS camera table the PCG point pass forms the rank-2
+    records itself (k_pcg_point_jf, no W written or read) — the values
+    k_obs_w_rc<.., PC> stores (rounded to fp32 with MIXED_FP32), the record
+    and its products through the same contraction-free helpers (pc_record,
+    pc_v, pc_t) as the record-reading pair of passes (BA_PCG_JF=0).  lin_obs
+    is inlined into a different kernel, where the compiler may contract its
+    products into FMAs differently: the solves agree to rounding (costs
+    1e-12, parameters 1e-9) with the same CG counts and decisions."""
+    p = make_config("c4", scale=0.01) if shape == "c4" else make_synthetic(1300, 4000, obs_per_pt=4, seed=21)
+    kw = dict(preconditioner_type="SCHUR_JACOBI", max_num_iterations=6, precision=precision)
+    monkeypatch.setenv("BA_PCG_JF", "1")   # (the fp64 default; fp32 W keeps the records by default)
+    ca, xa, sa, la = gpu_solve(solver, p, **kw)
+    monkeypatch.setenv("BA_PCG_JF", "0")
+    cb, xb, sb, lb = gpu_solve(solver, p, **kw)
+    assert sa.final_cost == pytest.approx(sb.final_cost, rel=1e-12)
+    np.testing.assert_allclose(ca, cb, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(xa, xb, rtol=1e-9, atol=1e-12)
+    assert len(la) == len(lb)
+    for a, b in zip(la, lb):
+        assert a["cost"] == pytest.approx(b["cost"], rel=1e-12)
+        assert a["linear_solver_iterations"] == b["linear_solver_iterations"]
+        assert a["step_is_successful"] == b["step_is_successful"]
+    print("max |dcam| %.3g  max |dpt| %.3g" % (np.abs(ca - cb).max(), np.abs(xa - xb).max()))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("pc", PRECONDITIONERS)
 @pytest.mark.parametrize("cfg,scale", [("c1", 1.0), ("c2", 0.2), ("c3", 0.01)])
 @pytest.mark.parametrize("mv", MATVECS)
