@@ -102,6 +102,10 @@ struct DevWork {
   double* Minv;                      // [nvc][36] preconditioner block inverses
   double* pb; double* pr; double* pz; double* pp; double* pq;   // [n] CG vectors
   double* vpt;                       // [np][3] point-side products of one implicit matvec
+  double* vacc;                      // [np][3] sum over the CG iterations of alpha_k vpt(p_k) = vpt(y): the
+                                     // back substitution's E^T dc term without J (W.pacc; k_pcg_vacc)
+  bool pacc = false;
+  bool mcc_cam = true;               // this rank adds the camera terms of the block-form model cost change (rank 0)
   double* tobs;                      // [no][6] per-observation products W_o v_p (null: gather W in the camera pass)
   double* tpart;                     // [pcg_G][nvc][6] camera-side slices of one implicit matvec
   double* ppart;                     // [3][kMaxBlocks] per-block partials of the camera-side kernels
@@ -123,7 +127,11 @@ struct DevWork {
 // (PS_RHO1 / PS_Q01: the odd-iteration copies of rho and Q0 of the grid
 // kernels, whose lead block must not overwrite a value the other blocks of
 // the same launch still read)
-enum PcgState { PS_RHO = 0, PS_Q0, PS_ALPHA, PS_NORM_B, PS_ITER, PS_DONE, PS_TERM, PS_RHO1, PS_Q01, kPcgState };
+// PS_AAPP / PS_AAPP_IT: the step length of the last CG iteration that moved x,
+// and that iteration (k_pcg_vacc folds it into the points' accumulated
+// products)
+enum PcgState { PS_RHO = 0, PS_Q0, PS_ALPHA, PS_NORM_B, PS_ITER, PS_DONE, PS_TERM, PS_RHO1, PS_Q01, PS_AAPP, PS_AAPP_IT,
+                kPcgState };
 enum PcgTerm { PCG_SUCCESS = 0, PCG_NO_CONVERGENCE = 1, PCG_FAILURE = 2 };
 struct PcgOpts { double q_tolerance; int min_iter, max_iter, schur_jacobi; };
 
@@ -180,6 +188,10 @@ void launch_pcg_dup(const DevProblem& P, const DevWork& W, hipStream_t s);   // 
 void launch_pcg_matvec(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s);
 // the J-free point pass of one implicit matvec (W.pcgjf): v_p into W.vpt, t_o into W.tobs
 void launch_pcg_point_jf(const DevProblem& P, const DevWork& W, const double* vec, hipStream_t s);
+// W.pacc: after a CG update (set = false) W.vacc += alpha vpt when iteration
+// `it` moved x (W.vacc = alpha vpt at it = 1); after the residual reset's
+// matvec of y (set = true) W.vacc = vpt
+void launch_pcg_vacc(const DevProblem& P, const DevWork& W, int it, bool set, hipStream_t s);
 // exchange path: fold the matvec's camera slices into slice 0 (one 6 nvc all-reduce)
 void launch_pcg_tfold(const DevProblem& P, const DevWork& W, hipStream_t s);
 // mode 0: full CG iteration; 1: up to the x update; 2: residual reset from W.tpart = matvec(x)

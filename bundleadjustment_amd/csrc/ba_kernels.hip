@@ -2151,15 +2151,34 @@ __global__ __launch_bounds__(256) void k_cam_fold_diag(DevProblem P, const doubl
 // ---------------------------------------------------------------------------
 // one 64-lane block per camera: lanes 0..5 form the step, every lane
 // evaluates the (cheap) Rodrigues and writes record entries lane, lane + 64
+// Hcc, gc != nullptr (the block form of the model cost change, k_point_step_rc
+// ACC): + gc^T dc + dc^T Hcc dc / 2 per variable camera into SL_MCC_NEG
 __global__ __launch_bounds__(64) void k_cam_candidate(DevProblem P, const double* __restrict__ cams,
                                                       const double* __restrict__ y, const double* __restrict__ scale_c,
                                                       double* __restrict__ cams_c, double* __restrict__ delta_c,
-                                                      double* __restrict__ rec_c, double* __restrict__ part) {
-  __shared__ double lds[2 * 16];
+                                                      double* __restrict__ rec_c, double* __restrict__ part,
+                                                      const double* __restrict__ Hcc, const double* __restrict__ gc) {
+  __shared__ double lds[3 * 16];
   const int lane = threadIdx.x;
-  double acc[2] = {0.0, 0.0};  // step2, bad
+  double acc[3] = {0.0, 0.0, 0.0};  // step2, bad, model terms
   for (int c = blockIdx.x; c < P.nc; c += gridDim.x) {
     const int v = P.vc[c];
+    if (Hcc && v >= 0 && lane == 0) {
+      double d[6];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) d[a] = (-y[6 * v + a]) * scale_c[(size_t)v * 6 + a];
+      const double* h = Hcc + (size_t)v * 21;
+      double dhd = 0.0, gd = 0.0;
+      int t = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+#pragma unroll
+        for (int b = 0; b < a; ++b) dhd += 2.0 * h[t++] * d[a] * d[b];
+        dhd += h[t++] * d[a] * d[a];
+        gd += gc[(size_t)v * 6 + a] * d[a];
+      }
+      acc[2] += gd + 0.5 * dhd;
+    }
     double xc[6];
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
@@ -2191,11 +2210,12 @@ __global__ __launch_bounds__(64) void k_cam_candidate(DevProblem P, const double
       o[e] = val;
     }
   }
-  double out[2];
-  block_sum<2>(acc, lds, out);
+  double out[3];
+  block_sum<3>(acc, lds, out);
   if (threadIdx.x == 0) {
     part_of(part, SL_STEP2_C)[blockIdx.x] = out[0];
     part_of(part, SL_STEP_BAD)[blockIdx.x] += out[1];
+    if (Hcc) part_of(part, SL_MCC_NEG)[blockIdx.x] += out[2];
   }
 }
 
@@ -3113,14 +3133,26 @@ __global__ __launch_bounds__(NT) void k_cam_schur_diag_rc(DevProblem P, const do
 //           candidate residual at (camera', x'_p) per observation.
 // TB 2 (nc > kLinLdsCams): rec is the compact records crec, rec_c the
 // global candidate table ctbl (k_cand_table)
-template <int NT, int LANES, int KC = 3, int TB = 0>
+// ACC (ITERATIVE_SCHUR, W.pacc): no J at all.  Pass 1 is w = u_p - vacc_p
+// (vacc = vpt(y), accumulated over the CG iterations: k_pcg_vacc); the model
+// cost change is taken from the blocks instead of per observation:
+//   (J d)^T (r + J d / 2) summed = g^T d + d^T H d / 2 with
+//   d^T H d = sum_c dc^T Hcc dc + sum_p dp^T Hpp dp + 2 sum_p dp^T v_p,
+//   v_p = sum_o Jp^T Jc dc = -(L_p vacc_p) / s_p, so dp^T v_p = yp^T (L_p vacc_p)
+// — the point terms here (per point, Hpp and gp of the linearisation), the
+// camera terms in k_cam_candidate (mcc_cam).  The same quantity as Ceres'
+// per-residual sum, up to rounding.  Pass 2 is the candidate cost alone.
+template <int NT, int LANES, int KC = 3, int TB = 0, bool ACC = false>
 __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double* __restrict__ rec,
                                                       const double* __restrict__ pts,
                                                       const double* __restrict__ delta_c,
                                                       const double* __restrict__ rec_c, const double* __restrict__ u,
                                                       const double* __restrict__ Linv,
                                                       const double* __restrict__ scale_p, double* __restrict__ pts_c,
-                                                      double* __restrict__ delta_p, double* __restrict__ part) {
+                                                      double* __restrict__ delta_p, double* __restrict__ part,
+                                                      const double* __restrict__ vacc = nullptr,
+                                                      const double* __restrict__ Hpp = nullptr,
+                                                      const double* __restrict__ gp = nullptr) {
   __shared__ double lds[5 * 16];
   __shared__ __attribute__((aligned(16))) double tbl[TB ? 2 : kLinLdsCams * kTblRec];
   __shared__ float ktb[TB ? 1 : kLinLdsCams * 9];
@@ -3170,8 +3202,34 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
       // pass 1's J (Jc dc, Jp, r: 10 doubles), so pass 2 recomputes J only
       // past them (points with more than LANES * KC observations) and for
       // fixed points (no pass 1)
-      double kc[KC][10];
-      if (pv) {
+      double kc[ACC ? 1 : KC][10];
+      if (ACC && pv) {
+        // w = u_p - vpt_p(y), the point step and its model-cost terms (lane 0)
+        const double s0 = scale_p[p], s1 = scale_p[np + p], s2 = scale_p[2 * np + p];
+        const double i00 = Linv[p], i10 = Linv[np + p], i11 = Linv[2 * np + p];
+        const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
+        const double a0 = vacc[3 * (size_t)p], a1 = vacc[3 * (size_t)p + 1], a2 = vacc[3 * (size_t)p + 2];
+        const double w0 = u[4 * p] - a0, w1 = u[4 * p + 1] - a1, w2 = u[4 * p + 2] - a2;
+        const double yp[3] = {i00 * w0 + i10 * w1 + i20 * w2, i11 * w1 + i21 * w2, i22 * w2};
+        const double sp[3] = {s0, s1, s2};
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dX[k] = (-yp[k]) * sp[k];
+        if (sl == 0) {
+          // t = L_p vacc_p (L_p^-1 t = vacc_p)
+          const double t0 = a0 / i00;
+          const double t1 = (a1 - i10 * t0) / i11;
+          const double t2 = (a2 - i20 * t0 - i21 * t1) / i22;
+          const double h00 = Hpp[p], h10 = Hpp[np + p], h20 = Hpp[2 * np + p];
+          const double h11 = Hpp[3 * np + p], h21 = Hpp[4 * np + p], h22 = Hpp[5 * np + p];
+          const double hd0 = h00 * dX[0] + h10 * dX[1] + h20 * dX[2];
+          const double hd1 = h10 * dX[0] + h11 * dX[1] + h21 * dX[2];
+          const double hd2 = h20 * dX[0] + h21 * dX[1] + h22 * dX[2];
+          const double gd = gp[p] * dX[0] + gp[np + p] * dX[1] + gp[2 * np + p] * dX[2];
+          const double dhd = dX[0] * hd0 + dX[1] * hd1 + dX[2] * hd2;
+          const double ytv = yp[0] * t0 + yp[1] * t1 + yp[2] * t2;
+          acc[2] += gd + 0.5 * dhd + ytv;
+        }
+      } else if (!ACC && pv) {
         // pass 1: v = sum Jp^T (Jc dc)
         double v0 = 0.0, v1 = 0.0, v2 = 0.0;
         int o = o0 + sl;
@@ -3250,8 +3308,10 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
           const float2 uvn = P.uv[on];
           const bool cfix = P.cam_fixed && P.cam_fixed[c];
           // k_candidate_lds' arithmetic
-          double jd0, jd1, jp[6], r0, r1;
-          if (keep) {
+          double jd0 = 0.0, jd1 = 0.0, jp[6], r0 = 0.0, r1 = 0.0;
+          if constexpr (ACC) {
+            (void)jp;
+          } else if (keep) {
             jd0 = keep[0]; jd1 = keep[1];
 #pragma unroll
             for (int k = 0; k < 6; ++k) jp[k] = keep[2 + k];
@@ -3268,9 +3328,12 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
             for (int k = 0; k < 6; ++k) jp[k] = j[12 + k];
             r0 = j[18]; r1 = j[19];
           }
-          jd0 += jp[0] * dX[0] + jp[1] * dX[1] + jp[2] * dX[2];
-          jd1 += jp[3] * dX[0] + jp[4] * dX[1] + jp[5] * dX[2];
-          const double mneg = jd0 * (r0 + jd0 / 2.0) + jd1 * (r1 + jd1 / 2.0);
+          double mneg = 0.0;
+          if constexpr (!ACC) {
+            jd0 += jp[0] * dX[0] + jp[1] * dX[1] + jp[2] * dX[2];
+            jd1 += jp[3] * dX[0] + jp[4] * dX[1] + jp[5] * dX[2];
+            mneg = jd0 * (r0 + jd0 / 2.0) + jd1 * (r1 + jd1 / 2.0);
+          }
           double pcand[3];
           if (!cfix) {
             double cr[12];
@@ -3309,17 +3372,17 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
           const double rc0 = q[0] / q[2] - (double)uv.x, rc1 = q[1] / q[2] - (double)uv.y;
           double sc;
           const double rho = huber(rc0 * rc0 + rc1 * rc1, P.huber_a, P.huber_b, &sc);
-          acc[2] += mneg;
+          if constexpr (!ACC) acc[2] += mneg;
           acc[3] += 0.5 * rho;
           if (!isfinite(rc0) || !isfinite(rc1)) acc[4] += 1.0;
           c = cn;
           uv = uvn;
           o += LANES;
         };
-        if (pv) {
+        if (!ACC && pv) {
 #pragma unroll
           for (int k = 0; k < KC; ++k)
-            if (o < o1) obs2(kc[k]);
+            if (o < o1) obs2(kc[ACC ? 0 : k]);
         }
         while (o < o1) obs2(nullptr);
       }
@@ -3333,7 +3396,8 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
   if (threadIdx.x == 0) {
     part_of(part, SL_STEP2_P)[blockIdx.x] = tot[0];
     part_of(part, SL_STEP_BAD)[blockIdx.x] += tot[1];
-    part_of(part, SL_MCC_NEG)[blockIdx.x] = tot[2];
+    if (ACC) part_of(part, SL_MCC_NEG)[blockIdx.x] += tot[2];   // (k_cam_candidate's camera terms are there)
+    else part_of(part, SL_MCC_NEG)[blockIdx.x] = tot[2];
     part_of(part, SL_CCOST)[blockIdx.x] = tot[3];
     part_of(part, SL_CAND_BAD)[blockIdx.x] = tot[4];
   }
@@ -3673,8 +3737,12 @@ void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, h
 }
 void launch_cam_candidate(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nc == 0) return;
+  // (the camera terms of the block-form model cost change: once over the
+  // ranks, on rank 0 — SL_MCC_NEG is summed across them)
+  const bool mc = W.pacc && W.mcc_cam;
   hipLaunchKernelGGL(k_cam_candidate, dim3(P.nc < kMaxBlocks ? P.nc : kMaxBlocks), dim3(64), 0, s, P, W.cams, W.y,
-                     W.scale_c, W.cams_c, W.delta_c, W.rec_c, W.part);
+                     W.scale_c, W.cams_c, W.delta_c, W.rec_c, W.part, mc ? (const double*)W.Hcc : nullptr,
+                     mc ? (const double*)W.gc : nullptr);
 }
 // J-free: back substitution + model cost change + candidate cost in one
 // point-major pass (k_point_step_rc; separate back substitution and
@@ -3688,9 +3756,14 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
     constexpr int NT = 512, L = 4;
     const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
     const int g = std::max(1, std::min(want, kMaxBlocks));
-    hipLaunchKernelGGL((k_point_step_rc<NT, L, 3, 2>), dim3(g), dim3(NT), 0, s, P, (const double*)W.crec,
-                       (const double*)W.pts, W.delta_c, (const double*)W.ctbl, W.u, W.Linv, W.scale_p, W.pts_c,
-                       W.delta_p, W.part);
+    if (W.pacc)
+      hipLaunchKernelGGL((k_point_step_rc<NT, L, 3, 2, true>), dim3(g), dim3(NT), 0, s, P, (const double*)W.crec,
+                         (const double*)W.pts, W.delta_c, (const double*)W.ctbl, W.u, W.Linv, W.scale_p, W.pts_c,
+                         W.delta_p, W.part, (const double*)W.vacc, (const double*)W.Hpp, (const double*)W.gp);
+    else
+      hipLaunchKernelGGL((k_point_step_rc<NT, L, 3, 2>), dim3(g), dim3(NT), 0, s, P, (const double*)W.crec,
+                         (const double*)W.pts, W.delta_c, (const double*)W.ctbl, W.u, W.Linv, W.scale_p, W.pts_c,
+                         W.delta_p, W.part);
     return;
   }
   if (W.jrfree) {
@@ -3700,8 +3773,13 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
     constexpr int NT = 512, L = 4;
     const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
     const int g = std::max(1, std::min(want, lds_grid(1 << 30)));   // one 110-KB-LDS workgroup per CU
-    hipLaunchKernelGGL((k_point_step_rc<NT, L>), dim3(g), dim3(NT), 0, s, P, (const double*)W.rec,
-                       (const double*)W.pts, W.delta_c, W.rec_c, W.u, W.Linv, W.scale_p, W.pts_c, W.delta_p, W.part);
+    if (W.pacc)
+      hipLaunchKernelGGL((k_point_step_rc<NT, L, 3, 0, true>), dim3(g), dim3(NT), 0, s, P, (const double*)W.rec,
+                         (const double*)W.pts, W.delta_c, W.rec_c, W.u, W.Linv, W.scale_p, W.pts_c, W.delta_p, W.part,
+                         (const double*)W.vacc, (const double*)W.Hpp, (const double*)W.gp);
+    else
+      hipLaunchKernelGGL((k_point_step_rc<NT, L>), dim3(g), dim3(NT), 0, s, P, (const double*)W.rec,
+                         (const double*)W.pts, W.delta_c, W.rec_c, W.u, W.Linv, W.scale_p, W.pts_c, W.delta_p, W.part);
     return;
   }
   if (W.w32)

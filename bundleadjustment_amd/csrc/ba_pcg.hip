@@ -234,6 +234,7 @@ __global__ __launch_bounds__(64) void k_pcg_setup_fin(const double* __restrict__
   if (threadIdx.x == 0) {
     st[PS_RHO] = st[PS_RHO1] = 1.0; st[PS_Q0] = st[PS_Q01] = -0.0; st[PS_ALPHA] = 0.0; st[PS_NORM_B] = sqrt(bb);
     st[PS_ITER] = 0.0; st[PS_DONE] = 0.0; st[PS_TERM] = PCG_NO_CONVERGENCE;
+    st[PS_AAPP] = 0.0; st[PS_AAPP_IT] = 0.0;
     scal[SL_CHOL_BAD] = 0.0;   // linear-solver failure flag of this step
     scal[SL_CHOL_SPIN] = 0.0;  // (a dense step's spin on this context must not fail this one)
   }
@@ -662,6 +663,7 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(DevProblem P, int mo
       for (int a = 0; a < 6; ++a) xv[a] = xv[a] + alpha * pv[a];
       store6(x + o6, xv);
     }
+    if (threadIdx.x == 0) { st[PS_AAPP] = alpha; st[PS_AAPP_IT] = it; }   // x moved (k_pcg_vacc)
     if (mode == 1) {
       if (threadIdx.x == 0) st[PS_ALPHA] = alpha;
       return;
@@ -772,6 +774,7 @@ __global__ __launch_bounds__(256) void k_pcg_xr(DevProblem P, int mode, int it, 
     if (live)
 #pragma unroll
       for (int a = 0; a < 6; ++a) x[6 * (size_t)v + a] = x[6 * (size_t)v + a] + alpha * p[6 * (size_t)v + a];
+    if (blockIdx.x == 0 && threadIdx.x == 0) { st[PS_AAPP] = alpha; st[PS_AAPP_IT] = it; }   // (k_pcg_vacc)
     if (mode == 1) {
       if (blockIdx.x == 0 && threadIdx.x == 0) st[PS_ALPHA] = alpha;
       return;
@@ -837,9 +840,35 @@ __global__ __launch_bounds__(256) void k_pcg_p(DevProblem P, int it, PcgOpts o, 
   }
 }
 
+// The points' accumulated products: y = sum_k alpha_k p_k (x starts at 0), so
+// vpt(y) = sum_k alpha_k vpt(p_k) by linearity — the back substitution's
+// u_p - sum_o W_o^T y_c without a pass over the observations (W.pacc).  set:
+// the residual reset's matvec of y itself (skipped once the CG has stopped:
+// that matvec did not run).  Otherwise fold alpha vpt when the update of
+// iteration `it` moved x (PS_AAPP_IT), from zero at it = 1.
+__global__ __launch_bounds__(256) void k_pcg_vacc(int n3, int it, int set, const double* __restrict__ st,
+                                                  const double* __restrict__ vpt, double* __restrict__ vacc) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n3) return;
+  if (set) {
+    if (st[PS_DONE] == 0.0) vacc[e] = vpt[e];
+    return;
+  }
+  const bool moved = st[PS_AAPP_IT] == (double)it;
+  const double base = it == 1 ? 0.0 : vacc[e];
+  if (moved) vacc[e] = base + st[PS_AAPP] * vpt[e];
+  else if (it == 1) vacc[e] = 0.0;
+}
+
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+void launch_pcg_vacc(const DevProblem& P, const DevWork& W, int it, bool set, hipStream_t s) {
+  const int n3 = 3 * P.np;
+  if (n3 == 0) return;
+  hipLaunchKernelGGL(k_pcg_vacc, dim3((n3 + 255) / 256), dim3(256), 0, s, n3, it, set ? 1 : 0, W.scal + kNumSlots,
+                     W.vpt, W.vacc);
+}
 void launch_pcg_dup(const DevProblem& P, const DevWork& W, hipStream_t s) {
   if (P.nvc == 0) return;
   if (W.w32)

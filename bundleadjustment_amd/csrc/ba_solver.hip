@@ -596,6 +596,7 @@ void ensure_pcg(ba_ctx* ctx) {
   W.pp = ctx->dalloc<double>(n);
   W.pq = ctx->dalloc<double>(n);
   W.vpt = ctx->dalloc<double>(3 * (size_t)std::max(np, 1));
+  W.vacc = ctx->dalloc<double>(3 * (size_t)std::max(np, 1));
   W.tpart = ctx->dalloc<double>((size_t)W.pcg_G * 6 * std::max(nvc, 1));
   W.ppart = ctx->dalloc<double>(3 * (size_t)kMaxBlocks);
   if ((nvc + 255) / 256 > kMaxBlocks) throw BaError{BA_ERR_INVALID_ARGUMENT, "too many cameras for ITERATIVE_SCHUR"};
@@ -807,7 +808,10 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
   const size_t tcount = (size_t)6 * ctx->nvc;
   W.pcg_folded = ctx->coll();
   if (ctx->coll()) ctx->allreduce(W.Sd, 27 * (size_t)ctx->nvc);
-  if (ctx->nvc == 0) return 0;
+  if (ctx->nvc == 0) {
+    if (W.pacc && P.np > 0) HIP_OK(hipMemsetAsync(W.vacc, 0, sizeof(double) * 3 * (size_t)P.np, s));   // (y = 0)
+    return 0;
+  }
   launch_pcg_setup(P, W, radius, po, s);
   int it = 0, batch = 4;
   for (;;) {
@@ -818,10 +822,12 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
       if (it % 10 == 0) {   // ceres residual_reset_period: r = b - S x
         launch_pcg_update(P, W, 1, it, po, s);
         launch_pcg_matvec(P, W, W.y, s);
+        if (W.pacc) launch_pcg_vacc(P, W, it, true, s);   // vpt(y) itself
         if (ctx->coll()) { launch_pcg_tfold(P, W, s); ctx->allreduce(W.tpart, tcount); }
         launch_pcg_update(P, W, 2, it, po, s);
       } else {
         launch_pcg_update(P, W, 0, it, po, s);
+        if (W.pacc) launch_pcg_vacc(P, W, it, false, s);
       }
     }
     ctx->read_scalars();
@@ -877,6 +883,19 @@ void step_w_storage(ba_ctx* ctx, const ba_options& o) {
     // with fp32 W (64-B records) the stored records win (C5 shard 3.65 vs
     // 3.81 ms: profiles/r05_v5_pcg_jfree_ab.txt).  BA_PCG_JF=0 / 1 (read per
     // solve) forces it off / on
+    // fp64: the back substitution from the CG's accumulated point products
+    // (no J in k_point_step_rc: k_pcg_vacc, the block-form model cost change).
+    // Not with fp32 W: the products would carry the rounded blocks into the
+    // back substitution, which MIXED_FP32 keeps exact (the oracle's mixed
+    // modes restate it so).  BA_PCG_PACC=0 (read per solve) recomputes J per
+    // observation
+    W.pacc = false;
+    const char* ae = getenv("BA_PCG_PACC");
+    if (o.linear_solver == BA_ITERATIVE_SCHUR && W.jrfree && !W.w32 && !(ae && ae[0] == '0')) {
+      ensure_pcg(ctx);
+      W.pacc = W.npchunks > 0;
+    }
+    W.mcc_cam = ctx->rank == 0;
     const char* je = getenv("BA_PCG_JF");
     const bool jf_ok = W.pcgc && ctx->P.nc > bahip::kLinLdsCamsHost;
     W.pcgjf = jf_ok && (je ? je[0] != '0' : !W.w32);
