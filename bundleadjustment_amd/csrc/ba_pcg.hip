@@ -846,18 +846,29 @@ __global__ __launch_bounds__(256) void k_pcg_p(DevProblem P, int it, PcgOpts o, 
 // the residual reset's matvec of y itself (skipped once the CG has stopped:
 // that matvec did not run).  Otherwise fold alpha vpt when the update of
 // iteration `it` moved x (PS_AAPP_IT), from zero at it = 1.
+// (four doubles per thread as two 16-B pieces, grid-stride: 35 -> 14.6 us per
+// working launch at C4, profiles/r05_final_c4full_kernel_stats.csv)
 __global__ __launch_bounds__(256) void k_pcg_vacc(int n3, int it, int set, const double* __restrict__ st,
                                                   const double* __restrict__ vpt, double* __restrict__ vacc) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n3) return;
-  if (set) {
-    if (st[PS_DONE] == 0.0) vacc[e] = vpt[e];
-    return;
-  }
+  const bool done = st[PS_DONE] != 0.0;
   const bool moved = st[PS_AAPP_IT] == (double)it;
-  const double base = it == 1 ? 0.0 : vacc[e];
-  if (moved) vacc[e] = base + st[PS_AAPP] * vpt[e];
-  else if (it == 1) vacc[e] = 0.0;
+  const double al = st[PS_AAPP];
+  if (set ? done : (!moved && it != 1)) return;   // (nothing to write)
+  auto one = [&](double v, double a) { return set ? v : (moved ? (it == 1 ? 0.0 : a) + al * v : 0.0); };
+  const int n4 = n3 >> 2;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += gridDim.x * blockDim.x) {
+    const double2* v2 = reinterpret_cast<const double2*>(vpt) + 2 * q;
+    double2* a2 = reinterpret_cast<double2*>(vacc) + 2 * q;
+    const double2 v0 = v2[0], v1 = v2[1];
+    double2 a0 = make_double2(0.0, 0.0), a1 = make_double2(0.0, 0.0);
+    if (!set && it != 1) { a0 = a2[0]; a1 = a2[1]; }
+    a2[0] = make_double2(one(v0.x, a0.x), one(v0.y, a0.y));
+    a2[1] = make_double2(one(v1.x, a1.x), one(v1.y, a1.y));
+  }
+  if (blockIdx.x == 0 && (int)threadIdx.x < (n3 & 3)) {
+    const int e = 4 * n4 + threadIdx.x;
+    vacc[e] = one(vpt[e], (!set && it != 1) ? vacc[e] : 0.0);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -866,7 +877,8 @@ __global__ __launch_bounds__(256) void k_pcg_vacc(int n3, int it, int set, const
 void launch_pcg_vacc(const DevProblem& P, const DevWork& W, int it, bool set, hipStream_t s) {
   const int n3 = 3 * P.np;
   if (n3 == 0) return;
-  hipLaunchKernelGGL(k_pcg_vacc, dim3((n3 + 255) / 256), dim3(256), 0, s, n3, it, set ? 1 : 0, W.scal + kNumSlots,
+  const int g = std::max(1, std::min((n3 / 4 + 255) / 256, 2048));
+  hipLaunchKernelGGL(k_pcg_vacc, dim3(g), dim3(256), 0, s, n3, it, set ? 1 : 0, W.scal + kNumSlots,
                      W.vpt, W.vacc);
 }
 void launch_pcg_dup(const DevProblem& P, const DevWork& W, hipStream_t s) {
