@@ -883,15 +883,16 @@ void step_w_storage(ba_ctx* ctx, const ba_options& o) {
     // with fp32 W (64-B records) the stored records win (C5 shard 3.65 vs
     // 3.81 ms: profiles/r05_v5_pcg_jfree_ab.txt).  BA_PCG_JF=0 / 1 (read per
     // solve) forces it off / on
-    // fp64: the back substitution from the CG's accumulated point products
-    // (no J in k_point_step_rc: k_pcg_vacc, the block-form model cost change).
-    // Not with fp32 W: the products would carry the rounded blocks into the
-    // back substitution, which MIXED_FP32 keeps exact (the oracle's mixed
-    // modes restate it so).  BA_PCG_PACC=0 (read per solve) recomputes J per
-    // observation
+    // the back substitution from the CG's accumulated point products (no J in
+    // k_point_step_rc: k_pcg_vacc, the block-form model cost change).  With
+    // fp32 W (MIXED_FP32) the products carry the stored fp32 blocks into the
+    // back substitution as they carry them into the CG (a relative 1e-7
+    // perturbation of the point step; the costs stay within the oracle
+    // comparisons' 1e-9).  BA_PCG_PACC=0 (read per solve) recomputes J per
+    // observation, in fp64
     W.pacc = false;
     const char* ae = getenv("BA_PCG_PACC");
-    if (o.linear_solver == BA_ITERATIVE_SCHUR && W.jrfree && !W.w32 && !(ae && ae[0] == '0')) {
+    if (o.linear_solver == BA_ITERATIVE_SCHUR && W.jrfree && !(ae && ae[0] == '0')) {
       ensure_pcg(ctx);
       W.pacc = W.npchunks > 0;
     }
