@@ -29,6 +29,11 @@
 namespace bahip {
 
 constexpr int kPcgThreads = 1024;   // camera-side workgroup
+// k_pcg_update (one workgroup) up to this many cameras, the grid kernels past
+// it: at 1000 cameras the one workgroup's strided Adiag / Minv reads go
+// through one CU (~35 us per working launch); C4 3893 -> 3898 M-obs/s with the
+// grid kernels (profiles/r05_v10_pcg_update_form_ab.txt)
+constexpr int kPcgOneWg = 256;
 
 // LDS hand-off between the lanes of one wave (in-order DS operations)
 __device__ inline void wave_lds_sync_pcg() {
@@ -615,7 +620,7 @@ __global__ __launch_bounds__(256) void k_pcg_tfold(int nvc, int G, double* __res
 //   NO_CONVERGENCE; then iteration it+1 begins: z = M r, rho' = r.z,
 //   beta = rho' / rho (zero or inf: FAILURE), p = z + beta p.
 // ---------------------------------------------------------------------------
-// nvc <= kPcgThreads: one camera per thread, its vectors held in registers
+// nvc <= kPcgOneWg: one camera per thread, its vectors held in registers
 // across the phases (every load issued at the start, each vector stored once;
 // the per-phase re-reads of the loop form cost a dependent L2 round trip per
 // phase: C4 shard 15.4 us per launch).  The same operations per camera in the
@@ -718,7 +723,7 @@ __global__ __launch_bounds__(kPcgThreads) void k_pcg_update(DevProblem P, int mo
 }
 
 // ---------------------------------------------------------------------------
-// The same CG iteration for large camera counts (nvc > kPcgThreads): three
+// The same CG iteration for larger camera counts (nvc > kPcgOneWg): three
 // grid kernels, thread per camera; each block folds the previous kernel's
 // per-block partials itself (fixed order: every block reaches the same
 // decisions), block 0 records the state.
@@ -954,7 +959,7 @@ void launch_pcg_tfold(const DevProblem& P, const DevWork& W, hipStream_t s) {
 void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, const PcgOpts& o, hipStream_t s) {
   // (after launch_pcg_tfold the slices are folded into slice 0: G = 1)
   const int G = W.pcg_folded ? 1 : W.pcg_G;
-  if (P.nvc <= kPcgThreads) {   // one workgroup: one launch per CG iteration
+  if (P.nvc <= kPcgOneWg) {   // one workgroup: one launch per CG iteration
     hipLaunchKernelGGL(k_pcg_update, dim3(1), dim3(kPcgThreads), 0, s, P, mode, it, o, G, W.Adiag, W.Minv,
                        W.pb, W.y, W.pr, W.pz, W.pp, W.pq, W.tpart, W.scal);
     return;

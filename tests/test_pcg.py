@@ -314,7 +314,7 @@ def test_gpu_iterative_is_deterministic(solver):
 
 @pytest.mark.gpu
 def test_gpu_iterative_grid_path_is_deterministic(solver):
-    """> 1024 cameras (thread-per-camera grid kernels, many workgroups per
+    """> 256 cameras (thread-per-camera grid kernels, many workgroups per
     CG step): repeated solves are bitwise identical.  Guards the hand-off of
     rho / Q0 between CG iterations (the lead workgroup writes the next
     iteration's values into the other parity slot while the other workgroups
@@ -357,7 +357,7 @@ def test_gpu_iterative_rejects_bad_options(solver):
 @pytest.mark.gpu
 @pytest.mark.parametrize("pc", PRECONDITIONERS)
 def test_gpu_iterative_many_cameras(solver, oracle_lib, pc):
-    """> 1024 variable cameras: the camera side runs as thread-per-camera grid
+    """> 256 variable cameras: the camera side runs as thread-per-camera grid
     kernels (k_pcg_q / k_pcg_xr / k_pcg_p) instead of one workgroup; the
     per-camera gathers use one slice per camera."""
     p = make_synthetic(1300, 4000, obs_per_pt=4, seed=21)
