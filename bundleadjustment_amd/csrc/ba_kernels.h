@@ -168,8 +168,11 @@ void launch_point_elim(const DevProblem& P, const DevWork& W, double radius, hip
 // rank): add s Hcc s + D^2 and s g_c in the same pass (no launch_cam_add_diag)
 void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s, double* compact = nullptr,
                            double radius = 0.0, bool skip_fold = false);
-void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius = 0.0);
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius = 0.0,
+                        bool with_diag = false);
 bool pairs_take_fold(const DevProblem& P, const DevWork& W);
+bool pairs_take_diag(const DevProblem& P, const DevWork& W);
+void launch_cam_fold_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
 // ba_chol.hip; epoch: per-context launch counter (>= 1) tagging the
 // back substitution's hand-off flags

@@ -1851,6 +1851,9 @@ __device__ __forceinline__ void glds16(const double* src, double* lds_dst) {
   __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }
 constexpr int kPairsDmaLds = 4 * 2 * 64 * kWcRec * (int)sizeof(double);   // 64 KB: 4 waves x (row, partner) x 64 records
+#ifndef DIAG_IN_PAIRS
+#define DIAG_IN_PAIRS 1
+#endif
 
 // one camera slice (v, slice g of G) by one wave: the per-lane sums
 __device__ __forceinline__ void diag_cd_wave(const DevProblem& P, const double* __restrict__ Wc,
@@ -1984,18 +1987,41 @@ struct FoldArgs {
   const double* diag_c;
   double radius;
   double* scal;
+  // G > 0: those workgroups run the diagonal slices instead (four waves, each
+  // one (camera, slice) of k_cam_schur_diag_cd into cpart), independent of the
+  // pairs; the fold then follows in its own launch
+  const double* u = nullptr;
+  int G = 0;
 };
 __global__ __launch_bounds__(256) void k_schur_pairs_cd(DevProblem P, const int4* __restrict__ blocks,
                                                         const int* __restrict__ xoff, const int2* __restrict__ pairs,
                                                         const double* __restrict__ Wc,
                                                         const double* __restrict__ scale_c, double* __restrict__ S,
                                                         int pgrid, FoldArgs fa) {
+  extern __shared__ double dsm[];
   if ((int)blockIdx.x >= pgrid) {
+    if (fa.G > 0) {
+      const int wv = threadIdx.x >> 6;
+      const int unit = ((int)blockIdx.x - pgrid) * (int)(blockDim.x >> 6) + wv;
+      if (unit >= P.nvc * fa.G) return;
+      const int v = unit / fa.G, g = unit - v * fa.G;
+      double* rb = dsm + (size_t)wv * 2 * 64 * kWcRec;
+      double acc[27];
+      diag_cd_wave(P, Wc, scale_c, fa.u, v, g, fa.G, rb, rb + 64 * kWcRec, acc);
+      double tot[27];
+#pragma unroll
+      for (int k = 0; k < 27; ++k) tot[k] = 0.0 + wave_sum(acc[k]);   // (block_sum's value for one wave)
+      if ((threadIdx.x & 63) == 0) {
+        double* dst = const_cast<double*>(fa.cpart) + ((size_t)g * P.nvc + v) * 27;
+#pragma unroll
+        for (int k = 0; k < 27; ++k) dst[k] = tot[k];
+      }
+      return;
+    }
     cam_fold_diag_entry(P, fa.cpart, fa.nsl, fa.Hcc, fa.gc, scale_c, fa.diag_c, fa.radius, S, fa.scal,
                         ((int)blockIdx.x - pgrid) * blockDim.x + threadIdx.x);
     return;
   }
-  extern __shared__ double dsm[];
   WcCam* ctab = reinterpret_cast<WcCam*>(dsm + kPairsDmaLds / (int)sizeof(double));
   for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
   __syncthreads();
@@ -3665,7 +3691,14 @@ void launch_cam_schur_diag(const DevProblem& P, const DevWork& W, hipStream_t s,
 bool pairs_take_fold(const DevProblem& P, const DevWork& W) {
   return W.nblocks > 0 && W.wcompact && kPairsDmaLds + sizeof(WcCam) * (size_t)P.nvc <= 80 * 1024;
 }
-void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius) {
+void launch_cam_fold_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s) {
+  hipLaunchKernelGGL(k_cam_fold_diag, dim3((P.nvc * 27 + 255) / 256), dim3(256), 0, s, P, W.cpart,
+                     cam_split_count(W), W.Hcc, W.gc, W.scale_c, W.diag_c, radius, W.S, W.scal);
+}
+bool pairs_take_diag(const DevProblem& P, const DevWork& W) {
+  return DIAG_IN_PAIRS && pairs_take_fold(P, W) && !W.jdiag && !W.w32 && P.nvc > 0;
+}
+void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius, bool with_diag) {
   if (W.nblocks == 0) return;
   // 16 blocks per workgroup (4 waves of 4) over the largest XCD range, at
   // most 2048 workgroups (256 sweeping the ranges in rounds ties it:
@@ -3682,7 +3715,11 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, do
   if (W.wcompact && kPairsDmaLds + ctab_bytes <= 80 * 1024) {
     FoldArgs fa{W.cpart, 0, W.Hcc, W.gc, W.diag_c, fold_radius, W.scal};
     int fgrid = 0;
-    if (fold_radius > 0.0) {   // the diagonal fold rides in this launch
+    if (with_diag) {   // the diagonal slices ride in this launch (dispatched last: they fill the pairs' tail)
+      fa.u = W.u;
+      fa.G = cam_split_count(W);
+      fgrid = (P.nvc * fa.G + 3) / 4;
+    } else if (fold_radius > 0.0) {   // the diagonal fold rides in this launch
       fa.nsl = cam_split_count(W);
       fgrid = (P.nvc * 27 + 255) / 256;
     }

@@ -741,8 +741,15 @@ void form_reduced_dense(ba_ctx* ctx, double radius) {
   // ... and that fold rides in the pair pass's launch when it can (one
   // launch fewer; the fold writes only the diagonal blocks and the rhs)
   const bool fold_in_pairs = fused_diag && radius > 0.0 && pairs_take_fold(P, W);
-  launch_cam_schur_diag(P, W, s, nullptr, fused_diag ? radius : 0.0, fold_in_pairs);
-  launch_schur_pairs(P, W, s, fold_in_pairs ? radius : 0.0);
+  if (fold_in_pairs && pairs_take_diag(P, W)) {
+    // ... or rather the diagonal slices ride in it (dispatched after the pair
+    // workgroups, they fill the pass's tail) and the fold follows
+    launch_schur_pairs(P, W, s, 0.0, true);
+    launch_cam_fold_diag(P, W, radius, s);
+  } else {
+    launch_cam_schur_diag(P, W, s, nullptr, fused_diag ? radius : 0.0, fold_in_pairs);
+    launch_schur_pairs(P, W, s, fold_in_pairs ? radius : 0.0);
+  }
   if (ctx->coll()) launch_reduce(W, bit(SL_ELIM_BAD), 0, s);   // else folded with the step scalars
   if (ctx->coll()) {
     // only the lower triangle and the rhs row of S carry data: all-reduce
