@@ -3804,9 +3804,10 @@ void launch_backsub_candidate(const DevProblem& P, const DevWork& W, hipStream_t
     return;
   }
   if (W.jrfree) {
-    // (fp32 W storage too: the back substitution is exact in fp64 from J,
-    // as the oracle's fp32-W mode restates it; only the matvec, the rhs and
-    // the preconditioner see the fp32 blocks)
+    // (fp32 W storage too: without W.pacc the back substitution is exact in
+    // fp64 from J, as the oracle's fp32-W mode restates it; with it, the
+    // accumulated products carry the stored fp32 blocks, as the matvec, the
+    // rhs and the preconditioner do)
     constexpr int NT = 512, L = 4;
     const int want = (int)std::min<long long>(((long long)P.np * L + NT - 1) / NT, 1LL << 30);
     const int g = std::max(1, std::min(want, lds_grid(1 << 30)));   // one 110-KB-LDS workgroup per CU
