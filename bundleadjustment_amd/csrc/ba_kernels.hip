@@ -1851,6 +1851,9 @@ __device__ __forceinline__ void glds16(const double* src, double* lds_dst) {
   __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }
 constexpr int kPairsDmaLds = 4 * 2 * 64 * kWcRec * (int)sizeof(double);   // 64 KB: 4 waves x (row, partner) x 64 records
+// the diagonal Schur slices in the pair pass's launch (pairs_take_diag);
+// building with -DDIAG_IN_PAIRS=0 keeps the separate diagonal launch (A/B:
+// profiles/r05_v12_diag_in_pairs_ab.txt)
 #ifndef DIAG_IN_PAIRS
 #define DIAG_IN_PAIRS 1
 #endif
