@@ -3221,38 +3221,11 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
     int o0 = P.pt_off[pc], o1 = P.pt_off[pc + 1];
     double X0 = pts[3 * pc], X1 = pts[3 * pc + 1], X2 = pts[3 * pc + 2];
     bool pv = P.pt_var[pc] != 0;
-    // ACC: the point's step inputs (scalings, L_p^-1, vacc, u; lane 0 also
-    // Hpp, gp) and its first observation's camera and pixel, loaded one point
-    // ahead like X (each was a dependent memory round trip per point)
-    struct AccPre { double s[3], L[6], a[3], w[3], h[6], g[3]; int c; float2 uv; };
-    auto acc_pre = [&](int q, int q0, AccPre& r) {
-      if constexpr (ACC) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) r.s[k] = scale_p[k * np + q];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) r.L[k] = Linv[k * np + q];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) { r.a[k] = vacc[3 * (size_t)q + k]; r.w[k] = u[4 * (size_t)q + k]; }
-        if (sl == 0) {
-#pragma unroll
-          for (int k = 0; k < 6; ++k) r.h[k] = Hpp[k * np + q];
-#pragma unroll
-          for (int k = 0; k < 3; ++k) r.g[k] = gp[k * np + q];
-        }
-        const int oq = min(q0 + sl, lasto);
-        r.c = P.obs_cam[oq];
-        r.uv = P.uv[oq];
-      }
-    };
-    AccPre pre;
-    acc_pre(pc, o0, pre);
     for (; p < P.np; p += gs) {   // uniform inside a lane group
       const int pn = min(p + gs, lastp);
       const int o0n = P.pt_off[pn], o1n = P.pt_off[pn + 1];
       const double Y0 = pts[3 * pn], Y1 = pts[3 * pn + 1], Y2 = pts[3 * pn + 2];
       const bool pvn = P.pt_var[pn] != 0;
-      const AccPre cur = pre;
-      if constexpr (ACC) acc_pre(pn, o0n, pre);
       double dX[3] = {0.0, 0.0, 0.0};
       // the first KC observations of the lane keep what pass 2 needs from
       // pass 1's J (Jc dc, Jp, r: 10 doubles), so pass 2 recomputes J only
@@ -3261,11 +3234,11 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
       double kc[ACC ? 1 : KC][10];
       if (ACC && pv) {
         // w = u_p - vpt_p(y), the point step and its model-cost terms (lane 0)
-        const double s0 = cur.s[0], s1 = cur.s[1], s2 = cur.s[2];
-        const double i00 = cur.L[0], i10 = cur.L[1], i11 = cur.L[2];
-        const double i20 = cur.L[3], i21 = cur.L[4], i22 = cur.L[5];
-        const double a0 = cur.a[0], a1 = cur.a[1], a2 = cur.a[2];
-        const double w0 = cur.w[0] - a0, w1 = cur.w[1] - a1, w2 = cur.w[2] - a2;
+        const double s0 = scale_p[p], s1 = scale_p[np + p], s2 = scale_p[2 * np + p];
+        const double i00 = Linv[p], i10 = Linv[np + p], i11 = Linv[2 * np + p];
+        const double i20 = Linv[3 * np + p], i21 = Linv[4 * np + p], i22 = Linv[5 * np + p];
+        const double a0 = vacc[3 * (size_t)p], a1 = vacc[3 * (size_t)p + 1], a2 = vacc[3 * (size_t)p + 2];
+        const double w0 = u[4 * p] - a0, w1 = u[4 * p + 1] - a1, w2 = u[4 * p + 2] - a2;
         const double yp[3] = {i00 * w0 + i10 * w1 + i20 * w2, i11 * w1 + i21 * w2, i22 * w2};
         const double sp[3] = {s0, s1, s2};
 #pragma unroll
@@ -3275,12 +3248,12 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
           const double t0 = a0 / i00;
           const double t1 = (a1 - i10 * t0) / i11;
           const double t2 = (a2 - i20 * t0 - i21 * t1) / i22;
-          const double h00 = cur.h[0], h10 = cur.h[1], h20 = cur.h[2];
-          const double h11 = cur.h[3], h21 = cur.h[4], h22 = cur.h[5];
+          const double h00 = Hpp[p], h10 = Hpp[np + p], h20 = Hpp[2 * np + p];
+          const double h11 = Hpp[3 * np + p], h21 = Hpp[4 * np + p], h22 = Hpp[5 * np + p];
           const double hd0 = h00 * dX[0] + h10 * dX[1] + h20 * dX[2];
           const double hd1 = h10 * dX[0] + h11 * dX[1] + h21 * dX[2];
           const double hd2 = h20 * dX[0] + h21 * dX[1] + h22 * dX[2];
-          const double gd = cur.g[0] * dX[0] + cur.g[1] * dX[1] + cur.g[2] * dX[2];
+          const double gd = gp[p] * dX[0] + gp[np + p] * dX[1] + gp[2 * np + p] * dX[2];
           const double dhd = dX[0] * hd0 + dX[1] * hd1 + dX[2] * hd2;
           const double ytv = yp[0] * t0 + yp[1] * t1 + yp[2] * t2;
           acc[2] += gd + 0.5 * dhd + ytv;
@@ -3354,15 +3327,9 @@ __global__ __launch_bounds__(NT) void k_point_step_rc(DevProblem P, const double
       // pass 2: model cost change and candidate cost per observation
       {
         int o = o0 + sl;
-        int c, oc = min(o, lasto);
-        float2 uv;
-        if constexpr (ACC) {
-          c = cur.c;
-          uv = cur.uv;
-        } else {
-          c = P.obs_cam[oc];
-          uv = P.uv[oc];
-        }
+        int oc = min(o, lasto);
+        int c = P.obs_cam[oc];
+        float2 uv = P.uv[oc];
         // keep: pass 1's values of this observation (nullptr: J again)
         auto obs2 = [&](const double* keep) {
           const int on = min(o + LANES, lasto);
