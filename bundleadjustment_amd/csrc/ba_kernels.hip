@@ -1852,11 +1852,8 @@ __device__ __forceinline__ void glds16(const double* src, double* lds_dst) {
 }
 constexpr int kPairsDmaLds = 4 * 2 * 64 * kWcRec * (int)sizeof(double);   // 64 KB: 4 waves x (row, partner) x 64 records
 // the diagonal Schur slices in the pair pass's launch (pairs_take_diag);
-// building with -DDIAG_IN_PAIRS=0 keeps the separate diagonal launch (A/B:
-// profiles/r05_v12_diag_in_pairs_ab.txt)
-#ifndef DIAG_IN_PAIRS
-#define DIAG_IN_PAIRS 1
-#endif
+// BA_DIAG_IN_PAIRS=0 (read per step: tests compare the two forms bitwise)
+// keeps the separate diagonal launch (A/B: profiles/r05_v12_diag_in_pairs_ab.txt)
 
 // one camera slice (v, slice g of G) by one wave: the per-lane sums
 __device__ __forceinline__ void diag_cd_wave(const DevProblem& P, const double* __restrict__ Wc,
@@ -3699,7 +3696,8 @@ void launch_cam_fold_diag(const DevProblem& P, const DevWork& W, double radius, 
                      cam_split_count(W), W.Hcc, W.gc, W.scale_c, W.diag_c, radius, W.S, W.scal);
 }
 bool pairs_take_diag(const DevProblem& P, const DevWork& W) {
-  return DIAG_IN_PAIRS && pairs_take_fold(P, W) && !W.jdiag && !W.w32 && P.nvc > 0;
+  const char* e = getenv("BA_DIAG_IN_PAIRS");
+  return !(e && e[0] == '0') && pairs_take_fold(P, W) && !W.jdiag && !W.w32 && P.nvc > 0;
 }
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius, bool with_diag) {
   if (W.nblocks == 0) return;

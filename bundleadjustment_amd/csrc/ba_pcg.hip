@@ -28,8 +28,8 @@
 
 namespace bahip {
 
-constexpr int kPcgThreads = 1024;   // camera-side workgroup
-// k_pcg_update (one workgroup) up to this many cameras, the grid kernels past
+// k_pcg_update (one workgroup, one thread per camera) up to this many
+// cameras, the grid kernels past
 // it: at 1000 cameras the one workgroup's strided Adiag / Minv reads go
 // through one CU (~35 us per working launch); C4 3893 -> 3898 M-obs/s with the
 // grid kernels (profiles/r05_v10_pcg_update_form_ab.txt)
@@ -625,7 +625,7 @@ __global__ __launch_bounds__(256) void k_pcg_tfold(int nvc, int G, double* __res
 // the per-phase re-reads of the loop form cost a dependent L2 round trip per
 // phase: C4 shard 15.4 us per launch).  The same operations per camera in the
 // same order and the same workgroup sums: bitwise the loop form.
-__global__ __launch_bounds__(kPcgThreads) void k_pcg_update(DevProblem P, int mode, int it, PcgOpts o, int G,
+__global__ __launch_bounds__(kPcgOneWg) void k_pcg_update(DevProblem P, int mode, int it, PcgOpts o, int G,
                                                             const double* __restrict__ Adiag,
                                                             const double* __restrict__ Minv,
                                                             const double* __restrict__ b, double* __restrict__ x,
@@ -960,7 +960,10 @@ void launch_pcg_update(const DevProblem& P, const DevWork& W, int mode, int it, 
   // (after launch_pcg_tfold the slices are folded into slice 0: G = 1)
   const int G = W.pcg_folded ? 1 : W.pcg_G;
   if (P.nvc <= kPcgOneWg) {   // one workgroup: one launch per CG iteration
-    hipLaunchKernelGGL(k_pcg_update, dim3(1), dim3(kPcgThreads), 0, s, P, mode, it, o, G, W.Adiag, W.Minv,
+    // (kPcgOneWg threads: the workgroup sums add the waves in index order, so
+    // the 1024-thread launch this replaced, whose extra waves added zeros,
+    // rounded identically)
+    hipLaunchKernelGGL(k_pcg_update, dim3(1), dim3(kPcgOneWg), 0, s, P, mode, it, o, G, W.Adiag, W.Minv,
                        W.pb, W.y, W.pr, W.pz, W.pp, W.pq, W.tpart, W.scal);
     return;
   }

@@ -597,6 +597,11 @@ void ensure_pcg(ba_ctx* ctx) {
   W.pq = ctx->dalloc<double>(n);
   W.vpt = ctx->dalloc<double>(3 * (size_t)std::max(np, 1));
   W.vacc = ctx->dalloc<double>(3 * (size_t)std::max(np, 1));
+  // a point with no observation never gets a vpt entry (the point passes
+  // store it at the end of a point's run), but k_pcg_vacc folds every point:
+  // zeros, so such a point's accumulated product and step stay 0
+  HIP_OK(hipMemsetAsync(W.vpt, 0, sizeof(double) * 3 * (size_t)std::max(np, 1), ctx->stream));
+  HIP_OK(hipMemsetAsync(W.vacc, 0, sizeof(double) * 3 * (size_t)std::max(np, 1), ctx->stream));
   W.tpart = ctx->dalloc<double>((size_t)W.pcg_G * 6 * std::max(nvc, 1));
   W.ppart = ctx->dalloc<double>(3 * (size_t)kMaxBlocks);
   if ((nvc + 255) / 256 > kMaxBlocks) throw BaError{BA_ERR_INVALID_ARGUMENT, "too many cameras for ITERATIVE_SCHUR"};
@@ -817,6 +822,11 @@ int reduced_solve_pcg(ba_ctx* ctx, double radius, const ba_options& o) {
   if (ctx->coll()) ctx->allreduce(W.Sd, 27 * (size_t)ctx->nvc);
   if (ctx->nvc == 0) {
     if (W.pacc && P.np > 0) HIP_OK(hipMemsetAsync(W.vacc, 0, sizeof(double) * 3 * (size_t)P.np, s));   // (y = 0)
+    // k_pcg_setup_fin, which clears them otherwise, does not run: a spin or
+    // pivot failure left by an earlier DENSE_SCHUR solve of this context must
+    // not be read back as this step's
+    HIP_OK(hipMemsetAsync(W.scal + SL_CHOL_SPIN, 0, sizeof(double), s));
+    HIP_OK(hipMemsetAsync(W.scal + SL_CHOL_BAD, 0, sizeof(double), s));
     return 0;
   }
   launch_pcg_setup(P, W, radius, po, s);

@@ -85,3 +85,23 @@ def test_jfree_blocks_and_reduced_system_match_oracle(oracle_lib, cfg, scale):
     assert np.allclose(got["S"][d, d], lhs[d, d], rtol=1e-11, atol=0), "S diagonal"
     close_to_scale(got["rhs"], rhs, 1e-10, "rhs")
 
+
+
+@pytest.mark.timeout(600)
+def test_diagonal_slices_in_the_pair_launch_are_bitwise_the_separate_launch(monkeypatch):
+    """C3 (compact W records): the diagonal Schur slices ride in the pair
+    pass's launch by default (one wave per camera slice, wave_sum); with
+    BA_DIAG_IN_PAIRS=0 they run as k_cam_schur_diag_cd (one 64-thread
+    workgroup per slice, block_sum) and the fold rides in the pair launch
+    instead.  Both reductions add the same lane values in the same tree, so
+    the reduced system and its rhs are bitwise equal."""
+    p = make_config("c3", scale=1.0)
+    with Solver(0) as s:
+        s.set_problem(p)
+        a = s.debug_blocks(1e4)
+        monkeypatch.setenv("BA_DIAG_IN_PAIRS", "0")
+        b = s.debug_blocks(1e4)
+    n = a["n"]
+    tril = np.tril_indices(n)
+    assert np.array_equal(a["S"][tril], b["S"][tril])
+    assert np.array_equal(a["rhs"], b["rhs"])

@@ -22,7 +22,11 @@ Tolerances (besides those of test_gpu_parity.py):
       monotone, bitwise deterministic, final cost within 1e-6 of the fp64
       path
   10k-camera ITERATIVE_SCHUR vs oracle .. cost rtol 1e-9 and identical CG
-      counts, fp64 and MIXED_FP32 (the oracle's fp32-W restatement)
+      counts, fp64 and MIXED_FP32 (the oracle's rank-2 fp32 restatement,
+      precision 3)
+  C5 shard at full size, MIXED_FP32 vs the oracle's precision 3, 2 LM
+      iterations ...................... cost rtol 1e-9, identical decisions
+      and CG counts
   converged gauge-free output (200 LM iterations, tight tolerances) ...
       cost 1e-9; after the Sim(3) aligning the camera centres: centres and
       points (99th percentile) 1e-5 of the scene extent (float resolution
@@ -126,19 +130,44 @@ def test_c5_shard_mixed_precision_properties():
 
 
 @pytest.mark.timeout(900)
+def test_c5_shard_mixed_precision_matches_oracle(solver, oracle_lib):
+    """The full-size C5 shard (10k cameras x 1.25M points x 12.5M
+    observations) in its own precision mode: MIXED_FP32 (the rank-2 records
+    c, Z in fp32, the back substitution from the CG's accumulated products)
+    against the oracle's restatement of those fp32 records (precision 3),
+    2 LM iterations: costs 1e-9, identical accept/reject decisions and CG
+    counts (Optimizer.cpp:242)."""
+    p = make_config("c5", scale=0.125)
+    assert p.n_cams == 10_000 and p.n_obs > 12_000_000
+    opts = Options(max_num_iterations=2, linear_solver_type="ITERATIVE_SCHUR", preconditioner_type="SCHUR_JACOBI",
+                   precision="MIXED_FP32")
+    cams, pts, summ, glog = run_gpu(solver, p, opts)
+    oc, op, osum, olog = oracle_lib.solve(p, oracle_lib.default_options(
+        max_num_iterations=2, linear_solver=1, preconditioner_type=1, precision=3))
+    compare_logs(glog, olog, rtol_cost=1e-9)
+    assert cg_counts(glog) == cg_counts(olog)
+    assert [r["step_is_successful"] for r in glog] == [r["step_is_successful"] for r in olog]
+    assert summ.final_cost == pytest.approx(osum["final_cost"], rel=1e-9)
+
+
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("precision", ["FP64", "MIXED_FP32"])
 def test_10k_cameras_iterative_matches_oracle(solver, oracle_lib, precision):
     """C5's camera count (10k cameras, 60k camera unknowns: the grid-kernel CG)
     on a reduced point set, against the oracle's ITERATIVE_SCHUR — in fp64,
-    and with the W blocks rounded to fp32 (the oracle's independent
-    restatement of MIXED_FP32, oracle/ba_oracle.cpp iterative_schur_solve_w)."""
+    and with the rank-2 W records (c, Z) rounded to fp32 (the oracle's
+    independent restatement of MIXED_FP32 on those records, precision 3 of
+    oracle/ba_oracle.cpp iterative_schur_solve_w)."""
     p = make_synthetic(10_000, 60_000, 10, seed=0xBA5E0004)
     assert p.n_cams == 10_000
     opts = Options(max_num_iterations=4, linear_solver_type="ITERATIVE_SCHUR", preconditioner_type="SCHUR_JACOBI",
                    precision=precision)
     cams, pts, summ, glog = run_gpu(solver, p, opts)
+    # MIXED_FP32 beyond 200 cameras runs the point pass over the 16-value
+    # rank-2 records with c and Z rounded to float (k_obs_w_rc<float, .., PC>):
+    # the oracle's precision 3, not precision 1 (which rounds the 18 W entries)
     oc, op, osum, olog = oracle_lib.solve(p, oracle_lib.default_options(
-        max_num_iterations=4, linear_solver=1, preconditioner_type=1, precision=int(precision == "MIXED_FP32")))
+        max_num_iterations=4, linear_solver=1, preconditioner_type=1, precision=3 if precision == "MIXED_FP32" else 0))
     compare_logs(glog, olog, rtol_cost=1e-9)
     assert cg_counts(glog) == cg_counts(olog)
     assert summ.final_cost == pytest.approx(osum["final_cost"], rel=1e-9)

@@ -206,6 +206,34 @@ def test_unobserved_blocks_untouched_and_duplicates(solver, oracle_lib):
     assert_close(x10, ox10, 1e-8, 1e-10, "points (10 iterations)")
 
 
+@pytest.mark.parametrize("dups", [False, True])
+@pytest.mark.parametrize("pacc", ["1", "0"])
+def test_unobserved_points_untouched_iterative(solver, oracle_lib, dups, pacc, monkeypatch):
+    """ITERATIVE_SCHUR with variable points no residual touches: the back
+    substitution from the CG's accumulated point products (k_pcg_vacc folds
+    every point, BA_PCG_PACC=1, the default) and the per-observation J form
+    (BA_PCG_PACC=0) leave them bitwise untouched, and the solve matches the
+    oracle's ITERATIVE_SCHUR (with and without duplicate observations)."""
+    monkeypatch.setenv("BA_PCG_PACC", pacc)
+    p = make_synthetic(6, 300, 3, seed=3)
+    p.pts = np.vstack([p.pts, np.ones((5, 3))])
+    if dups:
+        dup = np.arange(0, p.n_obs, 7)
+        p.obs_cam = np.concatenate([p.obs_cam, p.obs_cam[dup]])
+        p.obs_pt = np.concatenate([p.obs_pt, p.obs_pt[dup]])
+        p.obs_uv = np.concatenate([p.obs_uv, p.obs_uv[dup] + 0.5])
+    p = p.normalized()
+    bp.fix_camera(p, 1)
+    kw = dict(max_num_iterations=8)
+    cams, pts, summ, glog = run_gpu(solver, p, Options(linear_solver_type="ITERATIVE_SCHUR",
+                                                       preconditioner_type="SCHUR_JACOBI", **kw))
+    oc, op, osum, olog = oracle_lib.solve(p, oracle_lib.default_options(linear_solver=1, preconditioner_type=1, **kw))
+    assert np.array_equal(pts[-5:], p.pts[-5:])
+    assert np.isfinite(cams).all() and np.isfinite(pts).all()
+    compare_logs(glog, olog, rtol_cost=1e-9)
+    assert [r["linear_solver_iterations"] for r in glog] == [r["linear_solver_iterations"] for r in olog]
+
+
 def test_points_only_with_all_cameras_fixed(solver, oracle_lib):
     p = make_synthetic(5, 400, 3, seed=4)
     for c in range(p.n_cams):

@@ -391,7 +391,7 @@ def test_gpu_mixed_fp32_matches_fp64(solver, pc):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("pc", PRECONDITIONERS)
-@pytest.mark.parametrize("cfg,scale", [("c2", 0.2), ("c3", 0.01)])
+@pytest.mark.parametrize("cfg,scale", [("c2", 0.2), ("c3", 0.01), ("c4", 0.01)])
 @pytest.mark.parametrize("mv", MATVECS)
 def test_gpu_mixed_fp32_matches_oracle_mixed(solver, oracle_lib, cfg, scale, pc, mv, monkeypatch):
     """BA_MIXED_FP32 against the oracle's independent fp32 restatement: the
