@@ -306,6 +306,16 @@ int chol_split_blocks() { return kCholSplitBlocks; }
 void launch_chol_persist(double* A, double* L, int ld, int n, double* Vbuf, double* scal, unsigned* flags,
                          unsigned epoch, hipStream_t s);
 
+void launch_chol_persist_ov(const DevProblem& P, const DevWork& W, OvPlan& plan, double radius, int epoch,
+                            hipStream_t s, bool pass_only);
+void launch_cholesky_solve_ov(const DevProblem& P, const DevWork& W, OvPlan& plan, double radius, int epoch,
+                              hipStream_t s, bool pass_only) {
+  const int n = P.n, T = (n + CB - 1) / CB;
+  launch_chol_persist_ov(P, W, plan, radius, epoch, s, pass_only);
+  if (pass_only) return;
+  hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.yg, epoch, W.scal);
+}
+
 void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hipStream_t s) {
   const int n = P.n;
   if (n == 0) return;

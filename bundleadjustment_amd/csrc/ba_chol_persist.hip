@@ -36,6 +36,7 @@
 // grid must be resident at once: the host checks the occupancy first
 // (chol_persist_fits) and otherwise runs the per-step launches.
 #include "ba_chol.h"
+#include "ba_schur.h"
 
 namespace bahip {
 
@@ -174,6 +175,57 @@ __device__ __forceinline__ bool wait_flag(const unsigned* flag, unsigned epoch, 
   return ok;
 }
 
+// The overlapped form (OvArgs::on): the reduced system S is formed INSIDE
+// the launch, by the workgroups that do not yet hold a tile — the pair blocks
+// of k_schur_pairs_cd, the diagonal slices of k_cam_schur_diag_cd and the
+// fold of k_cam_fold_diag, as work items handed out in tile-column order
+// (the order the factorisation consumes S), with the same arithmetic in the
+// same order per S entry, so S (and with it L) is bitwise the serial form's.
+//   items: per XCD (blockIdx & 7) a queue of wave-sized work items — a pair
+//       item is 4 camera-pair blocks (16 lanes each, as k_schur_pairs_cd), a
+//       diagonal item is one (camera, slice) of diag_cd_wave; the wave that
+//       completes a camera's last slice folds it.  Each item stores its S
+//       entries write-through (agent-scope atomic stores: sc1), drains, and
+//       counts itself into every tile it wrote (cnt); the contribution that
+//       completes a tile raises the tile's pflag.
+//   workers (tile owners) take items until their own tile column comes up
+//       in their queue, then wait for their tile's pflag and factor as
+//       before; the critical workgroup waits for pflag of the tiles no worker
+//       owns (column 0 and (1, 1)); extra workgroups past the workers
+//       ("helpers") only take items.
+// Counters and tickets are cumulative over the launches (pe = the launch
+// count): nothing is reset, and every wave draws exactly one failing ticket
+// per launch, so queue x's tickets of launch pe start at qbase[x] = (pe - 1)
+// (items_x + 4 waves x its workgroups).  Items never wait, so the pass always
+// completes; a missing tile is a bounded spin like any other hand-off.
+struct OvArgs {
+  int on = 0;
+  int pass_only = 0;         // (diagnostics, ba_debug_blocks: every workgroup only takes items; no factorisation)
+  DevProblem P;
+  const int4* blocks;
+  const int2* pairs;
+  const double* Wc;          // compact W records (k_obs_w_rc<double, true>)
+  const double* scale_c;
+  const double* u;           // [np][4] u_p (diagonal slices)
+  const double* Hcc;
+  const double* gc;
+  const double* diag_c;
+  double radius;
+  double* cpart;             // [G][nvc][27] slices
+  int G;
+  const int* items;          // >= 0: pair item (4 blocks ov_blk[4 i ..]), < 0: -1 - (v G + g)
+  const int* item_col;       // the tile column each item belongs to
+  const int* ov_blk;
+  const unsigned* tgt;       // [TR][T] contributions per tile and launch
+  unsigned* cnt;             // [TR][T] contributions (cumulative)
+  unsigned* cam_cnt;         // [nvc] slices done (cumulative)
+  unsigned* q;               // [8] tickets drawn (cumulative)
+  unsigned* pflag;           // [TR][T] tile formed: the factorisation epoch
+  int ioff[9];               // queue x's items: items[ioff[x] .. ioff[x+1])
+  unsigned qbase[8];
+  unsigned pe;
+};
+
 struct PersistArgs {
   double* A;         // working matrix ((n+1) x ld)
   double* L;         // output factor
@@ -183,6 +235,7 @@ struct PersistArgs {
   int ld, n, T, TR;
   unsigned epoch;
   unsigned spin_max;   // polls per hand-off before SL_CHOL_SPIN (kPersistSpin)
+  OvArgs ov;           // ov.on: S formed inside the launch
 };
 
 // worker w (>= 1) -> its tile (I, J): tiles with J >= 1 and I >= J, in
@@ -316,12 +369,257 @@ struct PanelPrefetch {
   }
 };
 
+// ---------------------------------------------------------------- overlapped S
+// one tile's contribution counted; the one that completes the tile raises pflag
+__device__ __forceinline__ void ov_count(const OvArgs& o, int t, unsigned epoch) {
+  const unsigned old = __hip_atomic_fetch_add(&o.cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1u == o.pe * o.tgt[t]) __hip_atomic_store(&o.pflag[t], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// LDS-DMA issued by inline asm (the pair item's pipeline): the compiler,
+// which does not see these loads, then neither counts them nor inserts the
+// vmcnt(0) it puts before any LDS access that may follow an LDS-DMA
+// intrinsic (that wait would drain the second round at every round).  Every
+// wait on them is explicit.  M0 = the wave's LDS byte address; nothing else
+// in this kernel's pair path touches M0.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) const void*)p);
+}
+__device__ __forceinline__ void adma16(const void* src, unsigned lds) {   // 16 B per lane, lane-linear
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
+}
+__device__ __forceinline__ void adma4(const void* src, unsigned lds) {    // 4 B per lane, lane-linear
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
+}
+
+// one pair item by one wave: 4 camera-pair blocks, 16 lanes each — the lanes,
+// pairs, products and xor reduction of k_schur_pairs_cd (bitwise its S
+// blocks).  The records go through LDS by LDS-DMA as there, two rounds in
+// flight (region: 2 x (row, partner) x 64 records = 32 KB): the
+// factorisation's one workgroup per CU leaves each wave alone on its SIMD, so
+// the second round is what hides the gather latency.  The pair indices come
+// by LDS-DMA too, three rounds ahead (islot: 4 x 64 {x, y}), so no register
+// is ever loaded in flight.  Round r: wait vmcnt(16) (its records and round
+// r + 2's indices have landed: behind them are round r + 2's indices' two
+// pieces... see below), read them, then request round r + 3's indices (2
+// pieces) and round r + 2's records (16 pieces).  Rounds past a block's end
+// fetch its last pair again (L2 hits) and compute nothing, so the count of
+// memory operations per round never changes.
+__device__ __forceinline__ void ov_pair_item(const OvArgs& o, int g, double* region, int* islot, double* S, size_t ld,
+                                             int T, unsigned epoch) {
+  constexpr int PL = kPairLanes;
+  static_assert(64 / PL == 4, "a pair item is 4 blocks per wave");
+  const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
+  const int bi = o.ov_blk[4 * g + sub];
+  const bool live = bi >= 0;
+  const int4 blk = live ? o.blocks[bi] : make_int4(0, 0, 0, 0);
+  WcCam mI, mJ;
+  mI.load(o.P, o.scale_c, blk.x);
+  mJ.load(o.P, o.scale_c, blk.y);
+  // (the camera constants land here, before the pipeline: a wait for them
+  // at their first use would sit inside the round loop)
+  asm volatile("" ::"v"(mI.a0[0]), "v"(mI.a0[1]), "v"(mI.a0[2]), "v"(mI.a1[0]), "v"(mI.a1[1]), "v"(mI.a1[2]),
+               "v"(mI.b[0]), "v"(mI.b[1]), "v"(mI.b[2]));
+  asm volatile("" ::"v"(mJ.a0[0]), "v"(mJ.a0[1]), "v"(mJ.a0[2]), "v"(mJ.a1[0]), "v"(mJ.a1[1]), "v"(mJ.a1[2]),
+               "v"(mJ.b[0]), "v"(mJ.b[1]), "v"(mJ.b[2]));
+  const int swr = (lane >> 1) & 7;
+  const int len = blk.w - blk.z;
+  int nit = len > sl ? (len - sl + PL - 1) / PL : 0;
+#pragma unroll
+  for (int x = 32; x >= 1; x >>= 1) nit = max(nit, __shfl_xor(nit, x));
+  nit = __builtin_amdgcn_readfirstlane(nit);   // (a uniform loop)
+  const int e0 = blk.z + sl;
+  // round t's buffers: records (row at +0, partner at +64 records), indices
+  // (x at +0, y at +64 ints)
+  auto rbuf = [&](int t) { return region + (t & 1) * (128 * kWcRec); };
+  auto ibuf = [&](int t) { return islot + (t & 3) * 128; };
+  auto req_idx = [&](int t) {   // round t's pair of this lane -> ibuf(t)
+    const int2* p = o.pairs + max(min(e0 + t * PL, blk.w - 1), 0);
+    const int* ib = ibuf(t);
+    adma4(&p->x, lds_addr(ib));
+    adma4(&p->y, lds_addr(ib + 64));
+  };
+  auto req_rec = [&](int t) {   // round t's records (its indices in ibuf(t)) -> rbuf(t)
+    const int* ib = ibuf(t);
+    const int2 pr = make_int2(ib[lane], ib[64 + lane]);
+    double* rb = rbuf(t);
+    const unsigned lr = lds_addr(rb), lp = lds_addr(rb + 64 * kWcRec);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int q = (lane >> 3) + 8 * i;
+      const int ra = __shfl(pr.x, q), rq = __shfl(pr.y, q);
+      const int sp = 2 * ((lane & 7) ^ ((q >> 1) & 7));
+      adma16(o.Wc + (size_t)ra * kWcRec + sp, lr + i * 1024);
+      adma16(o.Wc + (size_t)rq * kWcRec + sp, lp + i * 1024);
+    }
+  };
+  auto read_rec = [&](const double* buf) {
+    WcRaw w;
+    const double* r = buf + lane * kWcRec;
+#pragma unroll
+    for (int p = 0; p < kWcRec / 2; ++p) {
+      const double2 t = *reinterpret_cast<const double2*>(r + 2 * (p ^ swr));
+      w.r[2 * p] = t.x;
+      w.r[2 * p + 1] = t.y;
+    }
+    return w;
+  };
+  double acc[36];
+#pragma unroll
+  for (int k = 0; k < 36; ++k) acc[k] = 0.0;
+  // prologue: indices of rounds 0, 1 (waited), records 0, indices 2, records 1
+  req_idx(0);
+  req_idx(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  req_rec(0);
+  req_idx(2);
+  req_rec(1);
+  for (int t = 0; t < nit; ++t) {
+    // behind round t's records: round t + 2's indices (2) and round t + 1's
+    // records (16); behind round t + 2's indices: 16
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    const WcRaw wa = read_rec(rbuf(t));
+    const WcRaw wb = read_rec(rbuf(t) + 64 * kWcRec);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the refill
+    req_idx(t + 3);
+    req_rec(t + 2);
+    if (e0 + t * PL < blk.w) {
+      double ca0[6], ca1[6], cb0[6], cb1[6];
+      wc_rows(wa, mI, ca0, ca1);
+      wc_rows(wb, mJ, cb0, cb1);
+      const double* za0 = wa.r + 9;
+      const double* za1 = wa.r + 12;
+      const double* zb0 = wb.r + 9;
+      const double* zb1 = wb.r + 12;
+      const double m00 = za0[0] * zb0[0] + za0[1] * zb0[1] + za0[2] * zb0[2];
+      const double m01 = za0[0] * zb1[0] + za0[1] * zb1[1] + za0[2] * zb1[2];
+      const double m10 = za1[0] * zb0[0] + za1[1] * zb0[1] + za1[2] * zb0[2];
+      const double m11 = za1[0] * zb1[0] + za1[1] * zb1[1] + za1[2] * zb1[2];
+      double n0[6], n1[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        n0[j] = m00 * cb0[j] + m01 * cb1[j];
+        n1[j] = m10 * cb0[j] + m11 * cb1[j];
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) acc[i * 6 + j] += ca0[i] * n0[j] + ca1[i] * n1[j];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the requests past the end land before the slices are reused)
+#pragma unroll
+  for (int k = 0; k < 36; ++k) {
+    double v = acc[k];
+#pragma unroll
+    for (int x = PL / 2; x >= 1; x >>= 1) v += __shfl_xor(v, x, PL);
+    acc[k] = v;
+  }
+  if (live) {
+    const int I = blk.x, Jb = blk.y;   // I > Jb (no point observed twice by one camera in this form)
+#pragma unroll
+    for (int k = 0; k < 36; ++k) {
+      if ((k % PL) != sl) continue;
+      const int i = k / 6, j = k % 6;
+      __hip_atomic_store(S + (size_t)(6 * I + i) * ld + 6 * Jb + j, -acc[k], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the S stores are done
+  if (live && sl == 0) {
+    const int r0 = (6 * blk.x) >> 6, r1 = (6 * blk.x + 5) >> 6;
+    const int c0 = (6 * blk.y) >> 6, c1 = (6 * blk.y + 5) >> 6;
+    ov_count(o, r0 * T + c0, epoch);
+    if (c1 != c0) ov_count(o, r0 * T + c1, epoch);
+    if (r1 != r0) {
+      ov_count(o, r1 * T + c0, epoch);
+      if (c1 != c0) ov_count(o, r1 * T + c1, epoch);
+    }
+  }
+}
+
+// one diagonal item by one wave: camera slice (v, g) of diag_cd_wave (the
+// one-wave sum of the pair launch's diagonal workgroups), stored to cpart;
+// the wave that stores a camera's last slice folds it (k_cam_fold_diag's
+// entries, lanes 0..26)
+__device__ __forceinline__ void ov_diag_item(const OvArgs& o, int unit, double* region, double* S, int T,
+                                          unsigned epoch) {
+  const int lane = threadIdx.x & 63;
+  const int nvc = o.P.nvc;
+  const int v = unit / o.G, g = unit - v * o.G;
+  double acc[27];
+  diag_cd_wave(o.P, o.Wc, o.scale_c, o.u, v, g, o.G, region, region + 64 * kWcRec, acc);
+  double tot[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) tot[k] = 0.0 + wave_sum(acc[k]);   // (block_sum's value for one wave)
+  if (lane == 0) {
+    double* dst = o.cpart + ((size_t)g * nvc + v) * 27;
+#pragma unroll
+    for (int k = 0; k < 27; ++k) __hip_atomic_store(dst + k, tot[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(&o.cam_cnt[v], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __builtin_amdgcn_readfirstlane(old);
+  if (old + 1u != o.pe * (unsigned)o.G) return;
+  // the fold of camera v
+  if (lane < 27)
+    cam_fold_diag_entry<true>(o.P, o.cpart, o.G, o.Hcc, o.gc, o.scale_c, o.diag_c, o.radius, S, nullptr,
+                              v * 27 + lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane < 27) {
+    int row, col;
+    fold_entry_pos(o.P.n, v, lane, row, col);
+    ov_count(o, (row >> 6) * T + (col >> 6), epoch);
+  }
+}
+
+// queue x: a ticket (wave-uniform); false: the queue is exhausted (this wave's
+// one failing draw of the launch)
+__device__ __forceinline__ bool ov_draw(const OvArgs& o, int x, int& item) {
+  unsigned t = 0;
+  if ((threadIdx.x & 63) == 0) t = __hip_atomic_fetch_add(&o.q[x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __builtin_amdgcn_readfirstlane(t) - o.qbase[x];
+  const unsigned nq = (unsigned)(o.ioff[x + 1] - o.ioff[x]);
+  if (t >= nq) return false;
+  item = o.ioff[x] + (int)t;
+  return true;
+}
+__device__ __forceinline__ void ov_run(const OvArgs& o, int item, double* region, int* islot, double* S, size_t ld,
+                                       int T, unsigned epoch) {
+  const int it = o.items[item];
+  if (it >= 0) ov_pair_item(o, it, region, islot, S, ld, T, epoch);
+  else ov_diag_item(o, -1 - it, region, S, T, epoch);
+}
+// items until the queue is exhausted (stop_col < 0) or, for a worker, until
+// the next item is of tile column >= stop_col (its own tile's column comes
+// up).  Returns whether this wave drew its failing ticket.
+__device__ __forceinline__ bool ov_take(const OvArgs& o, double* region, int* islot, double* S, size_t ld, int T,
+                                        unsigned epoch, int stop_col) {
+  const int x = blockIdx.x & 7;
+  for (;;) {
+    if (stop_col >= 0) {
+      unsigned h = 0;
+      if ((threadIdx.x & 63) == 0) h = __hip_atomic_load(&o.q[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      h = __builtin_amdgcn_readfirstlane(h) - o.qbase[x];
+      if (h < (unsigned)(o.ioff[x + 1] - o.ioff[x]) && o.item_col[o.ioff[x] + (int)h] >= stop_col) return false;
+    }
+    int item;
+    if (!ov_draw(o, x, item)) return true;
+    ov_run(o, item, region, islot, S, ld, T, epoch);
+  }
+}
+
 // block 0: the critical workgroup, block w > 0: worker w
 __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
-  __shared__ double S0[CB][LDP];
-  __shared__ double S1[CB][LDP];
-  __shared__ double S2[CB][LDP];
-  __shared__ double S3[CB][LDP];   // the next panel tile A_{c+1,c}, prefetched during the factor
+  // S0..S3; S3: the next panel tile A_{c+1,c}, prefetched during the factor.
+  // (Overlapped form: before a workgroup takes up its tile, its waves' 32-KB
+  // slices of this array are the work items' LDS-DMA rounds)
+  __shared__ __attribute__((aligned(16))) double Sall[4][CB][LDP];
+  double (*S0)[LDP] = Sall[0];
+  double (*S1)[LDP] = Sall[1];
+  double (*S2)[LDP] = Sall[2];
+  double (*S3)[LDP] = Sall[3];
   __shared__ int pref_ok[2];
   __shared__ int dready[1];        // the next diagonal tile's flag was up at the factor's end
   __shared__ CholLds cw;
@@ -333,10 +631,25 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   unsigned* tflag = a.flags + T;
   bool bad = false;    // a non-positive pivot
   bool spin = false;   // a hand-off spin bound hit
+  const OvArgs& ov = a.ov;
+  double* region = &Sall[0][0][0] + (size_t)(threadIdx.x >> 6) * (4 * 64 * kWcRec);   // this wave's 32 KB
+  __shared__ __attribute__((aligned(16))) int ov_islot[4][4][128];                        // its pair-index slots
+  int* islot = ov_islot[threadIdx.x >> 6][0];
+  // tiles no worker owns (column 0, and (1, 1)) are final once formed: with
+  // the overlapped form their pflag, else ready from before the launch
+  auto formed = [&](int I, int J) -> const unsigned* { return ov.on ? &ov.pflag[I * T + J] : nullptr; };
+  if (ov.on && ov.pass_only) {
+    ov_take(ov, region, islot, a.A, ld, T, a.epoch, -1);
+    return;
+  }
 
   if (blockIdx.x == 0) {
     // ---------------- critical workgroup: the diagonal chain
     if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
+    if (ov.on && threadIdx.x == 0) {   // (the serial form's fold clears them before the launch)
+      __hip_atomic_store(&a.scal[SL_CHOL_BAD], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.scal[SL_CHOL_SPIN], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // the end of step cp: V_cp cleaned in place (zero above the diagonal,
     // identity rows past b: exactly the Vbuf image the per-step form
     // re-stages) for the next panel GEMM, stored write-through and published
@@ -419,7 +732,12 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       if (threadIdx.x == 0 && c < 64) g_pstamps[c][7] = 0;
 #endif
       if (c == 0) {
-        stage64(S0, a.A, ld, 0, 0, nrows, b);     // written before the launch
+        if (ov.on) {                               // formed in this launch
+          spin |= !wait_flag(formed(0, 0), a.epoch, a.spin_max);
+          tile_put(S0, tile_fetch_sc1(rA, ld, 0, 0, nrows, b));
+        } else {
+          stage64(S0, a.A, ld, 0, 0, nrows, b);   // written before the launch
+        }
       } else {
         const int k = c - 1, kc = k * CB, kb = min(CB, n - kc);
         // A_{c,k} final (its worker; column 0 is never updated): prefetched
@@ -430,12 +748,14 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         const bool have_pref = pref_ok[0] == 1 && pref_ok[1] == 1;   // (read after the factor's last barrier)
         if (!have_pref) {
           if (k >= 1) spin |= !wait_flag(&tflag[c * T + k], a.epoch, a.spin_max);
+          else if (ov.on) spin |= !wait_flag(formed(c, 0), a.epoch, a.spin_max);
           const TileRegs tP = tile_fetch_sc1(rA, ld, s, kc, nrows, kc + kb);   // A_{c,k}
           tile_put(S3, tP);
         }
         // (its barrier also covers S3; the plain form is an LDS-only
         // barrier, so the diagonal tile's loads stay in flight across it)
         if (c >= 2 && !have_diag) spin |= !wait_flag(&tflag[c * T + c], a.epoch, a.spin_max);
+        else if (c == 1 && ov.on && !have_diag) spin |= !wait_flag(formed(1, 1), a.epoch, a.spin_max);
         else lds_barrier();
         if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
         PSTAMP(c, 1);
@@ -468,9 +788,9 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       if (c + 1 < T) {
         // next step's panel tile A_{c+1,c}: final once its worker published
         // it (column 0: from before the launch)
-        const PanelPrefetch pf{rA, ld, c >= 1 ? &tflag[(c + 1) * T + c] : nullptr, a.epoch, S3, pref_ok,
+        const PanelPrefetch pf{rA, ld, c >= 1 ? &tflag[(c + 1) * T + c] : formed(1, 0), a.epoch, S3, pref_ok,
                                (c + 1) * CB, c * CB, nrows, c * CB + min(CB, n - c * CB), c,
-                               c + 1 >= 2 ? &tflag[(c + 1) * T + c + 1] : nullptr, dready,
+                               c + 1 >= 2 ? &tflag[(c + 1) * T + c + 1] : formed(1, 1), dready,
                                rV, (size_t)c * CB * CB * sizeof(double), S2};
         factor_invert_blk<1>(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr, pf);   // b = m = CB before the last block
       } else {
@@ -487,17 +807,31 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
 #ifdef BA_CHOL_STAMPS
     if (threadIdx.x == 0) g_stamp_on = 1;
 #endif
+    if (ov.on) {   // this workgroup's failing draws (items left, if any, are run)
+      __syncthreads();
+      ov_take(ov, region, islot, a.A, ld, T, a.epoch, -1);
+    }
     return;
   }
 
-  // ---------------- worker: one lower tile (I, J), J >= 1
+  // ---------------- worker: one lower tile (I, J), J >= 1 (or a helper)
   int I, J;
-  if (!worker_tile(blockIdx.x, T, a.TR, I, J)) return;
+  const bool worker = worker_tile(blockIdx.x, T, a.TR, I, J);
+  bool drew_fail = false;   // (overlapped form: this wave's failing draw)
+  if (ov.on) {
+    // work items until this tile's column comes up (helpers: all of them)
+    drew_fail = ov_take(ov, region, islot, a.A, ld, T, a.epoch, worker ? J : -1);
+    if (!worker) return;
+    __syncthreads();   // (the waves' slices of Sall are the tiles' LDS again)
+    spin |= !wait_flag(&ov.pflag[I * T + J], a.epoch, a.spin_max);
+  }
+  if (!worker) return;
   const bool diag = I == J;
   const int r0 = I * CB, c0 = J * CB;
   const int mI = min(CB, nrows - r0);
   // the tile in the MFMA accumulator layout (acc_pos), initial values from
-  // before the launch (plain loads, clamped)
+  // before the launch (plain loads, clamped) or, overlapped, formed in this
+  // launch (sc1 loads)
   double own[2][2][4];
 #pragma unroll
   for (int x = 0; x < 2; ++x)
@@ -507,7 +841,8 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       for (int g = 0; g < 4; ++g) {
         int rr, cc;
         acc_pos(x, y, g, &rr, &cc);
-        own[x][y][g] = a.A[(size_t)min(r0 + rr, nrows - 1) * ld + min(c0 + cc, n - 1)];
+        const size_t off = (size_t)min(r0 + rr, nrows - 1) * ld + min(c0 + cc, n - 1);
+        own[x][y][g] = ov.on ? __hip_atomic_load(a.A + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.A[off];
       }
   const int kmax = diag ? J - 2 : J - 1;
   const bool stamp = I == J + 1;   // (diagnostics: the next-panel tiles' last update)
@@ -519,6 +854,9 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
     if (k >= 1) {
       spin |= !wait_flag(&tflag[I * T + k], a.epoch, a.spin_max);
       if (!diag) spin |= !wait_flag(&tflag[J * T + k], a.epoch, a.spin_max);
+    } else if (ov.on) {   // column 0: formed in this launch, never updated
+      spin |= !wait_flag(formed(I, 0), a.epoch, a.spin_max);
+      if (!diag) spin |= !wait_flag(formed(J, 0), a.epoch, a.spin_max);
     }
     const TileRegs tI = tile_fetch_sc1(rA, ld, r0, kc, nrows, kc + kb);        // A_{I,k}
     TileRegs tJ;
@@ -598,6 +936,10 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   if (I == J + 1) lds_to_global(S1, a.L, ld, c0, kmax * CB, CB, min(CB, n - kmax * CB));
   if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
   if (threadIdx.x == 0 && spin) atomicAdd(&a.scal[SL_CHOL_SPIN], 1.0);
+  if (ov.on) {   // this wave's failing draw, unless taken before its tile
+    __syncthreads();
+    if (!drew_fail) ov_take(ov, region, islot, a.A, ld, T, a.epoch, -1);
+  }
 }
 
 // grid of the persistent factorisation: 1 critical + one worker per tile
@@ -616,6 +958,49 @@ bool chol_persist_fits(int device, int n) {
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return false;
   return chol_persist_grid(n) <= per_cu * cus;
+}
+
+int chol_persist_capacity(int device) {
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_chol_persist), 256, 0) !=
+          hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return -1;
+  return per_cu * cus;
+}
+
+// the overlapped form: one launch of plan.grid workgroups forms S (pairs,
+// diagonal slices, fold at this step's radius) and factors it
+void launch_chol_persist_ov(const DevProblem& P, const DevWork& W, OvPlan& plan, double radius, int epoch,
+                            hipStream_t s, bool pass_only) {
+  const int n = P.n, T = (n + CB - 1) / CB, TR = (n + 1 + CB - 1) / CB;
+  PersistArgs a;
+  a.A = W.S; a.L = W.Lf; a.Vbuf = W.Vbuf; a.scal = W.scal; a.flags = W.cflags;
+  a.ld = P.ld; a.n = n; a.T = T; a.TR = TR;
+  a.epoch = (unsigned)epoch;
+  const char* e = getenv("BA_CHOL_SPIN_MAX");   // (read per launch: tests switch it)
+  a.spin_max = e && atoi(e) > 0 ? (unsigned)atoi(e) : kPersistSpin;
+  OvArgs& o = a.ov;
+  o.on = 1;
+  o.pass_only = pass_only ? 1 : 0;
+  o.P = P;
+  o.blocks = W.blocks; o.pairs = W.pairs; o.Wc = W.W; o.scale_c = W.scale_c; o.u = W.u;
+  o.Hcc = W.Hcc; o.gc = W.gc; o.diag_c = W.diag_c; o.radius = radius;
+  o.cpart = W.cpart; o.G = W.cam_split;
+  o.items = plan.items; o.item_col = plan.item_col; o.ov_blk = plan.ov_blk; o.tgt = plan.tgt;
+  o.cnt = plan.ctr;
+  o.cam_cnt = plan.ctr + (size_t)TR * T;
+  o.q = o.cam_cnt + P.nvc;
+  o.pflag = o.q + 8;
+  const unsigned pe = ++plan.launches;
+  o.pe = pe;
+  for (int x = 0; x < 9; ++x) o.ioff[x] = plan.ioff[x];
+  for (int x = 0; x < 8; ++x) {
+    const unsigned nwg = (unsigned)((plan.grid - x + 7) / 8);   // workgroups b = x mod 8
+    const unsigned D = (unsigned)(plan.ioff[x + 1] - plan.ioff[x]) + 4u * nwg;   // tickets per launch
+    o.qbase[x] = (pe - 1u) * D;
+  }
+  hipLaunchKernelGGL(k_chol_persist, dim3(plan.grid), dim3(256), 0, s, a);
 }
 
 void launch_chol_persist(double* A, double* L, int ld, int n, double* Vbuf, double* scal, unsigned* flags,

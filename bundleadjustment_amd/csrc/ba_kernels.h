@@ -55,6 +55,22 @@ struct DevProblem {
   const float* extr;         // [16*nc] (fixed cameras)
 };
 
+// The reduced system formed inside the persistent factorisation's launch
+// (ba_chol_persist.hip, OvArgs): per-XCD queues of wave-sized work items in
+// tile-column order, per-tile contribution counts, cumulative counters.
+// Built once per problem (ba_solver.hip ensure_overlap).
+struct OvPlan {
+  bool ok = false;                   // built, and the problem qualifies
+  const int* items = nullptr;        // >= 0: pair item (4 blocks of ov_blk), < 0: -1 - (v G + g) diagonal slice
+  const int* item_col = nullptr;     // tile column of each item
+  const int* ov_blk = nullptr;       // [4 * pair items] block indices (-1: none)
+  const unsigned* tgt = nullptr;     // [TR][T] contributions per tile and launch
+  unsigned* ctr = nullptr;           // cnt [TR][T] | cam_cnt [nvc] | q [8] | pflag [TR][T]: zeroed once, cumulative
+  int ioff[9] = {0};                 // queue x: items [ioff[x], ioff[x+1])
+  int grid = 0;                      // workgroups of the launch (every CU: critical + workers + helpers)
+  unsigned launches = 0;             // overlapped launches so far (pe of the next one - 1)
+};
+
 // Device workspace pointers (see ba_solver.hip for sizes).
 struct DevWork {
   double* cams;  double* pts;        // x
@@ -86,6 +102,7 @@ struct DevWork {
   double* yg;                        // [n][2] back-substitution hand-off granules {y, epoch} (zeroed once)
   unsigned* cflags;                  // [T + TR*T] persistent-Cholesky hand-off flags (epoch-tagged, zeroed once)
   bool chol_persist;                 // the factorisation runs as one persistent launch (ba_chol_persist.hip)
+  OvPlan ov;                         // ... with S formed in the same launch (the overlapped form)
   const int4* blocks; int nblocks;   // off-diagonal Schur blocks {I, J, start, end}, camera rows interleaved over the XCDs
   const int* xoff;                   // [9] k_schur_pairs* block range of XCD x: [xoff[x], xoff[x+1])
   int xmax;                          // largest XCD range
@@ -207,6 +224,12 @@ void launch_reduce(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, hipSt
 void launch_reduce_publish(const DevWork& W, uint32_t sum_mask, uint32_t max_mask, double* host, int n,
                            unsigned* host_seq, unsigned seq, unsigned* ticket, hipStream_t s);
 int back_flow_capacity(int device);
+int chol_persist_capacity(int device);   // resident k_chol_persist workgroups (occupancy x CUs; -1: query failed)
+// the persistent factorisation with S formed in the same launch (W.S holds
+// nothing on entry): pairs, diagonal slices and fold of this step at radius
+// (pass_only, diagnostics: S formed by that launch's work items, nothing factored)
+void launch_cholesky_solve_ov(const DevProblem& P, const DevWork& W, OvPlan& plan, double radius, int epoch,
+                              hipStream_t s, bool pass_only = false);
 bool obs_w_pc_ok(const DevProblem& P, const DevWork& W);   // k_obs_w_rc has the PCG record form for this source
 bool chol_persist_fits(int device, int n);   // every workgroup of k_chol_persist resident at once
 int chol_split_blocks();                     // block columns from which the split step form is used   // resident k_back_flow workgroups (-1: query failed)

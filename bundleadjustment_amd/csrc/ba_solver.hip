@@ -457,6 +457,108 @@ void set_problem(ba_ctx* ctx, const ba_problem* pb) {
   ctx->have_problem = true;
 }
 
+// The overlapped form's plan (ba_kernels.h OvPlan, ba_chol_persist.hip
+// OvArgs): every S entry of the lower tiles is rewritten each step (no empty
+// camera pair, no point observed twice by one camera), the persistent grid
+// fits, and the launch takes every CU.  Work items per XCD queue in tile-column
+// order: for each tile column, the diagonal slices of its cameras (dealt
+// round-robin over the queues), then its pair blocks in row-major order, cut
+// into 8 contiguous runs of equal pair count (one per queue: the runs of a
+// column are formed side by side) and grouped 4 to an item.
+void build_overlap_plan(ba_ctx* ctx, const std::vector<int4>& blocks) {
+  DevWork& W = ctx->W;
+  W.ov = OvPlan{};
+  const int n = ctx->n, nvc = ctx->nvc, G = W.cam_split;
+  const int T = (n + 63) / 64, TR = (n + 1 + 63) / 64;
+  if (!W.chol_persist || nvc == 0 || ctx->dup_diag || W.s_memset || W.neblocks != 0) return;
+  const int cap = bahip::chol_persist_capacity(ctx->device);
+  int grid = 1;
+  for (int j = 1; j < T; ++j) grid += TR - (j == 1 ? 2 : j);   // (chol_persist_grid)
+  // (at least one helper per XCD queue: a queue's last items are then always
+  // taken, whatever the workers are waiting for)
+  if (cap < grid + 8) return;
+  grid = cap;
+  std::vector<unsigned> tgt((size_t)TR * T, 0);
+  auto tile = [&](int r, int c) { return (size_t)(r >> 6) * T + (c >> 6); };
+  std::vector<std::vector<int>> colblk(T);
+  for (size_t b = 0; b < blocks.size(); ++b) {
+    const int I = blocks[b].x, J = blocks[b].y;
+    if (I <= J) return;   // (a diagonal pair block: not this form)
+    colblk[(6 * J) >> 6].push_back((int)b);
+    const int r0 = 6 * I, c0 = 6 * J;
+    std::vector<size_t> ts = {tile(r0, c0), tile(r0, c0 + 5), tile(r0 + 5, c0), tile(r0 + 5, c0 + 5)};
+    std::sort(ts.begin(), ts.end());
+    ts.erase(std::unique(ts.begin(), ts.end()), ts.end());
+    for (size_t t : ts) ++tgt[t];
+  }
+  for (int v = 0; v < nvc; ++v)
+    for (int k = 0; k < 27; ++k) {
+      int row, col;
+      if (k < 21) {
+        int a = 0;
+        while ((a + 1) * (a + 2) / 2 <= k) ++a;
+        row = 6 * v + a;
+        col = 6 * v + k - a * (a + 1) / 2;
+      } else {
+        row = n;
+        col = 6 * v + k - 21;
+      }
+      ++tgt[tile(row, col)];
+    }
+  for (int I = 0; I < TR; ++I)
+    for (int J = 0; J < T && J <= I; ++J)
+      if (tgt[(size_t)I * T + J] == 0) return;   // (a lower tile nothing writes)
+  std::vector<int> items[8], icol[8], ov_blk;
+  int unit_rr = 0;
+  for (int tc = 0; tc < T; ++tc) {
+    for (int v = 0; v < nvc; ++v) {
+      if ((6 * v) >> 6 != tc) continue;
+      for (int g = 0; g < G; ++g) {
+        const int x = unit_rr++ & 7;
+        items[x].push_back(-1 - (v * G + g));
+        icol[x].push_back(tc);
+      }
+    }
+    const std::vector<int>& cb = colblk[tc];
+    long long tot = 0;
+    for (int b : cb) tot += blocks[b].w - blocks[b].z;
+    size_t k = 0;
+    long long acc = 0;
+    for (int x = 0; x < 8; ++x) {
+      const long long until = tot * (x + 1) / 8;
+      std::vector<int> run;
+      while (k < cb.size() && (acc < until || x == 7)) {
+        acc += blocks[cb[k]].w - blocks[cb[k]].z;
+        run.push_back(cb[k++]);
+      }
+      for (size_t r = 0; r < run.size(); r += 4) {
+        items[x].push_back((int)ov_blk.size() / 4);
+        icol[x].push_back(tc);
+        for (int q = 0; q < 4; ++q) ov_blk.push_back(r + q < run.size() ? run[r + q] : -1);
+      }
+    }
+  }
+  std::vector<int> all, allc;
+  OvPlan& P = W.ov;
+  for (int x = 0; x < 8; ++x) {
+    P.ioff[x] = (int)all.size();
+    all.insert(all.end(), items[x].begin(), items[x].end());
+    allc.insert(allc.end(), icol[x].begin(), icol[x].end());
+  }
+  P.ioff[8] = (int)all.size();
+  if (ov_blk.empty()) ov_blk.assign(4, -1);
+  P.items = ctx->upload(all);
+  P.item_col = ctx->upload(allc);
+  P.ov_blk = ctx->upload(ov_blk);
+  P.tgt = ctx->upload(tgt);
+  const size_t nctr = 2 * (size_t)TR * T + nvc + 8;   // cnt | cam_cnt | q | pflag
+  P.ctr = ctx->dalloc<unsigned>(nctr);
+  HIP_OK(hipMemsetAsync(P.ctr, 0, sizeof(unsigned) * nctr, ctx->stream));
+  P.grid = grid;
+  P.launches = 0;
+  P.ok = true;
+}
+
 // DENSE_SCHUR structures (built on the first dense solve): the dense reduced
 // system S / factor Lf (16 n^2 bytes), Cholesky block inverses, and the Schur
 // pair lists.
@@ -574,6 +676,7 @@ void ensure_dense(ba_ctx* ctx) {
     }
   }
   HIP_OK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)(ctx->n + 1) * std::max(ctx->ld, 1), ctx->stream));
+  build_overlap_plan(ctx, blocks);
   HIP_OK(hipStreamSynchronize(ctx->stream));
   ctx->have_dense = true;
 }
@@ -730,11 +833,22 @@ struct StepResult { bool linear_ok; double mcc, cand_cost, step_norm; int ls_ite
 
 // DENSE_SCHUR: explicit reduced camera system (form_reduced_dense) + dense
 // Cholesky
-void form_reduced_dense(ba_ctx* ctx, double radius) {
+// Returns true when S is left to the factorisation's launch (the overlapped
+// form, launch_cholesky_solve_ov: single rank, compact W records, the
+// persistent factorisation; BA_CHOL_OVERLAP=0, read per step, or
+// allow_ov = false keeps the separate pair / diagonal / fold launches)
+bool form_reduced_dense(ba_ctx* ctx, double radius, bool allow_ov = true) {
   const hipStream_t s = ctx->stream;
   DevProblem& P = ctx->P;
   DevWork& W = ctx->W;
   ensure_dense(ctx);
+  const char* oe = getenv("BA_CHOL_OVERLAP");
+  const bool ov = allow_ov && !(oe && oe[0] == '0') && W.ov.ok && W.chol_persist && !ctx->coll() && !ctx->dup_diag &&
+                  radius > 0.0 && W.wcompact && !W.jdiag && !W.w32 && ctx->n > 0;
+  if (ov) {
+    launch_point_elim(P, W, radius, s, ctx->take_norms());
+    return true;
+  }
   if (ctx->n > 0) {
     if (W.s_memset) HIP_OK(hipMemsetAsync(W.S, 0, sizeof(double) * (size_t)(ctx->n + 1) * ctx->ld, s));
     else launch_zero_blocks(P, W, s);
@@ -767,10 +881,13 @@ void form_reduced_dense(ba_ctx* ctx, double radius) {
     launch_pack_lower(P, W, false, s);
   }
   if (!fused_diag) launch_cam_add_diag(P, W, radius, s);   // (after the exchange)
+  return false;
 }
 void reduced_solve_dense(ba_ctx* ctx, double radius) {
-  form_reduced_dense(ctx, radius);
-  launch_cholesky_solve2(ctx->P, ctx->W, ++ctx->chol_epoch, ctx->stream);
+  if (form_reduced_dense(ctx, radius))
+    launch_cholesky_solve_ov(ctx->P, ctx->W, ctx->W.ov, radius, ++ctx->chol_epoch, ctx->stream);
+  else
+    launch_cholesky_solve2(ctx->P, ctx->W, ++ctx->chol_epoch, ctx->stream);
 }
 
 // ITERATIVE_SCHUR: implicit Schur complement + PCG (ba_pcg.hip).  The host
@@ -1538,7 +1655,14 @@ int ba_debug_blocks(ba_ctx* ctx, double radius, double* Hpp, double* gp, double*
     const LinResult L = linearize(ctx, true, o.min_lm_diagonal, o.max_lm_diagonal);
     if (!L.ok) throw BaError{BA_ERR_DEVICE, "linearisation not finite"};
     step_w_storage(ctx, o);
-    form_reduced_dense(ctx, radius);
+    // BA_DEBUG_OV_PASS=1: S from the overlapped form's work items (a launch
+    // that only forms S), else from the separate pair / diagonal / fold passes
+    const char* dv = getenv("BA_DEBUG_OV_PASS");
+    const bool want_ov = dv && dv[0] == '1';
+    if (form_reduced_dense(ctx, radius, want_ov))
+      launch_cholesky_solve_ov(ctx->P, ctx->W, ctx->W.ov, radius, ++ctx->chol_epoch, ctx->stream, true);
+    else if (want_ov)
+      throw BaError{BA_ERR_INVALID_ARGUMENT, "BA_DEBUG_OV_PASS: the overlapped form does not apply to this problem"};
     const hipStream_t st = ctx->stream;
     const int np = ctx->np, nc = ctx->nc, nvc = ctx->nvc, n = ctx->n;
     HIP_OK(hipStreamSynchronize(st));

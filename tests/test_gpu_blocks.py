@@ -105,3 +105,30 @@ def test_diagonal_slices_in_the_pair_launch_are_bitwise_the_separate_launch(monk
     tril = np.tril_indices(n)
     assert np.array_equal(a["S"][tril], b["S"][tril])
     assert np.array_equal(a["rhs"], b["rhs"])
+
+
+@pytest.mark.timeout(600)
+def test_overlapped_pass_is_bitwise_the_separate_passes(monkeypatch):
+    """C3: the reduced system the overlapped factorisation forms inside its
+    own launch (ba_chol_persist.hip OvArgs: per-XCD queues of wave-sized work
+    items in tile-column order — pair blocks with two LDS-DMA rounds in
+    flight, diagonal slices, the fold by the wave that completes a camera)
+    is bitwise the reduced system of the separate pair / diagonal / fold
+    launches: the same lanes, pairs, products and reductions per entry.
+    BA_DEBUG_OV_PASS=1 makes ba_debug_blocks run that launch with the
+    factorisation switched off (and fail if the form does not apply)."""
+    p = make_config("c3", scale=1.0)
+    with Solver(0) as s:
+        s.set_problem(p)
+        a = s.debug_blocks(1e4)
+        monkeypatch.setenv("BA_DEBUG_OV_PASS", "1")
+        b = s.debug_blocks(1e4)
+        c = s.debug_blocks(3e2)    # a second launch: cumulative counters and tickets
+        monkeypatch.delenv("BA_DEBUG_OV_PASS")
+        d = s.debug_blocks(3e2)
+    n = a["n"]
+    tril = np.tril_indices(n)
+    assert np.array_equal(a["S"][tril], b["S"][tril])
+    assert np.array_equal(a["rhs"], b["rhs"])
+    assert np.array_equal(c["S"][tril], d["S"][tril])
+    assert np.array_equal(c["rhs"], d["rhs"])

@@ -355,6 +355,35 @@ def test_persistent_cholesky_spin_fallback_redoes_the_step(monkeypatch, spec):
         assert [x["step_is_successful"] for x in ref[3]] == [x["step_is_successful"] for x in r[3]]
 
 
+@pytest.mark.timeout(600)
+def test_overlapped_factorisation_is_bitwise_the_serial_forms(monkeypatch):
+    """C3 (200 cameras, every camera pair co-observed): the persistent
+    factorisation that forms S inside its own launch (the overlapped form,
+    the default there) against the persistent launch on an S formed by the
+    separate passes (BA_CHOL_OVERLAP=0) and the per-step launches
+    (BA_CHOL_PERSIST=0): bitwise identical trajectories.  Then the spin
+    fallback from the overlapped form (BA_CHOL_SPIN_MAX=1: the first tile
+    hand-off not yet up gives up) redoes the step with the per-step launches,
+    bitwise as well."""
+    p = make_config("c3")
+    opts = Options(max_num_iterations=5)
+    runs = {}
+    for name, env in (("ov", {}), ("serial", {"BA_CHOL_OVERLAP": "0"}), ("per_step", {"BA_CHOL_PERSIST": "0"}),
+                      ("spin", {"BA_CHOL_SPIN_MAX": "1"})):
+        for k in ("BA_CHOL_OVERLAP", "BA_CHOL_PERSIST", "BA_CHOL_SPIN_MAX"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with Solver(0) as s:
+            runs[name] = run_gpu(s, p, opts)
+    ref = runs["per_step"]
+    for name in ("ov", "serial", "spin"):
+        r = runs[name]
+        assert np.array_equal(ref[0], r[0]) and np.array_equal(ref[1], r[1]), name
+        assert [x["cost"] for x in ref[3]] == [x["cost"] for x in r[3]], name
+        assert [x["step_is_successful"] for x in ref[3]] == [x["step_is_successful"] for x in r[3]], name
+
+
 # ---------------------------------------------------------------------------
 # speculative linearisation (BA_SPEC_LIN: the linearisation at a step's
 # candidate is enqueued behind the step's scalar record; a rejected or invalid

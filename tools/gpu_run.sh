@@ -59,7 +59,7 @@ for step in "$@"; do
         python3 -u bench.py --no-cpu-baseline ${a2//+/ } > "$OUT/prof_$a1.json" 2> "$OUT/prof_$a1.err"
       rc=$?; show "$OUT/prof_$a1.json" "prof_$a1"
       f=$(find "$OUT/prof_$a1" -name '*kernel_stats.csv' | head -1)
-      [ -n "$f" ] && python3 tools/kstats.py "$f" | head -14 ;;
+      [ -n "$f" ] && { python3 tools/kstats.py "$f" > "$OUT/prof_$a1.txt" 2>&1; head -16 "$OUT/prof_$a1.txt"; } ;;
     hbm)
       rc=0
       for ctr in FETCH_SIZE WRITE_SIZE; do
