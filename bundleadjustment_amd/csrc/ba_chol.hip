@@ -10,8 +10,12 @@ namespace bahip {
 //   A    working matrix ((n+1) x ld), trailing part updated in place
 //   L    output factor ((n+1) x ld)
 //   Vbuf [T][64][64] inverses of the diagonal blocks
+//   U    update accumulator ((n+1) x ld): a trailing tile's updates are summed
+//        from zero, U = ((0 - u_0) - u_1) - ..., and its last update writes
+//        A + U into A (the persistent form's order, ba_chol_persist.hip)
 __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, double* __restrict__ L, int ld, int n,
-                                                   int k, double* __restrict__ Vbuf, double* __restrict__ scal) {
+                                                   int k, double* __restrict__ Vbuf, double* __restrict__ scal,
+                                                   double* __restrict__ U) {
   // XCD-aware tile order: workgroup b runs on XCD b % 8 (round-robin
   // dispatch).  The tiles (1,0) and (1,1) produce A_{k+2,k+1} and
   // A_{k+2,k+2}, the next launch's critical inputs; they take linear ids 8
@@ -124,6 +128,10 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
   const int mI = min(CB, nrows - r0);
   if (J == 0) lds_to_global(S0, L, lds, r0, kc, mI, kb);   // L_{I,k} final
   mfma_xyT_64(S0, I != J ? S1 : S0, acc);    // P_I P_J^T
+  // this tile's last update (absolute column k + 1 + J): step k + J off the
+  // diagonal, k + J - 1 on it (its update k + J is the next critical
+  // workgroup's C = A - P P^T) — i.e. relative column 0, resp. tile (1, 1)
+  const bool last = I == J ? J == 1 : J == 0;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -133,7 +141,12 @@ __global__ __launch_bounds__(256) void k_chol_step(double* __restrict__ A, doubl
         int rr, cc;
         acc_pos(a, b, g, &rr, &cc);
         const int ri = r0 + rr, cj = c0 + cc;
-        if (ri < nrows && cj < n && cj <= ri) A[(size_t)ri * ld + cj] -= acc[a][b][g];
+        if (ri < nrows && cj < n && cj <= ri) {
+          const size_t o = (size_t)ri * ld + cj;
+          const double u = (k == 0 ? 0.0 : U[o]) - acc[a][b][g];
+          if (last) A[o] = A[o] + u;
+          else U[o] = u;
+        }
       }
 }
 
@@ -327,14 +340,14 @@ void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hi
     hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.yg, epoch, W.scal);
     return;
   }
-  hipLaunchKernelGGL(k_chol_step, dim3(1, 1), dim3(256), 0, s, W.S, W.Lf, P.ld, n, -1, W.Vbuf, W.scal);
+  hipLaunchKernelGGL(k_chol_step, dim3(1, 1), dim3(256), 0, s, W.S, W.Lf, P.ld, n, -1, W.Vbuf, W.scal, W.Ubuf);
   for (int k = 0; k + 1 < T; ++k) {
     const int st = (k + 1) * CB;
     const int tr = (nrows - st + CB - 1) / CB, tc = (n - st + CB - 1) / CB;
     if (split) {
       launch_chol_split_step(W.S, W.Lf, P.ld, n, k, tc, tr, W.Vbuf, W.scal, s);
     } else {
-      hipLaunchKernelGGL(k_chol_step, dim3(tc, tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf, W.scal);
+      hipLaunchKernelGGL(k_chol_step, dim3(tc, tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf, W.scal, W.Ubuf);
     }
   }
   hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.yg, epoch, W.scal);

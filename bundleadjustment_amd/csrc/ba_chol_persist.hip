@@ -70,12 +70,36 @@ __device__ unsigned long long g_estamps[64][2];   // end_step: entered, V stores
 #define WSTAMP(j, i) do {} while (0)
 #endif
 
+// diagnostic build (tools/ov_trace.py, BA_OV_TRACE): s_memrealtime (100 MHz)
+// of the overlapped form's events: [0] the critical workgroup's start,
+// [8 + t] tile t formed (pflag raised), [512 + c] / [768 + c] the critical's
+// step c start / its inputs staged, [1024 + b] / [1536 + b] / [2048 + b]
+// workgroup b's last item taken / own tile formed (seen) / own tile published
+#ifdef BA_OV_TRACE
+__device__ unsigned long long g_ovt[4096];
+#define OVT(i)                                                                                \
+  do {                                                                                        \
+    unsigned long long t_;                                                                    \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+    if ((threadIdx.x & 63) == 0 && (i) < 4096) g_ovt[i] = t_;                                 \
+  } while (0)
+extern "C" int ba_debug_ov_trace(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ovt), sizeof(unsigned long long) * (n < 4096 ? n : 4096)) ==
+                 hipSuccess
+             ? 0
+             : 2;
+}
+#else
+#define OVT(i) do {} while (0)
+#endif
+
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 constexpr unsigned kPersistSpin = 1u << 17;   // ~0.2 s of polls: far beyond any real wait (~20 us)
 // (BA_CHOL_SPIN_MAX, diagnostics: a smaller bound, e.g. 1, so that the
 // spin-fallback path of ba_solve runs; tests/test_gpu_parity.py)
 constexpr int kAuxSc1 = 16;                    // buffer-instruction cache policy: sc1
+constexpr int kOvFar = 3;                      // overlapped form: a worker takes items while >= this many steps from its last update
 
 __device__ __forceinline__ Rsrc make_rsrc(const void* base, size_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
@@ -201,6 +225,7 @@ __device__ __forceinline__ bool wait_flag(const unsigned* flag, unsigned epoch, 
 struct OvArgs {
   int on = 0;
   int pass_only = 0;         // (diagnostics, ba_debug_blocks: every workgroup only takes items; no factorisation)
+  int worker_items = 0;      // (diagnostics, BA_OV_WORKERS: 0 items between updates, 1 all items first, 2 none)
   DevProblem P;
   const int4* blocks;
   const int2* pairs;
@@ -373,7 +398,14 @@ struct PanelPrefetch {
 // one tile's contribution counted; the one that completes the tile raises pflag
 __device__ __forceinline__ void ov_count(const OvArgs& o, int t, unsigned epoch) {
   const unsigned old = __hip_atomic_fetch_add(&o.cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (old + 1u == o.pe * o.tgt[t]) __hip_atomic_store(&o.pflag[t], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1u == o.pe * o.tgt[t]) {
+    __hip_atomic_store(&o.pflag[t], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef BA_OV_TRACE
+    unsigned long long t_;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+    if (8 + t < 512) g_ovt[8 + t] = t_;
+#endif
+  }
 }
 
 // LDS-DMA issued by inline asm (the pair item's pipeline): the compiler,
@@ -646,6 +678,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   if (blockIdx.x == 0) {
     // ---------------- critical workgroup: the diagonal chain
     if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
+    if (ov.on) OVT(0);
     if (ov.on && threadIdx.x == 0) {   // (the serial form's fold clears them before the launch)
       __hip_atomic_store(&a.scal[SL_CHOL_BAD], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&a.scal[SL_CHOL_SPIN], 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -727,6 +760,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         else publish(&vflag[c - 1], a.epoch);
       }
       PSTAMP(c, 0);
+      if (ov.on && threadIdx.x < 64) OVT(512 + c);
 #ifdef BA_CHOL_STAMPS
       if (threadIdx.x == 0) g_stamp_on = c == T / 2;   // the factor's inner stamps: one mid step
       if (threadIdx.x == 0 && c < 64) g_pstamps[c][7] = 0;
@@ -759,6 +793,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
         else lds_barrier();
         if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
         PSTAMP(c, 1);
+        if (ov.on && threadIdx.x < 64) OVT(768 + c);
         if (!have_diag) tD = tile_issue_sc1<true>(rA, ld, s, s, nrows, s + b);   // A_{c,c} (+ rhs row), in flight
         PSTAMP(c, 2);
         d4 acc[4];
@@ -815,35 +850,32 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   }
 
   // ---------------- worker: one lower tile (I, J), J >= 1 (or a helper)
+  // The tile's updates accumulate from zero, own = ((0 - u_0) - u_1) - ...,
+  // and the tile itself is added at the end, A + own (k_chol_step keeps the
+  // same order through its U buffer, so both forms round alike): a worker
+  // needs its tile only for its last update.  Overlapped form: while update k
+  // is not ready and this tile is at least kOvFar block steps from its last
+  // update, the waves take work items (one each per round); near it, and
+  // once the queue is empty, the worker only factors.
   int I, J;
   const bool worker = worker_tile(blockIdx.x, T, a.TR, I, J);
   bool drew_fail = false;   // (overlapped form: this wave's failing draw)
-  if (ov.on) {
-    // work items until this tile's column comes up (helpers: all of them)
-    drew_fail = ov_take(ov, region, islot, a.A, ld, T, a.epoch, worker ? J : -1);
-    if (!worker) return;
-    __syncthreads();   // (the waves' slices of Sall are the tiles' LDS again)
-    spin |= !wait_flag(&ov.pflag[I * T + J], a.epoch, a.spin_max);
+  if (ov.on && (!worker || ov.worker_items == 1)) {
+    drew_fail = ov_take(ov, region, islot, a.A, ld, T, a.epoch, -1);   // helpers: items until none is left
+    if (threadIdx.x < 64) OVT(1024 + blockIdx.x);
+    __syncthreads();
   }
   if (!worker) return;
   const bool diag = I == J;
   const int r0 = I * CB, c0 = J * CB;
   const int mI = min(CB, nrows - r0);
-  // the tile in the MFMA accumulator layout (acc_pos), initial values from
-  // before the launch (plain loads, clamped) or, overlapped, formed in this
-  // launch (sc1 loads)
-  double own[2][2][4];
+  double own[2][2][4];   // (the MFMA accumulator layout, acc_pos)
 #pragma unroll
   for (int x = 0; x < 2; ++x)
 #pragma unroll
     for (int y = 0; y < 2; ++y)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        int rr, cc;
-        acc_pos(x, y, g, &rr, &cc);
-        const size_t off = (size_t)min(r0 + rr, nrows - 1) * ld + min(c0 + cc, n - 1);
-        own[x][y][g] = ov.on ? __hip_atomic_load(a.A + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.A[off];
-      }
+      for (int g = 0; g < 4; ++g) own[x][y][g] = 0.0;
   const int kmax = diag ? J - 2 : J - 1;
   const bool stamp = I == J + 1;   // (diagnostics: the next-panel tiles' last update)
   // the panel tiles A_{I,k}, A_{J,k} of update k are final long before V_k
@@ -864,13 +896,65 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
     tile_put(S0, tI);
     if (!diag) tile_put(S1, tJ);
   };
-  if (kmax >= 0) stage_panels(0);
-  for (int k = 0; k <= kmax; ++k) {
+  __shared__ int ov_sh[2];   // (overlapped form: update k ready | the queue is empty)
+  bool no_items = !ov.on || ov.worker_items != 0;
+  if (threadIdx.x == 0) ov_sh[1] = 0;
+  auto up = [&](const unsigned* f) {
+    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
+  };
+  bool staged = false;
+  if (kmax >= 0 && (no_items || J < kOvFar)) {
+    stage_panels(0);
+    staged = true;
+  }
+  for (int k = 0; k <= kmax;) {
+    if (!no_items && J - k >= kOvFar) {
+      if (threadIdx.x == 0) {
+        bool r = up(&vflag[k]);
+        if (r) r = k >= 1 ? up(&tflag[I * T + k]) && (diag || up(&tflag[J * T + k]))
+                          : up(formed(I, 0)) && (diag || up(formed(J, 0)));
+        ov_sh[0] = r ? 1 : 0;
+      }
+      __syncthreads();
+      const bool ready = ov_sh[0] != 0;
+      if (!ready) {
+        int item;
+        if (ov_draw(ov, blockIdx.x & 7, item)) {
+          ov_run(ov, item, region, islot, a.A, ld, T, a.epoch);
+        } else {
+          drew_fail = true;
+          if ((threadIdx.x & 63) == 0) ov_sh[1] = 1;
+        }
+        __syncthreads();
+        no_items = ov_sh[1] != 0;
+        continue;
+      }
+      __syncthreads();   // (ov_sh[0] is read)
+    }
+    if (!staged) stage_panels(k);
     spin |= !wait_flag(&vflag[k], a.epoch, a.spin_max);
     if (stamp && k == kmax) WSTAMP(J, 0);
     tile_put(S2, tile_fetch_sc1(rV, CB, k * CB, 0, (k + 1) * CB, CB));          // V_k (stored cleaned)
     __syncthreads();
     if (stamp && k == kmax) WSTAMP(J, 1);
+    // the tile itself, for the last update: in flight under its GEMMs
+    // (overlapped: formed in this launch, sc1 loads)
+    double av[2][2][4];
+    if (k == kmax) {
+      if (ov.on) spin |= !wait_flag(&ov.pflag[I * T + J], a.epoch, a.spin_max);
+      if (ov.on && threadIdx.x < 64) OVT(1536 + blockIdx.x);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            int rr, cc;
+            acc_pos(x, y, g, &rr, &cc);
+            const size_t off = (size_t)min(r0 + rr, nrows - 1) * ld + min(c0 + cc, n - 1);
+            av[x][y][g] = ov.on ? __hip_atomic_load(a.A + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.A[off];
+          }
+    }
     // P_I = A_{I,k} V_k^T, P_J likewise: V_k is lower triangular, so the
     // strip products skip its zero blocks (40 instead of 64 MFMAs per wave;
     // the skipped terms are exact zeros, so the sums are those of the full
@@ -901,9 +985,22 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       for (int y = 0; y < 2; ++y)
 #pragma unroll
         for (int g = 0; g < 4; ++g) own[x][y][g] -= acc[x][y][g];
+    if (k == kmax) {
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) own[x][y][g] = av[x][y][g] + own[x][y][g];
+    }
     __syncthreads();                           // S0..S2 are restaged next
     if (stamp && k == kmax) WSTAMP(J, 3);
-    if (k < kmax) stage_panels(k + 1);
+    ++k;
+    staged = false;
+    if (k <= kmax && (no_items || J - k < kOvFar)) {
+      stage_panels(k);
+      staged = true;
+    }
   }
   // publish the tile (lower part; pairs that start on or left of the
   // diagonal on a diagonal tile): through S0, as row-contiguous 16-B sc1 stores
@@ -926,6 +1023,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   }
   publish(&tflag[I * T + J], a.epoch);
   if (stamp) WSTAMP(J, 4);
+  if (ov.on && threadIdx.x < 64) OVT(2048 + blockIdx.x);
   // L_{I,J-1} (the last update of an off-diagonal tile: J == k + 1) to the
   // factor, after the publish: no in-kernel reader, and its drain would
   // otherwise sit in the barriers before the tile's hand-off
@@ -983,6 +1081,8 @@ void launch_chol_persist_ov(const DevProblem& P, const DevWork& W, OvPlan& plan,
   OvArgs& o = a.ov;
   o.on = 1;
   o.pass_only = pass_only ? 1 : 0;
+  const char* we = getenv("BA_OV_WORKERS");
+  o.worker_items = we ? atoi(we) : 0;
   o.P = P;
   o.blocks = W.blocks; o.pairs = W.pairs; o.Wc = W.W; o.scale_c = W.scale_c; o.u = W.u;
   o.Hcc = W.Hcc; o.gc = W.gc; o.diag_c = W.diag_c; o.radius = radius;

@@ -96,6 +96,7 @@ struct DevWork {
   bool wcompact;                     // W as 128-B compact records (J-free fp64 DENSE_SCHUR; ba_kernels.hip)
   double* S;                         // [(n+1) x ld] reduced system, row n = rhs (working matrix)
   double* Lf;                        // [(n+1) x ld] Cholesky factor, row n = L^-1 rhs
+  double* Ubuf;                      // [(n+1) x ld] the per-step Cholesky's update accumulator (< kCholSplitBlocks block columns)
   double* Spk;                       // [n(n+1)/2 + n] packed lower triangle + rhs of S (multi-rank exchange)
   double* y;                         // [n] reduced solution
   double* Vbuf;                      // [ceil(n/64)][64][64] inverses of the diagonal Cholesky blocks

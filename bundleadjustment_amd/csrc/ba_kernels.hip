@@ -1839,6 +1839,11 @@ struct FoldArgs {
   const double* u = nullptr;
   int G = 0;
 };
+// CTAB: the camera constants in an LDS table (<= ~220 variable cameras);
+// else (1000 cameras: 72 KB of table beside the 64 KB of records would leave
+// one workgroup per CU) each block's two cameras' constants in registers,
+// loaded with the block — the same values, so the same S bitwise
+template <bool CTAB>
 __global__ __launch_bounds__(256) void k_schur_pairs_cd(DevProblem P, const int4* __restrict__ blocks,
                                                         const int* __restrict__ xoff, const int2* __restrict__ pairs,
                                                         const double* __restrict__ Wc,
@@ -1869,8 +1874,10 @@ __global__ __launch_bounds__(256) void k_schur_pairs_cd(DevProblem P, const int4
     return;
   }
   WcCam* ctab = reinterpret_cast<WcCam*>(dsm + kPairsDmaLds / (int)sizeof(double));
-  for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
-  __syncthreads();
+  if constexpr (CTAB) {
+    for (int v = threadIdx.x; v < P.nvc; v += blockDim.x) ctab[v].load(P, scale_c, v);
+    __syncthreads();
+  }
   constexpr int PL = kPairLanes, BPW = 64 / PL;
   const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
   const int xcd = blockIdx.x & 7, wx = blockIdx.x >> 3, nwx = pgrid >> 3;
@@ -1907,8 +1914,14 @@ __global__ __launch_bounds__(256) void k_schur_pairs_cd(DevProblem P, const int4
     const int bi = base + sub;
     const bool live = bi < r1;
     const int4 blk = live ? blocks[bi] : make_int4(0, 0, 0, 0);
-    const WcCam& mI = ctab[blk.x];
-    const WcCam& mJ = ctab[blk.y];
+    WcCam mI, mJ;
+    if constexpr (CTAB) {
+      mI = ctab[blk.x];
+      mJ = ctab[blk.y];
+    } else {
+      mI.load(P, scale_c, blk.x);
+      mJ.load(P, scale_c, blk.y);
+    }
     double acc[36];
 #pragma unroll
     for (int k = 0; k < 36; ++k) acc[k] = 0.0;
@@ -3559,7 +3572,15 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, do
   // the LDS (two workgroups per CU): C3 159 -> 121 us, 1409-1424 -> 1487-1503
   // M-obs/s (profiles/r04_v7_ab_pairs_dma.txt); beyond, the register form
   const size_t ctab_bytes = sizeof(WcCam) * (size_t)P.nvc;
-  if (W.wcompact && kPairsDmaLds + ctab_bytes <= 80 * 1024) {
+  const bool ctab = kPairsDmaLds + ctab_bytes <= 80 * 1024;
+  const char* de = getenv("BA_PAIRS_DMA");   // (0: the register gathers beyond the LDS camera table; A/B)
+  if (W.wcompact && !ctab && !(de && de[0] == '0')) {
+    // 1000 cameras (C4): LDS-DMA gathers with the camera constants per block
+    // in registers
+    hipLaunchKernelGGL(k_schur_pairs_cd<false>, dim3(grid), dim3(256), kPairsDmaLds, s, P, W.blocks, xoff, W.pairs,
+                       W.W, W.scale_c, W.S, grid, FoldArgs{W.cpart, 0, W.Hcc, W.gc, W.diag_c, 0.0, W.scal});
+  }
+  else if (W.wcompact && ctab) {
     FoldArgs fa{W.cpart, 0, W.Hcc, W.gc, W.diag_c, fold_radius, W.scal};
     int fgrid = 0;
     if (with_diag) {   // the diagonal slices ride in this launch (dispatched last: they fill the pairs' tail)
@@ -3570,7 +3591,7 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, do
       fa.nsl = cam_split_count(W);
       fgrid = (P.nvc * 27 + 255) / 256;
     }
-    hipLaunchKernelGGL(k_schur_pairs_cd, dim3(grid + fgrid), dim3(256), kPairsDmaLds + ctab_bytes, s, P, W.blocks,
+    hipLaunchKernelGGL(k_schur_pairs_cd<true>, dim3(grid + fgrid), dim3(256), kPairsDmaLds + ctab_bytes, s, P, W.blocks,
                        xoff, W.pairs, W.W, W.scale_c, W.S, grid, fa);
   }
   else if (W.wcompact)

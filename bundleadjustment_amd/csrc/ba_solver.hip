@@ -616,6 +616,8 @@ void ensure_dense(ba_ctx* ctx) {
   DevWork& W = ctx->W;
   W.S = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
   W.Lf = ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1));
+  W.Ubuf = (ctx->n + 63) / 64 < bahip::chol_split_blocks()
+               ? ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1)) : nullptr;
   W.Vbuf = ctx->dalloc<double>((size_t)((ctx->n + 63) / 64 + 1) * 64 * 64);
   W.yg = ctx->dalloc<double>(2 * (size_t)std::max(ctx->n, 1));
   {

@@ -55,6 +55,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dy, sizeof(double) * n));
   double* dF;
   CK(hipMalloc(&dF, sizeof(double) * 2 * n));
+  double* dU;   // the per-step form's update accumulator
+  CK(hipMalloc(&dU, sizeof(double) * A.size()));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -71,7 +73,7 @@ int main(int argc, char** argv) {
       if (k >= 0 && T >= kCholSplitBlocks) {
         launch_chol_split_step(dA, dL, ld, n, k, grid.x, grid.y, dV, dS, 0);
       } else {
-        hipLaunchKernelGGL(k_chol_step, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS);
+        hipLaunchKernelGGL(k_chol_step, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS, dU);
       }
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));

@@ -6,7 +6,7 @@
 #
 # Each STEP is one shell word; fields are ':'-separated, and '+' stands for a
 # space inside bench / pytest arguments:
-#   tests[:PYTEST_ARGS]        pytest -m gpu (e.g. tests:-k+blocks)
+#   tests[:EXPR]               pytest -m gpu [-k EXPR] (e.g. tests:blocks+or+persistent)
 #   smoke                      __graft_entry__.smoke()
 #   bench:TAG[:ARGS]           python bench.py ARGS > OUTDIR/bench_TAG.json
 #   prof:TAG[:ARGS]            rocprofv3 --kernel-trace --stats of bench.py ARGS
@@ -45,7 +45,8 @@ for step in "$@"; do
     env) export "$a1"; continue ;;
     unset) unset "$a1"; continue ;;
     tests)
-      timeout -k 10 1100 python3 -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ${a1//+/ } \
+      kexpr=(); [ -n "$a1" ] && kexpr=(-k "${a1//+/ }")
+      timeout -k 10 1100 python3 -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread "${kexpr[@]}" \
         > "$OUT/pytest_gpu.log" 2>&1
       rc=$?; tail -6 "$OUT/pytest_gpu.log" ;;
     smoke)
