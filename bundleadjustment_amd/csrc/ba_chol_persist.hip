@@ -99,7 +99,7 @@ constexpr unsigned kPersistSpin = 1u << 17;   // ~0.2 s of polls: far beyond any
 // (BA_CHOL_SPIN_MAX, diagnostics: a smaller bound, e.g. 1, so that the
 // spin-fallback path of ba_solve runs; tests/test_gpu_parity.py)
 constexpr int kAuxSc1 = 16;                    // buffer-instruction cache policy: sc1
-constexpr int kOvFar = 3;                      // overlapped form: a worker takes items while >= this many steps from its last update
+constexpr int kOvFar = 4;                      // overlapped form: a worker takes items while >= this many steps from its last update
 
 __device__ __forceinline__ Rsrc make_rsrc(const void* base, size_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
@@ -226,6 +226,7 @@ struct OvArgs {
   int on = 0;
   int pass_only = 0;         // (diagnostics, ba_debug_blocks: every workgroup only takes items; no factorisation)
   int worker_items = 0;      // (diagnostics, BA_OV_WORKERS: 0 items between updates, 1 all items first, 2 none)
+  int far = kOvFar;          // (BA_OV_FAR: the distance from its last update below which a worker takes no item)
   DevProblem P;
   const int4* blocks;
   const int2* pairs;
@@ -431,12 +432,12 @@ __device__ __forceinline__ void adma4(const void* src, unsigned lds) {    // 4 B
 // factorisation's one workgroup per CU leaves each wave alone on its SIMD, so
 // the second round is what hides the gather latency.  The pair indices come
 // by LDS-DMA too, three rounds ahead (islot: 4 x 64 {x, y}), so no register
-// is ever loaded in flight.  Round r: wait vmcnt(16) (its records and round
-// r + 2's indices have landed: behind them are round r + 2's indices' two
-// pieces... see below), read them, then request round r + 3's indices (2
-// pieces) and round r + 2's records (16 pieces).  Rounds past a block's end
-// fetch its last pair again (L2 hits) and compute nothing, so the count of
-// memory operations per round never changes.
+// is ever loaded in flight.  Round t requests round t + 3's indices (2
+// pieces, if that round exists) and round t + 2's records (16 pieces, if it
+// exists); so behind round t's records there are round t + 2's indices and
+// round t + 1's records, and behind round t + 2's indices round t + 1's
+// records: vmcnt(16) waits for both while round t + 1 exists, vmcnt(0) at
+// the last round.
 __device__ __forceinline__ void ov_pair_item(const OvArgs& o, int g, double* region, int* islot, double* S, size_t ld,
                                              int T, unsigned epoch) {
   constexpr int PL = kPairLanes;
@@ -501,20 +502,19 @@ __device__ __forceinline__ void ov_pair_item(const OvArgs& o, int g, double* reg
   for (int k = 0; k < 36; ++k) acc[k] = 0.0;
   // prologue: indices of rounds 0, 1 (waited), records 0, indices 2, records 1
   req_idx(0);
-  req_idx(1);
+  if (nit > 1) req_idx(1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   req_rec(0);
-  req_idx(2);
-  req_rec(1);
+  if (nit > 2) req_idx(2);
+  if (nit > 1) req_rec(1);
   for (int t = 0; t < nit; ++t) {
-    // behind round t's records: round t + 2's indices (2) and round t + 1's
-    // records (16); behind round t + 2's indices: 16
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    if (t + 1 < nit) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const WcRaw wa = read_rec(rbuf(t));
     const WcRaw wb = read_rec(rbuf(t) + 64 * kWcRec);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the refill
-    req_idx(t + 3);
-    req_rec(t + 2);
+    if (t + 3 < nit) req_idx(t + 3);
+    if (t + 2 < nit) req_rec(t + 2);
     if (e0 + t * PL < blk.w) {
       double ca0[6], ca1[6], cb0[6], cb1[6];
       wc_rows(wa, mI, ca0, ca1);
@@ -539,7 +539,6 @@ __device__ __forceinline__ void ov_pair_item(const OvArgs& o, int g, double* reg
         for (int j = 0; j < 6; ++j) acc[i * 6 + j] += ca0[i] * n0[j] + ca1[i] * n1[j];
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the requests past the end land before the slices are reused)
 #pragma unroll
   for (int k = 0; k < 36; ++k) {
     double v = acc[k];
@@ -903,12 +902,12 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
     return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
   };
   bool staged = false;
-  if (kmax >= 0 && (no_items || J < kOvFar)) {
+  if (kmax >= 0 && (no_items || J < ov.far)) {
     stage_panels(0);
     staged = true;
   }
   for (int k = 0; k <= kmax;) {
-    if (!no_items && J - k >= kOvFar) {
+    if (!no_items && J - k >= ov.far) {
       if (threadIdx.x == 0) {
         bool r = up(&vflag[k]);
         if (r) r = k >= 1 ? up(&tflag[I * T + k]) && (diag || up(&tflag[J * T + k]))
@@ -997,7 +996,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
     if (stamp && k == kmax) WSTAMP(J, 3);
     ++k;
     staged = false;
-    if (k <= kmax && (no_items || J - k < kOvFar)) {
+    if (k <= kmax && (no_items || J - k < ov.far)) {
       stage_panels(k);
       staged = true;
     }
@@ -1083,6 +1082,8 @@ void launch_chol_persist_ov(const DevProblem& P, const DevWork& W, OvPlan& plan,
   o.pass_only = pass_only ? 1 : 0;
   const char* we = getenv("BA_OV_WORKERS");
   o.worker_items = we ? atoi(we) : 0;
+  const char* fe = getenv("BA_OV_FAR");
+  o.far = fe && atoi(fe) > 0 ? atoi(fe) : kOvFar;
   o.P = P;
   o.blocks = W.blocks; o.pairs = W.pairs; o.Wc = W.W; o.scale_c = W.scale_c; o.u = W.u;
   o.Hcc = W.Hcc; o.gc = W.gc; o.diag_c = W.diag_c; o.radius = radius;
