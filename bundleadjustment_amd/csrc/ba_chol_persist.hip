@@ -99,6 +99,7 @@ constexpr unsigned kPersistSpin = 1u << 17;   // ~0.2 s of polls: far beyond any
 // (BA_CHOL_SPIN_MAX, diagnostics: a smaller bound, e.g. 1, so that the
 // spin-fallback path of ba_solve runs; tests/test_gpu_parity.py)
 constexpr int kAuxSc1 = 16;                    // buffer-instruction cache policy: sc1
+constexpr int kOvCams = 200;                   // overlapped form: variable cameras of the LDS camera table (kLinLdsCams)
 constexpr int kOvFar = 4;                      // overlapped form: a worker takes items while >= this many steps from its last update
 
 __device__ __forceinline__ Rsrc make_rsrc(const void* base, size_t bytes) {
@@ -239,15 +240,17 @@ struct OvArgs {
   double radius;
   double* cpart;             // [G][nvc][27] slices
   int G;
-  const int* items;          // >= 0: pair item (4 blocks ov_blk[4 i ..]), < 0: -1 - (v G + g)
+  // item i: irec[4 i .. 4 i + 3], one int4 per 16-lane group: a pair item's
+  // blocks {I, J, start, end} (no block: zeros), or a diagonal item's
+  // {-1 - (v G + g), 0, 0, 0} first
+  const int4* irec;
   const int* item_col;       // the tile column each item belongs to
-  const int* ov_blk;
   const unsigned* tgt;       // [TR][T] contributions per tile and launch
   unsigned* cnt;             // [TR][T] contributions (cumulative)
   unsigned* cam_cnt;         // [nvc] slices done (cumulative)
   unsigned* q;               // [8] tickets drawn (cumulative)
   unsigned* pflag;           // [TR][T] tile formed: the factorisation epoch
-  int ioff[9];               // queue x's items: items[ioff[x] .. ioff[x+1])
+  int ioff[9];               // queue x's items: [ioff[x], ioff[x+1])
   unsigned qbase[8];
   unsigned pe;
 };
@@ -418,12 +421,17 @@ __device__ __forceinline__ void ov_count(const OvArgs& o, int t, unsigned epoch)
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) const void*)p);
 }
+// (M0 is a reserved register: clang warns on the clobber, which the compiler
+// honours — it re-sets M0 before each of its own uses)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void adma16(const void* src, unsigned lds) {   // 16 B per lane, lane-linear
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
 }
 __device__ __forceinline__ void adma4(const void* src, unsigned lds) {    // 4 B per lane, lane-linear
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
 }
+#pragma clang diagnostic pop
 
 // one pair item by one wave: 4 camera-pair blocks, 16 lanes each — the lanes,
 // pairs, products and xor reduction of k_schur_pairs_cd (bitwise its S
@@ -438,23 +446,14 @@ __device__ __forceinline__ void adma4(const void* src, unsigned lds) {    // 4 B
 // round t + 1's records, and behind round t + 2's indices round t + 1's
 // records: vmcnt(16) waits for both while round t + 1 exists, vmcnt(0) at
 // the last round.
-__device__ __forceinline__ void ov_pair_item(const OvArgs& o, int g, double* region, int* islot, double* S, size_t ld,
-                                             int T, unsigned epoch) {
+__device__ __forceinline__ void ov_pair_item(const OvArgs& o, int4 blk, const WcCam* ctab, double* region, int* islot,
+                                             double* S, size_t ld, int T, unsigned epoch) {
   constexpr int PL = kPairLanes;
   static_assert(64 / PL == 4, "a pair item is 4 blocks per wave");
-  const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
-  const int bi = o.ov_blk[4 * g + sub];
-  const bool live = bi >= 0;
-  const int4 blk = live ? o.blocks[bi] : make_int4(0, 0, 0, 0);
-  WcCam mI, mJ;
-  mI.load(o.P, o.scale_c, blk.x);
-  mJ.load(o.P, o.scale_c, blk.y);
-  // (the camera constants land here, before the pipeline: a wait for them
-  // at their first use would sit inside the round loop)
-  asm volatile("" ::"v"(mI.a0[0]), "v"(mI.a0[1]), "v"(mI.a0[2]), "v"(mI.a1[0]), "v"(mI.a1[1]), "v"(mI.a1[2]),
-               "v"(mI.b[0]), "v"(mI.b[1]), "v"(mI.b[2]));
-  asm volatile("" ::"v"(mJ.a0[0]), "v"(mJ.a0[1]), "v"(mJ.a0[2]), "v"(mJ.a1[0]), "v"(mJ.a1[1]), "v"(mJ.a1[2]),
-               "v"(mJ.b[0]), "v"(mJ.b[1]), "v"(mJ.b[2]));
+  const int lane = threadIdx.x & 63, sl = lane & (PL - 1);
+  const bool live = blk.w > blk.z;
+  const WcCam& mI = ctab[blk.x];   // (the workgroup's LDS camera table)
+  const WcCam& mJ = ctab[blk.y];
   const int swr = (lane >> 1) & 7;
   const int len = blk.w - blk.z;
   int nit = len > sl ? (len - sl + PL - 1) / PL : 0;
@@ -616,17 +615,18 @@ __device__ __forceinline__ bool ov_draw(const OvArgs& o, int x, int& item) {
   item = o.ioff[x] + (int)t;
   return true;
 }
-__device__ __forceinline__ void ov_run(const OvArgs& o, int item, double* region, int* islot, double* S, size_t ld,
-                                       int T, unsigned epoch) {
-  const int it = o.items[item];
-  if (it >= 0) ov_pair_item(o, it, region, islot, S, ld, T, epoch);
-  else ov_diag_item(o, -1 - it, region, S, T, epoch);
+__device__ __forceinline__ void ov_run(const OvArgs& o, int item, const WcCam* ctab, double* region, int* islot,
+                                       double* S, size_t ld, int T, unsigned epoch) {
+  const int4 mine = o.irec[4 * (size_t)item + ((threadIdx.x & 63) >> 4)];
+  const int head = __builtin_amdgcn_readfirstlane(mine.x);   // (lanes 0..15: the item's first record)
+  if (head >= 0) ov_pair_item(o, mine, ctab, region, islot, S, ld, T, epoch);
+  else ov_diag_item(o, -1 - head, region, S, T, epoch);
 }
 // items until the queue is exhausted (stop_col < 0) or, for a worker, until
 // the next item is of tile column >= stop_col (its own tile's column comes
 // up).  Returns whether this wave drew its failing ticket.
-__device__ __forceinline__ bool ov_take(const OvArgs& o, double* region, int* islot, double* S, size_t ld, int T,
-                                        unsigned epoch, int stop_col) {
+__device__ __forceinline__ bool ov_take(const OvArgs& o, const WcCam* ctab, double* region, int* islot, double* S,
+                                        size_t ld, int T, unsigned epoch, int stop_col) {
   const int x = blockIdx.x & 7;
   for (;;) {
     if (stop_col >= 0) {
@@ -637,7 +637,7 @@ __device__ __forceinline__ bool ov_take(const OvArgs& o, double* region, int* is
     }
     int item;
     if (!ov_draw(o, x, item)) return true;
-    ov_run(o, item, region, islot, S, ld, T, epoch);
+    ov_run(o, item, ctab, region, islot, S, ld, T, epoch);
   }
 }
 
@@ -662,15 +662,20 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   unsigned* tflag = a.flags + T;
   bool bad = false;    // a non-positive pivot
   bool spin = false;   // a hand-off spin bound hit
-  const OvArgs& ov = a.ov;
   double* region = &Sall[0][0][0] + (size_t)(threadIdx.x >> 6) * (4 * 64 * kWcRec);   // this wave's 32 KB
   __shared__ __attribute__((aligned(16))) int ov_islot[4][4][128];                        // its pair-index slots
   int* islot = ov_islot[threadIdx.x >> 6][0];
+  __shared__ WcCam ov_ctab[kOvCams];   // (overlapped form: the pair items' camera constants)
+  const OvArgs& ov = a.ov;
+  if (ov.on && blockIdx.x != 0) {   // (the critical workgroup takes items only at its end, and fills it then)
+    for (int v = threadIdx.x; v < ov.P.nvc; v += 256) ov_ctab[v].load(ov.P, ov.scale_c, v);
+    __syncthreads();
+  }
   // tiles no worker owns (column 0, and (1, 1)) are final once formed: with
   // the overlapped form their pflag, else ready from before the launch
   auto formed = [&](int I, int J) -> const unsigned* { return ov.on ? &ov.pflag[I * T + J] : nullptr; };
   if (ov.on && ov.pass_only) {
-    ov_take(ov, region, islot, a.A, ld, T, a.epoch, -1);
+    ov_take(ov, ov_ctab, region, islot, a.A, ld, T, a.epoch, -1);
     return;
   }
 
@@ -826,7 +831,8 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
                                (c + 1) * CB, c * CB, nrows, c * CB + min(CB, n - c * CB), c,
                                c + 1 >= 2 ? &tflag[(c + 1) * T + c + 1] : formed(1, 1), dready,
                                rV, (size_t)c * CB * CB * sizeof(double), S2};
-        factor_invert_blk<1>(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr, pf);   // b = m = CB before the last block
+        // (inlined: as a call its prefetch hook object would live in scratch)
+        [[clang::always_inline]] factor_invert_blk<1>(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr, pf);   // b = m = CB before the last block
       } else {
         factor_invert_blk<0>(S0, S2, S1, cw, b, m, c > 0 ? S1 : nullptr);
       }
@@ -843,7 +849,9 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
 #endif
     if (ov.on) {   // this workgroup's failing draws (items left, if any, are run)
       __syncthreads();
-      ov_take(ov, region, islot, a.A, ld, T, a.epoch, -1);
+      for (int v = threadIdx.x; v < ov.P.nvc; v += 256) ov_ctab[v].load(ov.P, ov.scale_c, v);
+      __syncthreads();
+      ov_take(ov, ov_ctab, region, islot, a.A, ld, T, a.epoch, -1);
     }
     return;
   }
@@ -860,7 +868,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   const bool worker = worker_tile(blockIdx.x, T, a.TR, I, J);
   bool drew_fail = false;   // (overlapped form: this wave's failing draw)
   if (ov.on && (!worker || ov.worker_items == 1)) {
-    drew_fail = ov_take(ov, region, islot, a.A, ld, T, a.epoch, -1);   // helpers: items until none is left
+    drew_fail = ov_take(ov, ov_ctab, region, islot, a.A, ld, T, a.epoch, -1);   // helpers: items until none is left
     if (threadIdx.x < 64) OVT(1024 + blockIdx.x);
     __syncthreads();
   }
@@ -919,7 +927,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
       if (!ready) {
         int item;
         if (ov_draw(ov, blockIdx.x & 7, item)) {
-          ov_run(ov, item, region, islot, a.A, ld, T, a.epoch);
+          ov_run(ov, item, ov_ctab, region, islot, a.A, ld, T, a.epoch);
         } else {
           drew_fail = true;
           if ((threadIdx.x & 63) == 0) ov_sh[1] = 1;
@@ -1035,7 +1043,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   if (threadIdx.x == 0 && spin) atomicAdd(&a.scal[SL_CHOL_SPIN], 1.0);
   if (ov.on) {   // this wave's failing draw, unless taken before its tile
     __syncthreads();
-    if (!drew_fail) ov_take(ov, region, islot, a.A, ld, T, a.epoch, -1);
+    if (!drew_fail) ov_take(ov, ov_ctab, region, islot, a.A, ld, T, a.epoch, -1);
   }
 }
 
@@ -1088,7 +1096,7 @@ void launch_chol_persist_ov(const DevProblem& P, const DevWork& W, OvPlan& plan,
   o.blocks = W.blocks; o.pairs = W.pairs; o.Wc = W.W; o.scale_c = W.scale_c; o.u = W.u;
   o.Hcc = W.Hcc; o.gc = W.gc; o.diag_c = W.diag_c; o.radius = radius;
   o.cpart = W.cpart; o.G = W.cam_split;
-  o.items = plan.items; o.item_col = plan.item_col; o.ov_blk = plan.ov_blk; o.tgt = plan.tgt;
+  o.irec = plan.irec; o.item_col = plan.item_col; o.tgt = plan.tgt;
   o.cnt = plan.ctr;
   o.cam_cnt = plan.ctr + (size_t)TR * T;
   o.q = o.cam_cnt + P.nvc;

@@ -61,9 +61,9 @@ struct DevProblem {
 // Built once per problem (ba_solver.hip ensure_overlap).
 struct OvPlan {
   bool ok = false;                   // built, and the problem qualifies
-  const int* items = nullptr;        // >= 0: pair item (4 blocks of ov_blk), < 0: -1 - (v G + g) diagonal slice
+  const int4* irec = nullptr;        // [items][4]: a pair item's 4 blocks {I, J, start, end} (zeros: none),
+                                     //   or {-1 - (v G + g), 0, 0, 0} first: a diagonal slice
   const int* item_col = nullptr;     // tile column of each item
-  const int* ov_blk = nullptr;       // [4 * pair items] block indices (-1: none)
   const unsigned* tgt = nullptr;     // [TR][T] contributions per tile and launch
   unsigned* ctr = nullptr;           // cnt [TR][T] | cam_cnt [nvc] | q [8] | pflag [TR][T]: zeroed once, cumulative
   int ioff[9] = {0};                 // queue x: items [ioff[x], ioff[x+1])

@@ -470,7 +470,8 @@ void build_overlap_plan(ba_ctx* ctx, const std::vector<int4>& blocks) {
   W.ov = OvPlan{};
   const int n = ctx->n, nvc = ctx->nvc, G = W.cam_split;
   const int T = (n + 63) / 64, TR = (n + 1 + 63) / 64;
-  if (!W.chol_persist || nvc == 0 || ctx->dup_diag || W.s_memset || W.neblocks != 0) return;
+  if (!W.chol_persist || nvc == 0 || nvc > bahip::kLinLdsCamsHost || ctx->dup_diag || W.s_memset || W.neblocks != 0)
+    return;
   const int cap = bahip::chol_persist_capacity(ctx->device);
   int grid = 1;
   for (int j = 1; j < T; ++j) grid += TR - (j == 1 ? 2 : j);   // (chol_persist_grid)
@@ -508,14 +509,16 @@ void build_overlap_plan(ba_ctx* ctx, const std::vector<int4>& blocks) {
   for (int I = 0; I < TR; ++I)
     for (int J = 0; J < T && J <= I; ++J)
       if (tgt[(size_t)I * T + J] == 0) return;   // (a lower tile nothing writes)
-  std::vector<int> items[8], icol[8], ov_blk;
+  std::vector<int4> items[8];
+  std::vector<int> icol[8];
   int unit_rr = 0;
   for (int tc = 0; tc < T; ++tc) {
     for (int v = 0; v < nvc; ++v) {
       if ((6 * v) >> 6 != tc) continue;
       for (int g = 0; g < G; ++g) {
         const int x = unit_rr++ & 7;
-        items[x].push_back(-1 - (v * G + g));
+        items[x].push_back(make_int4(-1 - (v * G + g), 0, 0, 0));
+        for (int q = 1; q < 4; ++q) items[x].push_back(make_int4(0, 0, 0, 0));
         icol[x].push_back(tc);
       }
     }
@@ -532,24 +535,22 @@ void build_overlap_plan(ba_ctx* ctx, const std::vector<int4>& blocks) {
         run.push_back(cb[k++]);
       }
       for (size_t r = 0; r < run.size(); r += 4) {
-        items[x].push_back((int)ov_blk.size() / 4);
+        for (int q = 0; q < 4; ++q) items[x].push_back(r + q < run.size() ? blocks[run[r + q]] : make_int4(0, 0, 0, 0));
         icol[x].push_back(tc);
-        for (int q = 0; q < 4; ++q) ov_blk.push_back(r + q < run.size() ? run[r + q] : -1);
       }
     }
   }
-  std::vector<int> all, allc;
+  std::vector<int4> all;
+  std::vector<int> allc;
   OvPlan& P = W.ov;
   for (int x = 0; x < 8; ++x) {
-    P.ioff[x] = (int)all.size();
+    P.ioff[x] = (int)allc.size();
     all.insert(all.end(), items[x].begin(), items[x].end());
     allc.insert(allc.end(), icol[x].begin(), icol[x].end());
   }
-  P.ioff[8] = (int)all.size();
-  if (ov_blk.empty()) ov_blk.assign(4, -1);
-  P.items = ctx->upload(all);
+  P.ioff[8] = (int)allc.size();
+  P.irec = ctx->upload(all);
   P.item_col = ctx->upload(allc);
-  P.ov_blk = ctx->upload(ov_blk);
   P.tgt = ctx->upload(tgt);
   const size_t nctr = 2 * (size_t)TR * T + nvc + 8;   // cnt | cam_cnt | q | pflag
   P.ctr = ctx->dalloc<unsigned>(nctr);
