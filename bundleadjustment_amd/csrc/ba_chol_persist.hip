@@ -667,7 +667,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   int* islot = ov_islot[threadIdx.x >> 6][0];
   __shared__ WcCam ov_ctab[kOvCams];   // (overlapped form: the pair items' camera constants)
   const OvArgs& ov = a.ov;
-  if (ov.on && blockIdx.x != 0) {   // (the critical workgroup takes items only at its end, and fills it then)
+  if (ov.on && (blockIdx.x != 0 || ov.pass_only)) {   // (the critical workgroup takes items only at its end, and fills it then)
     for (int v = threadIdx.x; v < ov.P.nvc; v += 256) ov_ctab[v].load(ov.P, ov.scale_c, v);
     __syncthreads();
   }
