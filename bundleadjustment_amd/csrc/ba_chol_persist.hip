@@ -226,7 +226,7 @@ __device__ __forceinline__ bool wait_flag(const unsigned* flag, unsigned epoch, 
 struct OvArgs {
   int on = 0;
   int pass_only = 0;         // (diagnostics, ba_debug_blocks: every workgroup only takes items; no factorisation)
-  int worker_items = 0;      // (diagnostics, BA_OV_WORKERS: 0 items between updates, 1 all items first, 2 none)
+  int worker_items = 0;      // (diagnostics, BA_OV_WORKERS: 0 items between updates, 2 none)
   int far = kOvFar;          // (BA_OV_FAR: the distance from its last update below which a worker takes no item)
   DevProblem P;
   const int4* blocks;
@@ -240,10 +240,11 @@ struct OvArgs {
   double radius;
   double* cpart;             // [G][nvc][27] slices
   int G;
-  // item i: irec[4 i .. 4 i + 3], one int4 per 16-lane group: a pair item's
-  // blocks {I, J, start, end} (no block: zeros), or a diagonal item's
-  // {-1 - (v G + g), 0, 0, 0} first
+  // item i: irec[16 i ..]: a pair item's item_ng[i] groups of 4 blocks
+  // {I, J, start, end} (one per 16-lane group; no block: zeros), or
+  // (item_ng[i] = 0) a diagonal item's {-1 - (v G + g), 0, 0, 0}
   const int4* irec;
+  const int* item_ng;
   const int* item_col;       // the tile column each item belongs to
   const unsigned* tgt;       // [TR][T] contributions per tile and launch
   unsigned* cnt;             // [TR][T] contributions (cumulative)
@@ -433,48 +434,62 @@ __device__ __forceinline__ void adma4(const void* src, unsigned lds) {    // 4 B
 }
 #pragma clang diagnostic pop
 
-// one pair item by one wave: 4 camera-pair blocks, 16 lanes each — the lanes,
-// pairs, products and xor reduction of k_schur_pairs_cd (bitwise its S
-// blocks).  The records go through LDS by LDS-DMA as there, two rounds in
-// flight (region: 2 x (row, partner) x 64 records = 32 KB): the
-// factorisation's one workgroup per CU leaves each wave alone on its SIMD, so
-// the second round is what hides the gather latency.  The pair indices come
-// by LDS-DMA too, three rounds ahead (islot: 4 x 64 {x, y}), so no register
-// is ever loaded in flight.  Round t requests round t + 3's indices (2
-// pieces, if that round exists) and round t + 2's records (16 pieces, if it
-// exists); so behind round t's records there are round t + 2's indices and
-// round t + 1's records, and behind round t + 2's indices round t + 1's
-// records: vmcnt(16) waits for both while round t + 1 exists, vmcnt(0) at
-// the last round.
-__device__ __forceinline__ void ov_pair_item(const OvArgs& o, int4 blk, const WcCam* ctab, double* region, int* islot,
-                                             double* S, size_t ld, int T, unsigned epoch) {
+// one pair item by one wave: up to kOvGroups groups of 4 camera-pair blocks,
+// 16 lanes per block — the lanes, pairs, products and xor reduction of
+// k_schur_pairs_cd (bitwise its S blocks).  The records go through LDS by
+// LDS-DMA as there, two rounds in flight (region: 2 x (row, partner) x 64
+// records = 32 KB): the factorisation's one workgroup per CU leaves each
+// wave alone on its SIMD, so the second round is what hides the gather
+// latency, and the rounds of an item's groups run as one stream (a group's
+// sums are reduced and stored while the next group's first rounds are in
+// flight: the pipeline fills once per item).  The pair indices come by
+// LDS-DMA too, three rounds ahead (islot: 4 x 64 {x, y}), so no register is
+// ever loaded in flight.  Round R requests round R + 3's indices (2 pieces, if
+// that round exists) and round R + 2's records (16, if it exists), computes,
+// and at a group's last round stores the group's 36 x 4 sums (3 stores per
+// lane).  Behind round R + 2's indices there are then round R + 1's records
+// and round R - 1's stores, behind round R's records more: waiting for
+// vmcnt(r(R + 1) + s(R - 1)) covers both.
+constexpr int kOvGroups = 4;
+template <int N>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ void ov_pair_item(const OvArgs& o, int item, int ng, const WcCam* ctab, double* region,
+                                             int* islot, double* S, size_t ld, int T, unsigned epoch) {
   constexpr int PL = kPairLanes;
-  static_assert(64 / PL == 4, "a pair item is 4 blocks per wave");
-  const int lane = threadIdx.x & 63, sl = lane & (PL - 1);
-  const bool live = blk.w > blk.z;
-  const WcCam& mI = ctab[blk.x];   // (the workgroup's LDS camera table)
-  const WcCam& mJ = ctab[blk.y];
-  const int swr = (lane >> 1) & 7;
-  const int len = blk.w - blk.z;
-  int nit = len > sl ? (len - sl + PL - 1) / PL : 0;
+  static_assert(64 / PL == 4, "a pair item is groups of 4 blocks per wave");
+  const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
+  static_assert(kOvGroups == 4, "four named groups below (no register arrays: they would go to scratch)");
+  auto ld_blk = [&](int g) { return g < ng ? o.irec[(size_t)16 * item + 4 * g + sub] : make_int4(0, 0, 0, 0); };
+  const int4 b0 = ld_blk(0), b1 = ld_blk(1), b2 = ld_blk(2), b3 = ld_blk(3);
+  auto rounds = [&](int4 b) {   // rounds of a group: the most pairs per lane of its 4 blocks (uniform)
+    const int len = b.w - b.z;
+    int n = len > sl ? (len - sl + PL - 1) / PL : 0;
 #pragma unroll
-  for (int x = 32; x >= 1; x >>= 1) nit = max(nit, __shfl_xor(nit, x));
-  nit = __builtin_amdgcn_readfirstlane(nit);   // (a uniform loop)
-  const int e0 = blk.z + sl;
-  // round t's buffers: records (row at +0, partner at +64 records), indices
+    for (int x = 32; x >= 1; x >>= 1) n = max(n, __shfl_xor(n, x));
+    return __builtin_amdgcn_readfirstlane(n);
+  };
+  const int s1 = rounds(b0), s2 = s1 + rounds(b1), s3 = s2 + rounds(b2), nr = s3 + rounds(b3);
+  auto grp = [&](int R) { return (R >= s1 ? 1 : 0) + (R >= s2 ? 1 : 0) + (R >= s3 ? 1 : 0); };
+  auto blk_of = [&](int g) { return g == 0 ? b0 : g == 1 ? b1 : g == 2 ? b2 : b3; };
+  auto st_of = [&](int g) { return g == 0 ? 0 : g == 1 ? s1 : g == 2 ? s2 : s3; };
+  auto is_end = [&](int R) { return R >= 0 && (R + 1 == s1 || R + 1 == s2 || R + 1 == s3 || R + 1 == nr); };
+  const int swr = (lane >> 1) & 7;
+  // round R's buffers: records (row at +0, partner at +64 records), indices
   // (x at +0, y at +64 ints)
-  auto rbuf = [&](int t) { return region + (t & 1) * (128 * kWcRec); };
-  auto ibuf = [&](int t) { return islot + (t & 3) * 128; };
-  auto req_idx = [&](int t) {   // round t's pair of this lane -> ibuf(t)
-    const int2* p = o.pairs + max(min(e0 + t * PL, blk.w - 1), 0);
-    const int* ib = ibuf(t);
+  auto rbuf = [&](int R) { return region + (R & 1) * (128 * kWcRec); };
+  auto ibuf = [&](int R) { return islot + (R & 3) * 128; };
+  auto req_idx = [&](int R) {   // round R's pair of this lane -> ibuf(R)
+    const int g = grp(R);
+    const int4 b = blk_of(g);
+    const int2* p = o.pairs + max(min(b.z + sl + (R - st_of(g)) * PL, b.w - 1), 0);
+    const int* ib = ibuf(R);
     adma4(&p->x, lds_addr(ib));
     adma4(&p->y, lds_addr(ib + 64));
   };
-  auto req_rec = [&](int t) {   // round t's records (its indices in ibuf(t)) -> rbuf(t)
-    const int* ib = ibuf(t);
+  auto req_rec = [&](int R) {   // round R's records (its indices in ibuf(R)) -> rbuf(R)
+    const int* ib = ibuf(R);
     const int2 pr = make_int2(ib[lane], ib[64 + lane]);
-    double* rb = rbuf(t);
+    double* rb = rbuf(R);
     const unsigned lr = lds_addr(rb), lp = lds_addr(rb + 64 * kWcRec);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -501,20 +516,25 @@ __device__ __forceinline__ void ov_pair_item(const OvArgs& o, int4 blk, const Wc
   for (int k = 0; k < 36; ++k) acc[k] = 0.0;
   // prologue: indices of rounds 0, 1 (waited), records 0, indices 2, records 1
   req_idx(0);
-  if (nit > 1) req_idx(1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (nr > 1) req_idx(1);
+  vm_wait<0>();
   req_rec(0);
-  if (nit > 2) req_idx(2);
-  if (nit > 1) req_rec(1);
-  for (int t = 0; t < nit; ++t) {
-    if (t + 1 < nit) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const WcRaw wa = read_rec(rbuf(t));
-    const WcRaw wb = read_rec(rbuf(t) + 64 * kWcRec);
+  if (nr > 2) req_idx(2);
+  if (nr > 1) req_rec(1);
+  for (int R = 0; R < nr; ++R) {
+    const bool rn = R + 1 < nr, sp = is_end(R - 1);
+    if (rn) { if (sp) vm_wait<19>(); else vm_wait<16>(); }
+    else { if (sp) vm_wait<3>(); else vm_wait<0>(); }
+    const WcRaw wa = read_rec(rbuf(R));
+    const WcRaw wb = read_rec(rbuf(R) + 64 * kWcRec);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the refill
-    if (t + 3 < nit) req_idx(t + 3);
-    if (t + 2 < nit) req_rec(t + 2);
-    if (e0 + t * PL < blk.w) {
+    if (R + 3 < nr) req_idx(R + 3);
+    if (R + 2 < nr) req_rec(R + 2);
+    const int g = grp(R);
+    const int4 b = blk_of(g);
+    const WcCam& mI = ctab[b.x];   // (the workgroup's LDS camera table)
+    const WcCam& mJ = ctab[b.y];
+    if (b.z + sl + (R - st_of(g)) * PL < b.w) {
       double ca0[6], ca1[6], cb0[6], cb1[6];
       wc_rows(wa, mI, ca0, ca1);
       wc_rows(wb, mJ, cb0, cb1);
@@ -537,33 +557,47 @@ __device__ __forceinline__ void ov_pair_item(const OvArgs& o, int4 blk, const Wc
 #pragma unroll
         for (int j = 0; j < 6; ++j) acc[i * 6 + j] += ca0[i] * n0[j] + ca1[i] * n1[j];
     }
-  }
+    if (is_end(R)) {   // group g done: reduce, store (3 per lane), restart
 #pragma unroll
-  for (int k = 0; k < 36; ++k) {
-    double v = acc[k];
+      for (int k = 0; k < 36; ++k) {
+        double v = acc[k];
 #pragma unroll
-    for (int x = PL / 2; x >= 1; x >>= 1) v += __shfl_xor(v, x, PL);
-    acc[k] = v;
-  }
-  if (live) {
-    const int I = blk.x, Jb = blk.y;   // I > Jb (no point observed twice by one camera in this form)
+        for (int x = PL / 2; x >= 1; x >>= 1) v += __shfl_xor(v, x, PL);
+        acc[k] = v;
+      }
+      // lane sl stores entries sl, sl + 16, sl + 32 (< 36)
+      double v0 = 0.0, v1 = 0.0, v2 = 0.0;
 #pragma unroll
-    for (int k = 0; k < 36; ++k) {
-      if ((k % PL) != sl) continue;
-      const int i = k / 6, j = k % 6;
-      __hip_atomic_store(S + (size_t)(6 * I + i) * ld + 6 * Jb + j, -acc[k], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < 16; ++k) {
+        v0 = sl == k ? acc[k] : v0;
+        v1 = sl == k ? acc[k + 16] : v1;
+        if (k < 4) v2 = sl == k ? acc[k + 32] : v2;
+      }
+      const bool live = b.w > b.z;
+      const int I = b.x, Jb = b.y;   // I > Jb (no point observed twice by one camera in this form)
+      auto at = [&](int k) { return S + (size_t)(6 * I + k / 6) * ld + 6 * Jb + k % 6; };
+      // (always three store instructions: the waits above count them)
+      if (live) __hip_atomic_store(at(sl), -v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (live) __hip_atomic_store(at(sl + 16), -v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (live && sl < 4) __hip_atomic_store(at(sl + 32), -v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < 36; ++k) acc[k] = 0.0;
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the S stores are done
-  if (live && sl == 0) {
-    const int r0 = (6 * blk.x) >> 6, r1 = (6 * blk.x + 5) >> 6;
-    const int c0 = (6 * blk.y) >> 6, c1 = (6 * blk.y + 5) >> 6;
-    ov_count(o, r0 * T + c0, epoch);
-    if (c1 != c0) ov_count(o, r0 * T + c1, epoch);
-    if (r1 != r0) {
-      ov_count(o, r1 * T + c0, epoch);
-      if (c1 != c0) ov_count(o, r1 * T + c1, epoch);
+  vm_wait<0>();   // the S stores are done: count the item's blocks into their tiles
+  if (sl == 0) {
+#pragma unroll
+    for (int g = 0; g < kOvGroups; ++g) {
+      const int4 b = blk_of(g);
+      if (g >= ng || b.w <= b.z) continue;
+      const int r0 = (6 * b.x) >> 6, r1 = (6 * b.x + 5) >> 6;
+      const int c0 = (6 * b.y) >> 6, c1 = (6 * b.y + 5) >> 6;
+      ov_count(o, r0 * T + c0, epoch);
+      if (c1 != c0) ov_count(o, r0 * T + c1, epoch);
+      if (r1 != r0) {
+        ov_count(o, r1 * T + c0, epoch);
+        if (c1 != c0) ov_count(o, r1 * T + c1, epoch);
+      }
     }
   }
 }
@@ -617,10 +651,9 @@ __device__ __forceinline__ bool ov_draw(const OvArgs& o, int x, int& item) {
 }
 __device__ __forceinline__ void ov_run(const OvArgs& o, int item, const WcCam* ctab, double* region, int* islot,
                                        double* S, size_t ld, int T, unsigned epoch) {
-  const int4 mine = o.irec[4 * (size_t)item + ((threadIdx.x & 63) >> 4)];
-  const int head = __builtin_amdgcn_readfirstlane(mine.x);   // (lanes 0..15: the item's first record)
-  if (head >= 0) ov_pair_item(o, mine, ctab, region, islot, S, ld, T, epoch);
-  else ov_diag_item(o, -1 - head, region, S, T, epoch);
+  const int ng = o.item_ng[item];
+  if (ng > 0) ov_pair_item(o, item, ng, ctab, region, islot, S, ld, T, epoch);
+  else ov_diag_item(o, -1 - o.irec[(size_t)16 * item].x, region, S, T, epoch);
 }
 // items until the queue is exhausted (stop_col < 0) or, for a worker, until
 // the next item is of tile column >= stop_col (its own tile's column comes
@@ -674,12 +707,12 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   // tiles no worker owns (column 0, and (1, 1)) are final once formed: with
   // the overlapped form their pflag, else ready from before the launch
   auto formed = [&](int I, int J) -> const unsigned* { return ov.on ? &ov.pflag[I * T + J] : nullptr; };
-  if (ov.on && ov.pass_only) {
-    ov_take(ov, ov_ctab, region, islot, a.A, ld, T, a.epoch, -1);
-    return;
-  }
-
-  if (blockIdx.x == 0) {
+  // roles (pass-only diagnostics: none); then every workgroup's items (its
+  // waves' failing draws, and whatever is left) — one copy of the item code
+  bool drew_fail = false;   // (overlapped form: this wave's failing draw)
+  int I = 0, J = 0;
+  const bool worker = !ov.pass_only && blockIdx.x != 0 && worker_tile(blockIdx.x, T, a.TR, I, J);
+  if (blockIdx.x == 0 && !ov.pass_only) {
     // ---------------- critical workgroup: the diagonal chain
     if (threadIdx.x == 0) { pref_ok[0] = 0; pref_ok[1] = 0; dready[0] = 0; }
     if (ov.on) OVT(0);
@@ -847,203 +880,195 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
 #ifdef BA_CHOL_STAMPS
     if (threadIdx.x == 0) g_stamp_on = 1;
 #endif
-    if (ov.on) {   // this workgroup's failing draws (items left, if any, are run)
+    if (ov.on) {   // (its camera table, for the items it may still find)
       __syncthreads();
       for (int v = threadIdx.x; v < ov.P.nvc; v += 256) ov_ctab[v].load(ov.P, ov.scale_c, v);
-      __syncthreads();
-      ov_take(ov, ov_ctab, region, islot, a.A, ld, T, a.epoch, -1);
     }
-    return;
-  }
+  } else if (worker) {
 
-  // ---------------- worker: one lower tile (I, J), J >= 1 (or a helper)
-  // The tile's updates accumulate from zero, own = ((0 - u_0) - u_1) - ...,
-  // and the tile itself is added at the end, A + own (k_chol_step keeps the
-  // same order through its U buffer, so both forms round alike): a worker
-  // needs its tile only for its last update.  Overlapped form: while update k
-  // is not ready and this tile is at least kOvFar block steps from its last
-  // update, the waves take work items (one each per round); near it, and
-  // once the queue is empty, the worker only factors.
-  int I, J;
-  const bool worker = worker_tile(blockIdx.x, T, a.TR, I, J);
-  bool drew_fail = false;   // (overlapped form: this wave's failing draw)
-  if (ov.on && (!worker || ov.worker_items == 1)) {
-    drew_fail = ov_take(ov, ov_ctab, region, islot, a.A, ld, T, a.epoch, -1);   // helpers: items until none is left
-    if (threadIdx.x < 64) OVT(1024 + blockIdx.x);
-    __syncthreads();
-  }
-  if (!worker) return;
-  const bool diag = I == J;
-  const int r0 = I * CB, c0 = J * CB;
-  const int mI = min(CB, nrows - r0);
-  double own[2][2][4];   // (the MFMA accumulator layout, acc_pos)
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) own[x][y][g] = 0.0;
-  const int kmax = diag ? J - 2 : J - 1;
-  const bool stamp = I == J + 1;   // (diagnostics: the next-panel tiles' last update)
-  // the panel tiles A_{I,k}, A_{J,k} of update k are final long before V_k
-  // (their workers finished update k - 1 one step earlier): they are staged
-  // while V_k is awaited, so only V_k's fetch follows its flag
-  auto stage_panels = [&](int k) {
-    const int kc = k * CB, kb = min(CB, n - kc);
-    if (k >= 1) {
-      spin |= !wait_flag(&tflag[I * T + k], a.epoch, a.spin_max);
-      if (!diag) spin |= !wait_flag(&tflag[J * T + k], a.epoch, a.spin_max);
-    } else if (ov.on) {   // column 0: formed in this launch, never updated
-      spin |= !wait_flag(formed(I, 0), a.epoch, a.spin_max);
-      if (!diag) spin |= !wait_flag(formed(J, 0), a.epoch, a.spin_max);
-    }
-    const TileRegs tI = tile_fetch_sc1(rA, ld, r0, kc, nrows, kc + kb);        // A_{I,k}
-    TileRegs tJ;
-    if (!diag) tJ = tile_fetch_sc1(rA, ld, c0, kc, n, kc + kb);              // A_{J,k}
-    tile_put(S0, tI);
-    if (!diag) tile_put(S1, tJ);
-  };
-  __shared__ int ov_sh[2];   // (overlapped form: update k ready | the queue is empty)
-  bool no_items = !ov.on || ov.worker_items != 0;
-  if (threadIdx.x == 0) ov_sh[1] = 0;
-  auto up = [&](const unsigned* f) {
-    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
-  };
-  bool staged = false;
-  if (kmax >= 0 && (no_items || J < ov.far)) {
-    stage_panels(0);
-    staged = true;
-  }
-  for (int k = 0; k <= kmax;) {
-    if (!no_items && J - k >= ov.far) {
-      if (threadIdx.x == 0) {
-        bool r = up(&vflag[k]);
-        if (r) r = k >= 1 ? up(&tflag[I * T + k]) && (diag || up(&tflag[J * T + k]))
-                          : up(formed(I, 0)) && (diag || up(formed(J, 0)));
-        ov_sh[0] = r ? 1 : 0;
-      }
-      __syncthreads();
-      const bool ready = ov_sh[0] != 0;
-      if (!ready) {
-        int item;
-        if (ov_draw(ov, blockIdx.x & 7, item)) {
-          ov_run(ov, item, ov_ctab, region, islot, a.A, ld, T, a.epoch);
-        } else {
-          drew_fail = true;
-          if ((threadIdx.x & 63) == 0) ov_sh[1] = 1;
-        }
-        __syncthreads();
-        no_items = ov_sh[1] != 0;
-        continue;
-      }
-      __syncthreads();   // (ov_sh[0] is read)
-    }
-    if (!staged) stage_panels(k);
-    spin |= !wait_flag(&vflag[k], a.epoch, a.spin_max);
-    if (stamp && k == kmax) WSTAMP(J, 0);
-    tile_put(S2, tile_fetch_sc1(rV, CB, k * CB, 0, (k + 1) * CB, CB));          // V_k (stored cleaned)
-    __syncthreads();
-    if (stamp && k == kmax) WSTAMP(J, 1);
-    // the tile itself, for the last update: in flight under its GEMMs
-    // (overlapped: formed in this launch, sc1 loads)
-    double av[2][2][4];
-    if (k == kmax) {
-      if (ov.on) spin |= !wait_flag(&ov.pflag[I * T + J], a.epoch, a.spin_max);
-      if (ov.on && threadIdx.x < 64) OVT(1536 + blockIdx.x);
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            int rr, cc;
-            acc_pos(x, y, g, &rr, &cc);
-            const size_t off = (size_t)min(r0 + rr, nrows - 1) * ld + min(c0 + cc, n - 1);
-            av[x][y][g] = ov.on ? __hip_atomic_load(a.A + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.A[off];
-          }
-    }
-    // P_I = A_{I,k} V_k^T, P_J likewise: V_k is lower triangular, so the
-    // strip products skip its zero blocks (40 instead of 64 MFMAs per wave;
-    // the skipped terms are exact zeros, so the sums are those of the full
-    // product)
-    d4 sI[4], sJ[4];
-    mfma_xVT_strip(S0, S2, sI);
-    if (!diag) mfma_xVT_strip(S1, S2, sJ);
-    __syncthreads();
-    if (stamp && k == kmax) WSTAMP(J, 2);
-    {
-      const int lane = ctid() & 63, wv = cwave();
-#pragma unroll
-      for (int bc = 0; bc < 4; ++bc)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int rr = 16 * wv + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
-          S0[rr][cc] = sI[bc][g];
-          if (!diag) S1[rr][cc] = sJ[bc][g];
-          if (J == k + 1) S3[rr][cc] = sI[bc][g];   // L_{I,k} final: stored after the publish
-        }
-    }
-    __syncthreads();
-    d4 acc[2][2];
-    mfma_xyT_64(S0, diag ? S0 : S1, acc);      // P_I P_J^T
-#pragma unroll
+    // ---------------- worker: one lower tile (I, J), J >= 1 (or a helper)
+    // The tile's updates accumulate from zero, own = ((0 - u_0) - u_1) - ...,
+    // and the tile itself is added at the end, A + own (k_chol_step keeps the
+    // same order through its U buffer, so both forms round alike): a worker
+    // needs its tile only for its last update.  Overlapped form: while update k
+    // is not ready and this tile is at least kOvFar block steps from its last
+    // update, the waves take work items (one each per round); near it, and
+    // once the queue is empty, the worker only factors.
+    const bool diag = I == J;
+    const int r0 = I * CB, c0 = J * CB;
+    const int mI = min(CB, nrows - r0);
+    double own[2][2][4];   // (the MFMA accumulator layout, acc_pos)
+  #pragma unroll
     for (int x = 0; x < 2; ++x)
-#pragma unroll
+  #pragma unroll
       for (int y = 0; y < 2; ++y)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) own[x][y][g] -= acc[x][y][g];
-    if (k == kmax) {
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) own[x][y][g] = av[x][y][g] + own[x][y][g];
-    }
-    __syncthreads();                           // S0..S2 are restaged next
-    if (stamp && k == kmax) WSTAMP(J, 3);
-    ++k;
-    staged = false;
-    if (k <= kmax && (no_items || J - k < ov.far)) {
-      stage_panels(k);
+  #pragma unroll
+        for (int g = 0; g < 4; ++g) own[x][y][g] = 0.0;
+    const int kmax = diag ? J - 2 : J - 1;
+    const bool stamp = I == J + 1;   // (diagnostics: the next-panel tiles' last update)
+    // the panel tiles A_{I,k}, A_{J,k} of update k are final long before V_k
+    // (their workers finished update k - 1 one step earlier): they are staged
+    // while V_k is awaited, so only V_k's fetch follows its flag
+    auto stage_panels = [&](int k) {
+      const int kc = k * CB, kb = min(CB, n - kc);
+      if (k >= 1) {
+        spin |= !wait_flag(&tflag[I * T + k], a.epoch, a.spin_max);
+        if (!diag) spin |= !wait_flag(&tflag[J * T + k], a.epoch, a.spin_max);
+      } else if (ov.on) {   // column 0: formed in this launch, never updated
+        spin |= !wait_flag(formed(I, 0), a.epoch, a.spin_max);
+        if (!diag) spin |= !wait_flag(formed(J, 0), a.epoch, a.spin_max);
+      }
+      const TileRegs tI = tile_fetch_sc1(rA, ld, r0, kc, nrows, kc + kb);        // A_{I,k}
+      TileRegs tJ;
+      if (!diag) tJ = tile_fetch_sc1(rA, ld, c0, kc, n, kc + kb);              // A_{J,k}
+      tile_put(S0, tI);
+      if (!diag) tile_put(S1, tJ);
+    };
+    __shared__ int ov_sh[2];   // (overlapped form: update k ready | the queue is empty)
+    bool no_items = !ov.on || ov.worker_items != 0;
+    if (threadIdx.x == 0) ov_sh[1] = 0;
+    auto up = [&](const unsigned* f) {
+      return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.epoch;
+    };
+    bool staged = false;
+    if (kmax >= 0 && (no_items || J < ov.far)) {
+      stage_panels(0);
       staged = true;
     }
-  }
-  // publish the tile (lower part; pairs that start on or left of the
-  // diagonal on a diagonal tile): through S0, as row-contiguous 16-B sc1 stores
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        int rr, cc;
-        acc_pos(x, y, g, &rr, &cc);
-        S0[rr][cc] = own[x][y][g];
+    for (int k = 0; k <= kmax;) {
+      if (!no_items && J - k >= ov.far) {
+        if (threadIdx.x == 0) {
+          bool r = up(&vflag[k]);
+          if (r) r = k >= 1 ? up(&tflag[I * T + k]) && (diag || up(&tflag[J * T + k]))
+                            : up(formed(I, 0)) && (diag || up(formed(J, 0)));
+          ov_sh[0] = r ? 1 : 0;
+        }
+        __syncthreads();
+        const bool ready = ov_sh[0] != 0;
+        if (!ready) {
+          int item;
+          if (ov_draw(ov, blockIdx.x & 7, item)) {
+            ov_run(ov, item, ov_ctab, region, islot, a.A, ld, T, a.epoch);
+          } else {
+            drew_fail = true;
+            if ((threadIdx.x & 63) == 0) ov_sh[1] = 1;
+          }
+          __syncthreads();
+          no_items = ov_sh[1] != 0;
+          continue;
+        }
+        __syncthreads();   // (ov_sh[0] is read)
       }
-  __syncthreads();
-  for (int e2 = ctid(); e2 < CB * CB / 2; e2 += 256) {
-    const int i = (2 * e2) / CB, j = (2 * e2) % CB;
-    const int ri = r0 + i, cj = c0 + j;
-    if (ri < nrows && cj < n && (!diag || j <= i))   // n = 6 cameras: even, whole pairs
-      st_sc1(rA, ((size_t)ri * ld + cj) * sizeof(double), make_double2(S0[i][j], S0[i][j + 1]));
+      if (!staged) stage_panels(k);
+      spin |= !wait_flag(&vflag[k], a.epoch, a.spin_max);
+      if (stamp && k == kmax) WSTAMP(J, 0);
+      tile_put(S2, tile_fetch_sc1(rV, CB, k * CB, 0, (k + 1) * CB, CB));          // V_k (stored cleaned)
+      __syncthreads();
+      if (stamp && k == kmax) WSTAMP(J, 1);
+      // the tile itself, for the last update: in flight under its GEMMs
+      // (overlapped: formed in this launch, sc1 loads)
+      double av[2][2][4];
+      if (k == kmax) {
+        if (ov.on) spin |= !wait_flag(&ov.pflag[I * T + J], a.epoch, a.spin_max);
+        if (ov.on && threadIdx.x < 64) OVT(1536 + blockIdx.x);
+  #pragma unroll
+        for (int x = 0; x < 2; ++x)
+  #pragma unroll
+          for (int y = 0; y < 2; ++y)
+  #pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              int rr, cc;
+              acc_pos(x, y, g, &rr, &cc);
+              const size_t off = (size_t)min(r0 + rr, nrows - 1) * ld + min(c0 + cc, n - 1);
+              av[x][y][g] = ov.on ? __hip_atomic_load(a.A + off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : a.A[off];
+            }
+      }
+      // P_I = A_{I,k} V_k^T, P_J likewise: V_k is lower triangular, so the
+      // strip products skip its zero blocks (40 instead of 64 MFMAs per wave;
+      // the skipped terms are exact zeros, so the sums are those of the full
+      // product)
+      d4 sI[4], sJ[4];
+      mfma_xVT_strip(S0, S2, sI);
+      if (!diag) mfma_xVT_strip(S1, S2, sJ);
+      __syncthreads();
+      if (stamp && k == kmax) WSTAMP(J, 2);
+      {
+        const int lane = ctid() & 63, wv = cwave();
+  #pragma unroll
+        for (int bc = 0; bc < 4; ++bc)
+  #pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int rr = 16 * wv + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
+            S0[rr][cc] = sI[bc][g];
+            if (!diag) S1[rr][cc] = sJ[bc][g];
+            if (J == k + 1) S3[rr][cc] = sI[bc][g];   // L_{I,k} final: stored after the publish
+          }
+      }
+      __syncthreads();
+      d4 acc[2][2];
+      mfma_xyT_64(S0, diag ? S0 : S1, acc);      // P_I P_J^T
+  #pragma unroll
+      for (int x = 0; x < 2; ++x)
+  #pragma unroll
+        for (int y = 0; y < 2; ++y)
+  #pragma unroll
+          for (int g = 0; g < 4; ++g) own[x][y][g] -= acc[x][y][g];
+      if (k == kmax) {
+  #pragma unroll
+        for (int x = 0; x < 2; ++x)
+  #pragma unroll
+          for (int y = 0; y < 2; ++y)
+  #pragma unroll
+            for (int g = 0; g < 4; ++g) own[x][y][g] = av[x][y][g] + own[x][y][g];
+      }
+      __syncthreads();                           // S0..S2 are restaged next
+      if (stamp && k == kmax) WSTAMP(J, 3);
+      ++k;
+      staged = false;
+      if (k <= kmax && (no_items || J - k < ov.far)) {
+        stage_panels(k);
+        staged = true;
+      }
+    }
+    // publish the tile (lower part; pairs that start on or left of the
+    // diagonal on a diagonal tile): through S0, as row-contiguous 16-B sc1 stores
+  #pragma unroll
+    for (int x = 0; x < 2; ++x)
+  #pragma unroll
+      for (int y = 0; y < 2; ++y)
+  #pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          int rr, cc;
+          acc_pos(x, y, g, &rr, &cc);
+          S0[rr][cc] = own[x][y][g];
+        }
+    __syncthreads();
+    for (int e2 = ctid(); e2 < CB * CB / 2; e2 += 256) {
+      const int i = (2 * e2) / CB, j = (2 * e2) % CB;
+      const int ri = r0 + i, cj = c0 + j;
+      if (ri < nrows && cj < n && (!diag || j <= i))   // n = 6 cameras: even, whole pairs
+        st_sc1(rA, ((size_t)ri * ld + cj) * sizeof(double), make_double2(S0[i][j], S0[i][j + 1]));
+    }
+    publish(&tflag[I * T + J], a.epoch);
+    if (stamp) WSTAMP(J, 4);
+    if (ov.on && threadIdx.x < 64) OVT(2048 + blockIdx.x);
+    // L_{I,J-1} (the last update of an off-diagonal tile: J == k + 1) to the
+    // factor, after the publish: no in-kernel reader, and its drain would
+    // otherwise sit in the barriers before the tile's hand-off
+    if (!diag && kmax == J - 1) lds_to_global(S3, a.L, ld, r0, kmax * CB, mI, min(CB, n - kmax * CB));
+    // the worker (J+1, J) also stores P_J = L_{J,J-1}, the critical
+    // workgroup's panel product of step J (bitwise the same: the same tiles
+    // through the same strip product; block row J has no rhs row here)
+    if (I == J + 1) lds_to_global(S1, a.L, ld, c0, kmax * CB, CB, min(CB, n - kmax * CB));
+    if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
+    if (threadIdx.x == 0 && spin) atomicAdd(&a.scal[SL_CHOL_SPIN], 1.0);
   }
-  publish(&tflag[I * T + J], a.epoch);
-  if (stamp) WSTAMP(J, 4);
-  if (ov.on && threadIdx.x < 64) OVT(2048 + blockIdx.x);
-  // L_{I,J-1} (the last update of an off-diagonal tile: J == k + 1) to the
-  // factor, after the publish: no in-kernel reader, and its drain would
-  // otherwise sit in the barriers before the tile's hand-off
-  if (!diag && kmax == J - 1) lds_to_global(S3, a.L, ld, r0, kmax * CB, mI, min(CB, n - kmax * CB));
-  // the worker (J+1, J) also stores P_J = L_{J,J-1}, the critical
-  // workgroup's panel product of step J (bitwise the same: the same tiles
-  // through the same strip product; block row J has no rhs row here)
-  if (I == J + 1) lds_to_global(S1, a.L, ld, c0, kmax * CB, CB, min(CB, n - kmax * CB));
-  if (threadIdx.x == 0 && bad) atomicAdd(&a.scal[SL_CHOL_BAD], 1.0);
-  if (threadIdx.x == 0 && spin) atomicAdd(&a.scal[SL_CHOL_SPIN], 1.0);
-  if (ov.on) {   // this wave's failing draw, unless taken before its tile
+  // ---------------- every workgroup: items (helpers: all of theirs), then
+  // each wave's one failing draw of the launch
+  if (ov.on) {
     __syncthreads();
     if (!drew_fail) ov_take(ov, ov_ctab, region, islot, a.A, ld, T, a.epoch, -1);
+    if (!worker && blockIdx.x != 0 && threadIdx.x < 64) OVT(1024 + blockIdx.x);
   }
 }
 
@@ -1096,7 +1121,7 @@ void launch_chol_persist_ov(const DevProblem& P, const DevWork& W, OvPlan& plan,
   o.blocks = W.blocks; o.pairs = W.pairs; o.Wc = W.W; o.scale_c = W.scale_c; o.u = W.u;
   o.Hcc = W.Hcc; o.gc = W.gc; o.diag_c = W.diag_c; o.radius = radius;
   o.cpart = W.cpart; o.G = W.cam_split;
-  o.irec = plan.irec; o.item_col = plan.item_col; o.tgt = plan.tgt;
+  o.irec = plan.irec; o.item_ng = plan.item_ng; o.item_col = plan.item_col; o.tgt = plan.tgt;
   o.cnt = plan.ctr;
   o.cam_cnt = plan.ctr + (size_t)TR * T;
   o.q = o.cam_cnt + P.nvc;
