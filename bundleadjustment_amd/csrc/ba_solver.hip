@@ -511,10 +511,13 @@ void build_overlap_plan(ba_ctx* ctx, const std::vector<int4>& blocks) {
       if (tgt[(size_t)I * T + J] == 0) return;   // (a lower tile nothing writes)
   std::vector<int4> items[8];
   std::vector<int> icol[8], ing[8];
-  // pair items of the first kOvSmallCols tile columns are one group of 4
-  // blocks (the chain waits for them: short items complete sooner), later
-  // ones up to kOvGroups groups (one pipeline fill per item)
-  constexpr int kOvSmallCols = 3, kOvGroups = 4;
+  // pair items are one group of 4 blocks: larger items (up to 4 groups, one
+  // pipeline fill each) leave too few items per tile column for the waves,
+  // and the last ones make a long tail: C3 0.70 vs 0.59 ms per LM iteration
+  // with 4 groups from tile column 3 on (profiles/r06_v4_ov_groups_ab.txt);
+  // BA_OV_GROUPS (diagnostics, read when the plan is built) sets the groups
+  const char* ge = getenv("BA_OV_GROUPS");
+  const int kOvGroups = ge ? std::max(1, std::min(4, atoi(ge))) : 1, kOvSmallCols = 3;
   int unit_rr = 0;
   for (int tc = 0; tc < T; ++tc) {
     for (int v = 0; v < nvc; ++v) {
