@@ -240,11 +240,10 @@ struct OvArgs {
   double radius;
   double* cpart;             // [G][nvc][27] slices
   int G;
-  // item i: irec[16 i ..]: a pair item's item_ng[i] groups of 4 blocks
-  // {I, J, start, end} (one per 16-lane group; no block: zeros), or
-  // (item_ng[i] = 0) a diagonal item's {-1 - (v G + g), 0, 0, 0}
+  // item i: irec[4 i .. 4 i + 3], one int4 per 16-lane group: a pair item's
+  // blocks {I, J, start, end} (no block: zeros), or a diagonal item's
+  // {-1 - (v G + g), 0, 0, 0} first
   const int4* irec;
-  const int* item_ng;
   const int* item_col;       // the tile column each item belongs to
   const unsigned* tgt;       // [TR][T] contributions per tile and launch
   unsigned* cnt;             // [TR][T] contributions (cumulative)
@@ -434,62 +433,48 @@ __device__ __forceinline__ void adma4(const void* src, unsigned lds) {    // 4 B
 }
 #pragma clang diagnostic pop
 
-// one pair item by one wave: up to kOvGroups groups of 4 camera-pair blocks,
-// 16 lanes per block — the lanes, pairs, products and xor reduction of
-// k_schur_pairs_cd (bitwise its S blocks).  The records go through LDS by
-// LDS-DMA as there, two rounds in flight (region: 2 x (row, partner) x 64
-// records = 32 KB): the factorisation's one workgroup per CU leaves each
-// wave alone on its SIMD, so the second round is what hides the gather
-// latency, and the rounds of an item's groups run as one stream (a group's
-// sums are reduced and stored while the next group's first rounds are in
-// flight: the pipeline fills once per item).  The pair indices come by
-// LDS-DMA too, three rounds ahead (islot: 4 x 64 {x, y}), so no register is
-// ever loaded in flight.  Round R requests round R + 3's indices (2 pieces, if
-// that round exists) and round R + 2's records (16, if it exists), computes,
-// and at a group's last round stores the group's 36 x 4 sums (3 stores per
-// lane).  Behind round R + 2's indices there are then round R + 1's records
-// and round R - 1's stores, behind round R's records more: waiting for
-// vmcnt(r(R + 1) + s(R - 1)) covers both.
-constexpr int kOvGroups = 4;
-template <int N>
-__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-__device__ __forceinline__ void ov_pair_item(const OvArgs& o, int item, int ng, const WcCam* ctab, double* region,
-                                             int* islot, double* S, size_t ld, int T, unsigned epoch) {
+// one pair item by one wave: 4 camera-pair blocks, 16 lanes each — the lanes,
+// pairs, products and xor reduction of k_schur_pairs_cd (bitwise its S
+// blocks).  The records go through LDS by LDS-DMA as there, two rounds in
+// flight (region: 2 x (row, partner) x 64 records = 32 KB): the
+// factorisation's one workgroup per CU leaves each wave alone on its SIMD, so
+// the second round is what hides the gather latency.  The pair indices come
+// by LDS-DMA too, three rounds ahead (islot: 4 x 64 {x, y}), so no register
+// is ever loaded in flight.  Round t requests round t + 3's indices (2
+// pieces, if that round exists) and round t + 2's records (16 pieces, if it
+// exists); so behind round t's records there are round t + 2's indices and
+// round t + 1's records, and behind round t + 2's indices round t + 1's
+// records: vmcnt(16) waits for both while round t + 1 exists, vmcnt(0) at
+// the last round.
+__device__ __forceinline__ void ov_pair_item(const OvArgs& o, int4 blk, const WcCam* ctab, double* region, int* islot,
+                                             double* S, size_t ld, int T, unsigned epoch) {
   constexpr int PL = kPairLanes;
-  static_assert(64 / PL == 4, "a pair item is groups of 4 blocks per wave");
-  const int lane = threadIdx.x & 63, sl = lane & (PL - 1), sub = lane / PL;
-  static_assert(kOvGroups == 4, "four named groups below (no register arrays: they would go to scratch)");
-  auto ld_blk = [&](int g) { return g < ng ? o.irec[(size_t)16 * item + 4 * g + sub] : make_int4(0, 0, 0, 0); };
-  const int4 b0 = ld_blk(0), b1 = ld_blk(1), b2 = ld_blk(2), b3 = ld_blk(3);
-  auto rounds = [&](int4 b) {   // rounds of a group: the most pairs per lane of its 4 blocks (uniform)
-    const int len = b.w - b.z;
-    int n = len > sl ? (len - sl + PL - 1) / PL : 0;
-#pragma unroll
-    for (int x = 32; x >= 1; x >>= 1) n = max(n, __shfl_xor(n, x));
-    return __builtin_amdgcn_readfirstlane(n);
-  };
-  const int s1 = rounds(b0), s2 = s1 + rounds(b1), s3 = s2 + rounds(b2), nr = s3 + rounds(b3);
-  auto grp = [&](int R) { return (R >= s1 ? 1 : 0) + (R >= s2 ? 1 : 0) + (R >= s3 ? 1 : 0); };
-  auto blk_of = [&](int g) { return g == 0 ? b0 : g == 1 ? b1 : g == 2 ? b2 : b3; };
-  auto st_of = [&](int g) { return g == 0 ? 0 : g == 1 ? s1 : g == 2 ? s2 : s3; };
-  auto is_end = [&](int R) { return R >= 0 && (R + 1 == s1 || R + 1 == s2 || R + 1 == s3 || R + 1 == nr); };
+  static_assert(64 / PL == 4, "a pair item is 4 blocks per wave");
+  const int lane = threadIdx.x & 63, sl = lane & (PL - 1);
+  const bool live = blk.w > blk.z;
+  const WcCam& mI = ctab[blk.x];   // (the workgroup's LDS camera table)
+  const WcCam& mJ = ctab[blk.y];
   const int swr = (lane >> 1) & 7;
-  // round R's buffers: records (row at +0, partner at +64 records), indices
+  const int len = blk.w - blk.z;
+  int nit = len > sl ? (len - sl + PL - 1) / PL : 0;
+#pragma unroll
+  for (int x = 32; x >= 1; x >>= 1) nit = max(nit, __shfl_xor(nit, x));
+  nit = __builtin_amdgcn_readfirstlane(nit);   // (a uniform loop)
+  const int e0 = blk.z + sl;
+  // round t's buffers: records (row at +0, partner at +64 records), indices
   // (x at +0, y at +64 ints)
-  auto rbuf = [&](int R) { return region + (R & 1) * (128 * kWcRec); };
-  auto ibuf = [&](int R) { return islot + (R & 3) * 128; };
-  auto req_idx = [&](int R) {   // round R's pair of this lane -> ibuf(R)
-    const int g = grp(R);
-    const int4 b = blk_of(g);
-    const int2* p = o.pairs + max(min(b.z + sl + (R - st_of(g)) * PL, b.w - 1), 0);
-    const int* ib = ibuf(R);
+  auto rbuf = [&](int t) { return region + (t & 1) * (128 * kWcRec); };
+  auto ibuf = [&](int t) { return islot + (t & 3) * 128; };
+  auto req_idx = [&](int t) {   // round t's pair of this lane -> ibuf(t)
+    const int2* p = o.pairs + max(min(e0 + t * PL, blk.w - 1), 0);
+    const int* ib = ibuf(t);
     adma4(&p->x, lds_addr(ib));
     adma4(&p->y, lds_addr(ib + 64));
   };
-  auto req_rec = [&](int R) {   // round R's records (its indices in ibuf(R)) -> rbuf(R)
-    const int* ib = ibuf(R);
+  auto req_rec = [&](int t) {   // round t's records (its indices in ibuf(t)) -> rbuf(t)
+    const int* ib = ibuf(t);
     const int2 pr = make_int2(ib[lane], ib[64 + lane]);
-    double* rb = rbuf(R);
+    double* rb = rbuf(t);
     const unsigned lr = lds_addr(rb), lp = lds_addr(rb + 64 * kWcRec);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -516,25 +501,20 @@ __device__ __forceinline__ void ov_pair_item(const OvArgs& o, int item, int ng, 
   for (int k = 0; k < 36; ++k) acc[k] = 0.0;
   // prologue: indices of rounds 0, 1 (waited), records 0, indices 2, records 1
   req_idx(0);
-  if (nr > 1) req_idx(1);
-  vm_wait<0>();
+  if (nit > 1) req_idx(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   req_rec(0);
-  if (nr > 2) req_idx(2);
-  if (nr > 1) req_rec(1);
-  for (int R = 0; R < nr; ++R) {
-    const bool rn = R + 1 < nr, sp = is_end(R - 1);
-    if (rn) { if (sp) vm_wait<19>(); else vm_wait<16>(); }
-    else { if (sp) vm_wait<3>(); else vm_wait<0>(); }
-    const WcRaw wa = read_rec(rbuf(R));
-    const WcRaw wb = read_rec(rbuf(R) + 64 * kWcRec);
+  if (nit > 2) req_idx(2);
+  if (nit > 1) req_rec(1);
+  for (int t = 0; t < nit; ++t) {
+    if (t + 1 < nit) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const WcRaw wa = read_rec(rbuf(t));
+    const WcRaw wb = read_rec(rbuf(t) + 64 * kWcRec);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read out before the refill
-    if (R + 3 < nr) req_idx(R + 3);
-    if (R + 2 < nr) req_rec(R + 2);
-    const int g = grp(R);
-    const int4 b = blk_of(g);
-    const WcCam& mI = ctab[b.x];   // (the workgroup's LDS camera table)
-    const WcCam& mJ = ctab[b.y];
-    if (b.z + sl + (R - st_of(g)) * PL < b.w) {
+    if (t + 3 < nit) req_idx(t + 3);
+    if (t + 2 < nit) req_rec(t + 2);
+    if (e0 + t * PL < blk.w) {
       double ca0[6], ca1[6], cb0[6], cb1[6];
       wc_rows(wa, mI, ca0, ca1);
       wc_rows(wb, mJ, cb0, cb1);
@@ -557,47 +537,33 @@ __device__ __forceinline__ void ov_pair_item(const OvArgs& o, int item, int ng, 
 #pragma unroll
         for (int j = 0; j < 6; ++j) acc[i * 6 + j] += ca0[i] * n0[j] + ca1[i] * n1[j];
     }
-    if (is_end(R)) {   // group g done: reduce, store (3 per lane), restart
+  }
 #pragma unroll
-      for (int k = 0; k < 36; ++k) {
-        double v = acc[k];
+  for (int k = 0; k < 36; ++k) {
+    double v = acc[k];
 #pragma unroll
-        for (int x = PL / 2; x >= 1; x >>= 1) v += __shfl_xor(v, x, PL);
-        acc[k] = v;
-      }
-      // lane sl stores entries sl, sl + 16, sl + 32 (< 36)
-      double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+    for (int x = PL / 2; x >= 1; x >>= 1) v += __shfl_xor(v, x, PL);
+    acc[k] = v;
+  }
+  if (live) {
+    const int I = blk.x, Jb = blk.y;   // I > Jb (no point observed twice by one camera in this form)
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        v0 = sl == k ? acc[k] : v0;
-        v1 = sl == k ? acc[k + 16] : v1;
-        if (k < 4) v2 = sl == k ? acc[k + 32] : v2;
-      }
-      const bool live = b.w > b.z;
-      const int I = b.x, Jb = b.y;   // I > Jb (no point observed twice by one camera in this form)
-      auto at = [&](int k) { return S + (size_t)(6 * I + k / 6) * ld + 6 * Jb + k % 6; };
-      // (always three store instructions: the waits above count them)
-      if (live) __hip_atomic_store(at(sl), -v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (live) __hip_atomic_store(at(sl + 16), -v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (live && sl < 4) __hip_atomic_store(at(sl + 32), -v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-      for (int k = 0; k < 36; ++k) acc[k] = 0.0;
+    for (int k = 0; k < 36; ++k) {
+      if ((k % PL) != sl) continue;
+      const int i = k / 6, j = k % 6;
+      __hip_atomic_store(S + (size_t)(6 * I + i) * ld + 6 * Jb + j, -acc[k], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  vm_wait<0>();   // the S stores are done: count the item's blocks into their tiles
-  if (sl == 0) {
-#pragma unroll
-    for (int g = 0; g < kOvGroups; ++g) {
-      const int4 b = blk_of(g);
-      if (g >= ng || b.w <= b.z) continue;
-      const int r0 = (6 * b.x) >> 6, r1 = (6 * b.x + 5) >> 6;
-      const int c0 = (6 * b.y) >> 6, c1 = (6 * b.y + 5) >> 6;
-      ov_count(o, r0 * T + c0, epoch);
-      if (c1 != c0) ov_count(o, r0 * T + c1, epoch);
-      if (r1 != r0) {
-        ov_count(o, r1 * T + c0, epoch);
-        if (c1 != c0) ov_count(o, r1 * T + c1, epoch);
-      }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the S stores are done
+  if (live && sl == 0) {
+    const int r0 = (6 * blk.x) >> 6, r1 = (6 * blk.x + 5) >> 6;
+    const int c0 = (6 * blk.y) >> 6, c1 = (6 * blk.y + 5) >> 6;
+    ov_count(o, r0 * T + c0, epoch);
+    if (c1 != c0) ov_count(o, r0 * T + c1, epoch);
+    if (r1 != r0) {
+      ov_count(o, r1 * T + c0, epoch);
+      if (c1 != c0) ov_count(o, r1 * T + c1, epoch);
     }
   }
 }
@@ -651,26 +617,28 @@ __device__ __forceinline__ bool ov_draw(const OvArgs& o, int x, int& item) {
 }
 __device__ __forceinline__ void ov_run(const OvArgs& o, int item, const WcCam* ctab, double* region, int* islot,
                                        double* S, size_t ld, int T, unsigned epoch) {
-  const int ng = o.item_ng[item];
-  if (ng > 0) ov_pair_item(o, item, ng, ctab, region, islot, S, ld, T, epoch);
-  else ov_diag_item(o, -1 - o.irec[(size_t)16 * item].x, region, S, T, epoch);
+  const int4 mine = o.irec[4 * (size_t)item + ((threadIdx.x & 63) >> 4)];
+  const int head = __builtin_amdgcn_readfirstlane(mine.x);   // (lanes 0..15: the item's first record)
+  if (head >= 0) ov_pair_item(o, mine, ctab, region, islot, S, ld, T, epoch);
+  else ov_diag_item(o, -1 - head, region, S, T, epoch);
 }
-// items until the queue is exhausted (stop_col < 0) or, for a worker, until
-// the next item is of tile column >= stop_col (its own tile's column comes
-// up).  Returns whether this wave drew its failing ticket.
-__device__ __forceinline__ bool ov_take(const OvArgs& o, const WcCam* ctab, double* region, int* islot, double* S,
-                                        size_t ld, int T, unsigned epoch, int stop_col) {
+// items until the queue is exhausted; this wave's failing draw is the last.
+// The next item's ticket is drawn as the current one starts, so its atomic's
+// round trip runs under the item (its value is read only after the item).
+__device__ __forceinline__ void ov_take(const OvArgs& o, const WcCam* ctab, double* region, int* islot, double* S,
+                                        size_t ld, int T, unsigned epoch) {
   const int x = blockIdx.x & 7;
-  for (;;) {
-    if (stop_col >= 0) {
-      unsigned h = 0;
-      if ((threadIdx.x & 63) == 0) h = __hip_atomic_load(&o.q[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      h = __builtin_amdgcn_readfirstlane(h) - o.qbase[x];
-      if (h < (unsigned)(o.ioff[x + 1] - o.ioff[x]) && o.item_col[o.ioff[x] + (int)h] >= stop_col) return false;
-    }
-    int item;
-    if (!ov_draw(o, x, item)) return true;
-    ov_run(o, item, ctab, region, islot, S, ld, T, epoch);
+  const unsigned nq = (unsigned)(o.ioff[x + 1] - o.ioff[x]);
+  auto ticket = [&]() {
+    unsigned t = 0;
+    if ((threadIdx.x & 63) == 0) t = __hip_atomic_fetch_add(&o.q[x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return t;
+  };
+  unsigned t = __builtin_amdgcn_readfirstlane(ticket()) - o.qbase[x];
+  while (t < nq) {
+    const unsigned raw = ticket();   // (the next one)
+    ov_run(o, o.ioff[x] + (int)t, ctab, region, islot, S, ld, T, epoch);
+    t = __builtin_amdgcn_readfirstlane(raw) - o.qbase[x];
   }
 }
 
@@ -1067,7 +1035,7 @@ __global__ __launch_bounds__(256) void k_chol_persist(PersistArgs a) {
   // each wave's one failing draw of the launch
   if (ov.on) {
     __syncthreads();
-    if (!drew_fail) ov_take(ov, ov_ctab, region, islot, a.A, ld, T, a.epoch, -1);
+    if (!drew_fail) ov_take(ov, ov_ctab, region, islot, a.A, ld, T, a.epoch);
     if (!worker && blockIdx.x != 0 && threadIdx.x < 64) OVT(1024 + blockIdx.x);
   }
 }
@@ -1121,7 +1089,7 @@ void launch_chol_persist_ov(const DevProblem& P, const DevWork& W, OvPlan& plan,
   o.blocks = W.blocks; o.pairs = W.pairs; o.Wc = W.W; o.scale_c = W.scale_c; o.u = W.u;
   o.Hcc = W.Hcc; o.gc = W.gc; o.diag_c = W.diag_c; o.radius = radius;
   o.cpart = W.cpart; o.G = W.cam_split;
-  o.irec = plan.irec; o.item_ng = plan.item_ng; o.item_col = plan.item_col; o.tgt = plan.tgt;
+  o.irec = plan.irec; o.item_col = plan.item_col; o.tgt = plan.tgt;
   o.cnt = plan.ctr;
   o.cam_cnt = plan.ctr + (size_t)TR * T;
   o.q = o.cam_cnt + P.nvc;

@@ -61,9 +61,8 @@ struct DevProblem {
 // Built once per problem (ba_solver.hip ensure_overlap).
 struct OvPlan {
   bool ok = false;                   // built, and the problem qualifies
-  const int4* irec = nullptr;        // [items][16]: a pair item's groups of 4 blocks {I, J, start, end}
-                                     //   (zeros: none), or {-1 - (v G + g), 0, 0, 0} first: a diagonal slice
-  const int* item_ng = nullptr;      // groups of 4 blocks per item (0: a diagonal slice)
+  const int4* irec = nullptr;        // [items][4]: a pair item's 4 blocks {I, J, start, end} (zeros: none),
+                                     //   or {-1 - (v G + g), 0, 0, 0} first: a diagonal slice
   const int* item_col = nullptr;     // tile column of each item
   const unsigned* tgt = nullptr;     // [TR][T] contributions per tile and launch
   unsigned* ctr = nullptr;           // cnt [TR][T] | cam_cnt [nvc] | q [8] | pflag [TR][T]: zeroed once, cumulative

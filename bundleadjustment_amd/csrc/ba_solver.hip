@@ -510,14 +510,7 @@ void build_overlap_plan(ba_ctx* ctx, const std::vector<int4>& blocks) {
     for (int J = 0; J < T && J <= I; ++J)
       if (tgt[(size_t)I * T + J] == 0) return;   // (a lower tile nothing writes)
   std::vector<int4> items[8];
-  std::vector<int> icol[8], ing[8];
-  // pair items are one group of 4 blocks: larger items (up to 4 groups, one
-  // pipeline fill each) leave too few items per tile column for the waves,
-  // and the last ones make a long tail: C3 0.70 vs 0.59 ms per LM iteration
-  // with 4 groups from tile column 3 on (profiles/r06_v4_ov_groups_ab.txt);
-  // BA_OV_GROUPS (diagnostics, read when the plan is built) sets the groups
-  const char* ge = getenv("BA_OV_GROUPS");
-  const int kOvGroups = ge ? std::max(1, std::min(4, atoi(ge))) : 1, kOvSmallCols = 3;
+  std::vector<int> icol[8];
   int unit_rr = 0;
   for (int tc = 0; tc < T; ++tc) {
     for (int v = 0; v < nvc; ++v) {
@@ -525,9 +518,8 @@ void build_overlap_plan(ba_ctx* ctx, const std::vector<int4>& blocks) {
       for (int g = 0; g < G; ++g) {
         const int x = unit_rr++ & 7;
         items[x].push_back(make_int4(-1 - (v * G + g), 0, 0, 0));
-        for (int q = 1; q < 16; ++q) items[x].push_back(make_int4(0, 0, 0, 0));
+        for (int q = 1; q < 4; ++q) items[x].push_back(make_int4(0, 0, 0, 0));
         icol[x].push_back(tc);
-        ing[x].push_back(0);
       }
     }
     const std::vector<int>& cb = colblk[tc];
@@ -542,28 +534,23 @@ void build_overlap_plan(ba_ctx* ctx, const std::vector<int4>& blocks) {
         acc += blocks[cb[k]].w - blocks[cb[k]].z;
         run.push_back(cb[k++]);
       }
-      const size_t per = 4 * (tc < kOvSmallCols ? 1 : kOvGroups);
-      for (size_t r = 0; r < run.size(); r += per) {
-        const size_t m = std::min(per, run.size() - r);
-        for (size_t q = 0; q < 16; ++q) items[x].push_back(q < m ? blocks[run[r + q]] : make_int4(0, 0, 0, 0));
+      for (size_t r = 0; r < run.size(); r += 4) {
+        for (int q = 0; q < 4; ++q) items[x].push_back(r + q < run.size() ? blocks[run[r + q]] : make_int4(0, 0, 0, 0));
         icol[x].push_back(tc);
-        ing[x].push_back((int)((m + 3) / 4));
       }
     }
   }
   std::vector<int4> all;
-  std::vector<int> allc, alln;
+  std::vector<int> allc;
   OvPlan& P = W.ov;
   for (int x = 0; x < 8; ++x) {
     P.ioff[x] = (int)allc.size();
     all.insert(all.end(), items[x].begin(), items[x].end());
     allc.insert(allc.end(), icol[x].begin(), icol[x].end());
-    alln.insert(alln.end(), ing[x].begin(), ing[x].end());
   }
   P.ioff[8] = (int)allc.size();
   P.irec = ctx->upload(all);
   P.item_col = ctx->upload(allc);
-  P.item_ng = ctx->upload(alln);
   P.tgt = ctx->upload(tgt);
   const size_t nctr = 2 * (size_t)TR * T + nvc + 8;   // cnt | cam_cnt | q | pflag
   P.ctr = ctx->dalloc<unsigned>(nctr);
