@@ -623,23 +623,15 @@ __device__ __forceinline__ void ov_run(const OvArgs& o, int item, const WcCam* c
   else ov_diag_item(o, -1 - head, region, S, T, epoch);
 }
 // items until the queue is exhausted; this wave's failing draw is the last.
-// The next item's ticket is drawn as the current one starts, so its atomic's
-// round trip runs under the item (its value is read only after the item).
+// (Drawing the next ticket as the current item starts, to hide the atomic's
+// round trip, measured slower: a wave busy with its item then holds the next
+// one, and the early tile columns completed later — C3 pass alone 236 vs
+// 221 us, tile (0, 0) formed at 47 vs 38 us: profiles/r06_v5_ov_prefetch_ab.txt)
 __device__ __forceinline__ void ov_take(const OvArgs& o, const WcCam* ctab, double* region, int* islot, double* S,
                                         size_t ld, int T, unsigned epoch) {
   const int x = blockIdx.x & 7;
-  const unsigned nq = (unsigned)(o.ioff[x + 1] - o.ioff[x]);
-  auto ticket = [&]() {
-    unsigned t = 0;
-    if ((threadIdx.x & 63) == 0) t = __hip_atomic_fetch_add(&o.q[x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return t;
-  };
-  unsigned t = __builtin_amdgcn_readfirstlane(ticket()) - o.qbase[x];
-  while (t < nq) {
-    const unsigned raw = ticket();   // (the next one)
-    ov_run(o, o.ioff[x] + (int)t, ctab, region, islot, S, ld, T, epoch);
-    t = __builtin_amdgcn_readfirstlane(raw) - o.qbase[x];
-  }
+  int item;
+  while (ov_draw(o, x, item)) ov_run(o, item, ctab, region, islot, S, ld, T, epoch);
 }
 
 // block 0: the critical workgroup, block w > 0: worker w
