@@ -116,6 +116,22 @@ __device__ inline void mfma_xyT_64(const double (*Xs)[LDP], const double (*Ys)[L
   }
 }
 
+// the same product added to acc (a rank-K update accumulated over K / 64 tiles)
+__device__ inline void mfma_xyT_64_add(const double (*Xs)[LDP], const double (*Ys)[LDP], d4 acc[2][2]) {
+  const int lane = ctid() & 63, w = cwave();
+  const int r0 = (w >> 1) * 32, c0 = (w & 1) * 32;
+  const int li = lane & 15, lk = lane >> 4;
+#pragma unroll 4
+  for (int k0 = 0; k0 < CB; k0 += 4) {
+    const double x0 = Xs[r0 + li][k0 + lk], x1 = Xs[r0 + 16 + li][k0 + lk];
+    const double y0 = Ys[c0 + li][k0 + lk], y1 = Ys[c0 + 16 + li][k0 + lk];
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, y0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(x0, y1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, y0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(x1, y1, acc[1][1], 0, 0, 0);
+  }
+}
+
 // Lower 16x16 tiles (ti >= tj) of C = sum_k Xs[i][k] Xs[j][k] (a symmetric
 // product): 10 tiles over 4 waves (3, 3, 2, 2) instead of 16 (4 each).
 __device__ inline int lower_tiles_of(int w, int (*tl)[2]) {

@@ -113,6 +113,27 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&mb, e0, e1));
     if (verbose) printf("factor total %.1f us (%d steps), back-solve %.1f us\n", tot * 1e3, T, mb * 1e3);
   }
+  if (T >= kCholSplitBlocks) {
+    // the split form as the solver runs it: every step enqueued back to back
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(hipMemcpy(dA, A.data(), sizeof(double) * A.size(), hipMemcpyHostToDevice));
+      CK(hipMemset(dS, 0, sizeof(double) * 64));
+      CK(hipEventRecord(e0));
+      hipLaunchKernelGGL(k_chol_step, dim3(1, 1), dim3(256), 0, 0, dA, dL, ld, n, -1, dV, dS, dU);
+      for (int k = 0; k + 1 < T; ++k) {
+        const int st = (k + 1) * CB;
+        launch_chol_split_step(dA, dL, ld, n, k, (n - st + CB - 1) / CB, (nrows - st + CB - 1) / CB, dV, dS, 0);
+      }
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      printf("factor streamed %.1f us (%s form)\n", ms * 1e3, chol_grouped() ? "grouped rank-256" : "rank-64");
+    }
+    CK(hipMemset(dF, 0, sizeof(double) * 2 * n));
+    hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dA, dL, ld, n, dV, dy, dF, 2, dS);
+    CK(hipDeviceSynchronize());
+  }
   std::vector<double> y(n), Sh(64);
   CK(hipMemcpy(y.data(), dy, sizeof(double) * n, hipMemcpyDeviceToHost));
   // the persistent form (one launch, look-ahead): time it and check that it
