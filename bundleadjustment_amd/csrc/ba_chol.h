@@ -91,6 +91,39 @@ __device__ inline void tile_put(double (*D)[LDP], const TileRegs& t) {
     D[i][j + 1] = t.v[it].y;
   }
 }
+// The same staging in two halves for a pipelined consumer: tile_fetch_raw
+// only issues the loads (the out-of-tile zeroing is a per-element mask,
+// computed from indices, applied by tile_put_masked) — with the selects of
+// tile_fetch next to the loads, the compiler waits for the loads right there,
+// and the next operand tiles' loads never overlapped the current MFMAs.
+struct TileRaw { double2 v[8]; unsigned mask; };
+__device__ inline TileRaw tile_fetch_raw(const double* __restrict__ M, size_t ld, int r0, int c0, int rmax, int cmax) {
+  TileRaw t;
+  t.mask = 0;
+  const int tid = ctid();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int e = tid + 256 * it;
+    const int i = e >> 5, j = (e & 31) * 2;
+    const int ri = r0 + i, cj = c0 + j;
+    const int ric = min(ri, rmax - 1), cjc = min(cj, cmax - 2) & ~1;
+    t.v[it] = *reinterpret_cast<const double2*>(M + (size_t)ric * ld + cjc);
+    const bool rok = ri < rmax;
+    t.mask |= ((rok && cj < cmax) ? 1u : 0u) << (2 * it);
+    t.mask |= ((rok && cj + 1 < cmax) ? 2u : 0u) << (2 * it);
+  }
+  return t;
+}
+__device__ inline void tile_put_masked(double (*D)[LDP], const TileRaw& t) {
+  const int tid = ctid();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int e = tid + 256 * it;
+    const int i = e >> 5, j = (e & 31) * 2;
+    D[i][j] = (t.mask >> (2 * it)) & 1u ? t.v[it].x : 0.0;
+    D[i][j + 1] = (t.mask >> (2 * it)) & 2u ? t.v[it].y : 0.0;
+  }
+}
 __device__ inline void stage64(double (*D)[LDP], const double* __restrict__ M, size_t ld, int r0, int c0, int rmax,
                                int cmax) {
   tile_put(D, tile_fetch(M, ld, r0, c0, rmax, cmax));

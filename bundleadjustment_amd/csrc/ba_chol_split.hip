@@ -6,6 +6,10 @@
 // the inlining of the critical workgroup's factor_invert_blk).
 #include "ba_chol.h"
 
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
 namespace bahip {
 
 // One block step.  k < 0: factor block 0 only (grid 1x1).
@@ -164,43 +168,6 @@ __global__ __launch_bounds__(256) void k_chol_panel(const double* __restrict__ A
     }
 }
 
-// ---- grouped form (default): the trailing matrix takes the panels of a
-// group of 4 block columns as ONE rank-256 update per tile instead of four
-// rank-64 ones, so a trailing tile is read and written once per 4 block steps
-// (A's read-modify-write traffic / 4; each tile's operand tiles come from L,
-// which the L2 / Infinity Cache serves).  The chain keeps its one-step
-// look-ahead: block step k forms panel k (k_chol_panel) and then launches
-// k_chol_upd with the critical workgroup (diagonal block k + 1, panel k) and
-// tile tasks A_IJ -= sum_{p in [pa, pb)} L_Ip L_Jp^T in up to 4 segments:
-//   (i)   within group G = k / 4: columns (k + 1 .. 4G + 3], all rows, panel k
-//         (the column k + 1 itself below the diagonal too);
-//   (ii)  the next group's first diagonal tile D = (4G + 4, 4G + 4): panels
-//         [4G - 4, 4G + 1) at k = 4G (group G - 1 and panel 4G), else panel k;
-//         the critical workgroup applies panel 4G + 3 to it at k = 4G + 3;
-//   (iii) k = 4G + 3: group G to the next group's columns [4G + 4, 4G + 8)
-//         (their diagonal D excepted), due before panel 4G + 4;
-//   (iv)  k = 4G + j, j < 3: a third of group G - 1's update of the columns
-//         >= 4G + 4 (D excepted), column-ordered — due from step 4G + 7 on.
-// Every tile (I, J) so receives the panels p < J exactly once before panel J
-// (or diagonal block J) is formed, and no two tasks of one launch write the
-// same tile.  Bitwise deterministic; not bitwise the rank-64 form (the sums
-// are grouped differently): parity is against the oracle, as before.
-struct CholUpdSeg {
-  int ja, jb;      // block columns [ja, jb)
-  int pa, pb;      // panels [pa, pb)
-  int xd;          // column whose diagonal tile the segment skips (-1: none)
-  int diag;        // 1: the diagonal tiles only
-  int cnt;         // tiles
-};
-struct CholUpd {
-  int k, nseg, TR;
-  CholUpdSeg seg[4];
-};
-
-__host__ __device__ __forceinline__ int upd_col_tiles(const CholUpdSeg& g, int J, int TR) {
-  return g.diag ? 1 : TR - J - (J == g.xd ? 1 : 0);
-}
-
 // A_IJ -= sum_{p in [pa, pb)} L_Ip L_Jp^T: operand tiles of panel p + 1 are
 // fetched into registers while panel p's MFMAs run; A is read once, written once
 __device__ __forceinline__ void upd_tile(double* __restrict__ A, const double* __restrict__ L, int ld, int n, int I,
@@ -209,9 +176,9 @@ __device__ __forceinline__ void upd_tile(double* __restrict__ A, const double* _
   const size_t lds = (size_t)ld;
   const int r0 = I * CB, c0 = J * CB;
   const bool off = I != J;
-  TileRegs tI = tile_fetch(L, lds, r0, pa * CB, nrows, min(pa * CB + CB, n));
-  TileRegs tJ;
-  if (off) tJ = tile_fetch(L, lds, c0, pa * CB, n, min(pa * CB + CB, n));
+  TileRaw tI = tile_fetch_raw(L, lds, r0, pa * CB, nrows, min(pa * CB + CB, n));
+  TileRaw tJ;
+  if (off) tJ = tile_fetch_raw(L, lds, c0, pa * CB, n, min(pa * CB + CB, n));
   double av[2][2][4];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -230,13 +197,13 @@ __device__ __forceinline__ void upd_tile(double* __restrict__ A, const double* _
     for (int b = 0; b < 2; ++b) acc[a][b] = d4{0.0, 0.0, 0.0, 0.0};
   for (int p = pa; p < pb; ++p) {
     if (p > pa) __syncthreads();             // the previous panel's MFMAs are done with the tiles
-    tile_put(S0, tI);
-    if (off) tile_put(S1, tJ);
+    tile_put_masked(S0, tI);
+    if (off) tile_put_masked(S1, tJ);
     __syncthreads();
     if (p + 1 < pb) {
       const int kc = (p + 1) * CB, ke = min(kc + CB, n);
-      tI = tile_fetch(L, lds, r0, kc, nrows, ke);
-      if (off) tJ = tile_fetch(L, lds, c0, kc, n, ke);
+      tI = tile_fetch_raw(L, lds, r0, kc, nrows, ke);
+      if (off) tJ = tile_fetch_raw(L, lds, c0, kc, n, ke);
     }
     mfma_xyT_64_add(S0, off ? S1 : S0, acc);
   }
@@ -253,85 +220,152 @@ __device__ __forceinline__ void upd_tile(double* __restrict__ A, const double* _
       }
 }
 
-// Grid: 1 (critical) + the segments' tiles.
-__global__ __launch_bounds__(256) void k_chol_upd(double* __restrict__ A, double* __restrict__ L, int ld, int n,
-                                                  double* __restrict__ Vbuf, double* __restrict__ scal, CholUpd u) {
+// ---- scheduled form (default): a host-planned task table replaces the
+// per-step "every trailing tile takes panel k" update.  A task is one tile
+// and a contiguous range of panels, A_IJ -= sum_{p in [pa, pb)} L_Ip L_Jp^T,
+// so a tile is read and written once per range instead of once per panel
+// (ranges of up to `rank` panels: 4 -> a quarter of the rank-64 form's tile
+// read-modify-write traffic; the operand tiles come from L through the
+// L2 / Infinity Cache).  The chain keeps its one-step look-ahead: block step
+// k forms panel k (k_chol_panel) and then launches k_chol_upd with the
+// critical workgroup (diagonal block k + 1, panel k) and the step's tasks.
+// Plan (chol_split_plan, host, once per order):
+//  - a tile (I, J) takes the panels p < J (a diagonal tile: p < J - 1, the
+//    critical workgroup applies panel J - 1), in order, each exactly once;
+//  - due: an off-diagonal tile of column J by the launch of step J - 1 (panel
+//    J is formed next), a diagonal tile by step J - 2; a due tile takes all
+//    its remaining available panels in one task;
+//  - the rest is spread evenly over the steps: each launch takes the least
+//    work (in panels) that still meets every later due step if the steps
+//    after it work at that same rate, filled earliest-due first with tasks
+//    of `rank` panels (or a tile's last, shorter range) — right-looking's
+//    front-loaded trailing work becomes a steady background the chain's
+//    serial steps hide.
+// At most one task per tile per launch; bitwise deterministic for a given
+// order (not bitwise the rank-64 form: the sums are grouped differently —
+// parity is against the oracle, as before).
+struct CholSplitPlan {
+  std::vector<int4> tasks;   // {I, J, pa, pb}, step-major
+  std::vector<int> off;      // step k's tasks: [off[k], off[k + 1])
+};
+static void chol_split_plan(int T, int TR, int rank, double budget, CholSplitPlan& P) {
+  P.tasks.clear();
+  P.off.assign(std::max(T, 1), 0);
+  if (T < 2) return;
+  struct Tile { int I, J, a, need, due; };
+  std::vector<Tile> tl;
+  for (int J = 1; J < T; ++J)
+    for (int I = J; I < TR; ++I) {
+      const int need = I == J ? J - 1 : J;
+      if (need > 0) tl.push_back({I, J, 0, need, I == J ? J - 2 : J - 1});
+    }
+  // earliest due first; within a due step, column then row order
+  std::sort(tl.begin(), tl.end(), [](const Tile& x, const Tile& y) {
+    return x.due != y.due ? x.due < y.due : (x.J != y.J ? x.J < y.J : x.I < y.I);
+  });
+  std::vector<long> due_work(T, 0);
+  for (const Tile& t : tl) due_work[t.due] += t.need;
+  for (int k = 0; k + 1 < T; ++k) {
+    P.off[k] = (int)P.tasks.size();
+    long spent = 0;
+    // due tasks first (the longest first), then the background
+    const size_t first = P.tasks.size();
+    for (Tile& t : tl) {
+      if (t.due != k || t.a >= t.need) continue;
+      P.tasks.push_back(make_int4(t.I, t.J, t.a, t.need));
+      spent += t.need - t.a;
+      due_work[t.due] -= t.need - t.a;
+      t.a = t.need;
+    }
+    std::stable_sort(P.tasks.begin() + first, P.tasks.end(),
+                     [](const int4& x, const int4& y) { return x.w - x.z > y.w - y.z; });
+    // the least constant rate that meets every later due step, given that a
+    // tile advances by at most `rank` panels per launch: by step s a tile
+    // must have done all but rank x (due - s) of its remaining panels
+    double rate = 0;
+    for (int s = k + 1; s + 1 < T; ++s) {
+      long req = 0;
+      for (const Tile& t : tl)
+        if (t.due > k && t.a < t.need) req += std::max(0L, (long)(t.need - t.a) - (long)rank * std::max(0, t.due - s));
+      rate = std::max(rate, (double)req / (double)(s - k + 1));
+    }
+    const double target = budget * rate;   // this launch's share (the due work above is in it too)
+    // least laxity first: a tile whose remaining ranges need every step left
+    // before its due step goes now whatever the share (a tile advances by at
+    // most `rank` panels per launch), then the share fills earliest-due first
+    struct Cand { int slack, idx; };
+    std::vector<Cand> cand;
+    for (int i = 0; i < (int)tl.size(); ++i) {
+      const Tile& t = tl[i];
+      if (t.due <= k || t.a >= t.need) continue;
+      const int avail = std::min(t.need, k + 1) - t.a;   // panels <= k exist
+      const int take = std::min(avail, rank);
+      if (take <= 0 || (take < rank && t.a + take < t.need)) continue;   // a full range, or the tile's last
+      const int left = t.due - k, needed = (t.need - t.a + rank - 1) / rank;   // (the due step takes the rest)
+      cand.push_back({left - needed, i});
+    }
+    std::stable_sort(cand.begin(), cand.end(), [](const Cand& x, const Cand& y) { return x.slack < y.slack; });
+    for (const Cand& c : cand) {
+      if (c.slack > 0 && spent >= target) continue;   // (earliest-due order within a slack: tl's order)
+      Tile& t = tl[c.idx];
+      const int take = std::min(std::min(t.need, k + 1) - t.a, rank);
+      P.tasks.push_back(make_int4(t.I, t.J, t.a, t.a + take));
+      spent += take;
+      due_work[t.due] -= take;
+      t.a += take;
+    }
+  }
+  P.off[T - 1] = (int)P.tasks.size();
+}
+
+// Grid: 1 (critical) + the step's tasks.
+__global__ __launch_bounds__(256) void k_chol_upd(double* __restrict__ A, double* __restrict__ L, int ld, int n, int k,
+                                                  double* __restrict__ Vbuf, double* __restrict__ scal,
+                                                  const int4* __restrict__ tasks) {
   __shared__ double S0[CB][LDP];
   __shared__ double S1[CB][LDP];
   __shared__ double Zs[CB][18];
   __shared__ CholLds cw;
   if (blockIdx.x == 0) {
-    split_critical(A, L, ld, n, u.k, Vbuf, scal, S0, S1, Zs, cw);
+    if (k >= -1) split_critical(A, L, ld, n, k, Vbuf, scal, S0, S1, Zs, cw);   // (k = -2: tasks only, tools/chol_bench)
     return;
   }
-  int b = blockIdx.x - 1, sg = 0;
-  while (sg < u.nseg && b >= u.seg[sg].cnt) b -= u.seg[sg++].cnt;
-  if (sg >= u.nseg) return;
-  const CholUpdSeg g = u.seg[sg];
-  int J = g.ja;
-  for (; J < g.jb; ++J) {
-    const int c = upd_col_tiles(g, J, u.TR);
-    if (b < c) break;
-    b -= c;
-  }
-  if (J >= g.jb) return;
-  const int I = g.diag ? J : J + (J == g.xd ? 1 : 0) + b;
-  upd_tile(A, L, ld, n, I, J, g.pa, g.pb, S0, S1);
+  const int4 t = tasks[blockIdx.x - 1];
+  upd_tile(A, L, ld, n, t.x, t.y, t.z, t.w, S0, S1);
 }
 
-// The segments of block step k (T block columns, TR tile rows).
-static CholUpd chol_upd_plan(int k, int T, int TR) {
-  CholUpd u{};
-  u.k = k;
-  u.TR = TR;
-  const int G = k / 4, r = k % 4, D = 4 * G + 4;
-  auto add = [&](int ja, int jb, int pa, int pb, int xd, int diag) {
-    jb = std::min(jb, T);
-    if (ja >= jb) return;
-    CholUpdSeg g{ja, jb, pa, pb, xd, diag, 0};
-    for (int J = ja; J < jb; ++J) g.cnt += diag ? 1 : TR - J - (J == xd ? 1 : 0);
-    if (g.cnt > 0) u.seg[u.nseg++] = g;
-  };
-  if (r < 3) {
-    add(k + 1, 4 * G + 4, k, k + 1, k + 1, 0);                          // (i)
-    add(D, D + 1, r == 0 ? std::max(0, 4 * G - 4) : k, k + 1, -1, 1);    // (ii)
-    if (G >= 1 && D < T) {                                               // (iv)
-      // column-ordered thirds of the tiles of columns [D, T)
-      long tot = 0;
-      for (int J = D; J < T; ++J) tot += TR - J - (J == D ? 1 : 0);
-      int ja = D, jb = D;
-      long acc = 0;
-      for (int J = D; J < T; ++J) {
-        const long before = acc;
-        acc += TR - J - (J == D ? 1 : 0);
-        if (before * 3 < tot * r) ja = J + 1;
-        if (before * 3 < tot * (r + 1)) jb = J + 1;
-      }
-      add(ja, jb, 4 * G - 4, 4 * G, D, 0);
-    }
-  } else {
-    add(D, D + 4, 4 * G, 4 * G + 4, D, 0);                               // (iii)
-  }
-  return u;
-}
-
-static int chol_grouped() {
-  static const int on = [] {
-    const char* e = getenv("BA_CHOL_GROUP");
-    return e && e[0] == '0' ? 0 : 1;
+int chol_split_rank() {
+  static const int r = [] {
+    const char* e = getenv("BA_CHOL_RANK");
+    const int v = e ? atoi(e) : 4;
+    return v < 0 ? 4 : v;
   }();
-  return on;
+  return r;   // 0: the rank-64 form (k_chol_step_split)
+}
+static double chol_split_budget() {
+  static const double b = [] {
+    const char* e = getenv("BA_CHOL_BUDGET");
+    const double v = e ? atof(e) : 1.0;
+    return v > 0 ? v : 1.0;
+  }();
+  return b;
+}
+
+// The task table of an order-n system (device copy + host step offsets).
+void chol_split_tasks(int n, std::vector<int4>& tasks, std::vector<int>& off) {
+  const int T = (n + CB - 1) / CB, TR = (n + 1 + CB - 1) / CB;
+  CholSplitPlan P;
+  chol_split_plan(T, TR, std::max(1, chol_split_rank()), chol_split_budget(), P);
+  tasks.swap(P.tasks);
+  off.swap(P.off);
 }
 
 void launch_chol_split_step(double* A, double* L, int ld, int n, int k, int tc, int tr, double* Vbuf, double* scal,
-                            hipStream_t s) {
+                            const int4* tasks, const int* off, hipStream_t s) {
   hipLaunchKernelGGL(k_chol_panel, dim3(tr), dim3(256), 0, s, A, L, ld, n, k, Vbuf);
-  if (chol_grouped()) {
-    const int T = (n + CB - 1) / CB, TR = (n + 1 + CB - 1) / CB;
-    const CholUpd u = chol_upd_plan(k, T, TR);
-    int grid = 1;
-    for (int g = 0; g < u.nseg; ++g) grid += u.seg[g].cnt;
-    hipLaunchKernelGGL(k_chol_upd, dim3(grid), dim3(256), 0, s, A, L, ld, n, Vbuf, scal, u);
+  if (tasks) {
+    hipLaunchKernelGGL(k_chol_upd, dim3(1 + off[k + 1] - off[k]), dim3(256), 0, s, A, L, ld, n, k, Vbuf, scal,
+                       tasks + off[k]);
     return;
   }
   const int ntiles = tc * (tc + 1) / 2 + (tr > tc ? tc : 0);   // lower tiles (+ a rhs-only tile row)

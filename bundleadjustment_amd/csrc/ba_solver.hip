@@ -84,6 +84,7 @@ struct ba_ctx {
   bool have_problem = false;
   int nc = 0, np = 0, no = 0, nvc = 0, n = 0, ld = 0;
   std::vector<int> perm;         // sorted obs -> caller obs
+  std::vector<int> chol_off;     // split Cholesky task table: host step offsets (W.ctask_off)
   std::vector<int> cam_of_vc;
   std::vector<uint8_t> cam_fixed_h;
   double huber_a = 0.0;
@@ -620,6 +621,14 @@ void ensure_dense(ba_ctx* ctx) {
   W.Ubuf = (ctx->n + 63) / 64 < bahip::chol_split_blocks()
                ? ctx->dalloc<double>((size_t)(ctx->n + 1) * std::max(ctx->ld, 1)) : nullptr;
   W.Vbuf = ctx->dalloc<double>((size_t)((ctx->n + 63) / 64 + 1) * 64 * 64);
+  W.ctask = nullptr;
+  W.ctask_off = nullptr;
+  if ((ctx->n + 63) / 64 >= bahip::chol_split_blocks() && bahip::chol_split_rank() > 0) {
+    std::vector<int4> tasks;
+    bahip::chol_split_tasks(ctx->n, tasks, ctx->chol_off);
+    W.ctask = ctx->upload(tasks);
+    W.ctask_off = ctx->chol_off.data();
+  }
   W.yg = ctx->dalloc<double>(2 * (size_t)std::max(ctx->n, 1));
   {
     // persistent factorisation (one launch) when the per-step form would not

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstring>
 #include <cstdio>
+#include <algorithm>
 #include <random>
 #include <vector>
 
@@ -57,6 +58,16 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dF, sizeof(double) * 2 * n));
   double* dU;   // the per-step form's update accumulator
   CK(hipMalloc(&dU, sizeof(double) * A.size()));
+  // the split form's task table (null: the rank-64 form, BA_CHOL_RANK=0)
+  int4* dtask = nullptr;
+  std::vector<int4> tasks;
+  std::vector<int> toff;
+  if (T >= kCholSplitBlocks && chol_split_rank() > 0) {
+    chol_split_tasks(n, tasks, toff);
+    CK(hipMalloc(&dtask, sizeof(int4) * std::max<size_t>(tasks.size(), 1)));
+    CK(hipMemcpy(dtask, tasks.data(), sizeof(int4) * tasks.size(), hipMemcpyHostToDevice));
+    printf("task table: %zu tasks over %d steps (rank %d)\n", tasks.size(), T - 1, chol_split_rank());
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -71,7 +82,7 @@ int main(int argc, char** argv) {
       dim3 grid = k < 0 ? dim3(1, 1) : dim3(tc, tr);
       CK(hipEventRecord(e0));
       if (k >= 0 && T >= kCholSplitBlocks) {
-        launch_chol_split_step(dA, dL, ld, n, k, grid.x, grid.y, dV, dS, 0);
+        launch_chol_split_step(dA, dL, ld, n, k, grid.x, grid.y, dV, dS, dtask, toff.data(), 0);
       } else {
         hipLaunchKernelGGL(k_chol_step, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS, dU);
       }
@@ -122,13 +133,14 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL(k_chol_step, dim3(1, 1), dim3(256), 0, 0, dA, dL, ld, n, -1, dV, dS, dU);
       for (int k = 0; k + 1 < T; ++k) {
         const int st = (k + 1) * CB;
-        launch_chol_split_step(dA, dL, ld, n, k, (n - st + CB - 1) / CB, (nrows - st + CB - 1) / CB, dV, dS, 0);
+        launch_chol_split_step(dA, dL, ld, n, k, (n - st + CB - 1) / CB, (nrows - st + CB - 1) / CB, dV, dS, dtask,
+                               toff.data(), 0);
       }
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
-      printf("factor streamed %.1f us (%s form)\n", ms * 1e3, chol_grouped() ? "grouped rank-256" : "rank-64");
+      printf("factor streamed %.1f us (%s)\n", ms * 1e3, dtask ? "scheduled tasks" : "rank-64 form");
     }
     CK(hipMemset(dF, 0, sizeof(double) * 2 * n));
     hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dA, dL, ld, n, dV, dy, dF, 2, dS);
@@ -232,6 +244,35 @@ int main(int argc, char** argv) {
     printf("persistent form: grid %d does not fit\n", chol_persist_grid(n));
   }
   CK(hipMemcpy(Sh.data(), dS, sizeof(double) * 64, hipMemcpyDeviceToHost));
+  if (T >= 16 && getenv("CHOL_TASK_PROBE")) {
+    // throughput of the split form's tile tasks alone (k_chol_upd with k = -2:
+    // no critical workgroup): N distinct tiles, each A_IJ -= sum of R panels
+    // (values: the factor above; A is overwritten, the checks are done)
+    std::vector<int4> pt;
+    for (int I = 8; I < T && (int)pt.size() < 4096; ++I)
+      for (int J = 8; J <= I && (int)pt.size() < 4096; ++J) pt.push_back(make_int4(I, J, 0, 0));
+    int4* dpt;
+    CK(hipMalloc(&dpt, sizeof(int4) * pt.size()));
+    for (int R : {1, 2, 4, 8})
+      for (int N : {1, 64, 256, 512, 1024, 2048}) {
+        if (N > (int)pt.size()) continue;
+        for (auto& q : pt) { q.z = 0; q.w = R; }
+        CK(hipMemcpy(dpt, pt.data(), sizeof(int4) * N, hipMemcpyHostToDevice));
+        float best = 1e30f;
+        for (int rep = 0; rep < 3; ++rep) {
+          CK(hipEventRecord(e0));
+          hipLaunchKernelGGL(k_chol_upd, dim3(1 + N), dim3(256), 0, 0, dA, dL, ld, n, -2, dV, dS, dpt);
+          CK(hipEventRecord(e1));
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          best = std::min(best, ms);
+        }
+        const double fl = 2.0 * 64 * 64 * 64 * R * (double)N;
+        printf("task probe: rank %d x64, %5d tiles: %8.1f us  %6.2f TF/s  %.2f us per tile-panel per CU\n", R, N,
+               best * 1e3, fl / (best * 1e-3) / 1e12, best * 1e3 * std::min(N, 256) / ((double)N * R));
+      }
+  }
   // residual |S y - b| / |b|
   double rn = 0, bn = 0;
   for (int i = 0; i < n; ++i) {
