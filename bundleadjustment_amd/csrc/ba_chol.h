@@ -53,6 +53,55 @@ __device__ int g_stamp_on = 1;   // the persistent kernel records one chosen ste
 #define CHOL_STAMP(i) do {} while (0)
 #endif
 
+// Device-coherent (sc1) buffer loads / stores and the epoch-flag hand-offs of
+// the in-launch dataflows (persistent factorisation, split form's panels):
+// a value published by one CU is read by another, on any XCD.
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+constexpr int kAuxSc1 = 16;                    // buffer-instruction cache policy: sc1
+
+__device__ __forceinline__ Rsrc make_rsrc(const void* base, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double2 ld_sc1(Rsrc r, size_t byte_off) {
+  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, kAuxSc1);
+  return __builtin_bit_cast(double2, v);
+}
+__device__ __forceinline__ void st_sc1(Rsrc r, size_t byte_off, double2 x) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, x), r, (int)byte_off, 0, kAuxSc1);
+}
+
+// drain this wave's stores, join the workgroup, one lane raises the flag
+__device__ __forceinline__ void publish(unsigned* flag, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the same with the 8 tile loads of tile_fetch_sc1 issued after the stores
+// still in flight: vector memory operations complete in issue order, so
+// vmcnt(8) drains exactly the stores
+__device__ __forceinline__ void publish_before_loads(unsigned* flag, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane 0 polls (relaxed, bounded), the barrier releases the workgroup.
+// Returns false in thread 0 if the bound was hit (the failure is reported by
+// thread 0 alone; other threads return true)
+__device__ __forceinline__ bool wait_flag(const unsigned* flag, unsigned epoch, unsigned spin_max) {
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    unsigned it = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+      if (++it >= spin_max) { ok = false; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  return ok;
+}
+
 // Stage a 64x64 block M[r0 + i][c0 + j] (i < rmax - r0, j < cmax - c0, else
 // 0) into LDS: tile_load issues the 8 16-B loads of a thread, tile_put
 // writes them to LDS — several tiles' loads go out before the first store.
@@ -124,6 +173,27 @@ __device__ inline void tile_put_masked(double (*D)[LDP], const TileRaw& t) {
     D[i][j + 1] = (t.mask >> (2 * it)) & 2u ? t.v[it].y : 0.0;
   }
 }
+// tile_fetch with sc1 loads: the same clamped, branch-free
+// addresses and the same zeroing, so the staged tile is identical
+template <bool LOWER = false>
+__device__ inline TileRegs tile_fetch_sc1(Rsrc r, size_t ld, int r0, int c0, int rmax, int cmax) {
+  TileRegs t;
+  const int tid = ctid();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int e = tid + 256 * it;
+    const int i = e >> 5, j = (e & 31) * 2;
+    const bool up = LOWER && j > i;
+    const int ri = r0 + i, cj = c0 + (up ? (i & ~1) : j);
+    const int ric = min(ri, rmax - 1), cjc = min(cj, cmax - 2) & ~1;
+    const double2 v = ld_sc1(r, ((size_t)ric * ld + cjc) * sizeof(double));
+    const bool rok = ri < rmax && !up;
+    t.v[it].x = (rok && cj < cmax) ? v.x : 0.0;
+    t.v[it].y = (rok && cj + 1 < cmax) ? v.y : 0.0;
+  }
+  return t;
+}
+
 __device__ inline void stage64(double (*D)[LDP], const double* __restrict__ M, size_t ld, int r0, int c0, int rmax,
                                int cmax) {
   tile_put(D, tile_fetch(M, ld, r0, c0, rmax, cmax));

@@ -306,7 +306,7 @@ int back_flow_capacity(int device) {
 
 // split-form block step (ba_chol_split.hip)
 void launch_chol_split_step(double* A, double* L, int ld, int n, int k, int tc, int tr, double* Vbuf, double* scal,
-                            const int4* tasks, const int* off, hipStream_t s);
+                            const int4* tasks, const int* off, unsigned* vflag, unsigned epoch, hipStream_t s);
 
 // Block columns from which the split (panel + update) form is used: below it
 // the fused step's trailing tiles hide behind the critical workgroup and one
@@ -345,7 +345,8 @@ void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hi
     const int st = (k + 1) * CB;
     const int tr = (nrows - st + CB - 1) / CB, tc = (n - st + CB - 1) / CB;
     if (split) {
-      launch_chol_split_step(W.S, W.Lf, P.ld, n, k, tc, tr, W.Vbuf, W.scal, W.ctask, W.ctask_off, s);
+      launch_chol_split_step(W.S, W.Lf, P.ld, n, k, tc, tr, W.Vbuf, W.scal, W.ctask, W.ctask_off,
+                             W.chol_fuse ? W.cflags : nullptr, (unsigned)epoch, s);
     } else {
       hipLaunchKernelGGL(k_chol_step, dim3(tc, tr), dim3(256), 0, s, W.S, W.Lf, P.ld, n, k, W.Vbuf, W.scal, W.Ubuf);
     }

@@ -93,47 +93,13 @@ extern "C" int ba_debug_ov_trace(unsigned long long* out, int n) {
 #define OVT(i) do {} while (0)
 #endif
 
-typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-typedef __amdgpu_buffer_rsrc_t Rsrc;
 constexpr unsigned kPersistSpin = 1u << 17;   // ~0.2 s of polls: far beyond any real wait (~20 us)
 // (BA_CHOL_SPIN_MAX, diagnostics: a smaller bound, e.g. 1, so that the
 // spin-fallback path of ba_solve runs; tests/test_gpu_parity.py)
-constexpr int kAuxSc1 = 16;                    // buffer-instruction cache policy: sc1
 constexpr int kOvCams = 200;                   // overlapped form: variable cameras of the LDS camera table (kLinLdsCams)
 constexpr int kOvFar = 4;                      // overlapped form: a worker takes items while >= this many steps from its last update
 
-__device__ __forceinline__ Rsrc make_rsrc(const void* base, size_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ double2 ld_sc1(Rsrc r, size_t byte_off) {
-  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte_off, 0, kAuxSc1);
-  return __builtin_bit_cast(double2, v);
-}
-__device__ __forceinline__ void st_sc1(Rsrc r, size_t byte_off, double2 x) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, x), r, (int)byte_off, 0, kAuxSc1);
-}
-
-// tile_fetch (ba_chol.h) with sc1 loads: the same clamped, branch-free
-// addresses and the same zeroing, so the staged tile is identical
-template <bool LOWER = false>
-__device__ inline TileRegs tile_fetch_sc1(Rsrc r, size_t ld, int r0, int c0, int rmax, int cmax) {
-  TileRegs t;
-  const int tid = ctid();
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int e = tid + 256 * it;
-    const int i = e >> 5, j = (e & 31) * 2;
-    const bool up = LOWER && j > i;
-    const int ri = r0 + i, cj = c0 + (up ? (i & ~1) : j);
-    const int ric = min(ri, rmax - 1), cjc = min(cj, cmax - 2) & ~1;
-    const double2 v = ld_sc1(r, ((size_t)ric * ld + cjc) * sizeof(double));
-    const bool rok = ri < rmax && !up;
-    t.v[it].x = (rok && cj < cmax) ? v.x : 0.0;
-    t.v[it].y = (rok && cj + 1 < cmax) ? v.y : 0.0;
-  }
-  return t;
-}
-
+// (tile_fetch_sc1: ba_chol.h)
 // the same tile as tile_fetch_sc1 in two halves: the raw 16-B loads (clamped
 // addresses) now, the zeroing when the tile goes to LDS.  The masks read the
 // loaded registers, so formed at the fetch they made the compiler wait for
@@ -169,36 +135,7 @@ __device__ inline void tile_put_masked(double (*D)[LDP], const TileRegs& t, int 
   }
 }
 
-// drain this wave's stores, join the workgroup, one lane raises the flag
-__device__ __forceinline__ void publish(unsigned* flag, unsigned epoch) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // EVERY storing wave
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// the same with the 8 tile loads of tile_fetch_sc1 issued after the stores
-// still in flight: vector memory operations complete in issue order, so
-// vmcnt(8) drains exactly the stores
-__device__ __forceinline__ void publish_before_loads(unsigned* flag, unsigned epoch) {
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// lane 0 polls (relaxed, bounded), the barrier releases the workgroup.
-// Returns false in thread 0 if the bound was hit (the failure is reported by
-// thread 0 alone; other threads return true)
-__device__ __forceinline__ bool wait_flag(const unsigned* flag, unsigned epoch, unsigned spin_max) {
-  bool ok = true;
-  if (threadIdx.x == 0) {
-    unsigned it = 0;
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-      if (++it >= spin_max) { ok = false; break; }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  }
-  __syncthreads();
-  return ok;
-}
+// (publish, publish_before_loads, wait_flag, make_rsrc, ld_sc1, st_sc1: ba_chol.h)
 
 // The overlapped form (OvArgs::on): the reduced system S is formed INSIDE
 // the launch, by the workgroups that do not yet hold a tile — the pair blocks

@@ -35,9 +35,13 @@ __device__ inline void split_tile_of(int lin, int tc, int& I, int& J) {
 // The critical workgroup of block step k: C = A_{k+1,k+1} - L_{k+1,k}
 // L_{k+1,k}^T (the panel from k_chol_panel; k < 0: block 0 as it is), then
 // factor_invert_blk; V_{k+1} and the rhs row of L leave the workgroup.
+// vflag (fused panels, k_chol_upd): V_{k+1} leaves by device-coherent
+// stores and vflag[k + 1] = epoch publishes it to the column tasks of the
+// same launch.
 __device__ __forceinline__ void split_critical(double* __restrict__ A, double* __restrict__ L, int ld, int n, int k,
                                                double* __restrict__ Vbuf, double* __restrict__ scal,
-                                               double (*S0)[LDP], double (*S1)[LDP], double (*Zs)[18], CholLds& cw) {
+                                               double (*S0)[LDP], double (*S1)[LDP], double (*Zs)[18], CholLds& cw,
+                                               unsigned* vflag = nullptr, unsigned epoch = 0) {
   const int nrows = n + 1;
   const size_t lds = (size_t)ld;
   const int s = (k + 1) * CB;
@@ -72,11 +76,14 @@ __device__ __forceinline__ void split_critical(double* __restrict__ A, double* _
 #pragma unroll
       for (int h = 0; h < 2; ++h)
         v[h] = (j + h <= i && i < b && j + h < b) ? S1[i][j + h] : (i == j + h ? 1.0 : 0.0);
-      Vd[e2] = make_double2(v[0], v[1]);
+      if (vflag) st_sc1(make_rsrc(Vbuf, (size_t)(k + 2) * CB * CB * sizeof(double)),
+                        ((size_t)(k + 1) * CB * CB + 2 * (size_t)e2) * sizeof(double), make_double2(v[0], v[1]));
+      else Vd[e2] = make_double2(v[0], v[1]);
     }
     if (m > b)
       for (int j = threadIdx.x; j < b; j += 256) L[(size_t)(s + b) * ld + s + j] = S0[b][j];
   }
+  if (vflag) publish(&vflag[k + 1], epoch);
   CHOL_STAMP(6);
   if (threadIdx.x == 0 && cw.bad) scal[SL_CHOL_BAD] += 1.0;
 }
@@ -169,16 +176,24 @@ __global__ __launch_bounds__(256) void k_chol_panel(const double* __restrict__ A
 }
 
 // A_IJ -= sum_{p in [pa, pb)} L_Ip L_Jp^T: operand tiles of panel p + 1 are
-// fetched into registers while panel p's MFMAs run; A is read once, written once
-__device__ __forceinline__ void upd_tile(double* __restrict__ A, const double* __restrict__ L, int ld, int n, int I,
-                                         int J, int pa, int pb, double (*S0)[LDP], double (*S1)[LDP]) {
+// fetched into registers while panel p's MFMAs run; A is read once, written
+// once (not at all for an empty range).
+// vflag (a column task of the fused form, J = k + 1): the updated tile then
+// forms its panel L_IJ = A_IJ V_J^T, as k_chol_panel would in the next step —
+// V_J comes from this launch's critical workgroup (vflag[J] = epoch).
+__device__ __forceinline__ bool upd_tile(double* __restrict__ A, double* __restrict__ L, int ld, int n, int I,
+                                         int J, int pa, int pb, double (*S0)[LDP], double (*S1)[LDP],
+                                         const unsigned* vflag = nullptr, unsigned epoch = 0, unsigned spin_max = 0,
+                                         const double* __restrict__ Vbuf = nullptr) {
   const int nrows = n + 1;
   const size_t lds = (size_t)ld;
   const int r0 = I * CB, c0 = J * CB;
   const bool off = I != J;
-  TileRaw tI = tile_fetch_raw(L, lds, r0, pa * CB, nrows, min(pa * CB + CB, n));
-  TileRaw tJ;
-  if (off) tJ = tile_fetch_raw(L, lds, c0, pa * CB, n, min(pa * CB + CB, n));
+  TileRaw tI, tJ;
+  if (pb > pa) {
+    tI = tile_fetch_raw(L, lds, r0, pa * CB, nrows, min(pa * CB + CB, n));
+    if (off) tJ = tile_fetch_raw(L, lds, c0, pa * CB, n, min(pa * CB + CB, n));
+  }
   double av[2][2][4];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -216,8 +231,37 @@ __device__ __forceinline__ void upd_tile(double* __restrict__ A, const double* _
         int rr, cc;
         acc_pos(a, b, g, &rr, &cc);
         const int ri = r0 + rr, cj = c0 + cc;
-        if (ri < nrows && cj < n && cj <= ri) A[(size_t)ri * ld + cj] = av[a][b][g] - acc[a][b][g];
+        if (pb > pa && ri < nrows && cj < n && cj <= ri) A[(size_t)ri * ld + cj] = av[a][b][g] - acc[a][b][g];
       }
+  if (!vflag) return true;
+  // ---- the panel: S0 = the updated tile (bitwise what k_chol_panel reloads)
+  if (pb > pa) __syncthreads();               // the last MFMAs are done with S0 / S1
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int rr, cc;
+        acc_pos(a, b, g, &rr, &cc);
+        const int ri = r0 + rr, cj = c0 + cc;
+        S0[rr][cc] = (ri < nrows && cj < n) ? av[a][b][g] - acc[a][b][g] : 0.0;
+      }
+  const bool ok = wait_flag(&vflag[J], epoch, spin_max);
+  tile_put(S1, tile_fetch_sc1<true>(make_rsrc(Vbuf, (size_t)(J + 1) * CB * CB * sizeof(double)), CB, J * CB, 0,
+                                    (J + 1) * CB, CB));
+  __syncthreads();
+  d4 pacc[4];
+  mfma_xVT_strip(S0, S1, pacc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, m = min(CB, nrows - r0), kb = min(CB, n - c0);
+#pragma unroll
+  for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int rr = 16 * w + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
+      if (rr < m && cc < kb) L[(size_t)(r0 + rr) * ld + c0 + cc] = pacc[bc][g];
+    }
+  return ok;
 }
 
 // ---- scheduled form (default): a host-planned task table replaces the
@@ -271,14 +315,20 @@ static void chol_split_plan(int T, int TR, int rank, double budget, CholSplitPla
     // due tasks first (the longest first), then the background
     const size_t first = P.tasks.size();
     for (Tile& t : tl) {
-      if (t.due != k || t.a >= t.need) continue;
-      P.tasks.push_back(make_int4(t.I, t.J, t.a, t.need));
+      // (every off-diagonal tile of column k + 1 gets a column task — the
+      // fused form's panel — even with nothing left to apply)
+      const bool col = t.I != t.J;
+      if (t.due != k || (t.a >= t.need && !col)) continue;
+      P.tasks.push_back(make_int4(t.I | (col ? 1 << 20 : 0), t.J, t.a, t.need));
       spent += t.need - t.a;
       due_work[t.due] -= t.need - t.a;
       t.a = t.need;
     }
-    std::stable_sort(P.tasks.begin() + first, P.tasks.end(),
-                     [](const int4& x, const int4& y) { return x.w - x.z > y.w - y.z; });
+    // column tasks first (the next step waits on their panels), longest first
+    std::stable_sort(P.tasks.begin() + first, P.tasks.end(), [](const int4& x, const int4& y) {
+      const int px = (x.x >> 20) & 1, py = (y.x >> 20) & 1;
+      return px != py ? px > py : x.w - x.z > y.w - y.z;
+    });
     // the least constant rate that meets every later due step, given that a
     // tile advances by at most `rank` panels per launch: by step s a tile
     // must have done all but rank x (due - s) of its remaining panels
@@ -318,37 +368,40 @@ static void chol_split_plan(int T, int TR, int rank, double budget, CholSplitPla
   P.off[T - 1] = (int)P.tasks.size();
 }
 
-// Grid: 1 (critical) + the step's tasks.
+// Grid: 1 (critical) + the step's tasks {I | panel << 20, J, pa, pb}.
+// vflag (the fused form): the critical workgroup publishes V_{k+1}, and the
+// column tasks (panel bit) of column k + 1 form their panels after their
+// updates; without it the panel bit is ignored (k_chol_panel forms them in
+// the next step).
 __global__ __launch_bounds__(256) void k_chol_upd(double* __restrict__ A, double* __restrict__ L, int ld, int n, int k,
                                                   double* __restrict__ Vbuf, double* __restrict__ scal,
-                                                  const int4* __restrict__ tasks) {
+                                                  const int4* __restrict__ tasks, unsigned* vflag, unsigned epoch,
+                                                  unsigned spin_max) {
   __shared__ double S0[CB][LDP];
   __shared__ double S1[CB][LDP];
   __shared__ double Zs[CB][18];
   __shared__ CholLds cw;
   if (blockIdx.x == 0) {
-    if (k >= -1) split_critical(A, L, ld, n, k, Vbuf, scal, S0, S1, Zs, cw);   // (k = -2: tasks only, tools/chol_bench)
+    if (k >= -1) split_critical(A, L, ld, n, k, Vbuf, scal, S0, S1, Zs, cw, vflag, epoch);   // (k = -2: tasks only, tools/chol_bench)
     return;
   }
   const int4 t = tasks[blockIdx.x - 1];
-  upd_tile(A, L, ld, n, t.x, t.y, t.z, t.w, S0, S1);
+  const bool pan = vflag && ((t.x >> 20) & 1);
+  const bool ok = upd_tile(A, L, ld, n, t.x & 0xfffff, t.y, t.z, t.w, S0, S1, pan ? vflag : nullptr, epoch, spin_max,
+                           Vbuf);
+  if (threadIdx.x == 0 && !ok) atomicAdd(&scal[SL_CHOL_SPIN], 1.0);   // (V never came: the caller redoes the step unfused)
 }
 
+// (the switches are read when a system is set up: ensure_dense, tools/chol_bench)
 int chol_split_rank() {
-  static const int r = [] {
-    const char* e = getenv("BA_CHOL_RANK");
-    const int v = e ? atoi(e) : 4;
-    return v < 0 ? 4 : v;
-  }();
-  return r;   // 0: the rank-64 form (k_chol_step_split)
+  const char* e = getenv("BA_CHOL_RANK");
+  const int v = e ? atoi(e) : 4;
+  return v < 0 ? 4 : v;   // 0: the rank-64 form (k_chol_step_split)
 }
 static double chol_split_budget() {
-  static const double b = [] {
-    const char* e = getenv("BA_CHOL_BUDGET");
-    const double v = e ? atof(e) : 1.0;
-    return v > 0 ? v : 1.0;
-  }();
-  return b;
+  const char* e = getenv("BA_CHOL_BUDGET");
+  const double v = e ? atof(e) : 1.0;
+  return v > 0 ? v : 1.0;
 }
 
 // The task table of an order-n system (device copy + host step offsets).
@@ -360,12 +413,22 @@ void chol_split_tasks(int n, std::vector<int4>& tasks, std::vector<int>& off) {
   off.swap(P.off);
 }
 
+int chol_split_fused() {
+  const char* e = getenv("BA_CHOL_FUSE");
+  return e && e[0] == '0' ? 0 : 1;
+}
+
+// Block step k of the split form.  tasks == null: the rank-64 form.  vflag
+// (the fused form): panel k was formed by step k - 1's column tasks (k = 0:
+// k_chol_panel here), else k_chol_panel forms it now.
 void launch_chol_split_step(double* A, double* L, int ld, int n, int k, int tc, int tr, double* Vbuf, double* scal,
-                            const int4* tasks, const int* off, hipStream_t s) {
-  hipLaunchKernelGGL(k_chol_panel, dim3(tr), dim3(256), 0, s, A, L, ld, n, k, Vbuf);
+                            const int4* tasks, const int* off, unsigned* vflag, unsigned epoch, hipStream_t s) {
+  if (!vflag || !tasks || k == 0) hipLaunchKernelGGL(k_chol_panel, dim3(tr), dim3(256), 0, s, A, L, ld, n, k, Vbuf);
   if (tasks) {
+    const char* e = getenv("BA_CHOL_SPIN_MAX");   // (diagnostics: a small bound exercises the fallback)
+    const unsigned spin = e && atoi(e) > 0 ? (unsigned)atoi(e) : (1u << 17);
     hipLaunchKernelGGL(k_chol_upd, dim3(1 + off[k + 1] - off[k]), dim3(256), 0, s, A, L, ld, n, k, Vbuf, scal,
-                       tasks + off[k]);
+                       tasks + off[k], vflag, epoch, spin);
     return;
   }
   const int ntiles = tc * (tc + 1) / 2 + (tr > tc ? tc : 0);   // lower tiles (+ a rhs-only tile row)

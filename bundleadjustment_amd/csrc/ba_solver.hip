@@ -629,6 +629,7 @@ void ensure_dense(ba_ctx* ctx) {
     W.ctask = ctx->upload(tasks);
     W.ctask_off = ctx->chol_off.data();
   }
+  W.chol_fuse = W.ctask && bahip::chol_split_fused();
   W.yg = ctx->dalloc<double>(2 * (size_t)std::max(ctx->n, 1));
   {
     // persistent factorisation (one launch) when the per-step form would not
@@ -1216,9 +1217,10 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
       // substitution (k_back_flow) has no fallback: BA_ERR_DEVICE.  Under
       // collectives the spin slot is all-reduced with the step's scalars, so
       // every rank redoes (or throws) together.
-      if (!ctx->W.chol_persist)
+      if (!ctx->W.chol_persist && !ctx->W.chol_fuse)
         throw BaError{BA_ERR_DEVICE, "dense Cholesky: a hand-off spin bound was hit"};
       ctx->W.chol_persist = false;
+      ctx->W.chol_fuse = false;   // (the split form's in-launch panels: k_chol_panel launches instead)
       if (ctx->lin_at_cand) linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, false, true);
       ls = step_enqueue(ctx, radius, o);
       ctx->read_scalars();

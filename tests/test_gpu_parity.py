@@ -384,6 +384,33 @@ def test_overlapped_factorisation_is_bitwise_the_serial_forms(monkeypatch):
         assert [x["step_is_successful"] for x in ref[3]] == [x["step_is_successful"] for x in r[3]], name
 
 
+def test_split_factorisation_forms_are_bitwise(monkeypatch):
+    """Beyond 24 block columns (1000 cameras: n = 6000, the split Cholesky of
+    ba_chol_split.hip): the fused form (the column tasks of step k form panel
+    k + 1 in the same launch, after the critical workgroup publishes V_{k+1};
+    the default) against the separate k_chol_panel launches (BA_CHOL_FUSE=0)
+    — the same task table, so bitwise the same trajectory — and the spin
+    fallback (BA_CHOL_SPIN_MAX=1: a column task that finds V not yet up gives
+    up, and the step is redone with the panel launches), bitwise as well."""
+    p = make_config("c4", scale=0.01)
+    opts = Options(max_num_iterations=3)
+    runs = {}
+    for name, env in (("fused", {}), ("panels", {"BA_CHOL_FUSE": "0"}), ("spin", {"BA_CHOL_SPIN_MAX": "1"})):
+        for k in ("BA_CHOL_FUSE", "BA_CHOL_SPIN_MAX"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with Solver(0) as s:
+            runs[name] = run_gpu(s, p, opts)
+    ref = runs["panels"]
+    assert len(ref[3]) >= 2
+    for name in ("fused", "spin"):
+        r = runs[name]
+        assert np.array_equal(ref[0], r[0]) and np.array_equal(ref[1], r[1]), name
+        assert [x["cost"] for x in ref[3]] == [x["cost"] for x in r[3]], name
+        assert [x["step_is_successful"] for x in ref[3]] == [x["step_is_successful"] for x in r[3]], name
+
+
 # ---------------------------------------------------------------------------
 # speculative linearisation (BA_SPEC_LIN: the linearisation at a step's
 # candidate is enqueued behind the step's scalar record; a rejected or invalid

@@ -68,10 +68,17 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dtask, tasks.data(), sizeof(int4) * tasks.size(), hipMemcpyHostToDevice));
     printf("task table: %zu tasks over %d steps (rank %d)\n", tasks.size(), T - 1, chol_split_rank());
   }
+  // the fused form's V flags (epoch-tagged, one per block column)
+  unsigned* dvf = nullptr;
+  unsigned vepoch = 0;
+  CK(hipMalloc(&dvf, sizeof(unsigned) * T));
+  CK(hipMemset(dvf, 0, sizeof(unsigned) * T));
+  unsigned* vf = dtask && chol_split_fused() ? dvf : nullptr;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   for (int rep = 0; rep < 3; ++rep) {
+    ++vepoch;   // (a fresh flag epoch per factorisation)
     CK(hipMemcpy(dA, A.data(), sizeof(double) * A.size(), hipMemcpyHostToDevice));
     CK(hipMemset(dS, 0, sizeof(double) * 64));
     double tot = 0;
@@ -82,7 +89,7 @@ int main(int argc, char** argv) {
       dim3 grid = k < 0 ? dim3(1, 1) : dim3(tc, tr);
       CK(hipEventRecord(e0));
       if (k >= 0 && T >= kCholSplitBlocks) {
-        launch_chol_split_step(dA, dL, ld, n, k, grid.x, grid.y, dV, dS, dtask, toff.data(), 0);
+        launch_chol_split_step(dA, dL, ld, n, k, grid.x, grid.y, dV, dS, dtask, toff.data(), vf, vepoch, 0);
       } else {
         hipLaunchKernelGGL(k_chol_step, grid, dim3(256), 0, 0, dA, dL, ld, n, k, dV, dS, dU);
       }
@@ -127,6 +134,7 @@ int main(int argc, char** argv) {
   if (T >= kCholSplitBlocks) {
     // the split form as the solver runs it: every step enqueued back to back
     for (int rep = 0; rep < 3; ++rep) {
+    ++vepoch;   // (a fresh flag epoch per factorisation)
       CK(hipMemcpy(dA, A.data(), sizeof(double) * A.size(), hipMemcpyHostToDevice));
       CK(hipMemset(dS, 0, sizeof(double) * 64));
       CK(hipEventRecord(e0));
@@ -134,13 +142,14 @@ int main(int argc, char** argv) {
       for (int k = 0; k + 1 < T; ++k) {
         const int st = (k + 1) * CB;
         launch_chol_split_step(dA, dL, ld, n, k, (n - st + CB - 1) / CB, (nrows - st + CB - 1) / CB, dV, dS, dtask,
-                               toff.data(), 0);
+                               toff.data(), vf, vepoch, 0);
       }
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
-      printf("factor streamed %.1f us (%s)\n", ms * 1e3, dtask ? "scheduled tasks" : "rank-64 form");
+      printf("factor streamed %.1f us (%s)\n", ms * 1e3,
+             dtask ? (vf ? "scheduled tasks, fused panels" : "scheduled tasks") : "rank-64 form");
     }
     CK(hipMemset(dF, 0, sizeof(double) * 2 * n));
     hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dA, dL, ld, n, dV, dy, dF, 2, dS);
@@ -261,7 +270,7 @@ int main(int argc, char** argv) {
         float best = 1e30f;
         for (int rep = 0; rep < 3; ++rep) {
           CK(hipEventRecord(e0));
-          hipLaunchKernelGGL(k_chol_upd, dim3(1 + N), dim3(256), 0, 0, dA, dL, ld, n, -2, dV, dS, dpt);
+          hipLaunchKernelGGL(k_chol_upd, dim3(1 + N), dim3(256), 0, 0, dA, dL, ld, n, -2, dV, dS, dpt, nullptr, 0u, 1u);
           CK(hipEventRecord(e1));
           CK(hipEventSynchronize(e1));
           float ms;

@@ -34,12 +34,13 @@ static int check(int T, int TR, int rank, double budget, bool show) {
     long work = 0;
     for (int t = P.off[k]; t < P.off[k + 1]; ++t) {
       const int4 q = P.tasks[t];
-      const int I = q.x, J = q.y;
+      const int I = q.x & 0xfffff, J = q.y;
       if (I < J || I >= TR || J >= T || J < 1) { fail("outside the trapezoid", k, I, J, 0); continue; }
       if (touch[I][J]++) fail("two tasks in one launch", k, I, J, 0);
       if (q.z != a[I][J]) fail("range does not continue the applied prefix", k, I, J, q.z);
-      if (q.w <= q.z || q.w > k + 1) fail("panel range empty or not formed yet", k, I, J, q.w);
+      if ((q.w <= q.z && !(q.x >> 20)) || q.w > k + 1) fail("panel range empty or not formed yet", k, I, J, q.w);
       if (q.w > (I == J ? J - 1 : J)) fail("range beyond the tile's panels", k, I, J, q.w);
+      if (((q.x >> 20) & 1) != (J == k + 1 && I > J)) fail("column-task mark", k, I, J, q.x >> 20);
       a[I][J] = q.w;
       work += q.w - q.z;
     }
