@@ -315,6 +315,9 @@ void launch_chol_split_step(double* A, double* L, int ld, int n, int k, int tc, 
 constexpr int kCholSplitBlocks = 24;
 int chol_split_blocks() { return kCholSplitBlocks; }
 
+void launch_chol_flow(double* A, double* L, int ld, int n, double* Vbuf, double* scal, const int4* ftask, int nftask,
+                      unsigned* vflag, unsigned* tflag, unsigned* pflag, unsigned epoch, hipStream_t s);
+
 // the persistent form (ba_chol_persist.hip)
 void launch_chol_persist(double* A, double* L, int ld, int n, double* Vbuf, double* scal, unsigned* flags,
                          unsigned epoch, hipStream_t s);
@@ -341,6 +344,13 @@ void launch_cholesky_solve2(const DevProblem& P, const DevWork& W, int epoch, hi
     return;
   }
   hipLaunchKernelGGL(k_chol_step, dim3(1, 1), dim3(256), 0, s, W.S, W.Lf, P.ld, n, -1, W.Vbuf, W.scal, W.Ubuf);
+  if (split && W.chol_flow) {
+    const size_t TR = (size_t)(nrows + CB - 1) / CB;
+    launch_chol_flow(W.S, W.Lf, P.ld, n, W.Vbuf, W.scal, W.ftask, W.nftask, W.cflags, W.tflag, W.tflag + TR * T,
+                     (unsigned)epoch, s);
+    hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, s, W.S, W.Lf, P.ld, n, W.Vbuf, W.y, W.yg, epoch, W.scal);
+    return;
+  }
   for (int k = 0; k + 1 < T; ++k) {
     const int st = (k + 1) * CB;
     const int tr = (nrows - st + CB - 1) / CB, tc = (n - st + CB - 1) / CB;

@@ -38,6 +38,7 @@ __device__ inline void split_tile_of(int lin, int tc, int& I, int& J) {
 // vflag (fused panels, k_chol_upd): V_{k+1} leaves by device-coherent
 // stores and vflag[k + 1] = epoch publishes it to the column tasks of the
 // same launch.
+template <bool FLOW = false>
 __device__ __forceinline__ void split_critical(double* __restrict__ A, double* __restrict__ L, int ld, int n, int k,
                                                double* __restrict__ Vbuf, double* __restrict__ scal,
                                                double (*S0)[LDP], double (*S1)[LDP], double (*Zs)[18], CholLds& cw,
@@ -52,8 +53,13 @@ __device__ __forceinline__ void split_critical(double* __restrict__ A, double* _
   const int m = min(CB, nrows - s);         // rows in the tile (b or b + 1 with the rhs row)
   CHOL_STAMP(0);
   if (k >= 0) {
-    const TileRegs tA = tile_fetch<true>(A, lds, s, s, nrows, s + b);   // A_{k+1,k+1} (+ rhs row)
-    const TileRegs tP = tile_fetch(L, lds, s, kc, nrows, kc + kb);      // L_{k+1,k} (k_chol_panel)
+    // (FLOW: both tiles were written in this launch — device-coherent loads)
+    const Rsrc rA = make_rsrc(A, (size_t)nrows * ld * sizeof(double));
+    const Rsrc rL = make_rsrc(L, (size_t)nrows * ld * sizeof(double));
+    const TileRegs tA = FLOW ? tile_fetch_sc1<true>(rA, lds, s, s, nrows, s + b)
+                             : tile_fetch<true>(A, lds, s, s, nrows, s + b);   // A_{k+1,k+1} (+ rhs row)
+    const TileRegs tP = FLOW ? tile_fetch_sc1(rL, lds, s, kc, nrows, kc + kb)
+                             : tile_fetch(L, lds, s, kc, nrows, kc + kb);      // L_{k+1,k} (k_chol_panel)
     tile_put(S0, tA);
     tile_put(S1, tP);
     __syncthreads();
@@ -181,18 +187,74 @@ __global__ __launch_bounds__(256) void k_chol_panel(const double* __restrict__ A
 // vflag (a column task of the fused form, J = k + 1): the updated tile then
 // forms its panel L_IJ = A_IJ V_J^T, as k_chol_panel would in the next step —
 // V_J comes from this launch's critical workgroup (vflag[J] = epoch).
+// FLOW (k_chol_flow, one launch for the whole factorisation): the tile, its
+// operand panels and V are produced by other tasks of the same launch — the
+// task first waits on their flags (tile: its previous range's tag; panels:
+// the column tasks that formed them), reads and writes them device-coherent,
+// and publishes its own tile (and panel) when done.
+__device__ __forceinline__ unsigned flow_tag(unsigned epoch, int p) { return epoch * 4096u + (unsigned)p; }
+__device__ __forceinline__ TileRaw tile_fetch_raw_sc1(Rsrc r, size_t ld, int r0, int c0, int rmax, int cmax) {
+  TileRaw t;
+  t.mask = 0;
+  const int tid = ctid();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int e = tid + 256 * it;
+    const int i = e >> 5, j = (e & 31) * 2;
+    const int ri = r0 + i, cj = c0 + j;
+    const int ric = min(ri, rmax - 1), cjc = min(cj, cmax - 2) & ~1;
+    t.v[it] = ld_sc1(r, ((size_t)ric * ld + cjc) * sizeof(double));
+    const bool rok = ri < rmax;
+    t.mask |= ((rok && cj < cmax) ? 1u : 0u) << (2 * it);
+    t.mask |= ((rok && cj + 1 < cmax) ? 2u : 0u) << (2 * it);
+  }
+  return t;
+}
+// thread 0 polls every flag the task needs, then one barrier; false (thread
+// 0) if a bound was hit
+struct FlowFlags { unsigned* tflag; unsigned* pflag; unsigned epoch; unsigned spin_max; int T; };
+__device__ __forceinline__ bool flow_poll(const unsigned* f, unsigned want, unsigned spin_max) {
+  unsigned it = 0;
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+    if (++it >= spin_max) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+__device__ __forceinline__ bool flow_wait(const FlowFlags& ff, int I, int J, int pa, int pb) {
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    if (pa > 0) ok &= flow_poll(&ff.tflag[I * ff.T + J], flow_tag(ff.epoch, pa), ff.spin_max);
+    for (int p = max(pa, 1); p < pb; ++p) {   // (panel 0 precedes the launch)
+      ok &= flow_poll(&ff.pflag[I * ff.T + p], ff.epoch, ff.spin_max);
+      if (I != J) ok &= flow_poll(&ff.pflag[J * ff.T + p], ff.epoch, ff.spin_max);
+    }
+  }
+  __syncthreads();
+  return ok;
+}
+
+template <bool FLOW = false>
 __device__ __forceinline__ bool upd_tile(double* __restrict__ A, double* __restrict__ L, int ld, int n, int I,
                                          int J, int pa, int pb, double (*S0)[LDP], double (*S1)[LDP],
                                          const unsigned* vflag = nullptr, unsigned epoch = 0, unsigned spin_max = 0,
-                                         const double* __restrict__ Vbuf = nullptr) {
+                                         const double* __restrict__ Vbuf = nullptr, const FlowFlags* ff = nullptr) {
   const int nrows = n + 1;
   const size_t lds = (size_t)ld;
   const int r0 = I * CB, c0 = J * CB;
   const bool off = I != J;
+  bool ok = true;
+  if (FLOW) ok = flow_wait(*ff, I, J, pa, pb);
+  const Rsrc rL = make_rsrc(L, (size_t)nrows * ld * sizeof(double));
   TileRaw tI, tJ;
   if (pb > pa) {
-    tI = tile_fetch_raw(L, lds, r0, pa * CB, nrows, min(pa * CB + CB, n));
-    if (off) tJ = tile_fetch_raw(L, lds, c0, pa * CB, n, min(pa * CB + CB, n));
+    if (FLOW) {
+      tI = tile_fetch_raw_sc1(rL, lds, r0, pa * CB, nrows, min(pa * CB + CB, n));
+      if (off) tJ = tile_fetch_raw_sc1(rL, lds, c0, pa * CB, n, min(pa * CB + CB, n));
+    } else {
+      tI = tile_fetch_raw(L, lds, r0, pa * CB, nrows, min(pa * CB + CB, n));
+      if (off) tJ = tile_fetch_raw(L, lds, c0, pa * CB, n, min(pa * CB + CB, n));
+    }
   }
   double av[2][2][4];
 #pragma unroll
@@ -203,7 +265,8 @@ __device__ __forceinline__ bool upd_tile(double* __restrict__ A, double* __restr
       for (int g = 0; g < 4; ++g) {
         int rr, cc;
         acc_pos(a, b, g, &rr, &cc);
-        av[a][b][g] = A[(size_t)min(r0 + rr, nrows - 1) * ld + min(c0 + cc, n - 1)];
+        const size_t off_a = (size_t)min(r0 + rr, nrows - 1) * ld + min(c0 + cc, n - 1);
+        av[a][b][g] = FLOW ? __hip_atomic_load(A + off_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : A[off_a];
       }
   d4 acc[2][2];
 #pragma unroll
@@ -217,8 +280,13 @@ __device__ __forceinline__ bool upd_tile(double* __restrict__ A, double* __restr
     __syncthreads();
     if (p + 1 < pb) {
       const int kc = (p + 1) * CB, ke = min(kc + CB, n);
-      tI = tile_fetch_raw(L, lds, r0, kc, nrows, ke);
-      if (off) tJ = tile_fetch_raw(L, lds, c0, kc, n, ke);
+      if (FLOW) {
+        tI = tile_fetch_raw_sc1(rL, lds, r0, kc, nrows, ke);
+        if (off) tJ = tile_fetch_raw_sc1(rL, lds, c0, kc, n, ke);
+      } else {
+        tI = tile_fetch_raw(L, lds, r0, kc, nrows, ke);
+        if (off) tJ = tile_fetch_raw(L, lds, c0, kc, n, ke);
+      }
     }
     mfma_xyT_64_add(S0, off ? S1 : S0, acc);
   }
@@ -231,9 +299,14 @@ __device__ __forceinline__ bool upd_tile(double* __restrict__ A, double* __restr
         int rr, cc;
         acc_pos(a, b, g, &rr, &cc);
         const int ri = r0 + rr, cj = c0 + cc;
-        if (pb > pa && ri < nrows && cj < n && cj <= ri) A[(size_t)ri * ld + cj] = av[a][b][g] - acc[a][b][g];
+        if (pb > pa && ri < nrows && cj < n && cj <= ri) {
+          if (FLOW) __hip_atomic_store(A + (size_t)ri * ld + cj, av[a][b][g] - acc[a][b][g], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+          else A[(size_t)ri * ld + cj] = av[a][b][g] - acc[a][b][g];
+        }
       }
-  if (!vflag) return true;
+  if (FLOW && pb > pa) publish(&ff->tflag[I * ff->T + J], flow_tag(ff->epoch, pb));
+  if (!vflag) return ok;
   // ---- the panel: S0 = the updated tile (bitwise what k_chol_panel reloads)
   if (pb > pa) __syncthreads();               // the last MFMAs are done with S0 / S1
 #pragma unroll
@@ -247,7 +320,7 @@ __device__ __forceinline__ bool upd_tile(double* __restrict__ A, double* __restr
         const int ri = r0 + rr, cj = c0 + cc;
         S0[rr][cc] = (ri < nrows && cj < n) ? av[a][b][g] - acc[a][b][g] : 0.0;
       }
-  const bool ok = wait_flag(&vflag[J], epoch, spin_max);
+  ok &= wait_flag(&vflag[J], epoch, spin_max);
   tile_put(S1, tile_fetch_sc1<true>(make_rsrc(Vbuf, (size_t)(J + 1) * CB * CB * sizeof(double)), CB, J * CB, 0,
                                     (J + 1) * CB, CB));
   __syncthreads();
@@ -259,8 +332,13 @@ __device__ __forceinline__ bool upd_tile(double* __restrict__ A, double* __restr
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int rr = 16 * w + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
-      if (rr < m && cc < kb) L[(size_t)(r0 + rr) * ld + c0 + cc] = pacc[bc][g];
+      if (rr < m && cc < kb) {
+        if (FLOW) __hip_atomic_store(L + (size_t)(r0 + rr) * ld + c0 + cc, pacc[bc][g], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        else L[(size_t)(r0 + rr) * ld + c0 + cc] = pacc[bc][g];
+      }
     }
+  if (FLOW) publish(&ff->pflag[I * ff->T + J], ff->epoch);
   return ok;
 }
 
@@ -392,6 +470,42 @@ __global__ __launch_bounds__(256) void k_chol_upd(double* __restrict__ A, double
   if (threadIdx.x == 0 && !ok) atomicAdd(&scal[SL_CHOL_SPIN], 1.0);   // (V never came: the caller redoes the step unfused)
 }
 
+// ---- flow form (default): the whole factorisation in ONE launch.  The task
+// list is the scheduled form's, step by step, each step led by its critical
+// workgroup (bit 21, y = k); every task waits on the flags of what it reads
+// (FLOW above; the critical: its diagonal tile's tag and its panel row) and
+// publishes what it writes.  A task waits only on tasks before it in the
+// list, which the in-order dispatch has placed on the device before it, so
+// the grid needs no co-residency (as k_back_flow).  The steps overlap: a
+// step's background tasks run beside the next steps' chain, and no launch
+// boundary drains the device between steps.  Same arithmetic per task as
+// the per-step launches: bitwise the same factor.
+__global__ __launch_bounds__(256) void k_chol_flow(double* __restrict__ A, double* __restrict__ L, int ld, int n,
+                                                   double* __restrict__ Vbuf, double* __restrict__ scal,
+                                                   const int4* __restrict__ tasks, unsigned* vflag, unsigned* tflag,
+                                                   unsigned* pflag, unsigned epoch, unsigned spin_max, int T) {
+  __shared__ double S0[CB][LDP];
+  __shared__ double S1[CB][LDP];
+  __shared__ double Zs[CB][18];
+  __shared__ CholLds cw;
+  const int4 t = tasks[blockIdx.x];
+  const FlowFlags ff{tflag, pflag, epoch, spin_max, T};
+  bool ok = true;
+  if ((t.x >> 21) & 1) {
+    const int k = t.y, d = k + 1;
+    if (threadIdx.x == 0 && k > 0) {
+      ok &= flow_poll(&tflag[d * T + d], flow_tag(epoch, k), spin_max);   // A_dd holds panels < k
+      ok &= flow_poll(&pflag[d * T + k], epoch, spin_max);                // L_{d,k}
+    }
+    __syncthreads();
+    split_critical<true>(A, L, ld, n, k, Vbuf, scal, S0, S1, Zs, cw, vflag, epoch);
+  } else {
+    ok = upd_tile<true>(A, L, ld, n, t.x & 0xfffff, t.y, t.z, t.w, S0, S1, ((t.x >> 20) & 1) ? vflag : nullptr,
+                        epoch, spin_max, Vbuf, &ff);
+  }
+  if (threadIdx.x == 0 && !ok) atomicAdd(&scal[SL_CHOL_SPIN], 1.0);   // (the caller redoes the step per step)
+}
+
 // (the switches are read when a system is set up: ensure_dense, tools/chol_bench)
 int chol_split_rank() {
   const char* e = getenv("BA_CHOL_RANK");
@@ -411,6 +525,28 @@ void chol_split_tasks(int n, std::vector<int4>& tasks, std::vector<int>& off) {
   chol_split_plan(T, TR, std::max(1, chol_split_rank()), chol_split_budget(), P);
   tasks.swap(P.tasks);
   off.swap(P.off);
+}
+// ... as the flow form's one list: step k = its critical task, then its tasks
+void chol_flow_tasks(const std::vector<int4>& tasks, const std::vector<int>& off, std::vector<int4>& flow) {
+  flow.clear();
+  for (int k = 0; k + 1 < (int)off.size(); ++k) {
+    flow.push_back(make_int4(1 << 21, k, 0, 0));
+    flow.insert(flow.end(), tasks.begin() + off[k], tasks.begin() + off[k + 1]);
+  }
+}
+int chol_split_flow() {
+  const char* e = getenv("BA_CHOL_FLOW");
+  return e && e[0] == '0' ? 0 : 1;
+}
+void launch_chol_flow(double* A, double* L, int ld, int n, double* Vbuf, double* scal, const int4* ftask, int nftask,
+                      unsigned* vflag, unsigned* tflag, unsigned* pflag, unsigned epoch, hipStream_t s) {
+  const int T = (n + CB - 1) / CB, tr = (n + 1 - CB + CB - 1) / CB;
+  const char* e = getenv("BA_CHOL_SPIN_MAX");
+  const unsigned spin = e && atoi(e) > 0 ? (unsigned)atoi(e) : (1u << 17);
+  hipLaunchKernelGGL(k_chol_panel, dim3(tr), dim3(256), 0, s, A, L, ld, n, 0, Vbuf);   // panel 0
+  if (nftask > 0)
+    hipLaunchKernelGGL(k_chol_flow, dim3(nftask), dim3(256), 0, s, A, L, ld, n, Vbuf, scal, ftask, vflag, tflag,
+                       pflag, epoch, spin, T);
 }
 
 int chol_split_fused() {

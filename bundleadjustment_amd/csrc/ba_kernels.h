@@ -105,6 +105,9 @@ struct DevWork {
   const int4* ctask;                 // split Cholesky task table {I, J, pa, pb} (>= kCholSplitBlocks block columns; null: rank-64 form)
   const int* ctask_off;              // host: step k's tasks [ctask_off[k], ctask_off[k+1])
   bool chol_fuse;                    // split form: column tasks form the next panel in-launch (flags: cflags[0, T))
+  bool chol_flow;                    // split form: the whole factorisation as one dataflow launch (k_chol_flow)
+  const int4* ftask; int nftask;     // ... its task list
+  unsigned* tflag;                   // ... [TR][T] tile tags, then [TR][T] panel flags (epoch-tagged, zeroed once)
   double* yg;                        // [n][2] back-substitution hand-off granules {y, epoch} (zeroed once)
   unsigned* cflags;                  // [T + TR*T] persistent-Cholesky hand-off flags (epoch-tagged, zeroed once)
   bool chol_persist;                 // the factorisation runs as one persistent launch (ba_chol_persist.hip)
@@ -240,7 +243,9 @@ bool obs_w_pc_ok(const DevProblem& P, const DevWork& W);   // k_obs_w_rc has the
 bool chol_persist_fits(int device, int n);   // every workgroup of k_chol_persist resident at once
 void chol_split_tasks(int n, std::vector<int4>& tasks, std::vector<int>& off);   // the split form's task table
 int chol_split_rank();
-int chol_split_fused();                      // BA_CHOL_FUSE (default 1)                       // panels per split-Cholesky task (BA_CHOL_RANK, default 4; 0: rank-64 form)
+int chol_split_fused();                      // BA_CHOL_FUSE (default 1)
+int chol_split_flow();                       // BA_CHOL_FLOW (default 1)
+void chol_flow_tasks(const std::vector<int4>& tasks, const std::vector<int>& off, std::vector<int4>& flow);                       // panels per split-Cholesky task (BA_CHOL_RANK, default 4; 0: rank-64 form)
 int chol_split_blocks();                     // block columns from which the split step form is used   // resident k_back_flow workgroups (-1: query failed)
 constexpr int kLinLdsCamsHost = 200;   // = kLinLdsCams (ba_kernels.hip): cameras the LDS camera table holds
 constexpr int kWcCamsHost = 1024;      // variable cameras of the compact-W DENSE_SCHUR pair pass

@@ -623,13 +623,28 @@ void ensure_dense(ba_ctx* ctx) {
   W.Vbuf = ctx->dalloc<double>((size_t)((ctx->n + 63) / 64 + 1) * 64 * 64);
   W.ctask = nullptr;
   W.ctask_off = nullptr;
+  std::vector<int4> tasks_h;
   if ((ctx->n + 63) / 64 >= bahip::chol_split_blocks() && bahip::chol_split_rank() > 0) {
-    std::vector<int4> tasks;
-    bahip::chol_split_tasks(ctx->n, tasks, ctx->chol_off);
-    W.ctask = ctx->upload(tasks);
+    bahip::chol_split_tasks(ctx->n, tasks_h, ctx->chol_off);
+    W.ctask = ctx->upload(tasks_h);
     W.ctask_off = ctx->chol_off.data();
   }
   W.chol_fuse = W.ctask && bahip::chol_split_fused();
+  W.chol_flow = false;
+  W.ftask = nullptr;
+  W.nftask = 0;
+  W.tflag = nullptr;
+  if (W.ctask && bahip::chol_split_flow() &&
+      (size_t)(ctx->n + 1) * std::max(ctx->ld, 1) * sizeof(double) < ((size_t)1 << 31)) {   // (32-bit buffer offsets)
+    std::vector<int4> flow;
+    bahip::chol_flow_tasks(tasks_h, ctx->chol_off, flow);
+    W.ftask = ctx->upload(flow);
+    W.nftask = (int)flow.size();
+    const size_t T = (ctx->n + 63) / 64, TR = (ctx->n + 1 + 63) / 64;
+    W.tflag = ctx->dalloc<unsigned>(2 * TR * T);
+    HIP_OK(hipMemsetAsync(W.tflag, 0, sizeof(unsigned) * 2 * TR * T, ctx->stream));
+    W.chol_flow = true;
+  }
   W.yg = ctx->dalloc<double>(2 * (size_t)std::max(ctx->n, 1));
   {
     // persistent factorisation (one launch) when the per-step form would not
@@ -1217,10 +1232,11 @@ void solve(ba_ctx* ctx, const ba_options* opt, ba_summary* sum) {
       // substitution (k_back_flow) has no fallback: BA_ERR_DEVICE.  Under
       // collectives the spin slot is all-reduced with the step's scalars, so
       // every rank redoes (or throws) together.
-      if (!ctx->W.chol_persist && !ctx->W.chol_fuse)
+      if (!ctx->W.chol_persist && !ctx->W.chol_fuse && !ctx->W.chol_flow)
         throw BaError{BA_ERR_DEVICE, "dense Cholesky: a hand-off spin bound was hit"};
       ctx->W.chol_persist = false;
-      ctx->W.chol_fuse = false;   // (the split form's in-launch panels: k_chol_panel launches instead)
+      ctx->W.chol_flow = false;   // (the split form's one-launch dataflow: per-step launches instead,
+      ctx->W.chol_fuse = false;   //  and their in-launch panels: k_chol_panel launches)
       if (ctx->lin_at_cand) linearize_enqueue(ctx, false, o.min_lm_diagonal, o.max_lm_diagonal, false, true);
       ls = step_enqueue(ctx, radius, o);
       ctx->read_scalars();

@@ -386,17 +386,24 @@ def test_overlapped_factorisation_is_bitwise_the_serial_forms(monkeypatch):
 
 def test_split_factorisation_forms_are_bitwise(monkeypatch):
     """Beyond 24 block columns (1000 cameras: n = 6000, the split Cholesky of
-    ba_chol_split.hip): the fused form (the column tasks of step k form panel
-    k + 1 in the same launch, after the critical workgroup publishes V_{k+1};
-    the default) against the separate k_chol_panel launches (BA_CHOL_FUSE=0)
-    — the same task table, so bitwise the same trajectory — and the spin
-    fallback (BA_CHOL_SPIN_MAX=1: a column task that finds V not yet up gives
-    up, and the step is redone with the panel launches), bitwise as well."""
+    ba_chol_split.hip), one task table, four ways to run it — bitwise the
+    same trajectory:
+      flow   the whole factorisation as one dataflow launch (the default);
+      fused  one launch per block step, the column tasks of step k forming
+             panel k + 1 after the critical workgroup publishes V_{k+1}
+             (BA_CHOL_FLOW=0);
+      panels the per-step launches with separate k_chol_panel launches
+             (BA_CHOL_FLOW=0 BA_CHOL_FUSE=0);
+      spin   the flow form with a spin bound of one poll (BA_CHOL_SPIN_MAX=1):
+             tasks give up waiting, and the step is redone with the panel
+             launches."""
     p = make_config("c4", scale=0.01)
     opts = Options(max_num_iterations=3)
     runs = {}
-    for name, env in (("fused", {}), ("panels", {"BA_CHOL_FUSE": "0"}), ("spin", {"BA_CHOL_SPIN_MAX": "1"})):
-        for k in ("BA_CHOL_FUSE", "BA_CHOL_SPIN_MAX"):
+    keys = ("BA_CHOL_FLOW", "BA_CHOL_FUSE", "BA_CHOL_SPIN_MAX")
+    for name, env in (("flow", {}), ("fused", {"BA_CHOL_FLOW": "0"}),
+                      ("panels", {"BA_CHOL_FLOW": "0", "BA_CHOL_FUSE": "0"}), ("spin", {"BA_CHOL_SPIN_MAX": "1"})):
+        for k in keys:
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -404,7 +411,7 @@ def test_split_factorisation_forms_are_bitwise(monkeypatch):
             runs[name] = run_gpu(s, p, opts)
     ref = runs["panels"]
     assert len(ref[3]) >= 2
-    for name in ("fused", "spin"):
+    for name in ("flow", "fused", "spin"):
         r = runs[name]
         assert np.array_equal(ref[0], r[0]) and np.array_equal(ref[1], r[1]), name
         assert [x["cost"] for x in ref[3]] == [x["cost"] for x in r[3]], name

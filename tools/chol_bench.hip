@@ -155,6 +155,45 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dA, dL, ld, n, dV, dy, dF, 2, dS);
     CK(hipDeviceSynchronize());
   }
+  if (T >= kCholSplitBlocks && dtask) {
+    // the flow form: the whole factorisation as one dataflow launch; its
+    // solution must equal the per-step forms' bit for bit
+    std::vector<double> ys(n), yf(n);
+    CK(hipMemcpy(ys.data(), dy, sizeof(double) * n, hipMemcpyDeviceToHost));
+    std::vector<int4> flow;
+    chol_flow_tasks(tasks, toff, flow);
+    int4* dflow;
+    unsigned* dtf;
+    const int TRr = (nrows + CB - 1) / CB;
+    CK(hipMalloc(&dflow, sizeof(int4) * flow.size()));
+    CK(hipMemcpy(dflow, flow.data(), sizeof(int4) * flow.size(), hipMemcpyHostToDevice));
+    CK(hipMalloc(&dtf, sizeof(unsigned) * 2 * TRr * T));
+    CK(hipMemset(dtf, 0, sizeof(unsigned) * 2 * TRr * T));
+    for (int rep = 0; rep < 3; ++rep) {
+      ++vepoch;
+      CK(hipMemcpy(dA, A.data(), sizeof(double) * A.size(), hipMemcpyHostToDevice));
+      CK(hipMemset(dS, 0, sizeof(double) * 64));
+      CK(hipEventRecord(e0));
+      hipLaunchKernelGGL(k_chol_step, dim3(1, 1), dim3(256), 0, 0, dA, dL, ld, n, -1, dV, dS, dU);
+      launch_chol_flow(dA, dL, ld, n, dV, dS, dflow, (int)flow.size(), dvf, dtf, dtf + (size_t)TRr * T, vepoch, 0);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      double sh[64];
+      CK(hipMemcpy(sh, dS, sizeof(sh), hipMemcpyDeviceToHost));
+      printf("factor flow %.1f us (one launch, %zu tasks)  spin %g bad %g\n", ms * 1e3, flow.size(), sh[SL_CHOL_SPIN],
+             sh[SL_CHOL_BAD]);
+    }
+    CK(hipMemset(dF, 0, sizeof(double) * 2 * n));
+    hipLaunchKernelGGL(k_back_flow, dim3(T), dim3(256), 0, 0, dA, dL, ld, n, dV, dy, dF, 3, dS);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(yf.data(), dy, sizeof(double) * n, hipMemcpyDeviceToHost));
+    size_t diff = 0;
+    for (int i = 0; i < n; ++i) diff += std::memcmp(&ys[i], &yf[i], 8) != 0;
+    printf("flow vs per-step: y entries differing %zu\n", diff);
+    if (diff) return 5;
+  }
   std::vector<double> y(n), Sh(64);
   CK(hipMemcpy(y.data(), dy, sizeof(double) * n, hipMemcpyDeviceToHost));
   // the persistent form (one launch, look-ahead): time it and check that it
