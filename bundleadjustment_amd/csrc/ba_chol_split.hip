@@ -69,7 +69,9 @@ __device__ __forceinline__ void split_critical(double* __restrict__ A, double* _
   }
   if (threadIdx.x == 0) cw.bad = 0;
   CHOL_STAMP(1);
-  factor_invert_blk<-1, 18>(S0, S1, Zs, cw, b, m, k >= 0 ? S1 : nullptr);   // rows b..m-1 (rhs) come out as L rows too
+  // (forced inline: with three kernels calling it the inliner kept one out-of-line copy —
+  // an s_swappc call that took every caller to 248+ VGPRs, one workgroup per CU)
+  [[clang::always_inline]] factor_invert_blk<-1, 18>(S0, S1, Zs, cw, b, m, k >= 0 ? S1 : nullptr);   // rows b..m-1 (rhs) come out as L rows too
   CHOL_STAMP(5);
   __syncthreads();
   // only V_{k+1} and the rhs row of L leave the workgroup: the diagonal L
@@ -193,6 +195,27 @@ __global__ __launch_bounds__(256) void k_chol_panel(const double* __restrict__ A
 // the column tasks that formed them), reads and writes them device-coherent,
 // and publishes its own tile (and panel) when done.
 __device__ __forceinline__ unsigned flow_tag(unsigned epoch, int p) { return epoch * 4096u + (unsigned)p; }
+// Diagnostic build only (tools/chol_bench with -DBA_CHOL_FLOW_TRACE): per
+// flow task, s_memrealtime (100 MHz) at start, after its waits, at the end,
+// and the hardware id (XCC / SE / CU) it ran on; tools/flow_trace.py.
+#ifdef BA_CHOL_FLOW_TRACE
+__device__ unsigned long long g_ftrace[1 << 16][4];
+__shared__ unsigned flow_slot;   // 0: the chain; 1 + ticket: a tile task
+#define FLOW_STAMP(i)                                                                               \
+  do {                                                                                              \
+    if (threadIdx.x == 0 && flow_slot < (1u << 16)) g_ftrace[flow_slot][i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+__device__ unsigned long long g_fchain[4096][6];   // the chain: each step's inputs ready / V published / phases
+#define CHAIN_STAMP(k, i)                                                                           \
+  do {                                                                                              \
+    if (threadIdx.x == 0 && (k) < 4096) g_fchain[k][i] = __builtin_amdgcn_s_memrealtime();          \
+  } while (0)
+#define FLOW_SLOT(v) do { if (threadIdx.x == 0) flow_slot = (v); } while (0)
+#else
+#define FLOW_STAMP(i) do {} while (0)
+#define CHAIN_STAMP(k, i) do {} while (0)
+#define FLOW_SLOT(v) do {} while (0)
+#endif
 __device__ __forceinline__ TileRaw tile_fetch_raw_sc1(Rsrc r, size_t ld, int r0, int c0, int rmax, int cmax) {
   TileRaw t;
   t.mask = 0;
@@ -245,6 +268,7 @@ __device__ __forceinline__ bool upd_tile(double* __restrict__ A, double* __restr
   const bool off = I != J;
   bool ok = true;
   if (FLOW) ok = flow_wait(*ff, I, J, pa, pb);
+  if (FLOW) FLOW_STAMP(1);
   const Rsrc rL = make_rsrc(L, (size_t)nrows * ld * sizeof(double));
   TileRaw tI, tJ;
   if (pb > pa) {
@@ -470,6 +494,82 @@ __global__ __launch_bounds__(256) void k_chol_upd(double* __restrict__ A, double
   if (threadIdx.x == 0 && !ok) atomicAdd(&scal[SL_CHOL_SPIN], 1.0);   // (V never came: the caller redoes the step unfused)
 }
 
+// The flow form's chain: ONE workgroup (the list's first entry) factors every
+// diagonal block in turn, k = 0 .. T - 2 (d = k + 1).  It keeps V_k (cleaned,
+// as stored) in registers from its own previous step and forms the panel row
+// it needs itself, P = L_{d,k} = A_{d,k} V_k^T (bitwise what the column task
+// of tile (d, k) stores: the same tile values, V and MFMA strip), so a step
+// waits only on the two tiles' tags — tile (d, k) and the diagonal tile
+// holding panels < k — instead of on another task's panel after V_k (the
+// critical-task chain handed V_k out, waited for the column task to form and
+// publish L_{d,k}, and reloaded it: ~8 us per step).  Then C = A_dd - P P^T,
+// factor_invert_blk, V_d out (device-coherent) and vflag[d].
+__device__ __forceinline__ bool flow_chain(double* __restrict__ A, double* __restrict__ L, int ld, int n,
+                                           double* __restrict__ Vbuf, double* __restrict__ scal,
+                                           double (*S0)[LDP], double (*S1)[LDP], double (*Zs)[18], CholLds& cw,
+                                           unsigned* vflag, const unsigned* tflag, unsigned epoch, unsigned spin_max,
+                                           int T) {
+  const int nrows = n + 1;
+  const size_t lds = (size_t)ld;
+  const Rsrc rA = make_rsrc(A, (size_t)nrows * ld * sizeof(double));
+  const Rsrc rV = make_rsrc(Vbuf, (size_t)(T + 1) * CB * CB * sizeof(double));
+  bool ok = true;
+  TileRegs tV = tile_fetch<true>(Vbuf, CB, 0, 0, CB, CB);   // V_0 (the launch before)
+  for (int k = 0; k + 1 < T; ++k) {
+    const int d = k + 1, s = d * CB, kc = k * CB;
+    const int kb = min(CB, n - kc), b = min(CB, n - s), m = min(CB, nrows - s);
+    if (threadIdx.x == 0 && k > 0) {
+      ok &= flow_poll(&tflag[d * T + k], flow_tag(epoch, k), spin_max);   // A_{d,k}: panels < k
+      ok &= flow_poll(&tflag[d * T + d], flow_tag(epoch, k), spin_max);   // A_dd: panels < k
+    }
+    __syncthreads();                                                       // (and the previous step's LDS reads are done)
+    CHAIN_STAMP(k, 0);
+    const TileRegs tAk = tile_fetch_sc1(rA, lds, s, kc, nrows, kc + kb);
+    const TileRegs tA = tile_fetch_sc1<true>(rA, lds, s, s, nrows, s + b);
+    tile_put(S1, tV);
+    tile_put(S0, tAk);
+    __syncthreads();
+    CHAIN_STAMP(k, 2);
+    d4 pacc[4];
+    mfma_xVT_strip(S0, S1, pacc);
+    __syncthreads();
+    {
+      const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+      for (int bc = 0; bc < 4; ++bc)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int rr = 16 * w + (lane >> 4) + 4 * g, cc = 16 * bc + (lane & 15);
+          S1[rr][cc] = (rr < m && cc < kb) ? pacc[bc][g] : 0.0;   // (as the stored panel, reloaded)
+        }
+    }
+    tile_put(S0, tA);
+    __syncthreads();
+    CHAIN_STAMP(k, 3);
+    mfma_xxT_col0(S1, S0);
+    if (threadIdx.x == 0) cw.bad = 0;
+    [[clang::always_inline]] factor_invert_blk<-1, 18>(S0, S1, Zs, cw, b, m, S1);
+    __syncthreads();
+    CHAIN_STAMP(k, 4);
+    for (int it = 0; it < 8; ++it) {
+      const int e2 = threadIdx.x + 256 * it;
+      const int i = (2 * e2) / CB, j = (2 * e2) % CB;
+      double v[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        v[h] = (j + h <= i && i < b && j + h < b) ? S1[i][j + h] : (i == j + h ? 1.0 : 0.0);
+      tV.v[it] = make_double2(v[0], v[1]);
+      st_sc1(rV, ((size_t)d * CB * CB + 2 * (size_t)e2) * sizeof(double), tV.v[it]);
+    }
+    if (m > b)
+      for (int j = threadIdx.x; j < b; j += 256) L[(size_t)(s + b) * ld + s + j] = S0[b][j];
+    publish(&vflag[d], epoch);
+    CHAIN_STAMP(k, 1);
+    if (threadIdx.x == 0 && cw.bad) scal[SL_CHOL_BAD] += 1.0;
+  }
+  return ok;
+}
+
 // ---- flow form (default): the whole factorisation in ONE launch.  The task
 // list is the scheduled form's, step by step, each step led by its critical
 // workgroup (bit 21, y = k); every task waits on the flags of what it reads
@@ -480,29 +580,33 @@ __global__ __launch_bounds__(256) void k_chol_upd(double* __restrict__ A, double
 // step's background tasks run beside the next steps' chain, and no launch
 // boundary drains the device between steps.  Same arithmetic per task as
 // the per-step launches: bitwise the same factor.
-__global__ __launch_bounds__(256) void k_chol_flow(double* __restrict__ A, double* __restrict__ L, int ld, int n,
-                                                   double* __restrict__ Vbuf, double* __restrict__ scal,
-                                                   const int4* __restrict__ tasks, unsigned* vflag, unsigned* tflag,
-                                                   unsigned* pflag, unsigned epoch, unsigned spin_max, int T) {
+// Block 0 is the chain workgroup (flow_chain); block 1 + i runs task i.
+// (Measured and not kept: giving the chain a CU of its own — a workgroup the
+// dispatcher placed beside it waited there, the others drew tasks from an
+// atomic ticket counter: the chain's factor went from 14 to 11.5 us, but its
+// inputs came later (13.9 vs 6.7 us median wait) and n = 6000 took 2.9 vs
+// 2.6 ms; profiles/r06_v9_chol_flow_ab.txt.)
+__global__ __launch_bounds__(256, 2) void k_chol_flow(double* __restrict__ A, double* __restrict__ L, int ld, int n,
+                                                      double* __restrict__ Vbuf, double* __restrict__ scal,
+                                                      const int4* __restrict__ tasks, unsigned* vflag, unsigned* tflag,
+                                                      unsigned* pflag, unsigned epoch, unsigned spin_max, int T) {
   __shared__ double S0[CB][LDP];
   __shared__ double S1[CB][LDP];
   __shared__ double Zs[CB][18];
   __shared__ CholLds cw;
-  const int4 t = tasks[blockIdx.x];
-  const FlowFlags ff{tflag, pflag, epoch, spin_max, T};
-  bool ok = true;
-  if ((t.x >> 21) & 1) {
-    const int k = t.y, d = k + 1;
-    if (threadIdx.x == 0 && k > 0) {
-      ok &= flow_poll(&tflag[d * T + d], flow_tag(epoch, k), spin_max);   // A_dd holds panels < k
-      ok &= flow_poll(&pflag[d * T + k], epoch, spin_max);                // L_{d,k}
-    }
-    __syncthreads();
-    split_critical<true>(A, L, ld, n, k, Vbuf, scal, S0, S1, Zs, cw, vflag, epoch);
+  FLOW_SLOT(blockIdx.x);
+  FLOW_STAMP(0);
+  bool ok;
+  if (blockIdx.x == 0) {
+    FLOW_STAMP(1);
+    ok = flow_chain(A, L, ld, n, Vbuf, scal, S0, S1, Zs, cw, vflag, tflag, epoch, spin_max, T);
   } else {
-    ok = upd_tile<true>(A, L, ld, n, t.x & 0xfffff, t.y, t.z, t.w, S0, S1, ((t.x >> 20) & 1) ? vflag : nullptr,
-                        epoch, spin_max, Vbuf, &ff);
+    const int4 t = tasks[blockIdx.x - 1];
+    const FlowFlags ff{tflag, pflag, epoch, spin_max, T};
+    ok = upd_tile<true>(A, L, ld, n, t.x & 0xfffff, t.y, t.z, t.w, S0, S1, ((t.x >> 20) & 1) ? vflag : nullptr, epoch,
+                        spin_max, Vbuf, &ff);
   }
+  FLOW_STAMP(2);
   if (threadIdx.x == 0 && !ok) atomicAdd(&scal[SL_CHOL_SPIN], 1.0);   // (the caller redoes the step per step)
 }
 
@@ -526,13 +630,49 @@ void chol_split_tasks(int n, std::vector<int4>& tasks, std::vector<int>& off) {
   tasks.swap(P.tasks);
   off.swap(P.off);
 }
-// ... as the flow form's one list: step k = its critical task, then its tasks
+// ... as the flow form's one list: the chain workgroup first (flow_chain),
+// then the tile tasks.  A tile task waits only on tasks before it (its tile's
+// previous range, the column tasks that formed its panels) and on V from the
+// chain; the chain waits, at step k, on the tasks that finish tiles (k+1, k)
+// and (k+1, k+1) — which come before every task waiting on V_{k+1} or later
+// (their due steps precede), so the in-order dispatch never fills the device
+// with tasks the chain's next V would release while one it needs is still
+// queued.  Within that, the order is a priority: a step's background tasks
+// (tiles due more than lag + 1 steps later) move behind the next `lag` steps'
+// chain-bound tasks (BA_CHOL_FLOW_LAG, default 1; 0: step order).
 void chol_flow_tasks(const std::vector<int4>& tasks, const std::vector<int>& off, std::vector<int4>& flow) {
-  flow.clear();
-  for (int k = 0; k + 1 < (int)off.size(); ++k) {
-    flow.push_back(make_int4(1 << 21, k, 0, 0));
-    flow.insert(flow.end(), tasks.begin() + off[k], tasks.begin() + off[k + 1]);
+  const int T = (int)off.size();
+  const char* e = getenv("BA_CHOL_FLOW_LAG");
+  const int lag = e ? std::max(0, atoi(e)) : 1;
+  int TR = T;
+  for (const int4& t : tasks) TR = std::max(TR, (t.x & 0xfffff) + 1);
+  struct E { int4 t; double level; };
+  std::vector<E> es;
+  std::vector<int> last((size_t)TR * T, -1), colt((size_t)TR * T, -1);
+  const double eps = 1e-6;
+  for (int k = 0; k + 1 < T; ++k) {
+    for (int i = off[k]; i < off[k + 1]; ++i) {
+      const int4 t = tasks[i];
+      const int I = t.x & 0xfffff, J = t.y;
+      const bool col = (t.x >> 20) & 1;
+      const int due = I == J ? J - 2 : J - 1;
+      const bool chain = col || due <= k + lag + 1;
+      double lv = chain ? k + 0.25 : k + lag + 0.5;
+      const int prev = last[(size_t)I * T + J];
+      if (t.z > 0 && prev >= 0) lv = std::max(lv, es[prev].level + eps);
+      for (int p = std::max(t.z, 1); p < t.w; ++p) {
+        if (colt[(size_t)I * T + p] >= 0) lv = std::max(lv, es[colt[(size_t)I * T + p]].level + eps);
+        if (colt[(size_t)J * T + p] >= 0) lv = std::max(lv, es[colt[(size_t)J * T + p]].level + eps);
+      }
+      const int idx = (int)es.size();
+      es.push_back({t, lv});
+      if (t.w > t.z) last[(size_t)I * T + J] = idx;
+      if (col) colt[(size_t)I * T + J] = idx;
+    }
   }
+  std::stable_sort(es.begin(), es.end(), [](const E& a, const E& b) { return a.level < b.level; });
+  flow.clear();
+  for (const E& x : es) flow.push_back(x.t);   // (the chain workgroup, flow_chain, is block 0 beside them)
 }
 int chol_split_flow() {
   const char* e = getenv("BA_CHOL_FLOW");
@@ -544,9 +684,8 @@ void launch_chol_flow(double* A, double* L, int ld, int n, double* Vbuf, double*
   const char* e = getenv("BA_CHOL_SPIN_MAX");
   const unsigned spin = e && atoi(e) > 0 ? (unsigned)atoi(e) : (1u << 17);
   hipLaunchKernelGGL(k_chol_panel, dim3(tr), dim3(256), 0, s, A, L, ld, n, 0, Vbuf);   // panel 0
-  if (nftask > 0)
-    hipLaunchKernelGGL(k_chol_flow, dim3(nftask), dim3(256), 0, s, A, L, ld, n, Vbuf, scal, ftask, vflag, tflag,
-                       pflag, epoch, spin, T);
+  hipLaunchKernelGGL(k_chol_flow, dim3(1 + nftask), dim3(256), 0, s, A, L, ld, n, Vbuf, scal, ftask, vflag, tflag,
+                     pflag, epoch, spin, T);
 }
 
 int chol_split_fused() {

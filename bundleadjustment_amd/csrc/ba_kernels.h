@@ -107,7 +107,7 @@ struct DevWork {
   bool chol_fuse;                    // split form: column tasks form the next panel in-launch (flags: cflags[0, T))
   bool chol_flow;                    // split form: the whole factorisation as one dataflow launch (k_chol_flow)
   const int4* ftask; int nftask;     // ... its task list
-  unsigned* tflag;                   // ... [TR][T] tile tags, then [TR][T] panel flags (epoch-tagged, zeroed once)
+  unsigned* tflag;                   // ... [TR][T] tile tags, [TR][T] panel flags (epoch-tagged, zeroed once)
   double* yg;                        // [n][2] back-substitution hand-off granules {y, epoch} (zeroed once)
   unsigned* cflags;                  // [T + TR*T] persistent-Cholesky hand-off flags (epoch-tagged, zeroed once)
   bool chol_persist;                 // the factorisation runs as one persistent launch (ba_chol_persist.hip)

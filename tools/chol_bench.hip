@@ -167,8 +167,8 @@ int main(int argc, char** argv) {
     const int TRr = (nrows + CB - 1) / CB;
     CK(hipMalloc(&dflow, sizeof(int4) * flow.size()));
     CK(hipMemcpy(dflow, flow.data(), sizeof(int4) * flow.size(), hipMemcpyHostToDevice));
-    CK(hipMalloc(&dtf, sizeof(unsigned) * 2 * TRr * T));
-    CK(hipMemset(dtf, 0, sizeof(unsigned) * 2 * TRr * T));
+    CK(hipMalloc(&dtf, sizeof(unsigned) * (2 * TRr * T + 2)));
+    CK(hipMemset(dtf, 0, sizeof(unsigned) * (2 * TRr * T + 2)));
     for (int rep = 0; rep < 3; ++rep) {
       ++vepoch;
       CK(hipMemcpy(dA, A.data(), sizeof(double) * A.size(), hipMemcpyHostToDevice));
@@ -192,6 +192,26 @@ int main(int argc, char** argv) {
     size_t diff = 0;
     for (int i = 0; i < n; ++i) diff += std::memcmp(&ys[i], &yf[i], 8) != 0;
     printf("flow vs per-step: y entries differing %zu\n", diff);
+#ifdef BA_CHOL_FLOW_TRACE
+    {
+      // the last flow launch's task stamps + the list, for tools/flow_trace.py
+      std::vector<unsigned long long> tr((size_t)(1 << 16) * 4);
+      CK(hipMemcpyFromSymbol(tr.data(), HIP_SYMBOL(g_ftrace), sizeof(unsigned long long) * tr.size()));
+      FILE* f = fopen(getenv("FLOW_TRACE_OUT") ? getenv("FLOW_TRACE_OUT") : "flow_trace.bin", "wb");
+      std::vector<int4> lst(1, make_int4(1 << 21, 0, 0, 0));   // slot 0: the chain workgroup
+      lst.insert(lst.end(), flow.begin(), flow.end());
+      const unsigned nt = (unsigned)std::min<size_t>(lst.size(), 1 << 16);
+      fwrite(&nt, 4, 1, f);
+      fwrite(lst.data(), sizeof(int4), nt, f);
+      fwrite(tr.data(), sizeof(unsigned long long) * 4, nt, f);
+      std::vector<unsigned long long> ch(4096 * 6);
+      CK(hipMemcpyFromSymbol(ch.data(), HIP_SYMBOL(g_fchain), sizeof(unsigned long long) * ch.size()));
+      const unsigned nc = (unsigned)(T - 1);
+      fwrite(&nc, 4, 1, f);
+      fwrite(ch.data(), sizeof(unsigned long long) * 6, nc, f);
+      fclose(f);
+    }
+#endif
     if (diff) return 5;
   }
   std::vector<double> y(n), Sh(64);

@@ -53,6 +53,54 @@ static int check(int T, int TR, int rank, double budget, bool show) {
   return bad;
 }
 
+// the flow form's one list: replay it in order with the chain workgroup
+// advancing whenever its inputs are complete (step k: tiles (k+1, k) and
+// (k+1, k+1) at panel k), and check that every task's inputs are complete
+// when it comes (tile prefix, panels, V) — a task that needs a V the chain
+// cannot produce from the tasks before it could hold the last free slot
+static int check_flow(int T, int TR, int rank) {
+  CholSplitPlan P;
+  chol_split_plan(T, TR, rank, 1.0, P);
+  std::vector<int4> flow;
+  chol_flow_tasks(P.tasks, P.off, flow);
+  std::vector<std::vector<int>> a(TR, std::vector<int>(T, 0));
+  std::vector<std::vector<char>> pan(TR, std::vector<char>(T, 0));
+  std::vector<char> V(T, 0);
+  for (int I = 1; I < TR; ++I) pan[I][0] = 1;   // panel 0: before the launch
+  V[0] = 1;
+  int chain = 0;                                // next step of the chain workgroup
+  auto advance = [&]() {
+    while (chain + 1 < T && a[chain + 1][chain] == chain && a[chain + 1][chain + 1] == chain) {
+      a[chain + 1][chain + 1] = chain + 1;      // (the chain applies panel k to the diagonal itself)
+      V[chain + 1] = 1;
+      ++chain;
+    }
+  };
+  int bad = 0;
+  auto fail = [&](const char* what, int i, int x, int y) {
+    if (bad++ < 10) printf("flow T=%d TR=%d rank %d: entry %d (%d,%d): %s\n", T, TR, rank, i, x, y, what);
+  };
+  if (flow.size() != P.tasks.size()) fail("layout", 0, 0, 0);
+  advance();
+  for (int i = 0; i < (int)flow.size(); ++i) {
+    const int4 q = flow[i];
+    const int I = q.x & 0xfffff, J = q.y;
+    if (a[I][J] != q.z) fail("tile prefix", i, I, J);
+    for (int p = q.z; p < q.w; ++p)
+      if (!pan[I][p] || !pan[J][p]) fail("panel not formed", i, I, J);
+    a[I][J] = q.w;
+    if ((q.x >> 20) & 1) {
+      advance();
+      if (!V[J]) fail("V not reachable by the chain", i, I, J);
+      if (a[I][J] != J) fail("column task: tile incomplete", i, I, J);
+      pan[I][J] = 1;
+    }
+    advance();
+  }
+  if (chain != T - 1) fail("chain did not finish", 0, chain, T);
+  return bad;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1) {
     const int T = atoi(argv[1]);
@@ -63,6 +111,8 @@ int main(int argc, char** argv) {
     for (double budget : {0.5, 1.0, 1.5})
       for (int T = 2; T <= 100; ++T)
         for (int TR = T; TR <= T + 1; ++TR, ++cases) bad += check(T, TR, rank, budget, false);
+  for (int T = 2; T <= 100; ++T)
+    for (int TR = T; TR <= T + 1; ++TR, ++cases) bad += check_flow(T, TR, 4);
   printf("%d cases, %d violations\n", cases, bad);
   return bad ? 1 : 0;
 }

@@ -14,7 +14,7 @@
 #   hbm:TAG[:ARGS]             FETCH_SIZE and WRITE_SIZE passes (separate, as the
 #                              guide prescribes), summarised by tools/pmc_summary.py
 #   sq:TAG[:ARGS]              one SQ / LDS counter pass, tools/pmc_table.py
-#   chol:N[:BIN]               tools/chol_bench_ns (or BIN) at order N
+#   chol:N[:BIN[:TAG]]         tools/chol_bench_ns (or BIN) at order N (output file tagged TAG)
 #   env:VAR=VALUE              exported for the following steps
 #   unset:VAR                  unexported
 # Every GPU step has its own time limit; a step that faults, aborts or times
@@ -80,8 +80,9 @@ for step in "$@"; do
       head -20 "$OUT/pmc_${a1}_sq.txt" ;;
     chol)
       bin=${a2:-tools/chol_bench_ns}
-      timeout -k 5 180 "$bin" "$a1" > "$OUT/chol_$(basename "$bin")_$a1.txt" 2>&1
-      rc=$?; grep -E "factor|differing|residual" "$OUT/chol_$(basename "$bin")_$a1.txt" | head -6 ;;
+      cf="$OUT/chol_$(basename "$bin")_$a1${a3:+_$a3}.txt"
+      timeout -k 5 180 "$bin" "$a1" > "$cf" 2>&1
+      rc=$?; grep -E "factor (flow|streamed)|differing|residual" "$cf" | tail -5 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "$step rc=$rc"
