@@ -644,6 +644,12 @@ void chol_flow_tasks(const std::vector<int4>& tasks, const std::vector<int>& off
   const int T = (int)off.size();
   const char* e = getenv("BA_CHOL_FLOW_LAG");
   const int lag = e ? std::max(0, atoi(e)) : 1;
+  // the tasks on the tiles next to the diagonal (I - J <= 2: the chain's own
+  // inputs and the panel rows they are formed from) go `lead` steps ahead
+  // (BA_CHOL_FLOW_LEAD; the chain still waited ~6 us per step for them: the
+  // latency is the hand-offs themselves, not the dispatch order)
+  const char* e2 = getenv("BA_CHOL_FLOW_LEAD");
+  const int lead = e2 ? std::max(0, atoi(e2)) : 0;   // (2, 4, 8 measured slower: 2.66, 2.67, 2.73 vs 2.60 ms)
   int TR = T;
   for (const int4& t : tasks) TR = std::max(TR, (t.x & 0xfffff) + 1);
   struct E { int4 t; double level; };
@@ -657,7 +663,7 @@ void chol_flow_tasks(const std::vector<int4>& tasks, const std::vector<int>& off
       const bool col = (t.x >> 20) & 1;
       const int due = I == J ? J - 2 : J - 1;
       const bool chain = col || due <= k + lag + 1;
-      double lv = chain ? k + 0.25 : k + lag + 0.5;
+      double lv = I - J <= 2 ? k - lead + 0.125 : (chain ? k + 0.25 : k + lag + 0.5);
       const int prev = last[(size_t)I * T + J];
       if (t.z > 0 && prev >= 0) lv = std::max(lv, es[prev].level + eps);
       for (int p = std::max(t.z, 1); p < t.w; ++p) {
