@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "ba_chol_split.hip"
@@ -102,6 +103,14 @@ static int check_flow(int T, int TR, int rank) {
 }
 
 int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "quick") {   // (tests/test_chol_plan.py: T <= 40)
+    int bad = 0, cases = 0;
+    for (int rank : {1, 4})
+      for (int T = 2; T <= 40; ++T)
+        for (int TR = T; TR <= T + 1; ++TR, ++cases) bad += check(T, TR, rank, 1.0, false) + check_flow(T, TR, rank);
+    printf("%d cases, %d violations\n", cases, bad);
+    return bad ? 1 : 0;
+  }
   if (argc > 1) {
     const int T = atoi(argv[1]);
     return check(T, T, argc > 2 ? atoi(argv[2]) : 4, argc > 3 ? atof(argv[3]) : 1.0, true) ? 1 : 0;
