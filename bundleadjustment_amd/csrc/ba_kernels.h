@@ -198,6 +198,7 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, do
                         bool with_diag = false);
 bool pairs_take_fold(const DevProblem& P, const DevWork& W);
 bool pairs_take_diag(const DevProblem& P, const DevWork& W);
+bool pairs_take_diag_nt(const DevProblem& P, const DevWork& W);   // ... beyond the LDS camera table
 void launch_cam_fold_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
 void launch_cam_add_diag(const DevProblem& P, const DevWork& W, double radius, hipStream_t s);
 // ba_chol.hip; epoch: per-context launch counter (>= 1) tagging the

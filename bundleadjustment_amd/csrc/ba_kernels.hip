@@ -3558,6 +3558,15 @@ bool pairs_take_diag(const DevProblem& P, const DevWork& W) {
   const char* e = getenv("BA_DIAG_IN_PAIRS");
   return !(e && e[0] == '0') && pairs_take_fold(P, W) && !W.jdiag && !W.w32 && P.nvc > 0;
 }
+// ... beyond the LDS camera table (k_schur_pairs_cd<false>, 1000 cameras):
+// the diagonal slices' waves use the same 64 KB of DMA buffers, so they ride
+// there too (the fold then follows in its own launch)
+bool pairs_take_diag_nt(const DevProblem& P, const DevWork& W) {
+  const char* e = getenv("BA_DIAG_IN_PAIRS");
+  const char* de = getenv("BA_PAIRS_DMA");
+  return !(e && e[0] == '0') && !(de && de[0] == '0') && W.nblocks > 0 && W.wcompact && !pairs_take_fold(P, W) &&
+         !W.jdiag && !W.w32 && P.nvc > 0;
+}
 void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, double fold_radius, bool with_diag) {
   if (W.nblocks == 0) return;
   // 16 blocks per workgroup (4 waves of 4) over the largest XCD range, at
@@ -3577,8 +3586,15 @@ void launch_schur_pairs(const DevProblem& P, const DevWork& W, hipStream_t s, do
   if (W.wcompact && !ctab && !(de && de[0] == '0')) {
     // 1000 cameras (C4): LDS-DMA gathers with the camera constants per block
     // in registers
-    hipLaunchKernelGGL(k_schur_pairs_cd<false>, dim3(grid), dim3(256), kPairsDmaLds, s, P, W.blocks, xoff, W.pairs,
-                       W.W, W.scale_c, W.S, grid, FoldArgs{W.cpart, 0, W.Hcc, W.gc, W.diag_c, 0.0, W.scal});
+    FoldArgs fa{W.cpart, 0, W.Hcc, W.gc, W.diag_c, 0.0, W.scal};
+    int fgrid = 0;
+    if (with_diag) {   // the diagonal slices ride in this launch (dispatched last: they fill the pairs' tail)
+      fa.u = W.u;
+      fa.G = cam_split_count(W);
+      fgrid = (P.nvc * fa.G + 3) / 4;
+    }
+    hipLaunchKernelGGL(k_schur_pairs_cd<false>, dim3(grid + fgrid), dim3(256), kPairsDmaLds, s, P, W.blocks, xoff,
+                       W.pairs, W.W, W.scale_c, W.S, grid, fa);
   }
   else if (W.wcompact && ctab) {
     FoldArgs fa{W.cpart, 0, W.Hcc, W.gc, W.diag_c, fold_radius, W.scal};

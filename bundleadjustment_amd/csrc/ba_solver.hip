@@ -896,7 +896,7 @@ bool form_reduced_dense(ba_ctx* ctx, double radius, bool allow_ov = true) {
   // ... and that fold rides in the pair pass's launch when it can (one
   // launch fewer; the fold writes only the diagonal blocks and the rhs)
   const bool fold_in_pairs = fused_diag && radius > 0.0 && pairs_take_fold(P, W);
-  if (fold_in_pairs && pairs_take_diag(P, W)) {
+  if ((fold_in_pairs && pairs_take_diag(P, W)) || (fused_diag && radius > 0.0 && pairs_take_diag_nt(P, W))) {
     // ... or rather the diagonal slices ride in it (dispatched after the pair
     // workgroups, they fill the pass's tail) and the fold follows
     launch_schur_pairs(P, W, s, 0.0, true);

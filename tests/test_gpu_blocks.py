@@ -138,16 +138,23 @@ def test_overlapped_pass_is_bitwise_the_separate_passes(monkeypatch):
 def test_many_camera_dma_pairs_are_bitwise_the_register_pairs(monkeypatch):
     """The C4 shard (1000 cameras): the pair pass gathers the compact records
     by LDS-DMA with each block's camera constants in registers (the LDS
-    camera table does not fit beside the DMA buffers); BA_PAIRS_DMA=0 keeps
-    the per-lane register gathers with the table in LDS.  Same lanes, pairs
-    and products: the reduced system is bitwise the same."""
+    camera table does not fit beside the DMA buffers), and the diagonal
+    slices ride in its launch on the same DMA buffers (pairs_take_diag_nt);
+    BA_DIAG_IN_PAIRS=0 keeps their separate launch, BA_PAIRS_DMA=0 the
+    per-lane register gathers with the table in LDS and the separate
+    diagonal launch.  Same lanes, pairs, products and reductions: the reduced
+    system is bitwise the same in all three."""
     p = make_config("c4", scale=0.125)
     with Solver(0) as s:
         s.set_problem(p)
         a = s.debug_blocks(1e4)
+        monkeypatch.setenv("BA_DIAG_IN_PAIRS", "0")
+        c = s.debug_blocks(1e4)
+        monkeypatch.delenv("BA_DIAG_IN_PAIRS")
         monkeypatch.setenv("BA_PAIRS_DMA", "0")
         b = s.debug_blocks(1e4)
     n = a["n"]
     tril = np.tril_indices(n)
-    assert np.array_equal(a["S"][tril], b["S"][tril])
-    assert np.array_equal(a["rhs"], b["rhs"])
+    for other in (b, c):
+        assert np.array_equal(a["S"][tril], other["S"][tril])
+        assert np.array_equal(a["rhs"], other["rhs"])
