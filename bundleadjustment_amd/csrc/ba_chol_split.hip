@@ -1,9 +1,17 @@
-// ba_chol_split.hip — split form of the dense Cholesky block step for large
-// reduced systems (>= kCholSplitBlocks block columns, e.g. C4's 6000 rows):
-// k_chol_panel forms L_{I,k} = A_{I,k} V_k^T once per tile row, then every
-// trailing tile does a single GEMM.  Its own translation unit, so the fused
-// step of ba_chol.hip keeps its code generation (a shared template changed
-// the inlining of the critical workgroup's factor_invert_blk).
+// ba_chol_split.hip — the dense Cholesky of large reduced systems (>=
+// kCholSplitBlocks block columns, e.g. C4's 6000 rows), in three forms that
+// share one host-planned task table (chol_split_plan) and are bitwise equal:
+//   flow (default)  k_chol_flow: the whole factorisation as one dataflow
+//                   launch, a chain workgroup for the diagonal blocks and the
+//                   tile tasks, synchronised by epoch-tagged flags;
+//   fused           per block step, k_chol_upd: the critical workgroup and the
+//                   step's tile tasks, whose column tasks form the next panel;
+//   panels          the same with k_chol_panel launches (BA_CHOL_FUSE=0);
+// and the round-5 rank-64 form (k_chol_step_split, BA_CHOL_RANK=0), where
+// every trailing tile takes every panel.  DESIGN.md section 15.2.  Its own
+// translation unit, so the fused step of ba_chol.hip keeps its code
+// generation (a shared template changed the inlining of the critical
+// workgroup's factor_invert_blk; here the calls force it inline).
 #include "ba_chol.h"
 
 #include <algorithm>
@@ -12,7 +20,7 @@
 
 namespace bahip {
 
-// One block step.  k < 0: factor block 0 only (grid 1x1).
+// The rank-64 form: one block step.  k < 0: factor block 0 only (grid 1x1).
 //   A    working matrix ((n+1) x ld), trailing part updated in place
 //   L    output factor ((n+1) x ld)
 //   Vbuf [T][64][64] inverses of the diagonal blocks
