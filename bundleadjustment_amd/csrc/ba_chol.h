@@ -21,7 +21,10 @@
 namespace bahip {
 
 constexpr int CB = 64;           // block size
-constexpr int LDP = CB + 2;      // padded LDS row (doubles): conflict-free MFMA operand reads (16 rows x 4 k per wave)
+#ifndef BA_LDP
+#define BA_LDP (CB + 2)   // (diagnostic builds may pad differently: tools/chol_bench A/B, profiles/r06_v13_*)
+#endif
+constexpr int LDP = BA_LDP;      // padded LDS row (doubles): conflict-free MFMA operand reads (16 rows x 4 k per wave)
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 

@@ -18,7 +18,14 @@
 
 #include "ba_chol.hip"
 #include "ba_chol_split.hip"
+#ifndef CHOL_BENCH_NO_PERSIST   // (-DCHOL_BENCH_NO_PERSIST: a split-form-only build, e.g. with another LDS pad)
 #include "ba_chol_persist.hip"
+#else
+namespace bahip {   // (referenced by ba_chol.hip's solver entry points, never called here)
+void launch_chol_persist(double*, double*, int, int, double*, double*, unsigned*, unsigned, hipStream_t) { abort(); }
+void launch_chol_persist_ov(const DevProblem&, const DevWork&, OvPlan&, double, int, hipStream_t, bool) { abort(); }
+}  // namespace bahip
+#endif
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 
@@ -218,6 +225,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(y.data(), dy, sizeof(double) * n, hipMemcpyDeviceToHost));
   // the persistent form (one launch, look-ahead): time it and check that it
   // reproduces the per-step factorisation bit for bit
+#ifndef CHOL_BENCH_NO_PERSIST
   if (chol_persist_fits(0, n)) {
     unsigned* dflags;
     const int TR = (n + 1 + CB - 1) / CB;
@@ -311,6 +319,7 @@ int main(int argc, char** argv) {
   } else {
     printf("persistent form: grid %d does not fit\n", chol_persist_grid(n));
   }
+#endif
   CK(hipMemcpy(Sh.data(), dS, sizeof(double) * 64, hipMemcpyDeviceToHost));
   if (T >= 16 && getenv("CHOL_TASK_PROBE")) {
     // throughput of the split form's tile tasks alone (k_chol_upd with k = -2:
